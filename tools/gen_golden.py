@@ -1,0 +1,377 @@
+#!/usr/bin/env python3
+"""Generate golden vectors by running the REAL reference hot path in this container.
+
+Imports the reference read-only from /root/reference/source (with a no-op
+``torch.utils.tensorboard`` stub: tensorboard is not installed and the
+reference's utils/logger.py imports it at module top) and records inputs,
+initial weights and outputs of:
+
+  * GPI / get_successors              (sfdqn.py:153-240, 290-301)
+  * DeepSF.update_successor           (sfdqn.py:303-371), use_gpi True / False
+  * DeepSF.update_successor all-task  (features/deep.py:93-131 + agents/sfdqn.py:47-60,
+                                       with SF.update_reward LMS, features/successor.py:146-167)
+  * TSFDQN.update_successor           (tsfdqn.py:588-709) and the planar-flow twin (tsfdqn_nf.py)
+
+into small ``.npz`` fixtures under tests/golden/.  The fixtures are data only;
+this script never travels to the GPU box (it needs /root/reference).
+
+Usage:  python tools/gen_golden.py
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+REF = "/root/reference/source"
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from tests.golden.recipe import SHAPES, full_size_heads  # noqa: E402  (our own seed recipe)
+
+
+def _install_reference():
+    tb = types.ModuleType("torch.utils.tensorboard")
+
+    class _NoWriter:
+        def __init__(self, *a, **k):
+            pass
+
+        def add_scalar(self, *a, **k):
+            pass
+
+        add_scalars = add_histogram = flush = close = add_scalar
+
+    tb.SummaryWriter = _NoWriter
+    sys.modules["torch.utils.tensorboard"] = tb
+    sys.path.insert(0, REF)
+    from utils.torch import set_torch_device  # reference module
+    set_torch_device(False)
+    from utils.logger import set_logger_level
+    set_logger_level(False)
+
+
+_install_reference()
+import sfdqn as ref_sfdqn          # noqa: E402
+import tsfdqn as ref_tsfdqn        # noqa: E402
+import tsfdqn_nf as ref_tsfdqn_nf  # noqa: E402
+from features import deep as ref_deep  # noqa: E402
+
+HYPER = {
+    "learning_rate_sf": 1e-3, "learning_rate_w": 1e-3, "learning_rate_g": 1e-3,
+    "learning_rate_h": 1e-3, "weight_decay_sf": 0, "weight_decay_w": 0,
+    "weight_decay_g": 0, "weight_decay_h": 0, "g_h_function_dims": 16,
+    "n_coupling_layers": 3, "beta_loss_coefficient": 0.5, "learning_rate_w_lms": 0.05,
+}
+
+
+def psi_lambda(H, acts, lr=1e-3):
+    """The reference's ψ architecture (main_sfdqn_torch.py:44-78)."""
+    act_cls = {"relu": torch.nn.ReLU, "tanh": torch.nn.Tanh}
+
+    def build(num_inputs, output_dim, reshape_dim, reshape_axis=1):
+        layers = OrderedDict()
+        layers["layer_input"] = torch.nn.Linear(num_inputs, H)
+        for j, a in enumerate(acts):
+            layers[f"layer_{j}"] = torch.nn.Linear(H, H)
+            layers[f"activation_layer_{j}"] = act_cls[a]()
+        layers["layer_output"] = torch.nn.Linear(H, output_dim)
+        layers["layer_unflatten"] = torch.nn.Unflatten(reshape_axis, reshape_dim)
+        model = torch.nn.Sequential(layers)
+        return model, torch.nn.MSELoss(), torch.optim.Adam(model.parameters(), lr=lr)
+
+    return build
+
+
+class SynthTask:
+    """Minimal Task (tasks/task.py interface) for driving add_training_task."""
+
+    def __init__(self, n_s, A, d, idx):
+        self.n_s, self.A, self.d, self.idx = n_s, A, d, idx
+
+    def action_count(self):
+        return self.A
+
+    def feature_dim(self):
+        return self.d
+
+    def encode_dim(self):
+        return self.n_s
+
+    def features(self, state, action, next_state):
+        raise NotImplementedError("golden generation feeds transitions directly")
+
+    def get_w(self):
+        w = torch.zeros((self.d, 1))
+        w[self.idx % self.d, 0] = 1.0
+        return w
+
+    def __repr__(self):
+        return f"SynthTask({self.idx})"
+
+
+def flat(module):
+    return torch.cat([p.detach().reshape(-1) for p in module.parameters()]).clone()
+
+
+def adam_state(optim, params):
+    m, v = [], []
+    for p in params:
+        st = optim.state[p]
+        m.append(st["exp_avg"].reshape(-1))
+        v.append(st["exp_avg_sq"].reshape(-1))
+    return torch.cat(m).clone(), torch.cat(v).clone()
+
+
+def batch_stream(n_s, A, d, B, k, gen, terminal_p=0.1):
+    out = []
+    for _ in range(k):
+        s = torch.randn(B, n_s, generator=gen)
+        a = torch.randint(0, A, (B,), generator=gen)
+        phi = torch.rand(B, d, generator=gen)
+        r = torch.rand(B, 1, generator=gen)
+        s1 = torch.randn(B, n_s, generator=gen)
+        gamma = torch.where(torch.rand(B, generator=gen) < terminal_p, 0.0, 0.9).float()
+        out.append((s, a, r, phi, s1, gamma))
+    return out
+
+
+def stack_batches(batches):
+    names = ["s", "a", "r", "phi", "s1", "gamma"]
+    return {f"b_{n}": np.stack([b[j].numpy() for b in batches]) for j, n in enumerate(names)}
+
+
+def np_(t):
+    return t.detach().numpy().copy()
+
+
+# --------------------------------------------------------------------------------------
+def build_sfdqn(shape, T, target_update_ev=1000):
+    n_s, H, A, d, acts = shape
+    sf = ref_sfdqn.DeepSF(pytorch_model_handle=psi_lambda(H, acts), use_true_reward=False,
+                          target_update_ev=target_update_ev, hyperparameters=HYPER)
+    sf.reset()
+    for t in range(T):
+        sf.add_training_task(SynthTask(n_s, A, d, t))
+    return sf
+
+
+def sfdqn_weights(sf):
+    online = torch.stack([flat(sf.psi[t][0][0]) for t in range(sf.n_tasks)])
+    target = torch.stack([flat(sf.psi[t][1][0]) for t in range(sf.n_tasks)])
+    w = torch.stack([sf.fit_w[t].weight.detach().reshape(-1).clone() for t in range(sf.n_tasks)])
+    return online, target, w
+
+
+def load_sfdqn_weights(sf, online, w=None):
+    with torch.no_grad():
+        for t in range(sf.n_tasks):
+            off = 0
+            for mod in (sf.psi[t][0][0], sf.psi[t][1][0]):
+                off = 0
+                for p in mod.parameters():
+                    n = p.numel()
+                    p.copy_(online[t, off:off + n].view_as(p))
+                    off += n
+            if w is not None:
+                sf.fit_w[t].weight.copy_(w[t].view(1, -1))
+
+
+def gen_gpi(name, shape, T, tie=False):
+    torch.manual_seed(100 + T)
+    sf = build_sfdqn(shape, T)
+    n_s, H, A, d, acts = shape
+    online, _, w = sfdqn_weights(sf)
+    if tie:
+        # exact task tie: head 2 == head 0; exact action tie in head 1: action 3 == action 1
+        online[2] = online[0]
+        P_out = H * A * d + A * d
+        out_off = online.shape[1] - P_out
+        Wo = online[1, out_off:out_off + H * A * d].view(A * d, H)
+        bo = online[1, out_off + H * A * d:].view(A * d)
+        Wo[3 * d:4 * d] = Wo[1 * d:2 * d]
+        bo[3 * d:4 * d] = bo[1 * d:2 * d]
+        load_sfdqn_weights(sf, online)
+    gen = torch.Generator().manual_seed(7)
+    S1 = torch.randn(1, n_s, generator=gen)
+    S32 = torch.randn(32, n_s, generator=gen)
+    rec = dict(n_s=n_s, H=H, A=A, d=d, T=T, acts=np.array(acts), online=np_(online), w=np_(w),
+               S1=np_(S1), S32=np_(S32))
+    with torch.no_grad():
+        rec["psi1"] = np_(sf.get_successors(S1))
+        rec["psi32"] = np_(sf.get_successors(S32))
+        for i in range(T):
+            q, task = sf.GPI(S1, i)
+            rec[f"q1_{i}"], rec[f"task1_{i}"] = np_(q), np.array(int(task))
+            q, task = sf.GPI(S32, i)
+            rec[f"q32_{i}"], rec[f"task32_{i}"] = np_(q), np_(task)
+            rec[f"next32_{i}"] = np_(torch.argmax(torch.max(q, axis=1).values, axis=-1))
+    np.savez_compressed(os.path.join(OUT, f"gpi_{name}.npz"), **rec)
+
+
+def gen_full_size():
+    """Reacher-shape C2 at H=256, T=8: weights from our seed recipe (not stored)."""
+    n_s, H, A, d, acts = SHAPES["reacher17_full"]
+    T = 8
+    online, w = full_size_heads()
+    sf = build_sfdqn(SHAPES["reacher17_full"], T)
+    load_sfdqn_weights(sf, online, w)
+    gen = torch.Generator().manual_seed(11)
+    S32 = torch.randn(32, n_s, generator=gen)
+    S1 = S32[:1].clone()
+    rec = dict(n_s=n_s, H=H, A=A, d=d, T=T, acts=np.array(acts), S32=np_(S32),
+               online_sum=np.float64(online.double().sum()), w=np_(w))
+    with torch.no_grad():
+        rec["psi32"] = np_(sf.get_successors(S32))
+        for i in range(T):
+            q, task = sf.GPI(S32, i)
+            rec[f"q32_{i}"], rec[f"task32_{i}"] = np_(q), np_(task)
+            rec[f"next32_{i}"] = np_(torch.argmax(torch.max(q, axis=1).values, axis=-1))
+            q, task = sf.GPI(S1, i)
+            rec[f"task1_{i}"] = np.array(int(task))
+    np.savez_compressed(os.path.join(OUT, "gpi_reacher17_full.npz"), **rec)
+
+
+def gen_sfdqn_updates(name, shape, T, k, use_gpi, target_update_ev):
+    torch.manual_seed(200 + int(use_gpi))
+    sf = build_sfdqn(shape, T, target_update_ev)
+    n_s, H, A, d, acts = shape
+    online0, target0, w0 = sfdqn_weights(sf)
+    batches = batch_stream(n_s, A, d, 32, k, torch.Generator().manual_seed(3))
+    rec = dict(n_s=n_s, H=H, A=A, d=d, T=T, acts=np.array(acts), k=k, use_gpi=int(use_gpi),
+               target_update_ev=target_update_ev, online0=np_(online0), target0=np_(target0),
+               w0=np_(w0), **stack_batches(batches))
+    losses, nexts, policies = [], [], []
+    for j, b in enumerate(batches):
+        i = j % T
+        policies.append(i)
+        # reproduce next actions the reference uses (same code path, no state change)
+        with torch.no_grad():
+            if use_gpi:
+                q1, _ = sf.GPI(b[4], i)
+                na = torch.argmax(torch.max(q1, axis=1).values, axis=-1)
+            else:
+                na = torch.squeeze(torch.argmax(sf.fit_w[i](sf.get_successor(b[4], i)), axis=1), axis=1)
+        nexts.append(np_(na))
+        loss, l1, l2 = sf.update_successor(b, i, use_gpi)
+        losses.append([float(loss), float(l1), float(l2)])
+        if j == 0:
+            on1, ta1, w1 = sfdqn_weights(sf)
+            rec.update(online1=np_(on1), target1=np_(ta1), w1=np_(w1))
+    online, target, w = sfdqn_weights(sf)
+    m = torch.zeros_like(online); v = torch.zeros_like(online)
+    wm = torch.zeros_like(w); wv = torch.zeros_like(w)
+    steps = []
+    for t in range(T):
+        model = sf.psi[t][0][0]
+        optim = sf.psi[t][0][2]
+        if optim.state.get(next(model.parameters())) is None:
+            steps.append(0)
+            continue
+        m[t], v[t] = adam_state(optim, list(model.parameters()))
+        wm[t], wv[t] = adam_state(optim, list(sf.fit_w[t].parameters()))
+        steps.append(int(optim.state[next(model.parameters())]["step"]))
+    rec.update(policies=np.array(policies), losses=np.array(losses), next_actions=np.stack(nexts),
+               online=np_(online), target=np_(target), w=np_(w), m=np_(m), v=np_(v), wm=np_(wm),
+               wv=np_(wv), steps=np.array(steps), since_target=np.array(sf.updates_since_target_updated))
+    np.savez_compressed(os.path.join(OUT, f"upd_{name}.npz"), **rec)
+
+
+def gen_deep_alltask(shape, T, k, target_update_ev):
+    """features/deep.py DeepSF driven like agents/sfdqn.py:47-60 (LMS w, all heads per step)."""
+    torch.manual_seed(300)
+    n_s, H, A, d, acts = shape
+    lam = psi_lambda(H, acts, lr=1e-3)
+    sf = ref_deep.DeepSF(pytorch_model_handle=lam, target_update_ev=target_update_ev,
+                         hyperparameters={"learning_rate_w": HYPER["learning_rate_w_lms"]})
+    sf.reset()
+    for t in range(T):
+        sf.add_training_task(SynthTask(n_s, A, d, t))
+    online0 = torch.stack([flat(sf.psi[t][0][0]) for t in range(T)])
+    w0 = torch.stack([sf.fit_w[t].reshape(-1).clone() for t in range(T)])
+    gen = torch.Generator().manual_seed(5)
+    batches = batch_stream(n_s, A, d, 32, k, gen)
+    lms_phi = torch.rand(k, d, generator=gen)
+    lms_task = torch.randint(0, T, (k,), generator=gen)
+    lms_r = torch.stack([(lms_phi[j] * sf.true_w[int(lms_task[j])].reshape(-1)).sum() for j in range(k)])
+    rec = dict(n_s=n_s, H=H, A=A, d=d, T=T, acts=np.array(acts), k=k, target_update_ev=target_update_ev,
+               alpha_w=HYPER["learning_rate_w_lms"], online0=np_(online0), w0=np_(w0),
+               lms_phi=np_(lms_phi), lms_task=np_(lms_task), lms_r=np_(lms_r), **stack_batches(batches))
+    losses = []
+    for j, b in enumerate(batches):
+        sf.update_reward(lms_phi[j], lms_r[j], int(lms_task[j]))
+        s, a, r, phi, s1, gamma = b
+        step_l = []
+        for i in range(T):
+            sf.update_successor((s, a, phi, s1, gamma), i)
+        losses.append(step_l)
+        if j == 0:
+            rec["online1"] = np_(torch.stack([flat(sf.psi[t][0][0]) for t in range(T)]))
+    online = torch.stack([flat(sf.psi[t][0][0]) for t in range(T)])
+    target = torch.stack([flat(sf.psi[t][1][0]) for t in range(T)])
+    w = torch.stack([sf.fit_w[t].reshape(-1).clone() for t in range(T)])
+    m, v = zip(*[adam_state(sf.psi[t][0][2], list(sf.psi[t][0][0].parameters())) for t in range(T)])
+    rec.update(online=np_(online), target=np_(target), w=np_(w), m=np_(torch.stack(m)),
+               v=np_(torch.stack(v)), since_target=np.array(sf.updates_since_target_updated))
+    np.savez_compressed(os.path.join(OUT, "upd_deep_alltask.npz"), **rec)
+
+
+def gen_tsf(name, module, shape, T, k, K):
+    torch.manual_seed(400 + K)
+    n_s, H, A, d, acts = shape
+    hyper = dict(HYPER, n_coupling_layers=K)
+    sf = module.DeepTSF(pytorch_model_handle=psi_lambda(H, acts), use_true_reward=False,
+                        target_update_ev=4, hyperparameters=hyper)
+    agent = module.TSFDQN(deep_sf=sf, buffer_handle=lambda: None, gamma=0.9, T=500, encoding=None,
+                          use_gpi=True, hyperparameters=hyper)
+    agent.reset()
+    for t in range(T):
+        agent.add_training_task(SynthTask(n_s, A, d, t))
+    online0 = torch.stack([flat(sf.psi[t][0][0]) for t in range(T)])
+    w0 = torch.stack([sf.fit_w[t].weight.detach().reshape(-1).clone() for t in range(T)])
+    g0 = torch.stack([flat(agent.g_functions[t]) for t in range(T)])
+    h0 = flat(agent.h_function)
+    batches = batch_stream(n_s, A, d, 32, k, torch.Generator().manual_seed(9))
+    rec = dict(n_s=n_s, H=H, A=A, d=d, T=T, acts=np.array(acts), k=k, K=K, G=hyper["g_h_function_dims"],
+               beta=hyper["beta_loss_coefficient"], target_update_ev=4, online0=np_(online0),
+               w0=np_(w0), g0=np_(g0), h0=np_(h0), **stack_batches(batches))
+    losses, policies = [], []
+    for j, b in enumerate(batches):
+        i = j % T
+        policies.append(i)
+        loss, l1, l2 = agent.update_successor(b, i, True)
+        losses.append([float(loss), float(l1), float(l2)])
+    online = torch.stack([flat(sf.psi[t][0][0]) for t in range(T)])
+    target = torch.stack([flat(sf.psi[t][1][0]) for t in range(T)])
+    w = torch.stack([sf.fit_w[t].weight.detach().reshape(-1).clone() for t in range(T)])
+    g = torch.stack([flat(agent.g_functions[t]) for t in range(T)])
+    h = flat(agent.h_function)
+    rec.update(policies=np.array(policies), losses=np.array(losses), online=np_(online),
+               target=np_(target), w=np_(w), g=np_(g), h=np_(h))
+    np.savez_compressed(os.path.join(OUT, f"upd_{name}.npz"), **rec)
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    torch.set_num_threads(4)
+    gen_gpi("reacher17", SHAPES["reacher17"], 4)
+    gen_gpi("hopper11", SHAPES["hopper11"], 3)
+    gen_gpi("cartpole", SHAPES["cartpole"], 2)
+    gen_gpi("refreacher", SHAPES["refreacher"], 4)
+    gen_gpi("tanh_odd", SHAPES["tanh_odd"], 3)
+    gen_gpi("tie", SHAPES["reacher17"], 4, tie=True)
+    gen_full_size()
+    gen_sfdqn_updates("sfdqn_gpi", SHAPES["reacher17"], 4, 12, True, 5)
+    gen_sfdqn_updates("sfdqn_nogpi", SHAPES["reacher17"], 4, 12, False, 5)
+    gen_sfdqn_updates("sfdqn_tanh", SHAPES["tanh_odd"], 3, 7, True, 3)
+    gen_deep_alltask(SHAPES["reacher17"], 4, 6, 3)
+    gen_tsf("tsf", ref_tsfdqn, SHAPES["hopper11"], 3, 8, 0)
+    gen_tsf("tsf_nf", ref_tsfdqn_nf, SHAPES["hopper11"], 3, 6, 3)
+    print("golden vectors written to", os.path.abspath(OUT))
+
+
+if __name__ == "__main__":
+    main()
