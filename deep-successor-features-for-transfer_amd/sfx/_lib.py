@@ -1,0 +1,86 @@
+"""ctypes binding of libsfx.so (the C ABI declared in include/sfx.h).
+
+The library is the product path: there is no CPU fallback.  If libsfx.so is absent,
+importing this module raises; if no HIP device is present, compute calls fail loudly
+from the HIP runtime.  ``torch`` is imported first so the process uses the HIP
+runtime torch already loaded (libamdhip64.so.7), not a second copy.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before libsfx.so)
+
+LIB_PATH = os.environ.get("SFX_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsfx.so"))
+
+# name -> (restype, argtypes); every function declared in include/sfx.h
+_VP, _I, _D, _F = C.c_void_p, C.c_int, C.c_double, C.c_float
+_IP, _FP = C.POINTER(C.c_int), C.POINTER(C.c_float)
+SIGNATURES = {
+    "sfx_version": (C.c_char_p, []),
+    "sfx_last_error": (C.c_char_p, []),
+    "sfx_create": (_I, [C.POINTER(_VP), _I, _I, _I, _I, _IP, _I, _I, _I, _I, _VP]),
+    "sfx_destroy": (_I, [_VP]),
+    "sfx_set_stream": (_I, [_VP, _VP]),
+    "sfx_head_numel": (_I, [_VP]),
+    "sfx_set_adam": (_I, [_VP, _D, _D, _D, _D, _D, _D, _D]),
+    "sfx_load_head": (_I, [_VP, _I, _I, _FP]),
+    "sfx_get_head": (_I, [_VP, _I, _I, _FP]),
+    "sfx_load_adam": (_I, [_VP, _I, _FP, _FP, _I]),
+    "sfx_get_adam": (_I, [_VP, _I, _FP, _FP, _IP]),
+    "sfx_load_w": (_I, [_VP, _I, _FP]),
+    "sfx_get_w": (_I, [_VP, _I, _FP, _FP, _FP]),
+    "sfx_w_ptr": (_I, [_VP, _I, C.POINTER(_VP)]),
+    "sfx_gpi": (_I, [_VP, _VP, _I, _VP, _VP, _VP, _VP, _VP]),
+    "sfx_select_action": (_I, [_VP, _VP, _I, _I, _VP, _VP]),
+    "sfx_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP]),
+    "sfx_update_all": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _VP]),
+    "sfx_lms": (_I, [_VP, _I, _VP, _VP, _F]),
+    "sfx_set_target_update_ev": (_I, [_VP, _I]),
+    "sfx_get_since_target": (_I, [_VP, _I, _IP]),
+    "sfx_set_since_target": (_I, [_VP, _I, _I]),
+    "sfx_sync_target": (_I, [_VP, _I]),
+    "sfx_synchronize": (_I, [_VP]),
+}
+
+
+class SFXError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libsfx.so not found at {LIB_PATH}: build it first "
+            "(python -c 'import __graft_entry__ as g; g.build()' or make -C "
+            "deep-successor-features-for-transfer_amd/csrc)")
+    lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib.sfx_last_error().decode(errors="replace")
+        raise SFXError(f"{what or 'libsfx'} failed (status {rc}): {msg}")
+
+
+def version() -> str:
+    return lib.sfx_version().decode()
+
+
+def fptr(arr) -> "C.POINTER(C.c_float)":
+    """Host float32 numpy array -> float*."""
+    return arr.ctypes.data_as(_FP)
+
+
+def dptr(t) -> int:
+    """Device tensor (or None) -> raw device pointer for *_dev arguments."""
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,202 @@
+"""SFEngine: a device-resident library of T ψ heads driven through libsfx.so.
+
+One engine = one libsfx handle = the heads, target heads, Adam state and reward weights
+of T source tasks on one GPU.  Inputs are torch tensors (moved to the engine's device
+when needed); outputs are torch tensors on the device.  Every compute call runs the
+hand-written gfx950 kernels; there is no torch / CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ._lib import check, dptr, fptr, lib
+
+ACT_CODES = {"none": 0, "relu": 1, "tanh": 2}
+
+
+def _act_code(a) -> int:
+    if isinstance(a, int):
+        return a
+    return ACT_CODES[str(a).lower()]
+
+
+class SFEngine:
+    def __init__(self, T: int, n_s: int, H: int, A: int, d: int, acts: Sequence = ("relu", "relu"),
+                 max_batch: int = 32, device=None, stream: Optional[int] = None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("SFEngine needs a HIP device (libsfx.so has no CPU path)")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.T, self.n_s, self.H, self.A, self.d = T, n_s, H, A, d
+        self.acts = tuple(acts)
+        self.max_batch = max_batch
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        self.stream = stream
+        codes = (C.c_int * max(1, len(self.acts)))(*[_act_code(a) for a in self.acts])
+        h = C.c_void_p()
+        check(lib.sfx_create(C.byref(h), T, n_s, H, len(self.acts), codes, A, d, max_batch,
+                             self.device.index, C.c_void_p(stream)), "sfx_create")
+        self._h = h
+        self.P = lib.sfx_head_numel(h)
+        self._sel = torch.zeros(2, dtype=torch.long, device=self.device)
+        self._w_ptrs = []
+        for t in range(T):
+            p = C.c_void_p()
+            check(lib.sfx_w_ptr(h, t, C.byref(p)), "sfx_w_ptr")
+            self._w_ptrs.append(p.value)
+
+    # ---------------------------------------------------------------- lifecycle
+    def close(self):
+        if getattr(self, "_h", None):
+            lib.sfx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ---------------------------------------------------------------- helpers
+    def _f(self, x, shape=None) -> torch.Tensor:
+        t = torch.as_tensor(x).to(device=self.device, dtype=torch.float32)
+        if shape is not None:
+            t = t.reshape(shape)
+        return t.contiguous()
+
+    def _l(self, x) -> torch.Tensor:
+        return torch.as_tensor(x).to(device=self.device, dtype=torch.long).reshape(-1).contiguous()
+
+    # ---------------------------------------------------------------- configuration
+    def set_adam(self, lr_psi=1e-3, wd_psi=0.0, lr_w=1e-3, wd_w=0.0, betas=(0.9, 0.999), eps=1e-8):
+        check(lib.sfx_set_adam(self._h, float(lr_psi), float(wd_psi), float(lr_w), float(wd_w),
+                               float(betas[0]), float(betas[1]), float(eps)), "sfx_set_adam")
+
+    def set_target_update_ev(self, ev: int):
+        check(lib.sfx_set_target_update_ev(self._h, int(ev)), "sfx_set_target_update_ev")
+
+    # ---------------------------------------------------------------- state I/O (host, synchronous)
+    def load_head(self, t: int, flat, which: int = 0):
+        a = np.ascontiguousarray(torch.as_tensor(flat).detach().cpu().reshape(-1).numpy(), dtype=np.float32)
+        if a.size != self.P:
+            raise ValueError(f"head has {a.size} parameters, engine expects {self.P}")
+        check(lib.sfx_load_head(self._h, t, which, fptr(a)), "sfx_load_head")
+
+    def get_head(self, t: int, which: int = 0) -> torch.Tensor:
+        a = np.empty(self.P, dtype=np.float32)
+        check(lib.sfx_get_head(self._h, t, which, fptr(a)), "sfx_get_head")
+        return torch.from_numpy(a)
+
+    def load_adam(self, t: int, m, v, step: int):
+        m = np.ascontiguousarray(torch.as_tensor(m).cpu().reshape(-1).numpy(), dtype=np.float32)
+        v = np.ascontiguousarray(torch.as_tensor(v).cpu().reshape(-1).numpy(), dtype=np.float32)
+        check(lib.sfx_load_adam(self._h, t, fptr(m), fptr(v), int(step)), "sfx_load_adam")
+
+    def get_adam(self, t: int) -> Tuple[torch.Tensor, torch.Tensor, int]:
+        m = np.empty(self.P, dtype=np.float32)
+        v = np.empty(self.P, dtype=np.float32)
+        st = C.c_int()
+        check(lib.sfx_get_adam(self._h, t, fptr(m), fptr(v), C.byref(st)), "sfx_get_adam")
+        return torch.from_numpy(m), torch.from_numpy(v), st.value
+
+    def load_w(self, t: int, w):
+        a = np.ascontiguousarray(torch.as_tensor(w).detach().cpu().reshape(-1).numpy(), dtype=np.float32)
+        if a.size != self.d:
+            raise ValueError("w must have d entries")
+        check(lib.sfx_load_w(self._h, t, fptr(a)), "sfx_load_w")
+
+    def get_w(self, t: int):
+        w, m, v = (np.empty(self.d, dtype=np.float32) for _ in range(3))
+        check(lib.sfx_get_w(self._h, t, fptr(w), fptr(m), fptr(v)), "sfx_get_w")
+        return torch.from_numpy(w), torch.from_numpy(m), torch.from_numpy(v)
+
+    def since_target(self, t: int) -> int:
+        c = C.c_int()
+        check(lib.sfx_get_since_target(self._h, t, C.byref(c)), "sfx_get_since_target")
+        return c.value
+
+    def set_since_target(self, t: int, count: int):
+        check(lib.sfx_set_since_target(self._h, t, int(count)), "sfx_set_since_target")
+
+    def sync_target(self, t: int):
+        check(lib.sfx_sync_target(self._h, t), "sfx_sync_target")
+
+    def synchronize(self):
+        check(lib.sfx_synchronize(self._h), "sfx_synchronize")
+
+    # ---------------------------------------------------------------- hot path
+    def gpi(self, S, w=None, w_index: Optional[int] = None, want_psi: bool = False, want_q: bool = True):
+        """GPI over all heads.  Returns (psi [B,T,A,d] or None, q [B,T,A] or None, task [B], next [B])."""
+        S = self._f(S)
+        if S.dim() == 1:
+            S = S.reshape(1, -1)
+        B = S.shape[0]
+        if w_index is not None:
+            w_ptr = self._w_ptrs[w_index]
+            w_keep = None
+        else:
+            w_keep = self._f(w, (-1,))
+            w_ptr = w_keep.data_ptr()
+        psi = torch.empty(B, self.T, self.A, self.d, device=self.device) if want_psi else None
+        q = torch.empty(B, self.T, self.A, device=self.device) if want_q else None
+        task = torch.empty(B, dtype=torch.long, device=self.device)
+        nxt = torch.empty(B, dtype=torch.long, device=self.device)
+        check(lib.sfx_gpi(self._h, S.data_ptr(), B, w_ptr, dptr(psi), dptr(q), task.data_ptr(),
+                          nxt.data_ptr()), "sfx_gpi")
+        return psi, q, task, nxt
+
+    def successors(self, S) -> torch.Tensor:
+        """get_successors: [B, T, A, d]."""
+        psi, _, _, _ = self.gpi(S, w_index=0, want_psi=True, want_q=False)
+        return psi
+
+    def select_action(self, s, task_index: int, use_gpi: bool = True, q_out: Optional[torch.Tensor] = None):
+        """Greedy GPI action for one state; returns the device tensor [c, a] (not synchronized)."""
+        s = self._f(s, (-1,))
+        check(lib.sfx_select_action(self._h, s.data_ptr(), int(task_index), int(bool(use_gpi)), dptr(q_out),
+                                    self._sel.data_ptr()), "sfx_select_action")
+        return self._sel
+
+    def update(self, policy: int, s, a, r, phi, s1, gamma, use_gpi: bool = True,
+               losses: Optional[torch.Tensor] = None, next_actions: Optional[torch.Tensor] = None):
+        """One TD update of head `policy` (sfdqn.py:303-371 semantics).  r=None -> no l2 / w step."""
+        s, s1 = self._f(s), self._f(s1)
+        B = s.shape[0]
+        a = self._l(a)
+        phi = self._f(phi, (B, self.d))
+        gamma = self._f(gamma, (B,))
+        rr = None if r is None else self._f(r, (B,))
+        if losses is None:
+            losses = torch.empty(3, device=self.device)
+        check(lib.sfx_update(self._h, int(policy), s.data_ptr(), a.data_ptr(), dptr(rr), phi.data_ptr(),
+                             s1.data_ptr(), gamma.data_ptr(), B, int(bool(use_gpi)), losses.data_ptr(),
+                             dptr(next_actions)), "sfx_update")
+        return losses
+
+    def update_all(self, s, a, phi, s1, gamma, losses: Optional[torch.Tensor] = None):
+        """All-task update (agents/sfdqn.py:57-60 over features/deep.py:93-131)."""
+        s, s1 = self._f(s), self._f(s1)
+        B = s.shape[0]
+        a = self._l(a)
+        phi = self._f(phi, (B, self.d))
+        gamma = self._f(gamma, (B,))
+        if losses is None:
+            losses = torch.empty(self.T, 3, device=self.device)
+        check(lib.sfx_update_all(self._h, s.data_ptr(), a.data_ptr(), phi.data_ptr(), s1.data_ptr(),
+                                 gamma.data_ptr(), B, losses.data_ptr()), "sfx_update_all")
+        return losses
+
+    def lms(self, t: int, phi, r, alpha: float):
+        phi = self._f(phi, (-1,))
+        r = self._f(r, (1,))
+        check(lib.sfx_lms(self._h, int(t), phi.data_ptr(), r.data_ptr(), float(alpha)), "sfx_lms")

@@ -1,0 +1,141 @@
+/*
+ * sfx.h -- C ABI of libsfx.so, the MI355X (gfx950) successor-feature hot path.
+ *
+ * The reference (okgarces/deep-successor-features-for-transfer) is pure Python; its
+ * plugin surface for this path is the duck-typed SF object (features/successor.py:6-290,
+ * features/deep.py, sfdqn.py:94-371).  Each entry point below replaces the reference
+ * call cited next to it; the Python layer (deep-successor-features-for-transfer_amd/sfx)
+ * binds these with ctypes exactly as INTEGRATION.md shows.
+ *
+ * Conventions
+ *  - Every pointer argument named *_dev is a DEVICE pointer (hipMalloc / torch CUDA
+ *    tensor), read/written asynchronously on the handle's stream.  Host pointers are
+ *    named *_host and are read/written synchronously.
+ *  - All floating point data is fp32.  Actions and argmax indices are int64 (torch.long).
+ *  - A ψ head is packed as the reference's nn.Sequential parameters() in order:
+ *    for each Linear, weight[out][in] row-major then bias[out] ("torch packing").
+ *    Internally each tensor starts 16-byte aligned; load/get convert.
+ *  - Return value: 0 on success, a negative SFX_E* code otherwise; sfx_last_error()
+ *    returns a message.  The Python layer raises on any non-zero status.
+ *  - One handle = one device; calls are not thread-safe on the same handle.
+ */
+#ifndef SFX_H
+#define SFX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SFX_OK 0
+#define SFX_E_ARG (-1)
+#define SFX_E_HIP (-2)
+#define SFX_E_STATE (-3)
+
+#define SFX_ACT_NONE 0
+#define SFX_ACT_RELU 1
+#define SFX_ACT_TANH 2
+
+typedef struct sfx_handle* sfx_t;
+
+/* Version string of the build (for logs). */
+const char* sfx_version(void);
+/* Message describing the last failure on this thread. */
+const char* sfx_last_error(void);
+
+/*
+ * Create the per-device library state for T ψ heads of geometry
+ *   Linear(n_s,H) -> [Linear(H,H)+act_i for i < n_hidden] -> Linear(H, A*d)
+ * (the lambda of main_sfdqn_torch.py:44-78, built per task by DeepSF.build_successor,
+ * features/deep.py:39-78 / sfdqn.py:242-288).  max_batch bounds the minibatch rows of
+ * one update (reference buffer n_batch=32, configs/reacher.cfg:265-267).
+ * stream: hipStream_t the handle launches on (NULL = legacy default stream).
+ */
+int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts_host, int A,
+               int d, int max_batch, int device, void* stream);
+int sfx_destroy(sfx_t h);
+int sfx_set_stream(sfx_t h, void* stream);
+/* Packed parameter count of one head in torch packing. */
+int sfx_head_numel(sfx_t h);
+
+/*
+ * Adam hyper-parameters (torch.optim.Adam single-tensor semantics,
+ * torch/optim/adam.py:_single_tensor_adam) for the ψ group and the w group
+ * (sfdqn.py:282-286: {'lr': learning_rate_sf, 'weight_decay': weight_decay_sf},
+ *  {'lr': learning_rate_w, 'weight_decay': weight_decay_w}).
+ */
+int sfx_set_adam(sfx_t h, double lr_psi, double wd_psi, double lr_w, double wd_w, double beta1,
+                 double beta2, double eps);
+
+/* Parameter I/O (replaces building / reading the per-task nn.Sequential:
+ * features/deep.py:50-66, utils/torch.py:31-33).  which: 0 online, 1 target. */
+int sfx_load_head(sfx_t h, int t, int which, const float* params_host);
+int sfx_get_head(sfx_t h, int t, int which, float* params_host);
+/* Adam state of head t: m, v in torch packing; step = optimizer step count. */
+int sfx_load_adam(sfx_t h, int t, const float* m_host, const float* v_host, int step);
+int sfx_get_adam(sfx_t h, int t, float* m_host, float* v_host, int* step);
+/* Reward weights w_t (d floats): fit_w of SF.add_training_task (features/successor.py:134-139)
+ * or the Linear(d,1,bias=False) weight of sfdqn.py:196-204. */
+int sfx_load_w(sfx_t h, int t, const float* w_host);
+int sfx_get_w(sfx_t h, int t, float* w_host, float* wm_host, float* wv_host);
+/* Device pointer to w row t (d floats), stable for the handle's lifetime. */
+int sfx_w_ptr(sfx_t h, int t, float** w_dev);
+
+/*
+ * GPI over all heads (SF.GPI_w, features/successor.py:223-246; sfdqn.py:215-240;
+ * DeepSF.get_successors, features/deep.py:85-91):
+ *   psi[b,t,:,:] = ψ_t(S[b]);  q[b,t,a] = ψ[b,t,a,:]·w;
+ *   task[b] = argmax_t max_a q[b,t,a];  next[b] = argmax_a max_t q[b,t,a]
+ * (first index on ties, as torch.argmax).  S_dev [B, n_s], w_dev [d].  Any output
+ * pointer may be NULL.  psi_dev [B,T,A,d], q_dev [B,T,A], task_dev/next_dev [B].
+ */
+int sfx_gpi(sfx_t h, const float* S_dev, int B, const float* w_dev, float* psi_dev, float* q_dev,
+            int64_t* task_dev, int64_t* next_dev);
+
+/*
+ * Greedy action of Agent.next_sample for one encoded state (sfdqn.py:585-594;
+ * agents/sfdqn.py:39-45 + agents/agent.py:144-157 greedy branch):
+ *   (q, c) = GPI(s, task_index); c = task_index unless use_gpi; a = argmax_a q[0,c,:].
+ * out_dev[0] = c (GPI task), out_dev[1] = a.  q_dev [T, A] may be NULL.
+ */
+int sfx_select_action(sfx_t h, const float* s_dev, int task_index, int use_gpi, float* q_dev,
+                      int64_t* out_dev);
+
+/*
+ * One SF TD update of head `policy` (DeepSF.update_successor, sfdqn.py:303-371 ==
+ * features/deep_sequential.py:163-231): GPI (or own-ψ) next actions over S1, targets
+ * φ + γ ψ⁻_i(S1)[a'], l1 = MSE(ψ_i(S), merged) [+ l2 = MSE(w_i·φ, r) when r_dev != NULL,
+ * which also trains w_i], one Adam step, target sync every target_update_ev updates.
+ * Inputs: S, S1 [B, n_s]; a [B] int64; r [B] (or NULL); phi [B, d]; gamma [B].
+ * losses_dev[3] = (l1 + l2, l1, l2) (may be NULL); next_dev [B] (may be NULL).
+ */
+int sfx_update(sfx_t h, int policy, const float* S_dev, const int64_t* a_dev, const float* r_dev,
+               const float* phi_dev, const float* S1_dev, const float* gamma_dev, int B,
+               int use_gpi, float* losses_dev, int64_t* next_dev);
+
+/*
+ * All-task update (agents/sfdqn.py:57-60 looping features/deep.py:93-131 over every
+ * head in index order, each GPI seeing the heads already updated in this call).
+ * loss = l1 only, w_i not trained (LMS w).  losses_dev [T, 3] (may be NULL).
+ */
+int sfx_update_all(sfx_t h, const float* S_dev, const int64_t* a_dev, const float* phi_dev,
+                   const float* S1_dev, const float* gamma_dev, int B, float* losses_dev);
+
+/* LMS reward fit SF.update_reward (features/successor.py:164-167) on w_t:
+ * w <- w + alpha (r - φ·w) φ ;  phi_dev [d], r_dev [1]. */
+int sfx_lms(sfx_t h, int t, const float* phi_dev, const float* r_dev, float alpha);
+
+/* Target bookkeeping (sfdqn.py:366-369; utils/torch.py:31-33). */
+int sfx_set_target_update_ev(sfx_t h, int target_update_ev);
+int sfx_get_since_target(sfx_t h, int t, int* count);
+int sfx_set_since_target(sfx_t h, int t, int count);
+int sfx_sync_target(sfx_t h, int t);
+
+/* Block the host until all work queued on the handle's stream is done. */
+int sfx_synchronize(sfx_t h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SFX_H */
