@@ -6,13 +6,17 @@
 //   step                        : [T]         Adam step per head (device-resident)
 //   act                         : [role][T][actSize]   per-layer outputs, rows = max_batch
 //   dz                          : [T][actSize]         per-layer output gradients
-// Every kernel reads its pointers from static descriptor tables built at create time,
-// so the per-call host work is a handful of launches with scalar arguments.
+//   rowloss                     : [T][MMAX]            per-row TD loss of the last update
+// Kernels take the whole geometry by value (sfx::Geo) and derive every pointer from it.
+// Each entry point's launch sequence is captured once into a hipGraph (keyed by its
+// arguments) and replayed afterwards; SFX_GRAPHS=0 disables graphs.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -23,168 +27,233 @@ using namespace sfx;
 
 static thread_local std::string g_err;
 
-#define SFX_FAIL(code, msg)  \
-  do {                       \
-    g_err = (msg);           \
-    return (code);           \
+#define SFX_FAIL(code, msg) \
+  do {                      \
+    g_err = (msg);          \
+    return (code);          \
   } while (0)
 
-#define HIPCHK(x)                                                            \
-  do {                                                                       \
-    hipError_t e_ = (x);                                                     \
-    if (e_ != hipSuccess) {                                                  \
-      g_err = std::string(#x) + ": " + hipGetErrorString(e_);                \
-      return SFX_E_HIP;                                                      \
-    }                                                                        \
+#define HIPCHK(x)                                                     \
+  do {                                                                \
+    hipError_t e_ = (x);                                              \
+    if (e_ != hipSuccess) {                                           \
+      g_err = std::string(#x) + ": " + hipGetErrorString(e_);         \
+      return SFX_E_HIP;                                               \
+    }                                                                 \
   } while (0)
 
-#define LAUNCHCHK()                                                          \
-  do {                                                                       \
-    hipError_t e_ = hipGetLastError();                                       \
-    if (e_ != hipSuccess) {                                                  \
-      g_err = std::string("kernel launch: ") + hipGetErrorString(e_);        \
-      return SFX_E_HIP;                                                      \
-    }                                                                        \
+#define LAUNCHCHK()                                                   \
+  do {                                                                \
+    hipError_t e_ = hipGetLastError();                                \
+    if (e_ != hipSuccess) {                                           \
+      g_err = std::string("kernel launch: ") + hipGetErrorString(e_); \
+      return SFX_E_HIP;                                               \
+    }                                                                 \
+  } while (0)
+
+#define RC(x)            \
+  do {                   \
+    int rc_ = (x);       \
+    if (rc_) return rc_; \
   } while (0)
 
 namespace {
 
-struct Layer {
-  int N, K, wOff, bOff, actOut;
-};
-
-enum Role { R_S = 0, R_S1T = 1, R_S1 = 2, R_G = 3, R_A = 4, NROLE = 5 };
-
 inline int align4(int x) { return (x + 3) & ~3; }
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+struct GraphKey {
+  int op, a0, a1, a2;
+  const void* p[8];
+  bool operator<(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) < 0; }
+};
 
 }  // namespace
 
 struct sfx_handle {
   int T = 0, n_s = 0, H = 0, nh = 0, A = 0, d = 0, O = 0, NL = 0, Mmax = 0, device = 0;
   int P = 0, Ptorch = 0, dpad = 0, actSize = 0;
-  std::vector<Layer> L;
+  std::vector<LayerGeo> L;
   std::vector<int> actOff;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // caller's stream: everything is ordered on it
+  hipStream_t cap = nullptr;     // private stream used only to capture graphs
+  bool use_graphs = true;
   AdamHP hp_psi{1e-3, 0.0, 0.9, 0.999, 1e-8};
   AdamHP hp_w{1e-3, 0.0, 0.9, 0.999, 1e-8};
   int target_update_ev = 1000;
   std::vector<int> since_target, host_step;
+  std::map<GraphKey, hipGraphExec_t> graphs;
+  Geo G{};
 
   float *online = nullptr, *target = nullptr, *am = nullptr, *av = nullptr;
   float *w = nullptr, *wm = nullptr, *wv = nullptr;
   int* step = nullptr;
-  float* act = nullptr;
-  float* dz = nullptr;
+  float *act = nullptr, *dz = nullptr, *rowloss = nullptr;
 
-  FwdInst* d_fwd = nullptr;
-  BwdInst* d_bwd = nullptr;
-  TdgInst* d_tdg = nullptr;
-  // fwd plan bases (index into d_fwd)
-  std::vector<int> plan_upd[2];  // [use_gpi][policy]
-  int plan_all = 0;
-  std::vector<int> plan_refwd;   // [policy]
-  int plan_gpi = 0, plan_act = 0;
-
-  float* actp(int role, int head, int layer) const {
-    return act + ((size_t)role * T + head) * actSize + actOff[layer];
-  }
-  float* dzp(int head, int layer) const { return dz + (size_t)head * actSize + actOff[layer]; }
   float* params(int which, int head) const { return (which ? target : online) + (size_t)head * P; }
 };
 
 namespace {
 
-struct InstSpec {
-  int role, head, which, xsel;
-};
-
-int add_fwd_plan(const sfx_handle* h, std::vector<FwdInst>& all, const std::vector<InstSpec>& specs) {
-  const int base = (int)all.size();
-  for (int l = 0; l < h->NL; ++l) {
-    for (const InstSpec& s : specs) {
-      FwdInst f{};
-      const float* p = h->params(s.which, s.head);
-      f.W = p + h->L[l].wOff;
-      f.b = p + h->L[l].bOff;
-      f.Y = h->actp(s.role, s.head, l);
-      if (l == 0) {
-        f.xsel = s.xsel;
-        f.X = nullptr;
-      } else {
-        f.xsel = 0;
-        f.X = h->actp(s.role, s.head, l - 1);
-      }
-      all.push_back(f);
-    }
-  }
-  return base;
+void clear_graphs(sfx_handle* h) {
+  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+  h->graphs.clear();
 }
 
-int run_fwd(sfx_handle* h, int base, int ninst, int M, const float* xa, const float* xb) {
+// Capture `body` (which launches on h->stream) into a graph keyed by `key`, then replay.
+template <class F>
+int run_graph(sfx_handle* h, const GraphKey& key, F body) {
+  if (!h->use_graphs) return body();
+  auto it = h->graphs.find(key);
+  if (it == h->graphs.end()) {
+    hipStream_t saved = h->stream;
+    h->stream = h->cap;
+    HIPCHK(hipStreamBeginCapture(h->cap, hipStreamCaptureModeThreadLocal));
+    const int rc = body();
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(h->cap, &g);
+    h->stream = saved;
+    if (rc) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    HIPCHK(e);
+    hipGraphExec_t ex = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    HIPCHK(ei);
+    if (h->graphs.size() > 256) clear_graphs(h);
+    it = h->graphs.emplace(key, ex).first;
+  }
+  HIPCHK(hipGraphLaunch(it->second, h->stream));
+  return SFX_OK;
+}
+
+GraphKey make_key(int op, int a0, int a1, int a2, std::initializer_list<const void*> ptrs) {
+  GraphKey k;
+  std::memset(&k, 0, sizeof(k));
+  k.op = op;
+  k.a0 = a0;
+  k.a1 = a1;
+  k.a2 = a2;
+  int i = 0;
+  for (const void* p : ptrs) k.p[i++] = p;
+  return k;
+}
+
+int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const float* xa, const float* xb) {
+  FwdArgs F{};
+  F.M = M;
+  F.xa = xa;
+  F.xb = xb;
+  int ninst = 0;
+  FwdGroup* slots[4] = {&F.g0, &F.g1, &F.g2, &F.g3};
+  for (const FwdGroup& g : groups) {
+    *slots[F.ngroups++] = g;
+    ninst += g.n;
+  }
   for (int l = 0; l < h->NL; ++l) {
-    const Layer& L = h->L[l];
-    hipLaunchKernelGGL(k_fwd, dim3(cdiv(L.N, 16), ninst, cdiv(M, 32)), dim3(256), 0, h->stream,
-                       h->d_fwd + base + (size_t)l * ninst, M, L.N, L.K, L.actOut, xa, xb);
+    const LayerGeo& L = h->L[l];
+    F.N = L.N;
+    F.K = L.K;
+    F.act = L.actOut;
+    F.wOff = L.wOff;
+    F.bOff = L.bOff;
+    F.xOff = l == 0 ? -1 : h->actOff[l - 1];
+    F.yOff = h->actOff[l];
+    const dim3 grid(cdiv(L.N, 16), ninst, cdiv(M, 32));
+    // the vector path needs K % 64 == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
+    const bool vec = (L.K % 64) == 0 && (l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0));
+    if (vec)
+      hipLaunchKernelGGL(k_fwd<true>, grid, dim3(256), 0, h->stream, h->G, F);
+    else
+      hipLaunchKernelGGL(k_fwd<false>, grid, dim3(256), 0, h->stream, h->G, F);
   }
   LAUNCHCHK();
   return SFX_OK;
 }
 
-int run_bwd(sfx_handle* h, int desc, int ninst, int M, const float* x0) {
-  BwdArgs A{};
-  A.M = M;
-  for (int l = 0; l < h->NL; ++l) {
-    const Layer& L = h->L[l];
-    A.L[l] = LayerGeo{L.N, L.K, L.wOff, L.bOff, l > 0 ? h->L[l - 1].actOut : ACT_NONE};
-  }
-  A.hp = h->hp_psi;
-  A.x0 = x0;
-  auto dw_tiles = [&](int l) { return cdiv(h->L[l].N, 32) * cdiv(h->L[l].K, 64); };
-  for (int l = h->NL - 1; l >= 1; --l) {
-    A.la = l;
-    A.na = cdiv(M, 32) * cdiv(h->L[l].K, 16);
-    if (l + 1 <= h->NL - 1) {
-      A.lb = l + 1;
-      A.nb = dw_tiles(l + 1);
-    } else {
-      A.lb = -1;
-      A.nb = 0;
-    }
-    A.lc = -1;
-    A.nc = 0;
-    hipLaunchKernelGGL(k_bwd, dim3(A.na + A.nb, ninst), dim3(256), 0, h->stream, h->d_bwd + desc, A);
-  }
-  A.la = -1;
-  A.na = 0;
-  A.lb = 1;
-  A.nb = dw_tiles(1);
-  A.lc = 0;
-  A.nc = dw_tiles(0);
-  hipLaunchKernelGGL(k_bwd, dim3(A.nb + A.nc, ninst), dim3(256), 0, h->stream, h->d_bwd + desc, A);
-  LAUNCHCHK();
-  return SFX_OK;
-}
-
-int run_tdg(sfx_handle* h, int policy, int M, int use_gpi, const int64_t* a, const float* r,
-            const float* phi, const float* gamma, float* losses, int64_t* next) {
+int run_tdg(sfx_handle* h, int pol0, int npol, int M, int use_gpi, const int64_t* a, const float* phi,
+            const float* gamma, int64_t* next) {
   TdgArgs A{};
   A.M = M;
-  A.T = h->T;
-  A.A = h->A;
-  A.d = h->d;
   A.use_gpi = use_gpi;
-  A.train_w = r != nullptr;
-  A.inc_step = 1;
-  A.psiN_stride = h->actSize;
+  A.pol0 = pol0;
+  A.npol = npol;
   A.a = a;
   A.phi = phi;
   A.gamma = gamma;
-  A.r = r;
-  A.hpw = h->hp_w;
-  A.losses = losses;
   A.next = next;
-  hipLaunchKernelGGL(k_tdg, dim3(1), dim3(256), 0, h->stream, h->d_tdg + policy, A);
+  hipLaunchKernelGGL(k_tdg, dim3(M, npol), dim3(256), 0, h->stream, h->G, A);
+  LAUNCHCHK();
+  return SFX_OK;
+}
+
+int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const float* phi, const float* r,
+            float* losses) {
+  BwdArgs A{};
+  A.M = M;
+  A.head0 = head0;
+  A.hp = h->hp_psi;
+  A.hpw = h->hp_w;
+  A.x0 = x0;
+  A.phi = phi;
+  A.r = r;
+  A.train_w = r != nullptr;
+  A.losses = losses;
+  auto dw_tiles = [&](int l) { return cdiv(h->L[l].N, 32) * cdiv(h->L[l].K, 64); };
+  auto geo = [&](int l) {
+    const LayerGeo& L = h->L[l];
+    RoleGeo r{};
+    r.N = L.N;
+    r.K = L.K;
+    r.wOff = L.wOff;
+    r.bOff = L.bOff;
+    r.actIn = L.actIn;
+    r.xOff = l == 0 ? -1 : h->actOff[l - 1];
+    r.dzOff = h->actOff[l];
+    r.dzIn = l == 0 ? 0 : h->actOff[l - 1];
+    return r;
+  };
+  for (int l = h->NL - 1; l >= 1; --l) {
+    A.ra = geo(l);
+    A.na = cdiv(M, 32) * cdiv(h->L[l].K, 16);
+    if (l + 1 <= h->NL - 1) {
+      A.rb = geo(l + 1);
+      A.nb = dw_tiles(l + 1);
+    } else {
+      A.nb = 0;
+    }
+    A.nc = 0;
+    A.tail = l == h->NL - 1 ? 1 : 0;  // loss / w / step in the first launch
+    hipLaunchKernelGGL(k_bwd, dim3(A.na + A.nb + A.nc + A.tail, nhead), dim3(256), 0, h->stream, h->G, A);
+  }
+  A.na = 0;
+  A.rb = geo(1);
+  A.nb = dw_tiles(1);
+  A.rc = geo(0);
+  A.nc = dw_tiles(0);
+  A.tail = 0;
+  hipLaunchKernelGGL(k_bwd, dim3(A.nb + A.nc, nhead), dim3(256), 0, h->stream, h->G, A);
+  LAUNCHCHK();
+  return SFX_OK;
+}
+
+int run_gpi(sfx_handle* h, int role, int M, int row0, const float* w, float* psi, float* q, int64_t* task,
+            int64_t* next, int64_t* sel, int select_task, int use_gpi) {
+  GpiArgs A{};
+  A.M = M;
+  A.role = role;
+  A.row0 = row0;
+  A.select_task = select_task;
+  A.use_gpi = use_gpi;
+  A.w = w;
+  A.psi_out = psi;
+  A.q_out = q;
+  A.task_out = task;
+  A.next_out = next;
+  A.sel_out = sel;
+  hipLaunchKernelGGL(k_gpi, dim3(M), dim3(256), 0, h->stream, h->G, A);
   LAUNCHCHK();
   return SFX_OK;
 }
@@ -196,8 +265,8 @@ void after_update(sfx_handle* h, int t) {
 
 int maybe_sync_target(sfx_handle* h, int t) {
   if (h->since_target[t] >= h->target_update_ev) {
-    HIPCHK(hipMemcpyAsync(h->params(1, t), h->params(0, t), sizeof(float) * h->P,
-                          hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->params(1, t), h->params(0, t), sizeof(float) * h->P, hipMemcpyDeviceToDevice,
+                          h->stream));
     h->since_target[t] = 0;
   }
   return SFX_OK;
@@ -207,7 +276,7 @@ int maybe_sync_target(sfx_handle* h, int t) {
 void pack_head(const sfx_handle* h, const float* src, float* dst) {
   std::memset(dst, 0, sizeof(float) * h->P);
   size_t off = 0;
-  for (const Layer& L : h->L) {
+  for (const LayerGeo& L : h->L) {
     std::memcpy(dst + L.wOff, src + off, sizeof(float) * L.N * L.K);
     off += (size_t)L.N * L.K;
     std::memcpy(dst + L.bOff, src + off, sizeof(float) * L.N);
@@ -217,7 +286,7 @@ void pack_head(const sfx_handle* h, const float* src, float* dst) {
 
 void unpack_head(const sfx_handle* h, const float* src, float* dst) {
   size_t off = 0;
-  for (const Layer& L : h->L) {
+  for (const LayerGeo& L : h->L) {
     std::memcpy(dst + off, src + L.wOff, sizeof(float) * L.N * L.K);
     off += (size_t)L.N * L.K;
     std::memcpy(dst + off, src + L.bOff, sizeof(float) * L.N);
@@ -227,39 +296,29 @@ void unpack_head(const sfx_handle* h, const float* src, float* dst) {
 
 bool valid_head(const sfx_handle* h, int t) { return h && t >= 0 && t < h->T; }
 
-int free_all(sfx_handle* h) {
-  (void)hipFree(h->online);
-  (void)hipFree(h->target);
-  (void)hipFree(h->am);
-  (void)hipFree(h->av);
-  (void)hipFree(h->w);
-  (void)hipFree(h->wm);
-  (void)hipFree(h->wv);
-  (void)hipFree(h->step);
-  (void)hipFree(h->act);
-  (void)hipFree(h->dz);
-  (void)hipFree(h->d_fwd);
-  (void)hipFree(h->d_bwd);
-  (void)hipFree(h->d_tdg);
-  return SFX_OK;
+void free_all(sfx_handle* h) {
+  clear_graphs(h);
+  for (void* p : {(void*)h->online, (void*)h->target, (void*)h->am, (void*)h->av, (void*)h->w, (void*)h->wm,
+                  (void*)h->wv, (void*)h->step, (void*)h->act, (void*)h->dz, (void*)h->rowloss})
+    if (p) (void)hipFree(p);
+  if (h->cap) (void)hipStreamDestroy(h->cap);
 }
 
 }  // namespace
 
 extern "C" {
 
-const char* sfx_version(void) { return "sfx 0.1 gfx950 fp32-mfma"; }
+const char* sfx_version(void) { return "sfx 0.2 gfx950 fp32-mfma graphs"; }
 const char* sfx_last_error(void) { return g_err.c_str(); }
 
-int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts, int A, int d,
-               int max_batch, int device, void* stream) {
+int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts, int A, int d, int max_batch,
+               int device, void* stream) {
   if (!out) SFX_FAIL(SFX_E_ARG, "out is null");
   *out = nullptr;
-  if (T < 1 || n_s < 1 || H < 1 || n_hidden < 0 || n_hidden + 2 > NLMAX || A < 1 || d < 1 ||
-      max_batch < 1)
+  if (T < 1 || n_s < 1 || H < 1 || n_hidden < 0 || n_hidden + 2 > NLMAX || A < 1 || d < 1 || max_batch < 1)
     SFX_FAIL(SFX_E_ARG, "bad geometry");
-  if (d > TDG_DMAX || max_batch > TDG_MMAX || (long)max_batch * A > TDG_QMAX || (long)T * A > TDG_QMAX)
-    SFX_FAIL(SFX_E_ARG, "geometry exceeds kernel limits (d<=256, batch<=1024, batch*A and T*A <= 8192)");
+  if (d > DMAX || max_batch > MMAX || (long)T * A > QMAX || (long)A * d > OMAX)
+    SFX_FAIL(SFX_E_ARG, "geometry exceeds kernel limits (d<=256, batch<=1024, T*A<=8192, A*d<=4096)");
   for (int i = 0; i < n_hidden; ++i)
     if (!acts || acts[i] < ACT_NONE || acts[i] > ACT_TANH) SFX_FAIL(SFX_E_ARG, "bad activation code");
   HIPCHK(hipSetDevice(device));
@@ -276,10 +335,11 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->device = device;
   h->stream = (hipStream_t)stream;
   h->dpad = align4(d);
-  // layers
+  const char* eg = std::getenv("SFX_GRAPHS");
+  h->use_graphs = !(eg && eg[0] == '0');
   int off = 0, ptorch = 0;
   for (int l = 0; l < h->NL; ++l) {
-    Layer Lr{};
+    LayerGeo Lr{};
     if (l == 0) {
       Lr.N = H; Lr.K = n_s; Lr.actOut = ACT_NONE;
     } else if (l == h->NL - 1) {
@@ -287,6 +347,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
     } else {
       Lr.N = H; Lr.K = H; Lr.actOut = acts[l - 1];
     }
+    Lr.actIn = l > 0 ? h->L[l - 1].actOut : ACT_NONE;
     Lr.wOff = align4(off);
     off = Lr.wOff + Lr.N * Lr.K;
     Lr.bOff = align4(off);
@@ -325,80 +386,37 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   alloc((void**)&h->step, sizeof(int) * T);
   alloc((void**)&h->act, sizeof(float) * (size_t)NROLE * T * h->actSize);
   alloc((void**)&h->dz, sizeof(float) * (size_t)T * h->actSize);
+  alloc((void**)&h->rowloss, sizeof(float) * (size_t)T * MMAX);
+  if (rc == SFX_OK && hipStreamCreateWithFlags(&h->cap, hipStreamNonBlocking) != hipSuccess) {
+    g_err = "hipStreamCreate failed";
+    rc = SFX_E_HIP;
+  }
   if (rc != SFX_OK) {
     free_all(h);
     delete h;
     return rc;
   }
-
-  // static launch descriptors
-  std::vector<FwdInst> fwd;
-  for (int g = 0; g < 2; ++g) {
-    for (int i = 0; i < T; ++i) {
-      std::vector<InstSpec> specs = {{R_S, i, 0, 1}, {R_S1T, i, 1, 2}};
-      if (g) {
-        for (int t = 0; t < T; ++t) specs.push_back({R_S1, t, 0, 2});
-      } else {
-        specs.push_back({R_S1, i, 0, 2});
-      }
-      h->plan_upd[g].push_back(add_fwd_plan(h, fwd, specs));
-    }
-  }
-  {
-    std::vector<InstSpec> specs;
-    for (int t = 0; t < T; ++t) specs.push_back({R_S, t, 0, 1});
-    for (int t = 0; t < T; ++t) specs.push_back({R_S1T, t, 1, 2});
-    for (int t = 0; t < T; ++t) specs.push_back({R_S1, t, 0, 2});
-    h->plan_all = add_fwd_plan(h, fwd, specs);
-  }
-  for (int i = 0; i < T; ++i) h->plan_refwd.push_back(add_fwd_plan(h, fwd, {{R_S1, i, 0, 2}}));
-  {
-    std::vector<InstSpec> g, a;
-    for (int t = 0; t < T; ++t) {
-      g.push_back({R_G, t, 0, 1});
-      a.push_back({R_A, t, 0, 1});
-    }
-    h->plan_gpi = add_fwd_plan(h, fwd, g);
-    h->plan_act = add_fwd_plan(h, fwd, a);
-  }
-  std::vector<BwdInst> bwd(T);
-  std::vector<TdgInst> tdg(T);
-  for (int i = 0; i < T; ++i) {
-    BwdInst& b = bwd[i];
-    b.P = h->params(0, i);
-    b.Mo = h->am + (size_t)i * h->P;
-    b.Vo = h->av + (size_t)i * h->P;
-    b.step = h->step + i;
-    for (int l = 0; l < NLMAX; ++l) {
-      b.X[l] = (l >= 1 && l < h->NL) ? h->actp(R_S, i, l - 1) : nullptr;
-      b.dZ[l] = l < h->NL ? h->dzp(i, l) : nullptr;
-    }
-    TdgInst& t = tdg[i];
-    t.policy = i;
-    t.c = h->actp(R_S, i, h->NL - 1);
-    t.tpsi = h->actp(R_S1T, i, h->NL - 1);
-    t.psiN = h->actp(R_S1, 0, h->NL - 1);
-    t.w = h->w + (size_t)i * h->dpad;
-    t.wm = h->wm + (size_t)i * h->dpad;
-    t.wv = h->wv + (size_t)i * h->dpad;
-    t.step = h->step + i;
-    t.g = h->dzp(i, h->NL - 1);
-  }
-  auto upload = [&](void** dst, const void* src, size_t bytes) {
-    if (rc != SFX_OK) return;
-    if (hipMalloc(dst, bytes) != hipSuccess || hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) != hipSuccess) {
-      g_err = "descriptor upload failed";
-      rc = SFX_E_HIP;
-    }
-  };
-  upload((void**)&h->d_fwd, fwd.data(), sizeof(FwdInst) * fwd.size());
-  upload((void**)&h->d_bwd, bwd.data(), sizeof(BwdInst) * bwd.size());
-  upload((void**)&h->d_tdg, tdg.data(), sizeof(TdgInst) * tdg.size());
-  if (rc != SFX_OK) {
-    free_all(h);
-    delete h;
-    return rc;
-  }
+  Geo& G = h->G;
+  G.T = T;
+  G.NL = h->NL;
+  G.A = A;
+  G.d = d;
+  G.O = h->O;
+  G.dpad = h->dpad;
+  G.P = h->P;
+  G.actSize = h->actSize;
+  G.online = h->online;
+  G.target = h->target;
+  G.am = h->am;
+  G.av = h->av;
+  G.w = h->w;
+  G.wm = h->wm;
+  G.wv = h->wv;
+  G.step = h->step;
+  G.act = h->act;
+  G.dz = h->dz;
+  G.rowloss = h->rowloss;
+  G.lastOff = h->actOff[h->NL - 1];
   *out = h;
   return SFX_OK;
 }
@@ -417,13 +435,21 @@ int sfx_set_stream(sfx_t h, void* stream) {
   return SFX_OK;
 }
 
+int sfx_set_graphs(sfx_t h, int enable) {
+  if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
+  h->use_graphs = enable != 0;
+  if (!h->use_graphs) clear_graphs(h);
+  return SFX_OK;
+}
+
 int sfx_head_numel(sfx_t h) { return h ? h->Ptorch : SFX_E_ARG; }
 
-int sfx_set_adam(sfx_t h, double lr_psi, double wd_psi, double lr_w, double wd_w, double beta1,
-                 double beta2, double eps) {
+int sfx_set_adam(sfx_t h, double lr_psi, double wd_psi, double lr_w, double wd_w, double beta1, double beta2,
+                 double eps) {
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   h->hp_psi = AdamHP{lr_psi, wd_psi, beta1, beta2, eps};
   h->hp_w = AdamHP{lr_w, wd_w, beta1, beta2, eps};
+  clear_graphs(h);  // hyper-parameters are baked into captured launches
   return SFX_OK;
 }
 
@@ -498,51 +524,28 @@ int sfx_w_ptr(sfx_t h, int t, float** w_dev) {
   return SFX_OK;
 }
 
-int sfx_gpi(sfx_t h, const float* S, int B, const float* w, float* psi, float* q, int64_t* task,
-            int64_t* next) {
+int sfx_gpi(sfx_t h, const float* S, int B, const float* w, float* psi, float* q, int64_t* task, int64_t* next) {
   if (!h || !S || !w || B < 1) SFX_FAIL(SFX_E_ARG, "bad args");
-  for (int row0 = 0; row0 < B; row0 += h->Mmax) {
-    const int m = B - row0 < h->Mmax ? B - row0 : h->Mmax;
-    int rc = run_fwd(h, h->plan_gpi, h->T, m, S + (size_t)row0 * h->n_s, nullptr);
-    if (rc) return rc;
-    GpiArgs G{};
-    G.M = m;
-    G.T = h->T;
-    G.A = h->A;
-    G.d = h->d;
-    G.row0 = row0;
-    G.stride = h->actSize;
-    G.psiN = h->actp(R_G, 0, h->NL - 1);
-    G.w = w;
-    G.psi_out = psi;
-    G.q_out = q;
-    G.task_out = task;
-    G.next_out = next;
-    hipLaunchKernelGGL(k_gpi, dim3(m), dim3(256), 0, h->stream, G);
-    LAUNCHCHK();
-  }
-  return SFX_OK;
+  const GraphKey key = make_key(1, B, 0, 0, {S, w, psi, q, task, next});
+  return run_graph(h, key, [&]() -> int {
+    for (int row0 = 0; row0 < B; row0 += h->Mmax) {
+      const int m = B - row0 < h->Mmax ? B - row0 : h->Mmax;
+      RC(run_fwd(h, {{R_G, 0, 1, 0, h->T}}, m, S + (size_t)row0 * h->n_s, nullptr));
+      RC(run_gpi(h, R_G, m, row0, w, psi, q, task, next, nullptr, 0, 0));
+    }
+    return SFX_OK;
+  });
 }
 
 int sfx_select_action(sfx_t h, const float* s, int task_index, int use_gpi, float* q, int64_t* out) {
   if (!h || !s || !out || task_index < 0 || task_index >= h->T) SFX_FAIL(SFX_E_ARG, "bad args");
-  int rc = run_fwd(h, h->plan_act, h->T, 1, s, nullptr);
-  if (rc) return rc;
-  GpiArgs G{};
-  G.M = 1;
-  G.T = h->T;
-  G.A = h->A;
-  G.d = h->d;
-  G.select_task = task_index;
-  G.use_gpi = use_gpi;
-  G.stride = h->actSize;
-  G.psiN = h->actp(R_A, 0, h->NL - 1);
-  G.w = h->w + (size_t)task_index * h->dpad;
-  G.q_out = q;
-  G.sel_out = out;
-  hipLaunchKernelGGL(k_gpi, dim3(1), dim3(256), 0, h->stream, G);
-  LAUNCHCHK();
-  return SFX_OK;
+  use_gpi = use_gpi ? 1 : 0;
+  const GraphKey key = make_key(2, task_index, use_gpi, 0, {s, q, out});
+  return run_graph(h, key, [&]() -> int {
+    RC(run_fwd(h, {{R_A, 0, 1, 0, h->T}}, 1, s, nullptr));
+    return run_gpi(h, R_A, 1, 0, h->w + (size_t)task_index * h->dpad, nullptr, q, nullptr, nullptr, out, task_index,
+                   use_gpi);
+  });
 }
 
 int sfx_update(sfx_t h, int policy, const float* S, const int64_t* a, const float* r, const float* phi,
@@ -550,29 +553,37 @@ int sfx_update(sfx_t h, int policy, const float* S, const int64_t* a, const floa
   if (!valid_head(h, policy) || !S || !a || !phi || !S1 || !gamma) SFX_FAIL(SFX_E_ARG, "bad args");
   if (B < 1 || B > h->Mmax) SFX_FAIL(SFX_E_ARG, "batch exceeds max_batch");
   use_gpi = use_gpi ? 1 : 0;
-  const int ninst = 2 + (use_gpi ? h->T : 1);
-  int rc = run_fwd(h, h->plan_upd[use_gpi][policy], ninst, B, S, S1);
-  if (rc) return rc;
-  if ((rc = run_tdg(h, policy, B, use_gpi, a, r, phi, gamma, losses, next))) return rc;
-  if ((rc = run_bwd(h, policy, 1, B, S))) return rc;
+  const GraphKey key = make_key(3, policy, use_gpi, B, {S, a, r, phi, S1, gamma, losses, next});
+  RC(run_graph(h, key, [&]() -> int {
+    if (use_gpi)
+      RC(run_fwd(h, {{R_S, 0, 1, policy, 1}, {R_S1T, 1, 2, policy, 1}, {R_S1, 0, 2, 0, h->T}}, B, S, S1));
+    else
+      RC(run_fwd(h, {{R_S, 0, 1, policy, 1}, {R_S1T, 1, 2, policy, 1}, {R_S1, 0, 2, policy, 1}}, B, S, S1));
+    RC(run_tdg(h, policy, 1, B, use_gpi, a, phi, gamma, next));
+    return run_bwd(h, policy, 1, B, S, phi, r, losses);
+  }));
   after_update(h, policy);
   return maybe_sync_target(h, policy);
 }
 
-int sfx_update_all(sfx_t h, const float* S, const int64_t* a, const float* phi, const float* S1,
-                   const float* gamma, int B, float* losses) {
+int sfx_update_all(sfx_t h, const float* S, const int64_t* a, const float* phi, const float* S1, const float* gamma,
+                   int B, float* losses) {
   if (!h || !S || !a || !phi || !S1 || !gamma) SFX_FAIL(SFX_E_ARG, "bad args");
   if (B < 1 || B > h->Mmax) SFX_FAIL(SFX_E_ARG, "batch exceeds max_batch");
-  int rc = run_fwd(h, h->plan_all, 3 * h->T, B, S, S1);
-  if (rc) return rc;
+  const GraphKey key = make_key(4, B, 0, 0, {S, a, phi, S1, gamma, losses});
+  RC(run_graph(h, key, [&]() -> int {
+    RC(run_fwd(h, {{R_S, 0, 1, 0, h->T}, {R_S1T, 1, 2, 0, h->T}, {R_S1, 0, 2, 0, h->T}}, B, S, S1));
+    for (int i = 0; i < h->T; ++i) {
+      RC(run_tdg(h, i, 1, B, 1, a, phi, gamma, nullptr));
+      RC(run_bwd(h, i, 1, B, S, phi, nullptr, losses ? losses + 3 * i : nullptr));
+      if (i + 1 < h->T) RC(run_fwd(h, {{R_S1, 0, 2, i, 1}}, B, S, S1));
+    }
+    return SFX_OK;
+  }));
   for (int i = 0; i < h->T; ++i) {
-    if ((rc = run_tdg(h, i, B, 1, a, nullptr, phi, gamma, losses ? losses + 3 * i : nullptr, nullptr))) return rc;
-    if ((rc = run_bwd(h, i, 1, B, S))) return rc;
-    if (i + 1 < h->T && (rc = run_fwd(h, h->plan_refwd[i], 1, B, S, S1))) return rc;
     after_update(h, i);
+    RC(maybe_sync_target(h, i));
   }
-  for (int i = 0; i < h->T; ++i)
-    if ((rc = maybe_sync_target(h, i))) return rc;
   return SFX_OK;
 }
 
@@ -603,8 +614,7 @@ int sfx_set_since_target(sfx_t h, int t, int count) {
 
 int sfx_sync_target(sfx_t h, int t) {
   if (!valid_head(h, t)) SFX_FAIL(SFX_E_ARG, "bad head");
-  HIPCHK(hipMemcpyAsync(h->params(1, t), h->params(0, t), sizeof(float) * h->P, hipMemcpyDeviceToDevice,
-                        h->stream));
+  HIPCHK(hipMemcpyAsync(h->params(1, t), h->params(0, t), sizeof(float) * h->P, hipMemcpyDeviceToDevice, h->stream));
   return SFX_OK;
 }
 

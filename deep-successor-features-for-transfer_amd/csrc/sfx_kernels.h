@@ -2,6 +2,13 @@
 //
 // fp32 end to end: the dense products run on the exact-f32 matrix cores
 // (v_mfma_f32_16x16x4_f32, a k-ordered fmaf chain), element-wise work on VALU.
+//
+// Every problem here is tiny (minibatch M <= 32, heads of ~150k parameters), so each
+// kernel is LATENCY bound: the design rules are (1) every pointer is computed from
+// kernel arguments (no descriptor loads in front of the data loads), (2) all global
+// loads a thread needs are issued before the first use (compile-time unrolled,
+// predicated), (3) optimizer state is prefetched before the MFMA chain.
+//
 // Reference behaviour being implemented is cited per kernel (paths relative to
 // /root/reference/source).
 #pragma once
@@ -12,12 +19,15 @@ namespace sfx {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-constexpr int NLMAX = 8;        // Linear layers per head (n_hidden <= 6)
-constexpr int TDG_QMAX = 8192;  // M*A entries of the per-row GPI scratch in LDS
-constexpr int TDG_MMAX = 1024;
-constexpr int TDG_DMAX = 256;
+constexpr int NLMAX = 8;      // Linear layers per head (n_hidden <= 6)
+constexpr int MT = 32;        // minibatch rows per tile
+constexpr int QMAX = 8192;    // T*A entries of the per-row GPI scratch in LDS
+constexpr int OMAX = 4096;    // A*d (row of a ψ output) held in LDS
+constexpr int DMAX = 256;     // feature dimension d
+constexpr int MMAX = 1024;    // rows of one update
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2 };
+enum { R_S = 0, R_S1T = 1, R_S1 = 2, R_G = 3, R_A = 4, NROLE = 5 };
 
 __device__ __forceinline__ float act_fwd(float x, int code) {
   if (code == ACT_RELU) return x > 0.f ? x : 0.f;
@@ -37,14 +47,14 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// 16 consecutive floats row[kb .. kb+15], zero outside [0, K) or when !ok.
-__device__ __forceinline__ void load16(float (&v)[16], const float* row, int kb, int K, bool ok) {
-  if (ok && kb + 16 <= K && ((reinterpret_cast<uintptr_t>(row + kb) & 15u) == 0)) {
-    const float4* p = reinterpret_cast<const float4*>(row + kb);
+// 16 consecutive floats row[kb .. kb+15] (zero where !ok / outside [0, K)).  `vec` must be
+// wave-uniform (K % 64 == 0 with 16-B aligned rows): then four predicated float4 loads.
+__device__ __forceinline__ void load16u(float (&v)[16], const float* row, int kb, int K, bool ok, bool vec) {
+  if (vec) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float4 t = p[q];
-      v[4 * q + 0] = t.x;
+      const float4 t = ok ? reinterpret_cast<const float4*>(row + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[4 * q] = t.x;
       v[4 * q + 1] = t.y;
       v[4 * q + 2] = t.z;
       v[4 * q + 3] = t.w;
@@ -54,6 +64,39 @@ __device__ __forceinline__ void load16(float (&v)[16], const float* row, int kb,
     for (int j = 0; j < 16; ++j) v[j] = (ok && kb + j < K) ? row[kb + j] : 0.f;
   }
 }
+
+// -------------------------------------------------------------------------------------
+// Handle geometry, passed by value to every kernel (all pointers derive from it).
+// -------------------------------------------------------------------------------------
+struct LayerGeo {
+  int N, K, wOff, bOff, actIn, actOut;  // actIn: activation that produced this layer's input
+};
+
+struct Geo {
+  int T, NL, A, d, O, dpad;
+  long long P;        // packed head stride (floats)
+  long long actSize;  // one (role, head) activation block (floats)
+  float* online;      // [T][P]
+  float* target;
+  float* am;          // Adam m, v of ψ
+  float* av;
+  float* w;           // [T][dpad]
+  float* wm;
+  float* wv;
+  int* step;          // [T]
+  float* act;         // [NROLE][T][actSize]
+  float* dz;          // [T][actSize]
+  float* rowloss;     // [T][MMAX] per-row Σ (c - t)^2 of the last TD target
+  int lastOff;        // offset of the last layer's output inside an activation block
+
+  // off: per-layer offset inside a block (passed per launch as a scalar, never indexed)
+  __device__ __forceinline__ float* actp(int role, int head, int off) const {
+    return act + ((long long)role * T + head) * actSize + off;
+  }
+  __device__ __forceinline__ float* dzp(int head, int off) const {
+    return dz + (long long)head * actSize + off;
+  }
+};
 
 // -------------------------------------------------------------------------------------
 // Adam, torch 2.10 single-tensor semantics (torch/optim/adam.py:457,476,531-547):
@@ -84,56 +127,90 @@ __device__ __forceinline__ AdamC adam_consts(const AdamHP& hp, int step) {
   return c;
 }
 
-__device__ __forceinline__ void adam_el(float* __restrict__ p, float* __restrict__ m,
-                                        float* __restrict__ v, float g, const AdamC& c) {
-  float pp = *p, mm = *m, vv = *v;
+// one element, state already in registers; returns nothing, writes p/m/v back
+__device__ __forceinline__ void adam_apply(float& pp, float& mm, float& vv, float g, const AdamC& c) {
   if (c.wd != 0.f) g = __fadd_rn(g, __fmul_rn(c.wd, pp));
   mm = __builtin_fmaf(c.omb1, __fsub_rn(g, mm), mm);  // vectorized lerp: fmadd(w, end-start, start)
   vv = __fadd_rn(__fmul_rn(vv, c.b2), __fmul_rn(__fmul_rn(c.omb2, g), g));
   const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vv), c.bc2s), c.eps);
   pp = __fadd_rn(pp, __fdiv_rn(__fmul_rn(c.nss, mm), denom));
+}
+
+__device__ __forceinline__ void adam_el(float* p, float* m, float* v, float g, const AdamC& c) {
+  float pp = *p, mm = *m, vv = *v;
+  adam_apply(pp, mm, vv, g, c);
   *p = pp;
   *m = mm;
   *v = vv;
 }
 
 // -------------------------------------------------------------------------------------
-// Forward of one Linear (+activation) for a batch of (head, input-stream) instances:
+// K1  Forward of one Linear (+activation) for a set of (role, head) instances:
 //   Y[M,N] = act(X[M,K] W[N,K]^T + b)      (nn.Linear of the ψ lambda,
 //                                            main_sfdqn_torch.py:57-71)
 // Grid: (ceil(N/16), n_inst, ceil(M/32)), 256 threads.  A workgroup owns a 32x16 output
 // tile; its 4 waves split K in 64-wide chunks, each wave runs two 16x16x4 f32 MFMA
-// chains (rows m0..m0+15, m0+16..m0+31), partial tiles are summed through LDS in wave
-// order (deterministic).
+// chains, partial tiles are summed through LDS in wave order (deterministic).
+// Instances come in up to 4 groups of consecutive heads sharing (role, param set, input).
 // -------------------------------------------------------------------------------------
-struct FwdInst {
-  const float* X;  // layer input (used when xsel == 0)
-  const float* W;  // [N, K]
-  const float* b;  // [N]
-  float* Y;        // [M, N]
-  int xsel;        // 0: X, 1: kernel arg xa, 2: kernel arg xb
-  int pad_;
+struct FwdGroup {
+  int role, which, xsel, head0, n;  // which: 0 online, 1 target; xsel: 1 -> xa, 2 -> xb
 };
 
-__global__ __launch_bounds__(256) void k_fwd(const FwdInst* __restrict__ insts, int M, int N, int K,
-                                             int act, const float* __restrict__ xa,
-                                             const float* __restrict__ xb) {
-  const FwdInst in = insts[blockIdx.y];
-  const float* X = in.xsel == 0 ? in.X : (in.xsel == 1 ? xa : xb);
+struct FwdArgs {
+  int M, N, K, act, wOff, bOff, xOff, yOff;  // xOff < 0: layer input is xa / xb
+  int ngroups, pad_;
+  FwdGroup g0, g1, g2, g3;
+  const float* xa;
+  const float* xb;
+};
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_fwd(Geo G, FwdArgs F) {
+  // instance -> (group, head) with constant-index selects (no dynamic kernarg indexing)
+  int y = blockIdx.y;
+  FwdGroup grp = F.g0;
+  if (F.ngroups > 1 && y >= grp.n) { y -= grp.n; grp = F.g1; }
+  if (F.ngroups > 2 && y >= grp.n) { y -= grp.n; grp = F.g2; }
+  if (F.ngroups > 3 && y >= grp.n) { y -= grp.n; grp = F.g3; }
+  const int head = grp.head0 + y;
+  const int M = F.M, N = F.N, K = F.K;
+  const float* P = (grp.which ? G.target : G.online) + (long long)head * G.P;
+  const float* X = F.xOff < 0 ? (grp.xsel == 1 ? F.xa : F.xb) : G.actp(grp.role, head, F.xOff);
+  float* Y = G.actp(grp.role, head, F.yOff);
   const int n0 = blockIdx.x * 16, m0 = blockIdx.z * 32;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
   const int ma = m0 + r, mb = m0 + 16 + r, n = n0 + r;
   const bool oka = ma < M, okb = mb < M, okn = n < N;
   const float* xra = X + (size_t)ma * K;
   const float* xrb = X + (size_t)mb * K;
-  const float* wr = in.W + (size_t)n * K;
+  const float* wr = P + F.wOff + (size_t)n * K;
+  // the reducing threads fetch their bias early
+  const int Lx = threadIdx.x & 63, col = n0 + (Lx & 15);
+  const float bias = (threadIdx.x < 128 && col < N) ? P[F.bOff + col] : 0.f;
   floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   for (int kc = wave * 64; kc < K; kc += 256) {
     const int kb = kc + g * 16;
     float a0[16], a1[16], bw[16];
-    load16(a0, xra, kb, K, oka);
-    load16(a1, xrb, kb, K, okb);
-    load16(bw, wr, kb, K, okn);
+    if constexpr (VEC) {  // K % 64 == 0, rows 16-B aligned: four float4 per operand row
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 ta = oka ? reinterpret_cast<const float4*>(xra + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 tb = okb ? reinterpret_cast<const float4*>(xrb + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 tw = okn ? reinterpret_cast<const float4*>(wr + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        a0[4 * q] = ta.x; a0[4 * q + 1] = ta.y; a0[4 * q + 2] = ta.z; a0[4 * q + 3] = ta.w;
+        a1[4 * q] = tb.x; a1[4 * q + 1] = tb.y; a1[4 * q + 2] = tb.z; a1[4 * q + 3] = tb.w;
+        bw[4 * q] = tw.x; bw[4 * q + 1] = tw.y; bw[4 * q + 2] = tw.z; bw[4 * q + 3] = tw.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const bool kin = kb + j < K;
+        a0[j] = (oka && kin) ? xra[kb + j] : 0.f;
+        a1[j] = (okb && kin) ? xrb[kb + j] : 0.f;
+        bw[j] = (okn && kin) ? wr[kb + j] : 0.f;
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       acc0 = mfma4(a0[j], bw[j], acc0);
@@ -145,152 +222,122 @@ __global__ __launch_bounds__(256) void k_fwd(const FwdInst* __restrict__ insts, 
   red[wave][1][lane] = acc1;
   __syncthreads();
   if (threadIdx.x < 128) {
-    const int s = threadIdx.x >> 6, L = threadIdx.x & 63;
-    floatx4 v = red[0][s][L];
-    v += red[1][s][L];
-    v += red[2][s][L];
-    v += red[3][s][L];
-    const int col = n0 + (L & 15);
+    const int s = threadIdx.x >> 6;
+    floatx4 v = red[0][s][Lx];
+    v += red[1][s][Lx];
+    v += red[2][s][Lx];
+    v += red[3][s][Lx];
     if (col < N) {
-      const float bias = in.b[col];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int row = m0 + 16 * s + (L >> 4) * 4 + i;
-        if (row < M) in.Y[(size_t)row * N + col] = act_fwd(__fadd_rn(v[i], bias), act);
+        const int row = m0 + 16 * s + (Lx >> 4) * 4 + i;
+        if (row < M) Y[(size_t)row * N + col] = act_fwd(__fadd_rn(v[i], bias), F.act);
       }
     }
   }
 }
 
 // -------------------------------------------------------------------------------------
-// TD target and output gradient for one policy (sfdqn.py:313-345; features/deep.py:101-122)
+// K2  TD target and output gradient, one workgroup per (policy, minibatch row b)
+// (sfdqn.py:313-341; features/deep.py:101-120):
 //   a'_b = argmax_a max_t ψ_t(s1_b)[a]·w_i        (GPI branch)
 //        = argmax_a ψ_i(s1_b)[a]·w_i              (own-ψ branch)
 //   t_b  = φ_b + γ_b ψ⁻_i(s1_b)[a'_b]
 //   g[b, a_b, :] = 2 (c[b,a_b,:] - t_b) / (M*A*d), 0 elsewhere  (MSE vs merged clone)
-//   l1 = Σ (c - t)^2 / (M*A*d);  optional l2 = MSE(w_i·φ, r) with one Adam step on w_i.
-// One 256-thread workgroup per policy instance.
+//   rowloss[i][b] = Σ_k (c[b,a_b,k] - t_b[k])^2
+// Every load of the row (ψ(s1) of all heads, ψ⁻, c, φ) is issued before the reductions.
+// Grid (M, npol), 256 threads.  Policies pol0 .. pol0+npol-1.
 // -------------------------------------------------------------------------------------
-struct TdgInst {
-  int policy;
-  int pad_;
-  const float* c;     // ψ_i(S)    [M, O]
-  const float* tpsi;  // ψ⁻_i(S1)  [M, O]
-  const float* psiN;  // ψ_t(S1)   head t at psiN + t * psiN_stride, [M, O]
-  float* w;           // w_i [d]
-  float* wm;
-  float* wv;
-  int* step;          // Adam step counter of head i (incremented here when inc_step)
-  float* g;           // [M, O]
-};
-
 struct TdgArgs {
-  int M, T, A, d, use_gpi, train_w, inc_step, pad_;
-  long long psiN_stride;
+  int M, use_gpi, pol0, npol;
   const int64_t* a;
   const float* phi;
   const float* gamma;
-  const float* r;
-  float* losses;      // [n_inst][3] = (l1 + l2, l1, l2) or null
-  int64_t* next;      // [n_inst][M] or null
-  AdamHP hpw;
+  int64_t* next;  // [npol][M] or null
 };
 
-__device__ __forceinline__ float block_sum256(float v, float* sh) {
-  // deterministic tree sum over the 256 threads of a block
-  sh[threadIdx.x] = v;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) sh[threadIdx.x] = __fadd_rn(sh[threadIdx.x], sh[threadIdx.x + s]);
-    __syncthreads();
+__global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
+  const int b = blockIdx.x, pol = A.pol0 + blockIdx.y, tid = threadIdx.x;
+  const int T = G.T, Aa = G.A, d = G.d, O = G.O, M = A.M, NLm = G.lastOff;
+  __shared__ float s_w[DMAX];
+  __shared__ float s_q[QMAX];
+  __shared__ float s_t[OMAX];   // ψ⁻_i(s1_b) row
+  __shared__ float s_m[64];
+  __shared__ int s_next;
+  const float* wrow = G.w + (long long)pol * G.dpad;
+  for (int k = tid; k < d; k += 256) s_w[k] = wrow[k];
+  const float* trow = G.actp(R_S1T, pol, NLm) + (size_t)b * O;
+  for (int o = tid; o < O; o += 256) s_t[o] = trow[o];
+  // own-row data for the gradient: thread k < d handles feature k of the chosen action
+  const int ab = (int)A.a[b];
+  const bool aok = ab >= 0 && ab < Aa;
+  float cval = 0.f, phik = 0.f;
+  const float gam = A.gamma[b];
+  if (tid < d) {
+    phik = A.phi[(size_t)b * d + tid];
+    if (aok) cval = G.actp(R_S, pol, NLm)[(size_t)b * O + ab * d + tid];
   }
-  const float out = sh[0];
   __syncthreads();
-  return out;
-}
-
-__global__ __launch_bounds__(256) void k_tdg(const TdgInst* __restrict__ insts, TdgArgs A) {
-  const TdgInst I = insts[blockIdx.x];
-  const int M = A.M, Aa = A.A, d = A.d, O = Aa * d, tid = threadIdx.x;
-  __shared__ float s_w[TDG_DMAX];
-  __shared__ float s_q[TDG_QMAX];
-  __shared__ int s_next[TDG_MMAX];
-  __shared__ float s_red[256];
-  const int step = *I.step + 1;
-  for (int k = tid; k < d; k += 256) s_w[k] = I.w[k];
-  __syncthreads();
-  // q over (b, a): max over heads (GPI) or own head
-  for (int idx = tid; idx < M * Aa; idx += 256) {
-    const int b = idx / Aa, a = idx - b * Aa;
-    float best = -INFINITY;
-    const int t0 = A.use_gpi ? 0 : I.policy, t1 = A.use_gpi ? A.T : I.policy + 1;
-    for (int t = t0; t < t1; ++t) {
-      const float* p = I.psiN + (long long)t * A.psiN_stride + (size_t)b * O + a * d;
-      float q = 0.f;
-      for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
-      best = (t == t0 || q > best) ? q : best;
-    }
-    s_q[idx] = best;
+  const int t0 = A.use_gpi ? 0 : pol, nt = A.use_gpi ? T : 1;
+  for (int idx = tid; idx < nt * Aa; idx += 256) {
+    const int t = t0 + idx / Aa, a = idx % Aa;
+    const float* p = G.actp(R_S1, t, NLm) + (size_t)b * O + a * d;
+    float q = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
+    s_q[idx] = q;
   }
-  for (int idx = tid; idx < M * O; idx += 256) I.g[idx] = 0.f;
   __syncthreads();
-  for (int b = tid; b < M; b += 256) {
+  if (tid < Aa) {  // max over heads for action tid (torch.max(q1, axis=1))
+    float mx = s_q[tid];
+    for (int t = 1; t < nt; ++t) mx = fmaxf(mx, s_q[t * Aa + tid]);
+    s_m[tid] = mx;
+  }
+  __syncthreads();
+  if (tid == 0) {  // argmax over actions, first index on ties
     int am = 0;
-    float qm = s_q[b * Aa];
-    for (int a = 1; a < Aa; ++a) {
-      const float q = s_q[b * Aa + a];
-      if (q > qm) { qm = q; am = a; }
-    }
-    s_next[b] = am;
-    if (A.next) A.next[(size_t)blockIdx.x * M + b] = am;
+    float qm = s_m[0];
+    for (int a = 1; a < Aa; ++a)
+      if (s_m[a] > qm) {
+        qm = s_m[a];
+        am = a;
+      }
+    s_next = am;
+    if (A.next) A.next[(size_t)blockIdx.y * M + b] = am;
   }
-  __threadfence_block();
   __syncthreads();
   const float norm = (float)(2.0 / ((double)M * (double)O));
-  float sq = 0.f;
-  for (int idx = tid; idx < M * d; idx += 256) {
-    const int b = idx / d, k = idx - b * d;
-    const int ab = (int)A.a[b];
-    if (ab < 0 || ab >= Aa) continue;  // invalid action: contributes nothing (never indexes out of range)
-    const float tg = __fadd_rn(A.phi[idx], __fmul_rn(A.gamma[b], I.tpsi[(size_t)b * O + s_next[b] * d + k]));
-    const float diff = __fsub_rn(I.c[(size_t)b * O + ab * d + k], tg);
-    I.g[(size_t)b * O + ab * d + k] = __fmul_rn(norm, diff);
-    sq = __builtin_fmaf(diff, diff, sq);
-  }
-  const float l1 = (float)((double)block_sum256(sq, s_red) / ((double)M * (double)O));
-  float l2 = 0.f;
-  if (A.train_w) {
-    // r_fit = w·φ_b ; e_b = r_fit - r_b ; dw = Σ_b (2/M) e_b φ_b   (sfdqn.py:340-342)
-    __shared__ float s_e[TDG_MMAX];
-    float se = 0.f;
-    for (int b = tid; b < M; b += 256) {
-      float rf = 0.f;
-      for (int k = 0; k < d; ++k) rf = __builtin_fmaf(s_w[k], A.phi[(size_t)b * d + k], rf);
-      const float e = __fsub_rn(rf, A.r[b]);
-      s_e[b] = __fmul_rn((float)(2.0 / (double)M), e);
-      se = __builtin_fmaf(e, e, se);
+  float* grow = G.dzp(pol, NLm) + (size_t)b * O;
+  const int an = s_next;
+  float dsq = 0.f;
+  for (int o = tid; o < O; o += 256) {
+    float gv = 0.f;
+    if (aok && o >= ab * d && o < ab * d + d) {
+      const int k = o - ab * d;
+      const float tg = __fadd_rn(A.phi[(size_t)b * d + k], __fmul_rn(gam, s_t[an * d + k]));
+      const float diff = __fsub_rn(G.actp(R_S, pol, NLm)[(size_t)b * O + o], tg);
+      gv = __fmul_rn(norm, diff);
     }
-    l2 = (float)((double)block_sum256(se, s_red) / (double)M);
-    const AdamC c = adam_consts(A.hpw, step);
-    for (int k = tid; k < d; k += 256) {
-      float gw = 0.f;
-      for (int b = 0; b < M; ++b) gw = __builtin_fmaf(s_e[b], A.phi[(size_t)b * d + k], gw);
-      adam_el(I.w + k, I.wm + k, I.wv + k, gw, c);
-    }
+    grow[o] = gv;
   }
+  if (tid < d && aok) {
+    const float tg = __fadd_rn(phik, __fmul_rn(gam, s_t[an * d + tid]));
+    const float diff = __fsub_rn(cval, tg);
+    dsq = __fmul_rn(diff, diff);
+  }
+  // row Σ diff^2 in feature order
+  __shared__ float s_sq[DMAX];
+  if (tid < d) s_sq[tid] = dsq;
+  __syncthreads();
   if (tid == 0) {
-    if (A.losses) {
-      float* lo = A.losses + 3 * blockIdx.x;
-      lo[0] = __fadd_rn(l1, l2);
-      lo[1] = l1;
-      lo[2] = l2;
-    }
-    if (A.inc_step) *I.step = step;
+    float s = 0.f;
+    for (int k = 0; k < d; ++k) s = __fadd_rn(s, s_sq[k]);
+    G.rowloss[(long long)pol * MMAX + b] = s;
   }
 }
 
 // -------------------------------------------------------------------------------------
-// Backward through the ψ MLP with Adam fused into the weight-gradient epilogue
+// K3  Backward through the ψ MLP with Adam fused into the weight-gradient epilogue
 // (autograd of sfdqn.py:344-345 + optim.step() at :362).
 //
 // Layers are processed in a ping-pong so no launch both reads and rewrites a weight:
@@ -298,45 +345,61 @@ __global__ __launch_bounds__(256) void k_tdg(const TdgInst* __restrict__ insts, 
 // finishes the weight gradient of layer l+1 and applies Adam to it (dW roles).
 //   dX role : dZ_{l-1} = (dZ_l W_l) ⊙ act'(X_l)        32x16 tile, split over the 4 waves
 //   dW role : dW_l = dZ_l^T X_l ; db_l = Σ_m dZ_l ; Adam(W_l, b_l)
+//   tail    : (first launch only) l1 from the per-row losses, optional l2 = MSE(w_i·φ, r)
+//             with one Adam step on w_i (sfdqn.py:340-342), Adam step counter += 1.
 // blockIdx.x selects the role: [0, na) dX of layer la; [na, na+nb) dW of lb;
-// [na+nb, na+nb+nc) dW of lc.  blockIdx.y = updated head instance.
+// [na+nb, na+nb+nc) dW of lc; [.., +tail) tail.  blockIdx.y = head - head0.
 // -------------------------------------------------------------------------------------
-struct LayerGeo {
-  int N, K, wOff, bOff, actIn;  // actIn: activation that produced this layer's input
-};
-
-struct BwdInst {
-  float* P;                   // packed params of the head (online)
-  float* Mo;                  // Adam m
-  float* Vo;                  // Adam v
-  const int* step;            // Adam step (already incremented by k_tdg)
-  const float* X[NLMAX];      // input of each layer (X[0] == null -> BwdArgs.x0)
-  float* dZ[NLMAX];           // gradient w.r.t. each layer's output (pre-activation)
+struct RoleGeo {
+  int N, K, wOff, bOff, actIn;
+  int xOff;   // input activation offset (R_S block); < 0: the minibatch states x0
+  int dzOff;  // this layer's output-gradient offset (dz block)
+  int dzIn;   // dX role: offset of the gradient it writes (layer l-1)
 };
 
 struct BwdArgs {
-  int M, na, nb, nc, la, lb, lc, pad_;
-  LayerGeo L[NLMAX];
-  AdamHP hp;
-  const float* x0;
+  int M, na, nb, nc, tail, head0, train_w, pad_;
+  RoleGeo ra, rb, rc;  // dX role (layer la), dW roles (lb, lc)
+  AdamHP hp, hpw;
+  const float* x0;   // layer-0 input (the minibatch states S)
+  const float* phi;  // tail: [M, d]
+  const float* r;    // tail: [M] rewards (train_w)
+  float* losses;     // tail: [n_head][3] (l1+l2, l1, l2) or null
 };
 
-__device__ void role_dx(const BwdArgs& A, const BwdInst& I, int tile, floatx4 (*red)[2][64]) {
-  const LayerGeo L = A.L[A.la];
+__device__ __forceinline__ const float* layer_input(const Geo& G, const BwdArgs& A, int head, int xOff) {
+  return xOff < 0 ? A.x0 : G.actp(R_S, head, xOff);
+}
+
+__device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floatx4 (*red)[2][64]) {
+  const RoleGeo L = A.ra;
   const int N = L.N, K = L.K, M = A.M;
   const int ntk = (K + 15) >> 4;
   const int k0 = (tile % ntk) * 16, m0 = (tile / ntk) * 32;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
-  const float* dZ = I.dZ[A.la];
-  const float* W = I.P + L.wOff;
+  const float* dZ = G.dzp(head, L.dzOff);
+  const float* W = (G.online + (long long)head * G.P) + L.wOff;
+  const float* Xin = layer_input(G, A, head, L.xOff);
+  float* out = G.dzp(head, L.dzIn);
   const int ma = m0 + r, mb = m0 + 16 + r, kk = k0 + r;
   const bool oka = ma < M, okb = mb < M, okk = kk < K;
+  // activation outputs the reducing threads will need
+  const int s = (threadIdx.x >> 6) & 1, Lx = threadIdx.x & 63, col = k0 + (Lx & 15);
+  float xin[4] = {0.f, 0.f, 0.f, 0.f};
+  if (threadIdx.x < 128 && col < K) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = m0 + 16 * s + (Lx >> 4) * 4 + i;
+      if (row < M) xin[i] = Xin[(size_t)row * K + col];
+    }
+  }
   floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   for (int nc = wave * 64; nc < N; nc += 256) {
     const int nb = nc + g * 16;
     float a0[16], a1[16], bw[16];
-    load16(a0, dZ + (size_t)ma * N, nb, N, oka);
-    load16(a1, dZ + (size_t)mb * N, nb, N, okb);
+    const bool vec = (N & 63) == 0;
+    load16u(a0, dZ + (size_t)ma * N, nb, N, oka, vec);
+    load16u(a1, dZ + (size_t)mb * N, nb, N, okb, vec);
 #pragma unroll
     for (int j = 0; j < 16; ++j) bw[j] = (okk && nb + j < N) ? W[(size_t)(nb + j) * K + kk] : 0.f;
 #pragma unroll
@@ -349,147 +412,240 @@ __device__ void role_dx(const BwdArgs& A, const BwdInst& I, int tile, floatx4 (*
   red[wave][1][lane] = acc1;
   __syncthreads();
   if (threadIdx.x < 128) {
-    const int s = threadIdx.x >> 6, Lx = threadIdx.x & 63;
     floatx4 v = red[0][s][Lx];
     v += red[1][s][Lx];
     v += red[2][s][Lx];
     v += red[3][s][Lx];
-    const int col = k0 + (Lx & 15);
     if (col < K) {
-      const float* Xin = I.X[A.la];
-      float* out = I.dZ[A.la - 1];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = m0 + 16 * s + (Lx >> 4) * 4 + i;
-        if (row < M) out[(size_t)row * K + col] = act_bwd(v[i], Xin[(size_t)row * K + col], L.actIn);
+        if (row < M) out[(size_t)row * K + col] = act_bwd(v[i], xin[i], L.actIn);
       }
     }
   }
 }
 
-__device__ void role_dw(const BwdArgs& A, const BwdInst& I, int l, int tile) {
-  const LayerGeo L = A.L[l];
+__device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile) {
   const int N = L.N, K = L.K, M = A.M;
   const int ntk = (K + 63) >> 6;
   const int kt = tile % ntk, nt = tile / ntk;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
   const int nbase = nt * 32, n0 = nbase + (wave & 1) * 16, k0 = kt * 64 + (wave >> 1) * 32;
-  const float* dZ = I.dZ[l];
-  const float* X = I.X[l] ? I.X[l] : A.x0;
+  const float* dZ = G.dzp(head, L.dzOff);
+  const float* X = layer_input(G, A, head, L.xOff);
+  float* P = G.online + (long long)head * G.P;
+  float* Mo = G.am + (long long)head * G.P;
+  float* Vo = G.av + (long long)head * G.P;
+  const AdamC c = adam_consts(A.hp, G.step[head]);
   const int nn = n0 + r, kb0 = k0 + r, kb1 = k0 + 16 + r;
-  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  for (int mb = 0; mb < M; mb += 4) {
-    const int m = mb + g;
-    const bool okm = m < M;
-    const float a = (okm && nn < N) ? dZ[(size_t)m * N + nn] : 0.f;
-    const float b0 = (okm && kb0 < K) ? X[(size_t)m * K + kb0] : 0.f;
-    const float b1 = (okm && kb1 < K) ? X[(size_t)m * K + kb1] : 0.f;
-    acc0 = mfma4(a, b0, acc0);
-    acc1 = mfma4(a, b1, acc1);
-  }
-  const AdamC c = adam_consts(A.hp, *I.step);
-  float* P = I.P + L.wOff;
-  float* Mo = I.Mo + L.wOff;
-  float* Vo = I.Vo + L.wOff;
+  // prefetch the optimizer state of the 8 weights this lane will update
+  float pp[8], pm[8], pv[8];
+  bool ok[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int n = n0 + g * 4 + i;
-    if (n < N) {
-      if (kb0 < K) adam_el(P + (size_t)n * K + kb0, Mo + (size_t)n * K + kb0, Vo + (size_t)n * K + kb0, acc0[i], c);
-      if (kb1 < K) adam_el(P + (size_t)n * K + kb1, Mo + (size_t)n * K + kb1, Vo + (size_t)n * K + kb1, acc1[i], c);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = h ? kb1 : kb0;
+      const int e = i * 2 + h;
+      ok[e] = n < N && k < K;
+      const size_t off = (size_t)L.wOff + (size_t)n * K + k;
+      pp[e] = ok[e] ? P[off] : 0.f;
+      pm[e] = ok[e] ? Mo[off] : 0.f;
+      pv[e] = ok[e] ? Vo[off] : 0.f;
     }
   }
-  if (kt == 0 && threadIdx.x < 32) {
-    const int n = nbase + threadIdx.x;
-    if (n < N) {
-      float s = 0.f;
-      for (int m = 0; m < M; ++m) s = __fadd_rn(s, dZ[(size_t)m * N + n]);
-      adam_el(I.P + L.bOff + n, I.Mo + L.bOff + n, I.Vo + L.bOff + n, s, c);
+  // bias state (threads 0..31 of the kt == 0 tiles)
+  const bool dob = kt == 0 && threadIdx.x < 32 && nbase + (int)threadIdx.x < N;
+  const int nbias = nbase + threadIdx.x;
+  float bp = 0.f, bm = 0.f, bv = 0.f;
+  if (dob) {
+    bp = P[L.bOff + nbias];
+    bm = Mo[L.bOff + nbias];
+    bv = Vo[L.bOff + nbias];
+  }
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  for (int mc = 0; mc < M; mc += MT) {
+    float av[MT / 4], bv0[MT / 4], bv1[MT / 4];
+#pragma unroll
+    for (int j = 0; j < MT / 4; ++j) {
+      const int m = mc + 4 * j + g;
+      const bool okm = m < M;
+      av[j] = (okm && nn < N) ? dZ[(size_t)m * N + nn] : 0.f;
+      bv0[j] = (okm && kb0 < K) ? X[(size_t)m * K + kb0] : 0.f;
+      bv1[j] = (okm && kb1 < K) ? X[(size_t)m * K + kb1] : 0.f;
     }
+    float db[MT];
+    if (dob) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) db[m] = (mc + m < M) ? dZ[(size_t)(mc + m) * N + nbias] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < MT / 4; ++j) {
+      acc0 = mfma4(av[j], bv0[j], acc0);
+      acc1 = mfma4(av[j], bv1[j], acc1);
+    }
+    if (dob) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) bsum = __fadd_rn(bsum, db[m]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + g * 4 + i;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = i * 2 + h;
+      if (ok[e]) {
+        const size_t off = (size_t)L.wOff + (size_t)n * K + (h ? kb1 : kb0);
+        adam_apply(pp[e], pm[e], pv[e], h ? acc1[i] : acc0[i], c);
+        P[off] = pp[e];
+        Mo[off] = pm[e];
+        Vo[off] = pv[e];
+      }
+    }
+  }
+  if (dob) {
+    adam_apply(bp, bm, bv, bsum, c);
+    P[L.bOff + nbias] = bp;
+    Mo[L.bOff + nbias] = bm;
+    Vo[L.bOff + nbias] = bv;
   }
 }
 
-__global__ __launch_bounds__(256) void k_bwd(const BwdInst* __restrict__ insts, BwdArgs A) {
+// loss finalisation, optional w step, Adam step counter (one workgroup per head)
+__device__ void role_tail(const Geo& G, const BwdArgs& A, int head) {
+  const int M = A.M, d = G.d, tid = threadIdx.x;
+  __shared__ float s_e[MMAX];
+  __shared__ float s_x[256];
+  const int step = G.step[head] + 1;
+  const float* rl = G.rowloss + (long long)head * MMAX;
+  float* w = G.w + (long long)head * G.dpad;
+  float l2 = 0.f;
+  if (A.train_w) {
+    // r_fit = w·φ_b ; e_b = r_fit - r_b ; dw = Σ_b (2/M) e_b φ_b   (sfdqn.py:340-342)
+    for (int b = tid; b < M; b += 256) {
+      float rf = 0.f;
+      for (int k = 0; k < d; ++k) rf = __builtin_fmaf(w[k], A.phi[(size_t)b * d + k], rf);
+      s_e[b] = __fsub_rn(rf, A.r[b]);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float se = 0.f;
+      for (int b = 0; b < M; ++b) se = __builtin_fmaf(s_e[b], s_e[b], se);
+      s_x[0] = (float)((double)se / (double)M);
+    }
+    const AdamC c = adam_consts(A.hpw, step);
+    const float nrm = (float)(2.0 / (double)M);
+    float gw = 0.f;
+    if (tid < d) {
+      for (int b = 0; b < M; ++b) gw = __builtin_fmaf(__fmul_rn(nrm, s_e[b]), A.phi[(size_t)b * d + tid], gw);
+    }
+    __syncthreads();
+    if (tid < d) adam_el(w + tid, G.wm + (long long)head * G.dpad + tid, G.wv + (long long)head * G.dpad + tid, gw, c);
+    l2 = s_x[0];
+  }
+  if (tid == 0) {
+    float s = 0.f;
+    for (int b = 0; b < M; ++b) s = __fadd_rn(s, rl[b]);
+    const float l1 = (float)((double)s / ((double)M * (double)G.O));
+    if (A.losses) {
+      float* lo = A.losses + 3 * (head - A.head0);
+      lo[0] = __fadd_rn(l1, l2);
+      lo[1] = l1;
+      lo[2] = l2;
+    }
+    G.step[head] = step;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
   __shared__ floatx4 red[4][2][64];
-  const BwdInst& I = insts[blockIdx.y];
+  const int head = A.head0 + blockIdx.y;
   int bx = blockIdx.x;
   if (bx < A.na) {
-    role_dx(A, I, bx, red);
+    role_dx(G, A, head, bx, red);
     return;
   }
   bx -= A.na;
   if (bx < A.nb) {
-    role_dw(A, I, A.lb, bx);
+    role_dw(G, A, head, A.rb, bx);
     return;
   }
   bx -= A.nb;
-  role_dw(A, I, A.lc, bx);
+  if (bx < A.nc) {
+    role_dw(G, A, head, A.rc, bx);
+    return;
+  }
+  role_tail(G, A, head);
 }
 
 // -------------------------------------------------------------------------------------
-// GPI reduction over heads (SF.GPI_w, features/successor.py:243-246; sfdqn.py:235-240)
-// psiN: head t rows at psiN + t*stride, [M, O].  One workgroup per row b.
-// Also serves action selection (sfdqn.py:585-594): out[0] = c, out[1] = argmax_a q[c].
+// K4  GPI reduction over heads (SF.GPI_w, features/successor.py:243-246;
+// sfdqn.py:235-240) and action selection (sfdqn.py:585-594).  One workgroup per row.
+//   task = argmax_t max_a q ; next = argmax_a max_t q ; sel = (c, argmax_a q[c])
 // -------------------------------------------------------------------------------------
 struct GpiArgs {
-  int M, T, A, d, row0, select_task, use_gpi, pad_;
-  long long stride;
-  const float* psiN;
+  int M, role, row0, select_task, use_gpi, pad_;
   const float* w;
   float* psi_out;   // [B, T, A, d] or null  (row b -> row0 + b)
   float* q_out;     // [B, T, A] or null
   int64_t* task_out;
   int64_t* next_out;
-  int64_t* sel_out;  // [2] (action selection) or null
+  int64_t* sel_out;  // [2] or null
 };
 
-__global__ __launch_bounds__(256) void k_gpi(GpiArgs A) {
+__global__ __launch_bounds__(256) void k_gpi(Geo G, GpiArgs A) {
   const int b = blockIdx.x, tid = threadIdx.x;
-  const int T = A.T, Aa = A.A, d = A.d, O = Aa * d;
-  __shared__ float s_q[TDG_QMAX];
-  __shared__ float s_w[TDG_DMAX];
+  const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff;
+  __shared__ float s_q[QMAX];
+  __shared__ float s_w[DMAX];
+  __shared__ float s_mt[256], s_ma[256];
   for (int k = tid; k < d; k += 256) s_w[k] = A.w[k];
-  __syncthreads();
   const long long ob = (long long)(A.row0 + b);
+  if (A.psi_out) {
+    for (int idx = tid; idx < T * O; idx += 256) {
+      const int t = idx / O, o = idx - t * O;
+      A.psi_out[(ob * T + t) * O + o] = G.actp(A.role, t, NLm)[(size_t)b * O + o];
+    }
+  }
+  __syncthreads();
   for (int idx = tid; idx < T * Aa; idx += 256) {
     const int t = idx / Aa, a = idx - t * Aa;
-    const float* p = A.psiN + (long long)t * A.stride + (size_t)b * O + a * d;
+    const float* p = G.actp(A.role, t, NLm) + (size_t)b * O + a * d;
     float q = 0.f;
+#pragma unroll 8
     for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
     s_q[idx] = q;
     if (A.q_out) A.q_out[(ob * T + t) * Aa + a] = q;
   }
-  if (A.psi_out) {
-    for (int idx = tid; idx < T * O; idx += 256) {
-      const int t = idx / O, o = idx - t * O;
-      A.psi_out[(ob * T + t) * O + o] = A.psiN[(long long)t * A.stride + (size_t)b * O + o];
-    }
+  __syncthreads();
+  for (int t = tid; t < T; t += 256) {
+    float mx = s_q[t * Aa];
+    for (int a = 1; a < Aa; ++a) mx = fmaxf(mx, s_q[t * Aa + a]);
+    s_mt[t] = mx;
+  }
+  for (int a = tid; a < Aa; a += 256) {
+    float mx = s_q[a];
+    for (int t = 1; t < T; ++t) mx = fmaxf(mx, s_q[t * Aa + a]);
+    s_ma[a] = mx;
   }
   __syncthreads();
   if (tid == 0) {
-    // task = argmax_t max_a q ; next = argmax_a max_t q  (first index on ties)
-    int tb = 0;
-    float tv = -INFINITY;
-    for (int t = 0; t < T; ++t) {
-      float mx = s_q[t * Aa];
-      for (int a = 1; a < Aa; ++a) mx = s_q[t * Aa + a] > mx ? s_q[t * Aa + a] : mx;
-      if (t == 0 || mx > tv) { tv = mx; tb = t; }
-    }
-    int ab = 0;
-    float av = -INFINITY;
-    for (int a = 0; a < Aa; ++a) {
-      float mx = s_q[a];
-      for (int t = 1; t < T; ++t) mx = s_q[t * Aa + a] > mx ? s_q[t * Aa + a] : mx;
-      if (a == 0 || mx > av) { av = mx; ab = a; }
-    }
+    int tb = 0, ab = 0;
+    for (int t = 1; t < T; ++t)
+      if (s_mt[t] > s_mt[tb]) tb = t;
+    for (int a = 1; a < Aa; ++a)
+      if (s_ma[a] > s_ma[ab]) ab = a;
     if (A.task_out) A.task_out[ob] = tb;
     if (A.next_out) A.next_out[ob] = ab;
     if (A.sel_out) {
       const int c = A.use_gpi ? tb : A.select_task;
       int act = 0;
-      float best = s_q[c * Aa];
       for (int a = 1; a < Aa; ++a)
-        if (s_q[c * Aa + a] > best) { best = s_q[c * Aa + a]; act = a; }
+        if (s_q[c * Aa + a] > s_q[c * Aa + act]) act = a;
       A.sel_out[0] = c;
       A.sel_out[1] = act;
     }
@@ -499,13 +655,19 @@ __global__ __launch_bounds__(256) void k_gpi(GpiArgs A) {
 // LMS reward fit (features/successor.py:164-167): w += α (r - Σ φ⊙w) φ
 __global__ void k_lms(float* __restrict__ w, const float* __restrict__ phi, const float* __restrict__ r,
                       float alpha, int d) {
-  __shared__ float s_red[256];
+  __shared__ float s_p[DMAX];
   const int tid = threadIdx.x;
-  float p = 0.f;
-  for (int k = tid; k < d; k += 256) p = __fadd_rn(p, __fmul_rn(phi[k], w[k]));
-  const float rfit = block_sum256(p, s_red);
-  const float e = __fmul_rn(alpha, __fsub_rn(r[0], rfit));
-  for (int k = tid; k < d; k += 256) w[k] = __fadd_rn(w[k], __fmul_rn(e, phi[k]));
+  const float wk = tid < d ? w[tid] : 0.f, pk = tid < d ? phi[tid] : 0.f;
+  if (tid < d) s_p[tid] = __fmul_rn(pk, wk);
+  __syncthreads();
+  __shared__ float s_e;
+  if (tid == 0) {
+    float rf = 0.f;
+    for (int k = 0; k < d; ++k) rf = __fadd_rn(rf, s_p[k]);
+    s_e = __fmul_rn(alpha, __fsub_rn(r[0], rf));
+  }
+  __syncthreads();
+  if (tid < d) w[tid] = __fadd_rn(wk, __fmul_rn(s_e, pk));
 }
 
 }  // namespace sfx

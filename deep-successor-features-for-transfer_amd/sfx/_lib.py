@@ -23,6 +23,7 @@ SIGNATURES = {
     "sfx_create": (_I, [C.POINTER(_VP), _I, _I, _I, _I, _IP, _I, _I, _I, _I, _VP]),
     "sfx_destroy": (_I, [_VP]),
     "sfx_set_stream": (_I, [_VP, _VP]),
+    "sfx_set_graphs": (_I, [_VP, _I]),
     "sfx_head_numel": (_I, [_VP]),
     "sfx_set_adam": (_I, [_VP, _D, _D, _D, _D, _D, _D, _D]),
     "sfx_load_head": (_I, [_VP, _I, _I, _FP]),

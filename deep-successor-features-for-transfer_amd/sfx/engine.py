@@ -82,6 +82,9 @@ class SFEngine:
         check(lib.sfx_set_adam(self._h, float(lr_psi), float(wd_psi), float(lr_w), float(wd_w),
                                float(betas[0]), float(betas[1]), float(eps)), "sfx_set_adam")
 
+    def set_graphs(self, enable: bool):
+        check(lib.sfx_set_graphs(self._h, int(bool(enable))), "sfx_set_graphs")
+
     def set_target_update_ev(self, ev: int):
         check(lib.sfx_set_target_update_ev(self._h, int(ev)), "sfx_set_target_update_ev")
 

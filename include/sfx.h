@@ -56,6 +56,10 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts_
                int d, int max_batch, int device, void* stream);
 int sfx_destroy(sfx_t h);
 int sfx_set_stream(sfx_t h, void* stream);
+/* Each entry point's launch sequence is captured into a hipGraph keyed by its arguments
+ * and replayed on later calls with the same arguments (default on; SFX_GRAPHS=0 in the
+ * environment or enable=0 here launches eagerly). */
+int sfx_set_graphs(sfx_t h, int enable);
 /* Packed parameter count of one head in torch packing. */
 int sfx_head_numel(sfx_t h);
 

@@ -25,8 +25,11 @@ def timeit(name, fn, n=200):
     torch.cuda.synchronize(); dt = (time.perf_counter() - t0) / n
     print(f"{name:32s} {dt*1e6:9.1f} us")
 
-timeit("select_action (B=1, T=8)", lambda: eng.select_action(s_one, 0, True))
-timeit("select_action + D2H", lambda: eng.select_action(s_one, 0, True).cpu())
-timeit("update active (gpi)", lambda: eng.update(0, s, a, r, phi, s1, gamma, True, losses=l3))
-timeit("update_all (T=8)", lambda: eng.update_all(s, a, phi, s1, gamma, losses=losses))
-timeit("gpi B=32", lambda: eng.gpi(s, w_index=0))
+for graphs in (False, True):
+  eng.set_graphs(graphs)
+  print("graphs", graphs)
+  timeit("select_action (B=1, T=8)", lambda: eng.select_action(s_one, 0, True))
+  timeit("select_action + D2H", lambda: eng.select_action(s_one, 0, True).cpu())
+  timeit("update active (gpi)", lambda: eng.update(0, s, a, r, phi, s1, gamma, True, losses=l3))
+  timeit("update_all (T=8)", lambda: eng.update_all(s, a, phi, s1, gamma, losses=losses))
+  timeit("gpi B=32", lambda: eng.gpi(s, w_index=0))
