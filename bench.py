@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""bench.py -- env steps/sec of SF-DQN on synthetic Reacher-shape tasks, MI355X.
+
+Metric (BASELINE.json): "env steps/sec (whole node), Reacher 8-task SF-DQN at 1/2/4/8 MI355X".
+One step = one Agent.next_sample iteration (agents/agent.py:195-261): GPI action selection
+for the current state (B=1), ε-greedy, a synthetic Reacher-shape transition (|s|=17,
+|a|=7, d=8), the LMS reward fit, replay append + uniform B=32 sample, and the SF update.
+Default schedule "all" is the main_sfdqn_torch.py path (agents/sfdqn.py:47-60 over
+features/deep.py): every one of the 8 heads is updated per env step.
+
+Multi-GPU: one process per GPU (torchrun).  Weak scaling: each rank owns 8 heads; ranks
+run independent replicas of the env/replay stream.
+
+Prints ONE JSON line on rank 0.  `roofline` is for the dominant kernel kind, measured live
+in this process with HIP events (libsfx instrumentation, eager launches) right after the
+timed region; `cpu_baseline` times the CPU oracle (oracle/ref_cpu.py) on a bounded sample
+of the same workload on this box's host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "deep-successor-features-for-transfer_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "env steps/sec (whole node), Reacher 8-task SF-DQN at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SHAPE = dict(n_s=17, H=256, A=7, d=8, acts=("relu", "relu"))
+KIND_NAMES = {"fwd": "k_fwd", "tdg": "k_tdg", "bwd": "k_bwd", "gpi": "k_gpi", "lms": "k_lms"}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--warmup", type=int, default=200)
+    p.add_argument("--schedule", choices=["all", "active"], default="all")
+    p.add_argument("--heads", type=int, default=8, help="source tasks (ψ heads) per GPU")
+    p.add_argument("--batch", type=int, default=32)
+    p.add_argument("--prof-steps", type=int, default=50)
+    p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(args, seconds: float):
+    """The CPU oracle (a from-scratch PyTorch-CPU restatement of the reference path,
+    oracle/ref_cpu.py) running the same env-step loop on the host cores."""
+    from oracle import ref_cpu as R
+    from sfx.init import reference_heads
+    from sfx.runner import Replay, SynthReacher
+
+    cores = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count(), os.cpu_count())
+    torch.set_num_threads(cores)
+    T, B = args.heads, args.batch
+    spec = R.Spec(SHAPE["n_s"], SHAPE["H"], SHAPE["A"], SHAPE["d"], SHAPE["acts"])
+    online, w = reference_heads(T, spec.n_s, spec.H, spec.A, spec.d, spec.acts, seed=0)
+    st = R.SFState(spec, online.clone(), online.clone(), w.clone())
+    rng = np.random.default_rng(1)
+    task = SynthReacher(spec.n_s, spec.A, spec.d, 0, rng)
+    rep = Replay(100_000, spec.n_s, spec.d, rng)
+    for _ in range(1000):
+        s0 = task.initialize()
+        s1, phi, r, _ = task.transition(int(rng.integers(spec.A)))
+        rep.append(s0, 0, r, phi, s1, 0.9)
+    s = task.initialize()
+    steps = 0
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        while True:
+            q, c = R.gpi_w(R.psi_all(st.online, spec, torch.from_numpy(s).view(1, -1)), st.w[0])
+            a = R.select_action(q, c[0], 0, True)
+            if rng.random() <= 0.1:
+                a = int(rng.integers(spec.A))
+            s1, phi, r, _ = task.transition(a)
+            st.w[0] = R.lms_update(st.w[0].view(-1, 1), torch.from_numpy(phi), torch.tensor(r), 1e-3).view(-1)
+            rep.append(s, a, r, phi, s1, 0.9)
+            idx = rng.integers(0, rep.size, B)
+            batch = (torch.from_numpy(rep.s[idx]), torch.from_numpy(rep.a[idx]), torch.from_numpy(rep.phi[idx]),
+                     torch.from_numpy(rep.s1[idx]), torch.from_numpy(rep.gamma[idx]))
+            if args.schedule == "all":
+                R.deep_all_task_step(st, batch)
+            else:
+                b6 = (batch[0], batch[1], torch.from_numpy(rep.r[idx]).view(-1, 1), batch[2], batch[3], batch[4])
+                R.sf_update(st, b6, 0, use_gpi=True)
+            s = s1
+            steps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    return {"value": steps / el, "unit": "env steps/s", "cores": cores, "kind": "port",
+            "sample": f"{steps} env steps ({el:.1f} s) of the same {args.schedule}-task loop, T={T}, B={B}, "
+                      f"oracle/ref_cpu.py on torch CPU with {cores} threads"}
+
+
+def traffic_from_profiles(kind: str, workload: str):
+    """HBM bytes per launch of `kind` from a committed rocprofv3 --pmc pass (profiles/), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        rec = json.load(open(path))
+        ent = rec.get(workload, {}).get(KIND_NAMES[kind])
+        return None if ent is None else float(ent["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist = None
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from sfx.engine import SFEngine
+    from sfx.init import reference_heads
+    from sfx.runner import EnvLoop
+
+    T, B = args.heads, args.batch
+    eng = SFEngine(T, SHAPE["n_s"], SHAPE["H"], SHAPE["A"], SHAPE["d"], SHAPE["acts"], max_batch=B, device=device)
+    online, w = reference_heads(T, SHAPE["n_s"], SHAPE["H"], SHAPE["A"], SHAPE["d"], SHAPE["acts"], seed=rank)
+    for t in range(T):
+        eng.load_head(t, online[t], 0)
+        eng.load_head(t, online[t], 1)
+        eng.load_w(t, w[t])
+    eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
+    eng.set_target_update_ev(1000)
+    loop = EnvLoop(eng, schedule=args.schedule, batch=B, seed=1 + rank)
+    loop.prefill(1000)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    loop.run(args.warmup)
+    barrier()
+    t0 = time.perf_counter()
+    loop.run(args.steps)
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    value = world * args.steps / dt
+
+    # live per-kernel durations (HIP events around each launch) for the roofline figure
+    eng.prof_reset()
+    eng.prof_enable(True)
+    loop.run(args.prof_steps)
+    stats = eng.prof_collect()
+    eng.prof_enable(False)
+    eng.prof_reset()
+
+    workload = f"reacher17-{args.schedule}-T{T}-B{B}"
+    if rank == 0:
+        kind = max(stats, key=lambda k: stats[k][1])
+        n, us, by = stats[kind]
+        avg_us = us / max(n, 1)
+        bpl = by / max(n, 1)
+        achieved = bpl / (avg_us * 1e-6) / 1e9 if n else 0.0
+        traffic = traffic_from_profiles(kind, workload)
+        roofline = {"bound": "hbm", "kernel": KIND_NAMES[kind], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                    "bytes_per_launch": round(bpl), "avg_launch_us": round(avg_us, 3),
+                    "share_of_gpu_time": round(us / max(sum(v[1] for v in stats.values()), 1e-9), 3),
+                    "per_kind_avg_us": {KIND_NAMES[k]: round(v[1] / max(v[0], 1), 3) for k, v in stats.items() if v[0]}}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args, args.cpu_seconds)
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "env steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000.0 * dt / args.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": workload + f" (Reacher-shape |s|=17 |a|=7 d=8, psi MLP 256x2, "
+                                               f"{'all heads updated per env step: main_sfdqn_torch.py path' if args.schedule == 'all' else 'active head only: sfdqn.py path'})",
+                       "heads_per_gpu": T, "global_batch": B * world, "parallelism": f"replica{world}" if world > 1 else "single",
+                       "loop": "python host loop over libsfx graphs"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -10,6 +10,7 @@
 // Kernels take the whole geometry by value (sfx::Geo) and derive every pointer from it.
 // Each entry point's launch sequence is captured once into a hipGraph (keyed by its
 // arguments) and replayed afterwards; SFX_GRAPHS=0 disables graphs.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -84,6 +85,15 @@ struct sfx_handle {
   std::vector<int> since_target, host_step;
   std::map<GraphKey, hipGraphExec_t> graphs;
   Geo G{};
+  // event instrumentation (bench roofline): one (start, stop) pair per launch, eager only
+  bool prof = false;
+  struct ProfRec {
+    int kind;
+    double bytes;
+    hipEvent_t a, b;
+  };
+  std::vector<ProfRec> prof_recs;
+  std::vector<hipEvent_t> prof_pool;
 
   float *online = nullptr, *target = nullptr, *am = nullptr, *av = nullptr;
   float *w = nullptr, *wm = nullptr, *wv = nullptr;
@@ -100,10 +110,36 @@ void clear_graphs(sfx_handle* h) {
   h->graphs.clear();
 }
 
+enum { K_FWD = 0, K_TDG = 1, K_BWD = 2, K_GPI = 3, K_LMS = 4, K_NKIND = 5 };
+
+hipEvent_t prof_event(sfx_handle* h) {
+  if (!h->prof_pool.empty()) {
+    hipEvent_t e = h->prof_pool.back();
+    h->prof_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// Launch a kernel; when instrumentation is on, the dispatch packet itself records start and
+// stop timestamps into an event pair (hipExtLaunchKernelGGL: the timestamps rocprofv3 reads).
+template <typename... KArgs, typename... Args>
+void launch(sfx_handle* h, int kind, double bytes, void (*kern)(KArgs...), dim3 grid, dim3 block, Args... args) {
+  if (!h->prof) {
+    hipLaunchKernelGGL(kern, grid, block, 0, h->stream, args...);
+    return;
+  }
+  hipEvent_t a = prof_event(h), b = prof_event(h);
+  hipExtLaunchKernelGGL(kern, grid, block, 0, h->stream, a, b, 0, args...);
+  h->prof_recs.push_back({kind, bytes, a, b});
+}
+
 // Capture `body` (which launches on h->stream) into a graph keyed by `key`, then replay.
 template <class F>
 int run_graph(sfx_handle* h, const GraphKey& key, F body) {
-  if (!h->use_graphs) return body();
+  if (!h->use_graphs || h->prof) return body();
   auto it = h->graphs.find(key);
   if (it == h->graphs.end()) {
     hipStream_t saved = h->stream;
@@ -162,12 +198,10 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     F.xOff = l == 0 ? -1 : h->actOff[l - 1];
     F.yOff = h->actOff[l];
     const dim3 grid(cdiv(L.N, 16), ninst, cdiv(M, 32));
+    const double by = 4.0 * ninst * ((double)L.N * L.K + L.N + (double)M * L.K + (double)M * L.N);
     // the vector path needs K % 64 == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
     const bool vec = (L.K % 64) == 0 && (l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0));
-    if (vec)
-      hipLaunchKernelGGL(k_fwd<true>, grid, dim3(256), 0, h->stream, h->G, F);
-    else
-      hipLaunchKernelGGL(k_fwd<false>, grid, dim3(256), 0, h->stream, h->G, F);
+    launch(h, K_FWD, by, vec ? k_fwd<true> : k_fwd<false>, grid, dim3(256), h->G, F);
   }
   LAUNCHCHK();
   return SFX_OK;
@@ -184,7 +218,9 @@ int run_tdg(sfx_handle* h, int pol0, int npol, int M, int use_gpi, const int64_t
   A.phi = phi;
   A.gamma = gamma;
   A.next = next;
-  hipLaunchKernelGGL(k_tdg, dim3(M, npol), dim3(256), 0, h->stream, h->G, A);
+  const double nt = use_gpi ? h->T : 1;
+  launch(h, K_TDG, 4.0 * npol * M * (nt * h->O + 2.0 * h->O + 2.0 * h->d + 4), k_tdg, dim3(M, npol), dim3(256),
+         h->G, A);
   LAUNCHCHK();
   return SFX_OK;
 }
@@ -215,7 +251,18 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     r.dzIn = l == 0 ? 0 : h->actOff[l - 1];
     return r;
   };
+  // algorithmic bytes: dX reads W, dZ, X and writes dZ_{l-1}; dW reads dZ, X and does Adam's
+  // read p,m,v + write p,m,v (24 B per parameter)
+  auto dx_bytes = [&](int l) {
+    const LayerGeo& L = h->L[l];
+    return 4.0 * ((double)L.N * L.K + (double)M * L.N + 2.0 * M * L.K);
+  };
+  auto dw_bytes = [&](int l) {
+    const LayerGeo& L = h->L[l];
+    return 24.0 * ((double)L.N * L.K + L.N) + 4.0 * ((double)M * L.N + (double)M * L.K);
+  };
   for (int l = h->NL - 1; l >= 1; --l) {
+    const double by = nhead * (dx_bytes(l) + (l + 1 <= h->NL - 1 ? dw_bytes(l + 1) : 0.0));
     A.ra = geo(l);
     A.na = cdiv(M, 32) * cdiv(h->L[l].K, 16);
     if (l + 1 <= h->NL - 1) {
@@ -226,7 +273,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     }
     A.nc = 0;
     A.tail = l == h->NL - 1 ? 1 : 0;  // loss / w / step in the first launch
-    hipLaunchKernelGGL(k_bwd, dim3(A.na + A.nb + A.nc + A.tail, nhead), dim3(256), 0, h->stream, h->G, A);
+    launch(h, K_BWD, by, k_bwd, dim3(A.na + A.nb + A.nc + A.tail, nhead), dim3(256), h->G, A);
   }
   A.na = 0;
   A.rb = geo(1);
@@ -234,7 +281,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.rc = geo(0);
   A.nc = dw_tiles(0);
   A.tail = 0;
-  hipLaunchKernelGGL(k_bwd, dim3(A.nb + A.nc, nhead), dim3(256), 0, h->stream, h->G, A);
+  launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), k_bwd, dim3(A.nb + A.nc, nhead), dim3(256), h->G, A);
   LAUNCHCHK();
   return SFX_OK;
 }
@@ -253,7 +300,8 @@ int run_gpi(sfx_handle* h, int role, int M, int row0, const float* w, float* psi
   A.task_out = task;
   A.next_out = next;
   A.sel_out = sel;
-  hipLaunchKernelGGL(k_gpi, dim3(M), dim3(256), 0, h->stream, h->G, A);
+  launch(h, K_GPI, 4.0 * M * ((double)h->T * h->O * (psi ? 2 : 1) + h->d + (q ? h->T * h->A : 0)), k_gpi, dim3(M),
+         dim3(256), h->G, A);
   LAUNCHCHK();
   return SFX_OK;
 }
@@ -298,6 +346,11 @@ bool valid_head(const sfx_handle* h, int t) { return h && t >= 0 && t < h->T; }
 
 void free_all(sfx_handle* h) {
   clear_graphs(h);
+  for (auto& r : h->prof_recs) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  for (hipEvent_t e : h->prof_pool) (void)hipEventDestroy(e);
   for (void* p : {(void*)h->online, (void*)h->target, (void*)h->am, (void*)h->av, (void*)h->w, (void*)h->wm,
                   (void*)h->wv, (void*)h->step, (void*)h->act, (void*)h->dz, (void*)h->rowloss})
     if (p) (void)hipFree(p);
@@ -589,7 +642,8 @@ int sfx_update_all(sfx_t h, const float* S, const int64_t* a, const float* phi, 
 
 int sfx_lms(sfx_t h, int t, const float* phi, const float* r, float alpha) {
   if (!valid_head(h, t) || !phi || !r) SFX_FAIL(SFX_E_ARG, "bad args");
-  hipLaunchKernelGGL(k_lms, dim3(1), dim3(256), 0, h->stream, h->w + (size_t)t * h->dpad, phi, r, alpha, h->d);
+  launch(h, K_LMS, 4.0 * (3.0 * h->d + 1), k_lms, dim3(1), dim3(256), h->w + (size_t)t * h->dpad, phi, r, alpha,
+         h->d);
   LAUNCHCHK();
   return SFX_OK;
 }
@@ -615,6 +669,42 @@ int sfx_set_since_target(sfx_t h, int t, int count) {
 int sfx_sync_target(sfx_t h, int t) {
   if (!valid_head(h, t)) SFX_FAIL(SFX_E_ARG, "bad head");
   HIPCHK(hipMemcpyAsync(h->params(1, t), h->params(0, t), sizeof(float) * h->P, hipMemcpyDeviceToDevice, h->stream));
+  return SFX_OK;
+}
+
+int sfx_prof_enable(sfx_t h, int enable) {
+  if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
+  h->prof = enable != 0;
+  return SFX_OK;
+}
+
+int sfx_prof_collect(sfx_t h, int kind, int* count, double* total_us, double* bytes) {
+  if (!h || kind < 0 || kind >= K_NKIND) SFX_FAIL(SFX_E_ARG, "bad args");
+  HIPCHK(hipStreamSynchronize(h->stream));
+  int n = 0;
+  double us = 0.0, by = 0.0;
+  for (auto& r : h->prof_recs) {
+    if (r.kind != kind) continue;
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, r.a, r.b));
+    ++n;
+    us += 1000.0 * ms;
+    by += r.bytes;
+  }
+  if (count) *count = n;
+  if (total_us) *total_us = us;
+  if (bytes) *bytes = by;
+  return SFX_OK;
+}
+
+int sfx_prof_reset(sfx_t h) {
+  if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (auto& r : h->prof_recs) {
+    h->prof_pool.push_back(r.a);
+    h->prof_pool.push_back(r.b);
+  }
+  h->prof_recs.clear();
   return SFX_OK;
 }
 

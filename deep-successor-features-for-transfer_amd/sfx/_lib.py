@@ -42,6 +42,9 @@ SIGNATURES = {
     "sfx_get_since_target": (_I, [_VP, _I, _IP]),
     "sfx_set_since_target": (_I, [_VP, _I, _I]),
     "sfx_sync_target": (_I, [_VP, _I]),
+    "sfx_prof_enable": (_I, [_VP, _I]),
+    "sfx_prof_collect": (_I, [_VP, _I, _IP, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "sfx_prof_reset": (_I, [_VP]),
     "sfx_synchronize": (_I, [_VP]),
 }
 

@@ -134,6 +134,23 @@ class SFEngine:
     def sync_target(self, t: int):
         check(lib.sfx_sync_target(self._h, t), "sfx_sync_target")
 
+    KINDS = {"fwd": 0, "tdg": 1, "bwd": 2, "gpi": 3, "lms": 4}
+
+    def prof_enable(self, on: bool):
+        check(lib.sfx_prof_enable(self._h, int(bool(on))), "sfx_prof_enable")
+
+    def prof_reset(self):
+        check(lib.sfx_prof_reset(self._h), "sfx_prof_reset")
+
+    def prof_collect(self):
+        """{kind: (launches, total_us, algorithmic_bytes)} of the instrumented launches."""
+        out = {}
+        for name, k in self.KINDS.items():
+            n, us, by = C.c_int(), C.c_double(), C.c_double()
+            check(lib.sfx_prof_collect(self._h, k, C.byref(n), C.byref(us), C.byref(by)), "sfx_prof_collect")
+            out[name] = (n.value, us.value, by.value)
+        return out
+
     def synchronize(self):
         check(lib.sfx_synchronize(self._h), "sfx_synchronize")
 

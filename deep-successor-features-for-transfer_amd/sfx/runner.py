@@ -1,0 +1,185 @@
+"""Host-side env-step loop of SF-DQN driving the libsfx engine.
+
+Mirrors Agent.next_sample (agents/agent.py:195-261) + SFDQN.train_agent for the two
+schedules the reference has:
+
+  * "all":    agents/sfdqn.py:47-60 over features/deep.py (main_sfdqn_torch.py):
+              LMS reward fit on the active task, every head updated per env step, GPI next
+              actions, loss = l1.
+  * "active": sfdqn.py:462-471 / agents/sfdqn_sequential.py:63-76: only the active head is
+              updated (with l2 + Adam-trained w), next actions by GPI or own ψ (use_gpi).
+
+The environment is a synthetic Reacher-shape task: s ~ N(0,1)^n_s,
+φ ~ U[0,1)^d, r = φ·w_true with one-hot w_true (tasks/reacher.py:85-88), γ constant,
+episodes of T_ep steps.  Replay is a host ring (agents/buffer.py:34-82) sampled uniformly;
+each step's device inputs (the minibatch, the new transition's φ/r, the next state) travel
+in ONE pinned host->device copy.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .engine import SFEngine
+
+
+class SynthReacher:
+    """Synthetic Reacher-shape task (never terminates, like tasks/reacher.py:112)."""
+
+    def __init__(self, n_s: int, A: int, d: int, task_index: int, rng: np.random.Generator):
+        self.n_s, self.A, self.d, self.task_index, self.rng = n_s, A, d, task_index, rng
+        self.w_true = np.zeros(d, dtype=np.float32)
+        self.w_true[task_index % d] = 1.0
+
+    def initialize(self) -> np.ndarray:
+        return self.rng.standard_normal(self.n_s, dtype=np.float32)
+
+    def transition(self, a: int):
+        s1 = self.rng.standard_normal(self.n_s, dtype=np.float32)
+        phi = self.rng.random(self.d, dtype=np.float32)
+        r = float(phi @ self.w_true)
+        return s1, phi, r, False
+
+
+class Staging:
+    """One pinned host buffer + one device buffer with typed views at fixed offsets."""
+
+    def __init__(self, fields, device):
+        self.offsets, off = {}, 0
+        for name, shape, dtype in fields:
+            n = int(np.prod(shape)) * torch.empty((), dtype=dtype).element_size()
+            self.offsets[name] = (off, shape, dtype)
+            off += (n + 15) // 16 * 16
+        self.nbytes = off
+        self.host = torch.empty(off, dtype=torch.uint8, pin_memory=True)
+        self.dev = torch.empty(off, dtype=torch.uint8, device=device)
+        self.h = {k: self._view(self.host, k).numpy() for k in self.offsets}
+        self.d = {k: self._view(self.dev, k) for k in self.offsets}
+
+    def _view(self, buf, name):
+        off, shape, dtype = self.offsets[name]
+        n = int(np.prod(shape)) * torch.empty((), dtype=dtype).element_size()
+        return buf[off:off + n].view(dtype).view(*shape)
+
+    def upload(self):
+        self.dev.copy_(self.host, non_blocking=True)
+
+
+class Replay:
+    """Uniform replay ring (agents/buffer.py:34-82) with arrays instead of object tuples."""
+
+    def __init__(self, capacity: int, n_s: int, d: int, rng: np.random.Generator):
+        self.cap, self.rng = capacity, rng
+        self.s = np.zeros((capacity, n_s), np.float32)
+        self.s1 = np.zeros((capacity, n_s), np.float32)
+        self.phi = np.zeros((capacity, d), np.float32)
+        self.r = np.zeros(capacity, np.float32)
+        self.a = np.zeros(capacity, np.int64)
+        self.gamma = np.zeros(capacity, np.float32)
+        self.index = 0
+        self.size = 0
+
+    def append(self, s, a, r, phi, s1, gamma):
+        i = self.index
+        self.s[i], self.a[i], self.r[i], self.phi[i], self.s1[i], self.gamma[i] = s, a, r, phi, s1, gamma
+        self.size = min(self.size + 1, self.cap)
+        self.index = (i + 1) % self.cap
+
+    def sample_into(self, st: Staging, B: int) -> bool:
+        if self.size < B:
+            return False
+        idx = self.rng.integers(0, self.size, B)
+        np.take(self.s, idx, axis=0, out=st.h["s"])
+        np.take(self.s1, idx, axis=0, out=st.h["s1"])
+        np.take(self.phi, idx, axis=0, out=st.h["phi"])
+        np.take(self.r, idx, out=st.h["r"])
+        np.take(self.a, idx, out=st.h["a"])
+        np.take(self.gamma, idx, out=st.h["gamma"])
+        return True
+
+
+class EnvLoop:
+    """The training env-step loop of one active task over an SFEngine of T heads."""
+
+    def __init__(self, engine: SFEngine, schedule: str = "all", batch: int = 32, capacity: int = 1_000_000,
+                 gamma: float = 0.9, epsilon: float = 0.1, alpha_w: float = 1e-3, episode_len: int = 500,
+                 use_gpi: bool = True, seed: int = 1):
+        assert schedule in ("all", "active")
+        self.eng, self.schedule, self.B = engine, schedule, batch
+        self.gamma, self.epsilon, self.alpha_w, self.T_ep, self.use_gpi = gamma, epsilon, alpha_w, episode_len, use_gpi
+        e = engine
+        self.rng = np.random.default_rng(seed)
+        self.tasks = [SynthReacher(e.n_s, e.A, e.d, t, self.rng) for t in range(e.T)]
+        self.replay = Replay(capacity, e.n_s, e.d, self.rng)
+        self.st = Staging([("s", (batch, e.n_s), torch.float32), ("s1", (batch, e.n_s), torch.float32),
+                           ("phi", (batch, e.d), torch.float32), ("r", (batch,), torch.float32),
+                           ("a", (batch,), torch.int64), ("gamma", (batch,), torch.float32),
+                           ("snext", (1, e.n_s), torch.float32), ("phi1", (e.d,), torch.float32),
+                           ("r1", (1,), torch.float32)], e.device)
+        self.losses = torch.zeros(max(e.T, 1), 3, device=e.device)
+        self.sel_host = torch.zeros(2, dtype=torch.long, pin_memory=True)
+        self.gpi_counters = np.zeros((e.T, e.T), dtype=np.int64)
+        self.set_task(0)
+
+    def set_task(self, index: int):
+        """Agent.set_active_training_task (agents/agent.py:121-139)."""
+        self.task_index = index
+        self.task = self.tasks[index]
+        self.steps_in_episode = 0
+        self.s = self.task.initialize()
+        self.st.h["snext"][0] = self.s
+        self.st.upload()
+        self._issue_select()
+
+    def prefill(self, n: int):
+        """Random transitions into the replay (warm-up only; not an env step)."""
+        for _ in range(n):
+            s = self.task.initialize()
+            a = int(self.rng.integers(self.eng.A))
+            s1, phi, r, _ = self.task.transition(a)
+            self.replay.append(s, a, r, phi, s1, self.gamma)
+
+    def _issue_select(self):
+        e = self.eng
+        sel = e.select_action(self.st.d["snext"], self.task_index, self.use_gpi)
+        self.sel_host.copy_(sel, non_blocking=True)
+        self.sel_event = torch.cuda.Event()
+        self.sel_event.record()
+
+    def step(self):
+        """One env step: GPI action (already in flight), ε-greedy, transition, train."""
+        self.sel_event.synchronize()
+        c, a_greedy = int(self.sel_host[0]), int(self.sel_host[1])
+        self.gpi_counters[self.task_index, c] += 1
+        if self.rng.random() <= self.epsilon:
+            a = int(self.rng.integers(self.eng.A))
+        else:
+            a = a_greedy
+        s1, phi, r, terminal = self.task.transition(a)
+        g = 0.0 if terminal else self.gamma
+        st = self.st
+        self.replay.append(self.s, a, r, phi, s1, g)
+        have = self.replay.sample_into(st, self.B)
+        self.steps_in_episode += 1
+        s_next = s1
+        if terminal or self.steps_in_episode >= self.T_ep:  # new episode (agent.py:211-220, 248-249)
+            s_next = self.task.initialize()
+            self.steps_in_episode = 0
+        st.h["phi1"][:] = phi
+        st.h["r1"][0] = r
+        st.h["snext"][0] = s_next
+        st.upload()
+        d, e = st.d, self.eng
+        if self.schedule == "all":
+            e.lms(self.task_index, d["phi1"], d["r1"], self.alpha_w)
+            if have:
+                e.update_all(d["s"], d["a"], d["phi"], d["s1"], d["gamma"], losses=self.losses)
+        elif have:
+            e.update(self.task_index, d["s"], d["a"], d["r"], d["phi"], d["s1"], d["gamma"], self.use_gpi,
+                     losses=self.losses[0])
+        self.s = s_next
+        self._issue_select()
+
+    def run(self, n: int):
+        for _ in range(n):
+            self.step()

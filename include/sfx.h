@@ -136,6 +136,22 @@ int sfx_get_since_target(sfx_t h, int t, int* count);
 int sfx_set_since_target(sfx_t h, int t, int count);
 int sfx_sync_target(sfx_t h, int t);
 
+/*
+ * Event instrumentation for the benchmark's roofline figure: while enabled, graphs are
+ * bypassed and every kernel launch is bracketed by a hipEvent pair.  Kinds:
+ * 0 forward, 1 TD target, 2 backward+Adam, 3 GPI, 4 LMS.  collect() returns the number of
+ * launches of that kind, their summed event-measured duration (us) and their summed
+ * ALGORITHMIC bytes (what the launch must read/write at minimum, fp32).
+ */
+#define SFX_K_FWD 0
+#define SFX_K_TDG 1
+#define SFX_K_BWD 2
+#define SFX_K_GPI 3
+#define SFX_K_LMS 4
+int sfx_prof_enable(sfx_t h, int enable);
+int sfx_prof_collect(sfx_t h, int kind, int* count, double* total_us, double* bytes);
+int sfx_prof_reset(sfx_t h);
+
 /* Block the host until all work queued on the handle's stream is done. */
 int sfx_synchronize(sfx_t h);
 
