@@ -33,7 +33,7 @@ import torch  # noqa: E402
 METRIC = "env steps/sec (whole node), Reacher 8-task SF-DQN at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SHAPE = dict(n_s=17, H=256, A=7, d=8, acts=("relu", "relu"))
-KIND_NAMES = {"fwd": "k_fwd", "tdg": "k_tdg", "bwd": "k_bwd", "gpi": "k_gpi", "lms": "k_lms"}
+KIND_NAMES = {"fwd": "k_fwd", "tdg": "k_tdg", "bwd": "k_bwd", "gpi": "k_gpi", "lms": "k_lms", "ver": "k_ver"}
 
 
 def parse():
@@ -183,6 +183,7 @@ def main():
                     "bytes_per_launch": round(bpl), "avg_launch_us": round(avg_us, 3),
                     "share_of_gpu_time": round(us / max(sum(v[1] for v in stats.values()), 1e-9), 3),
                     "per_kind_avg_us": {KIND_NAMES[k]: round(v[1] / max(v[0], 1), 3) for k, v in stats.items() if v[0]}}
+        spec_stats = eng.step_stats()
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, args.cpu_seconds)
@@ -195,6 +196,7 @@ def main():
                        "heads_per_gpu": T, "global_batch": B * world, "parallelism": f"replica{world}" if world > 1 else "single",
                        "loop": "python host loop over libsfx graphs"},
             "roofline": roofline,
+            "speculation": spec_stats,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -1,15 +1,17 @@
 // sfx.hip -- libsfx.so: C ABI (include/sfx.h) + launch orchestration for gfx950.
 //
 // Device state of one handle (T local ψ heads), all fp32:
-//   online/target/adam_m/adam_v : [T][P]      packed heads, every tensor 16-B aligned
-//   w, wm, wv                   : [T][dpad]   reward weights and their Adam moments
-//   step                        : [T]         Adam step per head (device-resident)
-//   act                         : [role][T][actSize]   per-layer outputs, rows = max_batch
-//   dz                          : [T][actSize]         per-layer output gradients
-//   rowloss                     : [T][MMAX]            per-row TD loss of the last update
+//   online/adam_m/adam_v : [2][T][P]  packed heads, double-buffered (slot per head in `mask`)
+//   target               : [T][P]
+//   w, wm, wv            : [T][dpad]  reward weights and their Adam moments
+//   step                 : [T]        Adam step per head (device-resident)
+//   act                  : [role][T][actSize]   per-layer outputs, rows = max_batch + 1
+//   dz                   : [T][actSize]         per-layer output gradients
+//   rowloss              : [T][MMAX]            per-row TD loss of the last update
+//   spec_next            : [T][MMAX]            speculated next actions of the all-task step
 // Kernels take the whole geometry by value (sfx::Geo) and derive every pointer from it.
 // Each entry point's launch sequence is captured once into a hipGraph (keyed by its
-// arguments) and replayed afterwards; SFX_GRAPHS=0 disables graphs.
+// arguments, including the slot mask) and replayed afterwards; SFX_GRAPHS=0 disables graphs.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -64,9 +66,17 @@ inline int align4(int x) { return (x + 3) & ~3; }
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 struct GraphKey {
-  int op, a0, a1, a2;
-  const void* p[8];
+  int op, a0, a1, a2, a3, a4, a5, a6;
+  unsigned long long mask;
+  const void* p[12];
   bool operator<(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) < 0; }
+};
+
+// what the host reads back after a fused step: GPI task, greedy action, first re-run policy
+struct StepOut {
+  int64_t sel[2];
+  int flag;
+  int pad;
 };
 
 }  // namespace
@@ -83,9 +93,10 @@ struct sfx_handle {
   AdamHP hp_w{1e-3, 0.0, 0.9, 0.999, 1e-8};
   int target_update_ev = 1000;
   std::vector<int> since_target, host_step;
+  unsigned long long mask = 0;  // bit t: current slot of head t
   std::map<GraphKey, hipGraphExec_t> graphs;
   Geo G{};
-  // event instrumentation (bench roofline): one (start, stop) pair per launch, eager only
+  // event instrumentation (bench roofline): packet timestamps per launch, eager only
   bool prof = false;
   struct ProfRec {
     int kind;
@@ -94,13 +105,33 @@ struct sfx_handle {
   };
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> prof_pool;
+  // pending fused step (sfx_step_all -> sfx_step_finish)
+  struct Pending {
+    bool active = false, update = false, sel = false;
+    int B = 0, use_gpi = 1, task = 0, sel_use_gpi = 1;
+    const float *S = nullptr, *S1 = nullptr, *phi = nullptr, *gamma = nullptr, *s_next = nullptr;
+    const int64_t* a = nullptr;
+    float* losses = nullptr;
+  } pend;
+  // step statistics
+  long long steps_spec = 0, steps_fallback = 0, policies_rerun = 0, rounds_total = 0;
+  int force_rerun_from = -1;  // test hook: treat the speculation as failed from this policy on
+  int spec_rounds = 2;        // speculative rounds launched on the device per fused step
 
   float *online = nullptr, *target = nullptr, *am = nullptr, *av = nullptr;
   float *w = nullptr, *wm = nullptr, *wv = nullptr;
   int* step = nullptr;
   float *act = nullptr, *dz = nullptr, *rowloss = nullptr;
+  int64_t* spec_next = nullptr;
+  StepOut* dout = nullptr;  // device
+  StepOut* hout = nullptr;  // pinned host
 
-  float* params(int which, int head) const { return (which ? target : online) + (size_t)head * P; }
+  int slot(int head) const { return (int)((mask >> head) & 1ull); }
+  unsigned long long all_bits() const { return T >= 64 ? ~0ull : ((1ull << T) - 1ull); }
+  float* online_cur(int head) const { return online + ((size_t)slot(head) * T + head) * P; }
+  float* am_cur(int head) const { return am + ((size_t)slot(head) * T + head) * P; }
+  float* av_cur(int head) const { return av + ((size_t)slot(head) * T + head) * P; }
+  float* target_of(int head) const { return target + (size_t)head * P; }
 };
 
 namespace {
@@ -110,7 +141,7 @@ void clear_graphs(sfx_handle* h) {
   h->graphs.clear();
 }
 
-enum { K_FWD = 0, K_TDG = 1, K_BWD = 2, K_GPI = 3, K_LMS = 4, K_NKIND = 5 };
+enum { K_FWD = 0, K_TDG = 1, K_BWD = 2, K_GPI = 3, K_LMS = 4, K_VER = 5, K_NKIND = 6 };
 
 hipEvent_t prof_event(sfx_handle* h) {
   if (!h->prof_pool.empty()) {
@@ -165,30 +196,45 @@ int run_graph(sfx_handle* h, const GraphKey& key, F body) {
   return SFX_OK;
 }
 
-GraphKey make_key(int op, int a0, int a1, int a2, std::initializer_list<const void*> ptrs) {
+GraphKey make_key(int op, std::initializer_list<int> ints, unsigned long long mask,
+                  std::initializer_list<const void*> ptrs) {
   GraphKey k;
   std::memset(&k, 0, sizeof(k));
   k.op = op;
-  k.a0 = a0;
-  k.a1 = a1;
-  k.a2 = a2;
+  int* dst[7] = {&k.a0, &k.a1, &k.a2, &k.a3, &k.a4, &k.a5, &k.a6};
   int i = 0;
+  for (int v : ints) *dst[i++] = v;
+  k.mask = mask;
+  i = 0;
   for (const void* p : ptrs) k.p[i++] = p;
   return k;
 }
 
-int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const float* xa, const float* xb) {
+struct FwdExtra {
+  int l0 = 0;            // first layer to run
+  int lms_head = -1;     // LMS in block 0 of layer 0
+  const float* lms_phi = nullptr;
+  const float* lms_r = nullptr;
+  float lms_alpha = 0.f;
+  int* flag = nullptr;   // reset to flag_value in block 0 of the first layer
+  int flag_value = 0;
+};
+
+int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const float* xa, const float* xb,
+            const FwdExtra& ex = FwdExtra()) {
   FwdArgs F{};
   F.M = M;
   F.xa = xa;
   F.xb = xb;
+  F.mask = h->mask;
+  F.lms_head = -1;
   int ninst = 0;
   FwdGroup* slots[4] = {&F.g0, &F.g1, &F.g2, &F.g3};
   for (const FwdGroup& g : groups) {
     *slots[F.ngroups++] = g;
     ninst += g.n;
   }
-  for (int l = 0; l < h->NL; ++l) {
+  for (int l = ex.l0; l < h->NL; ++l) {
     const LayerGeo& L = h->L[l];
     F.N = L.N;
     F.K = L.K;
@@ -197,6 +243,13 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     F.bOff = L.bOff;
     F.xOff = l == 0 ? -1 : h->actOff[l - 1];
     F.yOff = h->actOff[l];
+    const bool first = l == ex.l0;
+    F.lms_head = first ? ex.lms_head : -1;
+    F.lms_phi = ex.lms_phi;
+    F.lms_r = ex.lms_r;
+    F.lms_alpha = ex.lms_alpha;
+    F.flag = first ? ex.flag : nullptr;
+    F.flag_value = ex.flag_value;
     const dim3 grid(cdiv(L.N, 16), ninst, cdiv(M, 32));
     const double by = 4.0 * ninst * ((double)L.N * L.K + L.N + (double)M * L.K + (double)M * L.N);
     // the vector path needs K % 64 == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
@@ -207,13 +260,17 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
   return SFX_OK;
 }
 
-int run_tdg(sfx_handle* h, int pol0, int npol, int M, int use_gpi, const int64_t* a, const float* phi,
-            const float* gamma, int64_t* next) {
+int run_tdg(sfx_handle* h, int pol0, int npol, int guess, int M, int use_gpi, const int64_t* a, const float* phi,
+            const float* gamma, int64_t* next, int next_stride, int* flag = nullptr) {
   TdgArgs A{};
   A.M = M;
   A.use_gpi = use_gpi;
   A.pol0 = pol0;
   A.npol = npol;
+  A.guess = guess;
+  A.flag = flag;
+  A.flag_value = h->T;
+  A.next_stride = next_stride;
   A.a = a;
   A.phi = phi;
   A.gamma = gamma;
@@ -225,11 +282,22 @@ int run_tdg(sfx_handle* h, int pol0, int npol, int M, int use_gpi, const int64_t
   return SFX_OK;
 }
 
+struct BwdExtra {
+  int inc_step = 1;
+  bool fuse_v0 = false;  // post-update forward of layer 0 into vRole (rows S1 ++ s_next)
+  int vRole = R_V;
+  const float* v_x = nullptr;
+  const float* v_xn = nullptr;
+};
+
+bool can_fuse_v0(const sfx_handle* h) { return h->L[0].K <= KFUSE; }
+
 int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const float* phi, const float* r,
-            float* losses) {
+            float* losses, const BwdExtra& ex = BwdExtra()) {
   BwdArgs A{};
   A.M = M;
   A.head0 = head0;
+  A.mask = h->mask;
   A.hp = h->hp_psi;
   A.hpw = h->hp_w;
   A.x0 = x0;
@@ -237,6 +305,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.r = r;
   A.train_w = r != nullptr;
   A.losses = losses;
+  A.inc_step = ex.inc_step;
   auto dw_tiles = [&](int l) { return cdiv(h->L[l].N, 32) * cdiv(h->L[l].K, 64); };
   auto geo = [&](int l) {
     const LayerGeo& L = h->L[l];
@@ -281,17 +350,25 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.rc = geo(0);
   A.nc = dw_tiles(0);
   A.tail = 0;
+  A.fuse_v0 = ex.fuse_v0 ? 1 : 0;
+  A.vM = M + (ex.v_xn ? 1 : 0);
+  A.vOff = h->actOff[0];
+  A.vRole = ex.vRole;
+  A.act0 = h->L[0].actOut;
+  A.v_x = ex.v_x;
+  A.v_xn = ex.v_xn;
   launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), k_bwd, dim3(A.nb + A.nc, nhead), dim3(256), h->G, A);
   LAUNCHCHK();
   return SFX_OK;
 }
 
-int run_gpi(sfx_handle* h, int role, int M, int row0, const float* w, float* psi, float* q, int64_t* task,
-            int64_t* next, int64_t* sel, int select_task, int use_gpi) {
+GpiArgs gpi_args(int role, int rowoff, int row0, const float* w, float* psi, float* q, int64_t* task, int64_t* next,
+                 int64_t* sel, int select_task, int use_gpi, int M) {
   GpiArgs A{};
   A.M = M;
   A.role = role;
   A.row0 = row0;
+  A.rowoff = rowoff;
   A.select_task = select_task;
   A.use_gpi = use_gpi;
   A.w = w;
@@ -300,8 +377,28 @@ int run_gpi(sfx_handle* h, int role, int M, int row0, const float* w, float* psi
   A.task_out = task;
   A.next_out = next;
   A.sel_out = sel;
-  launch(h, K_GPI, 4.0 * M * ((double)h->T * h->O * (psi ? 2 : 1) + h->d + (q ? h->T * h->A : 0)), k_gpi, dim3(M),
-         dim3(256), h->G, A);
+  return A;
+}
+
+int run_gpi(sfx_handle* h, const GpiArgs& A) {
+  launch(h, K_GPI, 4.0 * A.M * ((double)h->T * h->O * (A.psi_out ? 2 : 1) + h->d + (A.q_out ? h->T * h->A : 0)),
+         k_gpi, dim3(A.M), dim3(256), h->G, A);
+  LAUNCHCHK();
+  return SFX_OK;
+}
+
+int run_ver(sfx_handle* h, int M, int npol, bool sel, int post, const GpiArgs& g) {
+  VerArgs V{};
+  V.M = M;
+  V.post = post;
+  V.npol = npol;
+  V.sel = sel ? 1 : 0;
+  V.spec_stride = MMAX;
+  V.spec_next = h->spec_next;
+  V.flag = &h->dout->flag;
+  V.g = g;
+  launch(h, K_VER, 4.0 * (double)M * npol * h->T * h->O + 4.0 * h->T * h->O, k_ver, dim3(npol + 1), dim3(256),
+         h->G, V);
   LAUNCHCHK();
   return SFX_OK;
 }
@@ -313,7 +410,7 @@ void after_update(sfx_handle* h, int t) {
 
 int maybe_sync_target(sfx_handle* h, int t) {
   if (h->since_target[t] >= h->target_update_ev) {
-    HIPCHK(hipMemcpyAsync(h->params(1, t), h->params(0, t), sizeof(float) * h->P, hipMemcpyDeviceToDevice,
+    HIPCHK(hipMemcpyAsync(h->target_of(t), h->online_cur(t), sizeof(float) * h->P, hipMemcpyDeviceToDevice,
                           h->stream));
     h->since_target[t] = 0;
   }
@@ -352,26 +449,91 @@ void free_all(sfx_handle* h) {
   }
   for (hipEvent_t e : h->prof_pool) (void)hipEventDestroy(e);
   for (void* p : {(void*)h->online, (void*)h->target, (void*)h->am, (void*)h->av, (void*)h->w, (void*)h->wm,
-                  (void*)h->wv, (void*)h->step, (void*)h->act, (void*)h->dz, (void*)h->rowloss})
+                  (void*)h->wv, (void*)h->step, (void*)h->act, (void*)h->dz, (void*)h->rowloss, (void*)h->spec_next,
+                  (void*)h->dout})
     if (p) (void)hipFree(p);
+  if (h->hout) (void)hipHostFree(h->hout);
   if (h->cap) (void)hipStreamDestroy(h->cap);
+}
+
+inline int round_role(int r) { return (r & 1) ? R_V2 : R_V; }
+
+// One speculative round r of the all-task update: every policy takes its GPI next actions
+// with heads t < i seen through role `guess` (round 0: the pre-step heads), every head
+// updates from its read slot into its write slot, the post-update forward of S1 (++ s_next)
+// lands in round_role(r), and k_ver flags the first policy whose actions were wrong.
+int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r) {
+  const int T = h->T, B = p.B;
+  const int guess = r == 0 ? R_S1 : round_role(r - 1), out = round_role(r);
+  const float* wsel = h->w + (size_t)p.task * h->dpad;
+  RC(run_tdg(h, 0, T, guess, B, p.use_gpi, p.a, p.phi, p.gamma, h->spec_next, MMAX, &h->dout->flag));
+  BwdExtra bx;
+  bx.inc_step = r == 0 ? 1 : 0;  // later rounds redo the same optimizer step
+  bx.fuse_v0 = can_fuse_v0(h);
+  bx.vRole = out;
+  bx.v_x = p.S1;
+  bx.v_xn = p.sel ? p.s_next : nullptr;
+  RC(run_bwd(h, 0, T, B, p.S, p.phi, nullptr, p.losses, bx));
+  const int vM = B + (p.sel ? 1 : 0);
+  if (bx.fuse_v0) {
+    FwdExtra vx;
+    vx.l0 = 1;
+    RC(run_fwd(h, {{out, P_NEW, 0, 0, T}}, vM, nullptr, nullptr, vx));
+  } else {
+    RC(run_fwd(h, {{out, P_NEW, 2, 0, T}}, B, p.S1, p.S1));
+  }
+  const bool sel = p.sel && bx.fuse_v0;
+  const bool verify = p.use_gpi != 0;
+  if (verify || sel)
+    RC(run_ver(h, B, verify ? T : 1, sel, out,
+               gpi_args(out, B, 0, wsel, nullptr, nullptr, nullptr, nullptr, h->dout->sel, p.task, p.sel_use_gpi, 1)));
+  if (p.sel && !bx.fuse_v0) {  // selection through the plain forward path
+    RC(run_fwd(h, {{R_A, P_NEW, 1, 0, T}}, 1, p.s_next, nullptr));
+    RC(run_gpi(h, gpi_args(R_A, 0, 0, wsel, nullptr, nullptr, nullptr, nullptr, h->dout->sel, p.task, p.sel_use_gpi,
+                           1)));
+  }
+  return SFX_OK;
+}
+
+// The fused step: LMS + forward of the minibatch, then `rounds` speculative rounds (or just
+// LMS + action selection when there is no minibatch yet).
+int launch_step_all(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, const float* lms_phi, const float* lms_r,
+                    float lms_alpha, int rounds) {
+  const int T = h->T, B = p.B;
+  FwdExtra ex;
+  ex.lms_head = lms_task;
+  ex.lms_phi = lms_phi;
+  ex.lms_r = lms_r;
+  ex.lms_alpha = lms_alpha;
+  ex.flag = &h->dout->flag;
+  ex.flag_value = T;
+  if (!p.update) {
+    const float* wsel = h->w + (size_t)p.task * h->dpad;
+    RC(run_fwd(h, {{R_A, P_ONLINE, 1, 0, T}}, 1, p.s_next, nullptr, ex));
+    return run_gpi(h, gpi_args(R_A, 0, 0, wsel, nullptr, nullptr, nullptr, nullptr, h->dout->sel, p.task,
+                               p.sel_use_gpi, 1));
+  }
+  RC(run_fwd(h, {{R_S, P_ONLINE, 1, 0, T}, {R_S1T, P_TARGET, 2, 0, T}, {R_S1, P_ONLINE, 2, 0, T}}, B, p.S, p.S1, ex));
+  for (int r = 0; r < rounds; ++r) RC(launch_round(h, p, r));
+  return SFX_OK;
 }
 
 }  // namespace
 
 extern "C" {
 
-const char* sfx_version(void) { return "sfx 0.2 gfx950 fp32-mfma graphs"; }
+const char* sfx_version(void) { return "sfx 0.3 gfx950 fp32-mfma graphs speculative-gpi"; }
 const char* sfx_last_error(void) { return g_err.c_str(); }
 
 int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts, int A, int d, int max_batch,
                int device, void* stream) {
   if (!out) SFX_FAIL(SFX_E_ARG, "out is null");
   *out = nullptr;
-  if (T < 1 || n_s < 1 || H < 1 || n_hidden < 0 || n_hidden + 2 > NLMAX || A < 1 || d < 1 || max_batch < 1)
-    SFX_FAIL(SFX_E_ARG, "bad geometry");
-  if (d > DMAX || max_batch > MMAX || (long)T * A > QMAX || (long)A * d > OMAX)
-    SFX_FAIL(SFX_E_ARG, "geometry exceeds kernel limits (d<=256, batch<=1024, T*A<=8192, A*d<=4096)");
+  if (T < 1 || T > 64 || n_s < 1 || H < 1 || n_hidden < 0 || n_hidden + 2 > NLMAX || A < 1 || d < 1 ||
+      max_batch < 1)
+    SFX_FAIL(SFX_E_ARG, "bad geometry (1 <= T <= 64 heads per handle)");
+  if (d > DMAX || max_batch + 1 > MMAX || (long)T * A > QMAX || (long)A * d > OMAX)
+    SFX_FAIL(SFX_E_ARG, "geometry exceeds kernel limits (d<=256, batch<1024, T*A<=8192, A*d<=4096)");
   for (int i = 0; i < n_hidden; ++i)
     if (!acts || acts[i] < ACT_NONE || acts[i] > ACT_TANH) SFX_FAIL(SFX_E_ARG, "bad activation code");
   HIPCHK(hipSetDevice(device));
@@ -413,7 +575,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   int aoff = 0;
   for (int l = 0; l < h->NL; ++l) {
     h->actOff.push_back(aoff);
-    aoff += align4(max_batch * h->L[l].N);
+    aoff += align4((max_batch + 1) * h->L[l].N);  // +1 row: the next state of the fused step
   }
   h->actSize = (aoff + 63) & ~63;
   h->since_target.assign(T, 0);
@@ -429,10 +591,10 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
       rc = SFX_E_HIP;
     }
   };
-  alloc((void**)&h->online, headBytes);
+  alloc((void**)&h->online, 2 * headBytes);
   alloc((void**)&h->target, headBytes);
-  alloc((void**)&h->am, headBytes);
-  alloc((void**)&h->av, headBytes);
+  alloc((void**)&h->am, 2 * headBytes);
+  alloc((void**)&h->av, 2 * headBytes);
   alloc((void**)&h->w, wBytes);
   alloc((void**)&h->wm, wBytes);
   alloc((void**)&h->wv, wBytes);
@@ -440,6 +602,12 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   alloc((void**)&h->act, sizeof(float) * (size_t)NROLE * T * h->actSize);
   alloc((void**)&h->dz, sizeof(float) * (size_t)T * h->actSize);
   alloc((void**)&h->rowloss, sizeof(float) * (size_t)T * MMAX);
+  alloc((void**)&h->spec_next, sizeof(int64_t) * (size_t)T * MMAX);
+  alloc((void**)&h->dout, sizeof(StepOut));
+  if (rc == SFX_OK && hipHostMalloc((void**)&h->hout, sizeof(StepOut), hipHostMallocDefault) != hipSuccess) {
+    g_err = "hipHostMalloc failed";
+    rc = SFX_E_HIP;
+  }
   if (rc == SFX_OK && hipStreamCreateWithFlags(&h->cap, hipStreamNonBlocking) != hipSuccess) {
     g_err = "hipStreamCreate failed";
     rc = SFX_E_HIP;
@@ -511,7 +679,8 @@ int sfx_load_head(sfx_t h, int t, int which, const float* params_host) {
   std::vector<float> buf(h->P);
   pack_head(h, params_host, buf.data());
   HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipMemcpyAsync(h->params(which, t), buf.data(), sizeof(float) * h->P, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(which ? h->target_of(t) : h->online_cur(t), buf.data(), sizeof(float) * h->P,
+                        hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   return SFX_OK;
 }
@@ -519,7 +688,8 @@ int sfx_load_head(sfx_t h, int t, int which, const float* params_host) {
 int sfx_get_head(sfx_t h, int t, int which, float* params_host) {
   if (!valid_head(h, t) || !params_host) SFX_FAIL(SFX_E_ARG, "bad head / pointer");
   std::vector<float> buf(h->P);
-  HIPCHK(hipMemcpyAsync(buf.data(), h->params(which, t), sizeof(float) * h->P, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(buf.data(), which ? h->target_of(t) : h->online_cur(t), sizeof(float) * h->P,
+                        hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   unpack_head(h, buf.data(), params_host);
   return SFX_OK;
@@ -531,8 +701,8 @@ int sfx_load_adam(sfx_t h, int t, const float* m_host, const float* v_host, int 
   pack_head(h, m_host, bm.data());
   pack_head(h, v_host, bv.data());
   HIPCHK(hipStreamSynchronize(h->stream));
-  HIPCHK(hipMemcpyAsync(h->am + (size_t)t * h->P, bm.data(), sizeof(float) * h->P, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipMemcpyAsync(h->av + (size_t)t * h->P, bv.data(), sizeof(float) * h->P, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->am_cur(t), bm.data(), sizeof(float) * h->P, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->av_cur(t), bv.data(), sizeof(float) * h->P, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->step + t, &step, sizeof(int), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   h->host_step[t] = step;
@@ -543,8 +713,8 @@ int sfx_get_adam(sfx_t h, int t, float* m_host, float* v_host, int* step) {
   if (!valid_head(h, t)) SFX_FAIL(SFX_E_ARG, "bad head");
   std::vector<float> bm(h->P), bv(h->P);
   int st = 0;
-  HIPCHK(hipMemcpyAsync(bm.data(), h->am + (size_t)t * h->P, sizeof(float) * h->P, hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipMemcpyAsync(bv.data(), h->av + (size_t)t * h->P, sizeof(float) * h->P, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(bm.data(), h->am_cur(t), sizeof(float) * h->P, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(bv.data(), h->av_cur(t), sizeof(float) * h->P, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipMemcpyAsync(&st, h->step + t, sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   if (m_host) unpack_head(h, bm.data(), m_host);
@@ -579,12 +749,12 @@ int sfx_w_ptr(sfx_t h, int t, float** w_dev) {
 
 int sfx_gpi(sfx_t h, const float* S, int B, const float* w, float* psi, float* q, int64_t* task, int64_t* next) {
   if (!h || !S || !w || B < 1) SFX_FAIL(SFX_E_ARG, "bad args");
-  const GraphKey key = make_key(1, B, 0, 0, {S, w, psi, q, task, next});
+  const GraphKey key = make_key(1, {B}, h->mask, {S, w, psi, q, task, next});
   return run_graph(h, key, [&]() -> int {
     for (int row0 = 0; row0 < B; row0 += h->Mmax) {
       const int m = B - row0 < h->Mmax ? B - row0 : h->Mmax;
-      RC(run_fwd(h, {{R_G, 0, 1, 0, h->T}}, m, S + (size_t)row0 * h->n_s, nullptr));
-      RC(run_gpi(h, R_G, m, row0, w, psi, q, task, next, nullptr, 0, 0));
+      RC(run_fwd(h, {{R_G, P_ONLINE, 1, 0, h->T}}, m, S + (size_t)row0 * h->n_s, nullptr));
+      RC(run_gpi(h, gpi_args(R_G, 0, row0, w, psi, q, task, next, nullptr, 0, 0, m)));
     }
     return SFX_OK;
   });
@@ -593,11 +763,11 @@ int sfx_gpi(sfx_t h, const float* S, int B, const float* w, float* psi, float* q
 int sfx_select_action(sfx_t h, const float* s, int task_index, int use_gpi, float* q, int64_t* out) {
   if (!h || !s || !out || task_index < 0 || task_index >= h->T) SFX_FAIL(SFX_E_ARG, "bad args");
   use_gpi = use_gpi ? 1 : 0;
-  const GraphKey key = make_key(2, task_index, use_gpi, 0, {s, q, out});
+  const GraphKey key = make_key(2, {task_index, use_gpi}, h->mask, {s, q, out});
   return run_graph(h, key, [&]() -> int {
-    RC(run_fwd(h, {{R_A, 0, 1, 0, h->T}}, 1, s, nullptr));
-    return run_gpi(h, R_A, 1, 0, h->w + (size_t)task_index * h->dpad, nullptr, q, nullptr, nullptr, out, task_index,
-                   use_gpi);
+    RC(run_fwd(h, {{R_A, P_ONLINE, 1, 0, h->T}}, 1, s, nullptr));
+    return run_gpi(h, gpi_args(R_A, 0, 0, h->w + (size_t)task_index * h->dpad, nullptr, q, nullptr, nullptr, out,
+                               task_index, use_gpi, 1));
   });
 }
 
@@ -606,38 +776,129 @@ int sfx_update(sfx_t h, int policy, const float* S, const int64_t* a, const floa
   if (!valid_head(h, policy) || !S || !a || !phi || !S1 || !gamma) SFX_FAIL(SFX_E_ARG, "bad args");
   if (B < 1 || B > h->Mmax) SFX_FAIL(SFX_E_ARG, "batch exceeds max_batch");
   use_gpi = use_gpi ? 1 : 0;
-  const GraphKey key = make_key(3, policy, use_gpi, B, {S, a, r, phi, S1, gamma, losses, next});
+  const GraphKey key = make_key(3, {policy, use_gpi, B}, h->mask, {S, a, r, phi, S1, gamma, losses, next});
   RC(run_graph(h, key, [&]() -> int {
     if (use_gpi)
-      RC(run_fwd(h, {{R_S, 0, 1, policy, 1}, {R_S1T, 1, 2, policy, 1}, {R_S1, 0, 2, 0, h->T}}, B, S, S1));
+      RC(run_fwd(h, {{R_S, P_ONLINE, 1, policy, 1}, {R_S1T, P_TARGET, 2, policy, 1}, {R_S1, P_ONLINE, 2, 0, h->T}}, B,
+                 S, S1));
     else
-      RC(run_fwd(h, {{R_S, 0, 1, policy, 1}, {R_S1T, 1, 2, policy, 1}, {R_S1, 0, 2, policy, 1}}, B, S, S1));
-    RC(run_tdg(h, policy, 1, B, use_gpi, a, phi, gamma, next));
+      RC(run_fwd(h, {{R_S, P_ONLINE, 1, policy, 1}, {R_S1T, P_TARGET, 2, policy, 1}, {R_S1, P_ONLINE, 2, policy, 1}},
+                 B, S, S1));
+    RC(run_tdg(h, policy, 1, R_S1, B, use_gpi, a, phi, gamma, next, B));
     return run_bwd(h, policy, 1, B, S, phi, r, losses);
   }));
+  h->mask ^= 1ull << policy;
   after_update(h, policy);
   return maybe_sync_target(h, policy);
+}
+
+int sfx_step_all(sfx_t h, const float* S, const int64_t* a, const float* phi, const float* S1, const float* gamma,
+                 int B, int use_gpi, int lms_task, const float* lms_phi, const float* lms_r, float lms_alpha,
+                 const float* s_next, int task_index, int sel_use_gpi, float* losses) {
+  if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
+  if (h->pend.active) SFX_FAIL(SFX_E_STATE, "sfx_step_all: previous step not finished");
+  const bool update = B > 0;
+  if (update && (!S || !a || !phi || !S1 || !gamma || B > h->Mmax)) SFX_FAIL(SFX_E_ARG, "bad minibatch");
+  if (lms_task >= h->T || (lms_task >= 0 && (!lms_phi || !lms_r))) SFX_FAIL(SFX_E_ARG, "bad LMS args");
+  if (s_next && (task_index < 0 || task_index >= h->T)) SFX_FAIL(SFX_E_ARG, "bad task_index");
+  if (!update && !s_next) SFX_FAIL(SFX_E_ARG, "nothing to do");
+  sfx_handle::Pending p;
+  p.active = true;
+  p.update = update;
+  p.sel = s_next != nullptr;
+  p.B = update ? B : 0;
+  p.use_gpi = use_gpi ? 1 : 0;
+  p.task = s_next ? task_index : 0;
+  p.sel_use_gpi = sel_use_gpi ? 1 : 0;
+  p.S = S;
+  p.S1 = S1;
+  p.phi = phi;
+  p.gamma = gamma;
+  p.a = a;
+  p.s_next = s_next;
+  p.losses = losses;
+  unsigned alpha_bits;
+  std::memcpy(&alpha_bits, &lms_alpha, 4);
+  const GraphKey key = make_key(5, {p.B, p.use_gpi, lms_task, p.task, p.sel_use_gpi, (int)alpha_bits, h->spec_rounds}, h->mask,
+                                {S, a, phi, S1, gamma, lms_phi, lms_r, s_next, losses});
+  const int rounds = p.use_gpi ? h->spec_rounds : 1;
+  RC(run_graph(h, key, [&]() -> int { return launch_step_all(h, p, lms_task, lms_phi, lms_r, lms_alpha, rounds); }));
+  HIPCHK(hipMemcpyAsync(h->hout, h->dout, sizeof(StepOut), hipMemcpyDeviceToHost, h->stream));
+  h->pend = p;
+  return SFX_OK;
+}
+
+int sfx_step_finish(sfx_t h, int64_t* out_host) {
+  if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
+  if (!h->pend.active) SFX_FAIL(SFX_E_STATE, "sfx_step_finish without sfx_step_all");
+  sfx_handle::Pending p = h->pend;
+  h->pend.active = false;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  int first = h->T, dev_flag = h->T;
+  if (p.update) {
+    first = p.use_gpi ? h->hout->flag : h->T;
+    if (first < 0 || first > h->T) SFX_FAIL(SFX_E_STATE, "corrupt speculation flag");
+    if (h->force_rerun_from >= 0 && h->force_rerun_from < first) first = h->force_rerun_from;
+    int r = p.use_gpi ? h->spec_rounds : 1;
+    dev_flag = first;
+    h->steps_spec += 1;
+    if (first < h->T) {
+      h->steps_fallback += 1;
+      h->policies_rerun += h->T - first;
+    }
+    // more rounds until every policy's next actions are verified (each round fixes >= 1 head)
+    while (first < h->T) {
+      if (r > h->T + 1) SFX_FAIL(SFX_E_STATE, "speculation did not converge");
+      RC(launch_round(h, p, r));
+      HIPCHK(hipMemcpyAsync(h->hout, h->dout, sizeof(StepOut), hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(hipStreamSynchronize(h->stream));
+      ++r;
+      first = h->hout->flag;
+      if (first < 0 || first > h->T) SFX_FAIL(SFX_E_STATE, "corrupt speculation flag");
+      if (h->force_rerun_from >= 0 && r <= h->spec_rounds + 1 && h->force_rerun_from < first) first = h->force_rerun_from;
+    }
+    h->rounds_total += r;
+    h->mask ^= h->all_bits();
+    for (int t = 0; t < h->T; ++t) {
+      after_update(h, t);
+      RC(maybe_sync_target(h, t));
+    }
+  }
+  if (out_host) {
+    out_host[0] = p.sel ? h->hout->sel[0] : -1;
+    out_host[1] = p.sel ? h->hout->sel[1] : -1;
+    out_host[2] = dev_flag;
+  }
+  return SFX_OK;
+}
+
+int sfx_set_spec_rounds(sfx_t h, int rounds) {
+  if (!h || rounds < 1) SFX_FAIL(SFX_E_ARG, "bad args");
+  h->spec_rounds = rounds;
+  return SFX_OK;
+}
+
+int sfx_step_stats(sfx_t h, long long* steps, long long* fallbacks, long long* rerun_policies, long long* rounds) {
+  if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
+  if (rounds) *rounds = h->rounds_total;
+  if (steps) *steps = h->steps_spec;
+  if (fallbacks) *fallbacks = h->steps_fallback;
+  if (rerun_policies) *rerun_policies = h->policies_rerun;
+  return SFX_OK;
+}
+
+int sfx_debug_force_rerun(sfx_t h, int first_policy) {
+  if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
+  h->force_rerun_from = first_policy;
+  return SFX_OK;
 }
 
 int sfx_update_all(sfx_t h, const float* S, const int64_t* a, const float* phi, const float* S1, const float* gamma,
                    int B, float* losses) {
   if (!h || !S || !a || !phi || !S1 || !gamma) SFX_FAIL(SFX_E_ARG, "bad args");
   if (B < 1 || B > h->Mmax) SFX_FAIL(SFX_E_ARG, "batch exceeds max_batch");
-  const GraphKey key = make_key(4, B, 0, 0, {S, a, phi, S1, gamma, losses});
-  RC(run_graph(h, key, [&]() -> int {
-    RC(run_fwd(h, {{R_S, 0, 1, 0, h->T}, {R_S1T, 1, 2, 0, h->T}, {R_S1, 0, 2, 0, h->T}}, B, S, S1));
-    for (int i = 0; i < h->T; ++i) {
-      RC(run_tdg(h, i, 1, B, 1, a, phi, gamma, nullptr));
-      RC(run_bwd(h, i, 1, B, S, phi, nullptr, losses ? losses + 3 * i : nullptr));
-      if (i + 1 < h->T) RC(run_fwd(h, {{R_S1, 0, 2, i, 1}}, B, S, S1));
-    }
-    return SFX_OK;
-  }));
-  for (int i = 0; i < h->T; ++i) {
-    after_update(h, i);
-    RC(maybe_sync_target(h, i));
-  }
-  return SFX_OK;
+  RC(sfx_step_all(h, S, a, phi, S1, gamma, B, 1, -1, nullptr, nullptr, 0.f, nullptr, 0, 1, losses));
+  return sfx_step_finish(h, nullptr);
 }
 
 int sfx_lms(sfx_t h, int t, const float* phi, const float* r, float alpha) {
@@ -668,7 +929,7 @@ int sfx_set_since_target(sfx_t h, int t, int count) {
 
 int sfx_sync_target(sfx_t h, int t) {
   if (!valid_head(h, t)) SFX_FAIL(SFX_E_ARG, "bad head");
-  HIPCHK(hipMemcpyAsync(h->params(1, t), h->params(0, t), sizeof(float) * h->P, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->target_of(t), h->online_cur(t), sizeof(float) * h->P, hipMemcpyDeviceToDevice, h->stream));
   return SFX_OK;
 }
 

@@ -5,9 +5,15 @@
 //
 // Every problem here is tiny (minibatch M <= 32, heads of ~150k parameters), so each
 // kernel is LATENCY bound: the design rules are (1) every pointer is computed from
-// kernel arguments (no descriptor loads in front of the data loads), (2) all global
-// loads a thread needs are issued before the first use (compile-time unrolled,
-// predicated), (3) optimizer state is prefetched before the MFMA chain.
+// kernel arguments (no descriptor loads, no dynamically indexed kernel-argument arrays
+// in front of the data loads), (2) all global loads a thread needs are issued before the
+// first use (compile-time unrolled, predicated), (3) optimizer state is prefetched before
+// the MFMA chain, (4) as few dependent launches per env step as the algorithm allows.
+//
+// Online head state (params, Adam m, v) is double-buffered: head t reads slot
+// (mask >> t) & 1 and an optimizer step writes the other slot.  Nothing is updated in
+// place, so a speculative update can be discarded (see k_ver) and no launch both reads
+// and rewrites a weight.
 //
 // Reference behaviour being implemented is cited per kernel (paths relative to
 // /root/reference/source).
@@ -25,9 +31,15 @@ constexpr int QMAX = 8192;    // T*A entries of the per-row GPI scratch in LDS
 constexpr int OMAX = 4096;    // A*d (row of a ψ output) held in LDS
 constexpr int DMAX = 256;     // feature dimension d
 constexpr int MMAX = 1024;    // rows of one update
+constexpr int KFUSE = 64;     // layer-0 fan-in up to which the post-update forward is fused
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2 };
-enum { R_S = 0, R_S1T = 1, R_S1 = 2, R_G = 3, R_A = 4, NROLE = 5 };
+// activation-block roles: ψ(S) online (saved for backward), ψ⁻(S1) target, ψ(S1) online
+// before the step, GPI scratch, action selection, and two alternating buffers of
+// ψ(S1 ++ s_next) online after a speculative round of the step
+enum { R_S = 0, R_S1T = 1, R_S1 = 2, R_G = 3, R_A = 4, R_V = 5, R_V2 = 6, NROLE = 7 };
+// parameter sets a forward instance can read
+enum { P_ONLINE = 0, P_TARGET = 1, P_NEW = 2 };
 
 __device__ __forceinline__ float act_fwd(float x, int code) {
   if (code == ACT_RELU) return x > 0.f ? x : 0.f;
@@ -76,10 +88,10 @@ struct Geo {
   int T, NL, A, d, O, dpad;
   long long P;        // packed head stride (floats)
   long long actSize;  // one (role, head) activation block (floats)
-  float* online;      // [T][P]
-  float* target;
-  float* am;          // Adam m, v of ψ
-  float* av;
+  float* online;      // [2][T][P]   slot-major
+  float* target;      // [T][P]
+  float* am;          // [2][T][P]   Adam m of ψ
+  float* av;          // [2][T][P]   Adam v of ψ
   float* w;           // [T][dpad]
   float* wm;
   float* wv;
@@ -96,7 +108,12 @@ struct Geo {
   __device__ __forceinline__ float* dzp(int head, int off) const {
     return dz + (long long)head * actSize + off;
   }
+  __device__ __forceinline__ long long slot_off(int slot, int head) const {
+    return ((long long)slot * T + head) * P;
+  }
 };
+
+__device__ __forceinline__ int rslot(unsigned long long mask, int head) { return (int)((mask >> head) & 1ull); }
 
 // -------------------------------------------------------------------------------------
 // Adam, torch 2.10 single-tensor semantics (torch/optim/adam.py:457,476,531-547):
@@ -127,7 +144,6 @@ __device__ __forceinline__ AdamC adam_consts(const AdamHP& hp, int step) {
   return c;
 }
 
-// one element, state already in registers; returns nothing, writes p/m/v back
 __device__ __forceinline__ void adam_apply(float& pp, float& mm, float& vv, float g, const AdamC& c) {
   if (c.wd != 0.f) g = __fadd_rn(g, __fmul_rn(c.wd, pp));
   mm = __builtin_fmaf(c.omb1, __fsub_rn(g, mm), mm);  // vectorized lerp: fmadd(w, end-start, start)
@@ -152,18 +168,42 @@ __device__ __forceinline__ void adam_el(float* p, float* m, float* v, float g, c
 // tile; its 4 waves split K in 64-wide chunks, each wave runs two 16x16x4 f32 MFMA
 // chains, partial tiles are summed through LDS in wave order (deterministic).
 // Instances come in up to 4 groups of consecutive heads sharing (role, param set, input).
+// Block (0,0,0) of a layer-0 launch may also run the env step's LMS reward fit
+// (features/successor.py:164-167) and reset the speculation flag.
 // -------------------------------------------------------------------------------------
 struct FwdGroup {
-  int role, which, xsel, head0, n;  // which: 0 online, 1 target; xsel: 1 -> xa, 2 -> xb
+  int role, which, xsel, head0, n;  // which: P_*; xsel: 1 -> xa, 2 -> xb
 };
 
 struct FwdArgs {
   int M, N, K, act, wOff, bOff, xOff, yOff;  // xOff < 0: layer input is xa / xb
-  int ngroups, pad_;
+  int ngroups, lms_head, flag_value, pad_;
+  unsigned long long mask;
   FwdGroup g0, g1, g2, g3;
   const float* xa;
   const float* xb;
+  const float* lms_phi;  // LMS (lms_head >= 0): w[lms_head] += α (r - φ·w) φ
+  const float* lms_r;
+  float lms_alpha;
+  int* flag;             // set to flag_value when non-null
 };
+
+__device__ void lms_block(const Geo& G, const FwdArgs& F) {
+  __shared__ float s_p[DMAX];
+  __shared__ float s_e;
+  const int tid = threadIdx.x, d = G.d;
+  float* w = G.w + (long long)F.lms_head * G.dpad;
+  const float wk = tid < d ? w[tid] : 0.f, pk = tid < d ? F.lms_phi[tid] : 0.f;
+  if (tid < d) s_p[tid] = __fmul_rn(pk, wk);
+  __syncthreads();
+  if (tid == 0) {
+    float rf = 0.f;
+    for (int k = 0; k < d; ++k) rf = __fadd_rn(rf, s_p[k]);
+    s_e = __fmul_rn(F.lms_alpha, __fsub_rn(F.lms_r[0], rf));
+  }
+  __syncthreads();
+  if (tid < d) w[tid] = __fadd_rn(wk, __fmul_rn(s_e, pk));
+}
 
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_fwd(Geo G, FwdArgs F) {
@@ -175,7 +215,8 @@ __global__ __launch_bounds__(256) void k_fwd(Geo G, FwdArgs F) {
   if (F.ngroups > 3 && y >= grp.n) { y -= grp.n; grp = F.g3; }
   const int head = grp.head0 + y;
   const int M = F.M, N = F.N, K = F.K;
-  const float* P = (grp.which ? G.target : G.online) + (long long)head * G.P;
+  const float* P = grp.which == P_TARGET ? G.target + (long long)head * G.P
+                                         : G.online + G.slot_off(rslot(F.mask, head) ^ (grp.which == P_NEW), head);
   const float* X = F.xOff < 0 ? (grp.xsel == 1 ? F.xa : F.xb) : G.actp(grp.role, head, F.xOff);
   float* Y = G.actp(grp.role, head, F.yOff);
   const int n0 = blockIdx.x * 16, m0 = blockIdx.z * 32;
@@ -235,6 +276,10 @@ __global__ __launch_bounds__(256) void k_fwd(Geo G, FwdArgs F) {
       }
     }
   }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+    if (F.flag && threadIdx.x == 0) *F.flag = F.flag_value;
+    if (F.lms_head >= 0) lms_block(G, F);
+  }
 }
 
 // -------------------------------------------------------------------------------------
@@ -245,15 +290,19 @@ __global__ __launch_bounds__(256) void k_fwd(Geo G, FwdArgs F) {
 //   t_b  = φ_b + γ_b ψ⁻_i(s1_b)[a'_b]
 //   g[b, a_b, :] = 2 (c[b,a_b,:] - t_b) / (M*A*d), 0 elsewhere  (MSE vs merged clone)
 //   rowloss[i][b] = Σ_k (c[b,a_b,k] - t_b[k])^2
-// Every load of the row (ψ(s1) of all heads, ψ⁻, c, φ) is issued before the reductions.
+// Policy i takes ψ_t(s1) of heads t < i from role `guess` and of heads t >= i from R_S1
+// (before the step).  In the reference's in-order loop heads t < i are already updated;
+// guess = R_S1 speculates they did not move, guess = R_V/R_V2 uses the post-update values
+// of the previous speculative round (see k_ver).
 // Grid (M, npol), 256 threads.  Policies pol0 .. pol0+npol-1.
 // -------------------------------------------------------------------------------------
 struct TdgArgs {
-  int M, use_gpi, pol0, npol;
+  int M, use_gpi, pol0, npol, guess, next_stride, flag_value, pad_;
   const int64_t* a;
   const float* phi;
   const float* gamma;
-  int64_t* next;  // [npol][M] or null
+  int64_t* next;  // next[(policy - pol0) * next_stride + b] or null
+  int* flag;      // reset to flag_value by block (0, 0) when non-null
 };
 
 __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
@@ -261,14 +310,15 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   const int T = G.T, Aa = G.A, d = G.d, O = G.O, M = A.M, NLm = G.lastOff;
   __shared__ float s_w[DMAX];
   __shared__ float s_q[QMAX];
-  __shared__ float s_t[OMAX];   // ψ⁻_i(s1_b) row
-  __shared__ float s_m[64];
+  __shared__ float s_t[OMAX];  // ψ⁻_i(s1_b) row
+  __shared__ float s_m[256];
+  __shared__ float s_sq[DMAX];
   __shared__ int s_next;
   const float* wrow = G.w + (long long)pol * G.dpad;
   for (int k = tid; k < d; k += 256) s_w[k] = wrow[k];
+  if (A.flag && b == 0 && blockIdx.y == 0 && tid == 0) *A.flag = A.flag_value;
   const float* trow = G.actp(R_S1T, pol, NLm) + (size_t)b * O;
   for (int o = tid; o < O; o += 256) s_t[o] = trow[o];
-  // own-row data for the gradient: thread k < d handles feature k of the chosen action
   const int ab = (int)A.a[b];
   const bool aok = ab >= 0 && ab < Aa;
   float cval = 0.f, phik = 0.f;
@@ -281,17 +331,17 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   const int t0 = A.use_gpi ? 0 : pol, nt = A.use_gpi ? T : 1;
   for (int idx = tid; idx < nt * Aa; idx += 256) {
     const int t = t0 + idx / Aa, a = idx % Aa;
-    const float* p = G.actp(R_S1, t, NLm) + (size_t)b * O + a * d;
+    const float* p = G.actp(t < pol ? A.guess : R_S1, t, NLm) + (size_t)b * O + a * d;
     float q = 0.f;
 #pragma unroll 8
     for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
     s_q[idx] = q;
   }
   __syncthreads();
-  if (tid < Aa) {  // max over heads for action tid (torch.max(q1, axis=1))
-    float mx = s_q[tid];
-    for (int t = 1; t < nt; ++t) mx = fmaxf(mx, s_q[t * Aa + tid]);
-    s_m[tid] = mx;
+  for (int a = tid; a < Aa; a += 256) {  // max over heads for each action (torch.max(q1, axis=1))
+    float mx = s_q[a];
+    for (int t = 1; t < nt; ++t) mx = fmaxf(mx, s_q[t * Aa + a]);
+    s_m[a] = mx;
   }
   __syncthreads();
   if (tid == 0) {  // argmax over actions, first index on ties
@@ -303,33 +353,30 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
         am = a;
       }
     s_next = am;
-    if (A.next) A.next[(size_t)blockIdx.y * M + b] = am;
+    if (A.next) A.next[(size_t)blockIdx.y * A.next_stride + b] = am;
   }
   __syncthreads();
   const float norm = (float)(2.0 / ((double)M * (double)O));
   float* grow = G.dzp(pol, NLm) + (size_t)b * O;
+  const float* crow = G.actp(R_S, pol, NLm) + (size_t)b * O;
   const int an = s_next;
-  float dsq = 0.f;
   for (int o = tid; o < O; o += 256) {
     float gv = 0.f;
     if (aok && o >= ab * d && o < ab * d + d) {
       const int k = o - ab * d;
       const float tg = __fadd_rn(A.phi[(size_t)b * d + k], __fmul_rn(gam, s_t[an * d + k]));
-      const float diff = __fsub_rn(G.actp(R_S, pol, NLm)[(size_t)b * O + o], tg);
-      gv = __fmul_rn(norm, diff);
+      gv = __fmul_rn(norm, __fsub_rn(crow[o], tg));
     }
     grow[o] = gv;
   }
+  float dsq = 0.f;
   if (tid < d && aok) {
-    const float tg = __fadd_rn(phik, __fmul_rn(gam, s_t[an * d + tid]));
-    const float diff = __fsub_rn(cval, tg);
+    const float diff = __fsub_rn(cval, __fadd_rn(phik, __fmul_rn(gam, s_t[an * d + tid])));
     dsq = __fmul_rn(diff, diff);
   }
-  // row Σ diff^2 in feature order
-  __shared__ float s_sq[DMAX];
   if (tid < d) s_sq[tid] = dsq;
   __syncthreads();
-  if (tid == 0) {
+  if (tid == 0) {  // row Σ diff^2 in feature order
     float s = 0.f;
     for (int k = 0; k < d; ++k) s = __fadd_rn(s, s_sq[k]);
     G.rowloss[(long long)pol * MMAX + b] = s;
@@ -339,16 +386,15 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
 // -------------------------------------------------------------------------------------
 // K3  Backward through the ψ MLP with Adam fused into the weight-gradient epilogue
 // (autograd of sfdqn.py:344-345 + optim.step() at :362).
-//
-// Layers are processed in a ping-pong so no launch both reads and rewrites a weight:
-// the launch that back-propagates through layer l (dX role, reads W_l) is the one that
-// finishes the weight gradient of layer l+1 and applies Adam to it (dW roles).
 //   dX role : dZ_{l-1} = (dZ_l W_l) ⊙ act'(X_l)        32x16 tile, split over the 4 waves
-//   dW role : dW_l = dZ_l^T X_l ; db_l = Σ_m dZ_l ; Adam(W_l, b_l)
+//   dW role : dW_l = dZ_l^T X_l ; db_l = Σ_m dZ_l ; Adam(W_l, b_l) read slot -> write slot
 //   tail    : (first launch only) l1 from the per-row losses, optional l2 = MSE(w_i·φ, r)
 //             with one Adam step on w_i (sfdqn.py:340-342), Adam step counter += 1.
-// blockIdx.x selects the role: [0, na) dX of layer la; [na, na+nb) dW of lb;
-// [na+nb, na+nb+nc) dW of lc; [.., +tail) tail.  blockIdx.y = head - head0.
+// Layers are walked in a ping-pong (dX of l with dW of l+1) so each launch needs only one
+// dZ.  With fuse_v0 the layer-0 dW tiles also run the post-update forward of layer 0 for
+// the rows of S1 (and s_next) into R_V from the freshly written parameters.
+// blockIdx.x selects the role: [0, na) dX; [na, na+nb) dW rb; [.., +nc) dW rc; then tail.
+// blockIdx.y = head - head0.
 // -------------------------------------------------------------------------------------
 struct RoleGeo {
   int N, K, wOff, bOff, actIn;
@@ -358,13 +404,18 @@ struct RoleGeo {
 };
 
 struct BwdArgs {
-  int M, na, nb, nc, tail, head0, train_w, pad_;
+  int M, na, nb, nc, tail, head0, train_w, inc_step;
+  int fuse_v0, vM, vOff, act0;  // fused forward: rows (S1 ++ s_next), layer-0 offset, layer-0 act
+  int vRole, pad_;              // role block the fused forward writes
+  unsigned long long mask;
   RoleGeo ra, rb, rc;  // dX role (layer la), dW roles (lb, lc)
   AdamHP hp, hpw;
-  const float* x0;   // layer-0 input (the minibatch states S)
-  const float* phi;  // tail: [M, d]
-  const float* r;    // tail: [M] rewards (train_w)
-  float* losses;     // tail: [n_head][3] (l1+l2, l1, l2) or null
+  const float* x0;     // layer-0 input (the minibatch states S)
+  const float* phi;    // tail: [M, d]
+  const float* r;      // tail: [M] rewards (train_w)
+  float* losses;       // tail: [n_head][3] (l1+l2, l1, l2) or null
+  const float* v_x;    // fused forward input rows 0..M-1 (S1)
+  const float* v_xn;   // fused forward input row M (s_next) or null
 };
 
 __device__ __forceinline__ const float* layer_input(const Geo& G, const BwdArgs& A, int head, int xOff) {
@@ -378,7 +429,7 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
   const int k0 = (tile % ntk) * 16, m0 = (tile / ntk) * 32;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
   const float* dZ = G.dzp(head, L.dzOff);
-  const float* W = (G.online + (long long)head * G.P) + L.wOff;
+  const float* W = G.online + G.slot_off(rslot(A.mask, head), head) + L.wOff;
   const float* Xin = layer_input(G, A, head, L.xOff);
   float* out = G.dzp(head, L.dzIn);
   const int ma = m0 + r, mb = m0 + 16 + r, kk = k0 + r;
@@ -394,10 +445,10 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
     }
   }
   floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const bool vec = (N & 63) == 0;
   for (int nc = wave * 64; nc < N; nc += 256) {
     const int nb = nc + g * 16;
     float a0[16], a1[16], bw[16];
-    const bool vec = (N & 63) == 0;
     load16u(a0, dZ + (size_t)ma * N, nb, N, oka, vec);
     load16u(a1, dZ + (size_t)mb * N, nb, N, okb, vec);
 #pragma unroll
@@ -426,7 +477,23 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
   }
 }
 
-__device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile) {
+// post-update forward of layer 0 for the 32 output rows this tile just optimised
+__device__ void fused_v0(const Geo& G, const BwdArgs& A, const RoleGeo& L, int head, int nbase, float* sW,
+                         float* sB) {
+  __syncthreads();
+  const int K = L.K, N = L.N, VM = A.vM;
+  float* Y = G.actp(A.vRole, head, A.vOff);
+  for (int idx = threadIdx.x; idx < VM * 32; idx += 256) {
+    const int m = idx >> 5, nl = idx & 31, n = nbase + nl;
+    if (n >= N) continue;
+    const float* x = m < A.M ? A.v_x + (size_t)m * K : A.v_xn;
+    float acc = 0.f;
+    for (int k = 0; k < K; ++k) acc = __builtin_fmaf(x[k], sW[nl * KFUSE + k], acc);
+    Y[(size_t)m * N + n] = act_fwd(__fadd_rn(acc, sB[nl]), A.act0);
+  }
+}
+
+__device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile, bool fuse) {
   const int N = L.N, K = L.K, M = A.M;
   const int ntk = (K + 63) >> 6;
   const int kt = tile % ntk, nt = tile / ntk;
@@ -434,9 +501,14 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
   const int nbase = nt * 32, n0 = nbase + (wave & 1) * 16, k0 = kt * 64 + (wave >> 1) * 32;
   const float* dZ = G.dzp(head, L.dzOff);
   const float* X = layer_input(G, A, head, L.xOff);
-  float* P = G.online + (long long)head * G.P;
-  float* Mo = G.am + (long long)head * G.P;
-  float* Vo = G.av + (long long)head * G.P;
+  const int rs = rslot(A.mask, head);
+  const long long ro = G.slot_off(rs, head), wo = G.slot_off(rs ^ 1, head);
+  const float* Pr = G.online + ro;
+  const float* Mr = G.am + ro;
+  const float* Vr = G.av + ro;
+  float* Pw = G.online + wo;
+  float* Mw = G.am + wo;
+  float* Vw = G.av + wo;
   const AdamC c = adam_consts(A.hp, G.step[head]);
   const int nn = n0 + r, kb0 = k0 + r, kb1 = k0 + 16 + r;
   // prefetch the optimizer state of the 8 weights this lane will update
@@ -451,9 +523,9 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
       const int e = i * 2 + h;
       ok[e] = n < N && k < K;
       const size_t off = (size_t)L.wOff + (size_t)n * K + k;
-      pp[e] = ok[e] ? P[off] : 0.f;
-      pm[e] = ok[e] ? Mo[off] : 0.f;
-      pv[e] = ok[e] ? Vo[off] : 0.f;
+      pp[e] = ok[e] ? Pr[off] : 0.f;
+      pm[e] = ok[e] ? Mr[off] : 0.f;
+      pv[e] = ok[e] ? Vr[off] : 0.f;
     }
   }
   // bias state (threads 0..31 of the kt == 0 tiles)
@@ -461,9 +533,9 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
   const int nbias = nbase + threadIdx.x;
   float bp = 0.f, bm = 0.f, bv = 0.f;
   if (dob) {
-    bp = P[L.bOff + nbias];
-    bm = Mo[L.bOff + nbias];
-    bv = Vo[L.bOff + nbias];
+    bp = Pr[L.bOff + nbias];
+    bm = Mr[L.bOff + nbias];
+    bv = Vr[L.bOff + nbias];
   }
   floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
@@ -492,6 +564,8 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
       for (int m = 0; m < MT; ++m) bsum = __fadd_rn(bsum, db[m]);
     }
   }
+  __shared__ float sW[32 * KFUSE];
+  __shared__ float sB[32];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int n = n0 + g * 4 + i;
@@ -499,28 +573,32 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
     for (int h = 0; h < 2; ++h) {
       const int e = i * 2 + h;
       if (ok[e]) {
-        const size_t off = (size_t)L.wOff + (size_t)n * K + (h ? kb1 : kb0);
+        const int k = h ? kb1 : kb0;
+        const size_t off = (size_t)L.wOff + (size_t)n * K + k;
         adam_apply(pp[e], pm[e], pv[e], h ? acc1[i] : acc0[i], c);
-        P[off] = pp[e];
-        Mo[off] = pm[e];
-        Vo[off] = pv[e];
+        Pw[off] = pp[e];
+        Mw[off] = pm[e];
+        Vw[off] = pv[e];
+        if (fuse) sW[(n - nbase) * KFUSE + k] = pp[e];
       }
     }
   }
   if (dob) {
     adam_apply(bp, bm, bv, bsum, c);
-    P[L.bOff + nbias] = bp;
-    Mo[L.bOff + nbias] = bm;
-    Vo[L.bOff + nbias] = bv;
+    Pw[L.bOff + nbias] = bp;
+    Mw[L.bOff + nbias] = bm;
+    Vw[L.bOff + nbias] = bv;
+    if (fuse) sB[threadIdx.x] = bp;
   }
+  if (fuse) fused_v0(G, A, L, head, nbase, sW, sB);
 }
 
 // loss finalisation, optional w step, Adam step counter (one workgroup per head)
 __device__ void role_tail(const Geo& G, const BwdArgs& A, int head) {
   const int M = A.M, d = G.d, tid = threadIdx.x;
   __shared__ float s_e[MMAX];
-  __shared__ float s_x[256];
-  const int step = G.step[head] + 1;
+  __shared__ float s_x[1];
+  const int step = A.inc_step ? G.step[head] + 1 : G.step[head];
   const float* rl = G.rowloss + (long long)head * MMAX;
   float* w = G.w + (long long)head * G.dpad;
   float l2 = 0.f;
@@ -571,12 +649,12 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
   }
   bx -= A.na;
   if (bx < A.nb) {
-    role_dw(G, A, head, A.rb, bx);
+    role_dw(G, A, head, A.rb, bx, false);
     return;
   }
   bx -= A.nb;
   if (bx < A.nc) {
-    role_dw(G, A, head, A.rc, bx);
+    role_dw(G, A, head, A.rc, bx, A.fuse_v0 != 0);
     return;
   }
   role_tail(G, A, head);
@@ -588,7 +666,7 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
 //   task = argmax_t max_a q ; next = argmax_a max_t q ; sel = (c, argmax_a q[c])
 // -------------------------------------------------------------------------------------
 struct GpiArgs {
-  int M, role, row0, select_task, use_gpi, pad_;
+  int M, role, row0, select_task, use_gpi, rowoff;  // rowoff: first row of the role block used
   const float* w;
   float* psi_out;   // [B, T, A, d] or null  (row b -> row0 + b)
   float* q_out;     // [B, T, A] or null
@@ -597,24 +675,25 @@ struct GpiArgs {
   int64_t* sel_out;  // [2] or null
 };
 
-__global__ __launch_bounds__(256) void k_gpi(Geo G, GpiArgs A) {
-  const int b = blockIdx.x, tid = threadIdx.x;
+__device__ void gpi_row(const Geo& G, const GpiArgs& A, int b) {
+  const int tid = threadIdx.x;
   const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff;
   __shared__ float s_q[QMAX];
   __shared__ float s_w[DMAX];
   __shared__ float s_mt[256], s_ma[256];
   for (int k = tid; k < d; k += 256) s_w[k] = A.w[k];
   const long long ob = (long long)(A.row0 + b);
+  const int lb = A.rowoff + b;
   if (A.psi_out) {
     for (int idx = tid; idx < T * O; idx += 256) {
       const int t = idx / O, o = idx - t * O;
-      A.psi_out[(ob * T + t) * O + o] = G.actp(A.role, t, NLm)[(size_t)b * O + o];
+      A.psi_out[(ob * T + t) * O + o] = G.actp(A.role, t, NLm)[(size_t)lb * O + o];
     }
   }
   __syncthreads();
   for (int idx = tid; idx < T * Aa; idx += 256) {
     const int t = idx / Aa, a = idx - t * Aa;
-    const float* p = G.actp(A.role, t, NLm) + (size_t)b * O + a * d;
+    const float* p = G.actp(A.role, t, NLm) + (size_t)lb * O + a * d;
     float q = 0.f;
 #pragma unroll 8
     for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
@@ -650,6 +729,71 @@ __global__ __launch_bounds__(256) void k_gpi(Geo G, GpiArgs A) {
       A.sel_out[1] = act;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void k_gpi(Geo G, GpiArgs A) { gpi_row(G, A, blockIdx.x); }
+
+// -------------------------------------------------------------------------------------
+// K5  Verification of a speculative round of the all-task update + action selection.
+// Block i in [1, T): recompute policy i's next actions with heads t < i AFTER this round's
+// update (role `post`) and heads t >= i before it (R_S1) -- what policy i sees in the
+// reference's in-order loop (agents/sfdqn.py:59-60) -- and compare with the actions the
+// round used.  Mismatch: atomicMin(flag, i).  Heads below the flag are exact (induction
+// from policy 0, which only sees pre-step heads); the next round re-derives every
+// policy's actions from this round's post-update values and fixes at least one more head.
+// Block npol (when sel): GPI action for s_next (row M of `post`) with w[select_task].
+// -------------------------------------------------------------------------------------
+struct VerArgs {
+  int M, npol, sel, spec_stride, post, pad_;
+  const int64_t* spec_next;  // [T][spec_stride]
+  int* flag;
+  GpiArgs g;                 // action selection for s_next
+};
+
+__global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
+  const int i = blockIdx.x, tid = threadIdx.x;
+  if (i == V.npol) {
+    if (V.sel) gpi_row(G, V.g, 0);
+    return;
+  }
+  if (i == 0) return;  // policy 0 sees only pre-update heads: always exact
+  const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, M = V.M;
+  __shared__ float s_w[DMAX];
+  __shared__ float s_q[QMAX];
+  __shared__ int s_bad;
+  const float* wrow = G.w + (long long)i * G.dpad;
+  for (int k = tid; k < d; k += 256) s_w[k] = wrow[k];
+  if (tid == 0) s_bad = 0;
+  __syncthreads();
+  const int rows = QMAX / (T * Aa) < 1 ? 1 : QMAX / (T * Aa);
+  for (int b0 = 0; b0 < M; b0 += rows) {
+    const int nb = M - b0 < rows ? M - b0 : rows;
+    for (int idx = tid; idx < nb * T * Aa; idx += 256) {
+      const int bl = idx / (T * Aa), rem = idx - bl * T * Aa, t = rem / Aa, a = rem - t * Aa;
+      const float* p = G.actp(t < i ? V.post : R_S1, t, NLm) + (size_t)(b0 + bl) * O + a * d;
+      float q = 0.f;
+#pragma unroll 8
+      for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
+      s_q[idx] = q;
+    }
+    __syncthreads();
+    for (int bl = tid; bl < nb; bl += 256) {
+      const float* qb = s_q + bl * T * Aa;
+      int am = 0;
+      float best = -INFINITY;
+      for (int a = 0; a < Aa; ++a) {
+        float mx = qb[a];
+        for (int t = 1; t < T; ++t) mx = fmaxf(mx, qb[t * Aa + a]);
+        if (a == 0 || mx > best) {
+          best = mx;
+          am = a;
+        }
+      }
+      if (am != (int)V.spec_next[(size_t)i * V.spec_stride + b0 + bl]) s_bad = 1;
+    }
+    __syncthreads();
+  }
+  if (tid == 0 && s_bad) atomicMin(V.flag, i);
 }
 
 // LMS reward fit (features/successor.py:164-167): w += α (r - Σ φ⊙w) φ

@@ -38,6 +38,11 @@ SIGNATURES = {
     "sfx_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP]),
     "sfx_update_all": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _VP]),
     "sfx_lms": (_I, [_VP, _I, _VP, _VP, _F]),
+    "sfx_step_all": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _I, _VP, _VP, _F, _VP, _I, _I, _VP]),
+    "sfx_step_finish": (_I, [_VP, C.POINTER(C.c_int64)]),
+    "sfx_debug_force_rerun": (_I, [_VP, _I]),
+    "sfx_set_spec_rounds": (_I, [_VP, _I]),
+    "sfx_step_stats": (_I, [_VP] + [C.POINTER(C.c_longlong)] * 4),
     "sfx_set_target_update_ev": (_I, [_VP, _I]),
     "sfx_get_since_target": (_I, [_VP, _I, _IP]),
     "sfx_set_since_target": (_I, [_VP, _I, _I]),

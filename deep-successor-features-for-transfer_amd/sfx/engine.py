@@ -134,7 +134,7 @@ class SFEngine:
     def sync_target(self, t: int):
         check(lib.sfx_sync_target(self._h, t), "sfx_sync_target")
 
-    KINDS = {"fwd": 0, "tdg": 1, "bwd": 2, "gpi": 3, "lms": 4}
+    KINDS = {"fwd": 0, "tdg": 1, "bwd": 2, "gpi": 3, "lms": 4, "ver": 5}
 
     def prof_enable(self, on: bool):
         check(lib.sfx_prof_enable(self._h, int(bool(on))), "sfx_prof_enable")
@@ -215,6 +215,33 @@ class SFEngine:
         check(lib.sfx_update_all(self._h, s.data_ptr(), a.data_ptr(), phi.data_ptr(), s1.data_ptr(),
                                  gamma.data_ptr(), B, losses.data_ptr()), "sfx_update_all")
         return losses
+
+    def step_all(self, s=None, a=None, phi=None, s1=None, gamma=None, *, use_gpi: bool = True, lms_task: int = -1,
+                 lms_phi=None, lms_r=None, lms_alpha: float = 0.0, s_next=None, task_index: int = 0,
+                 sel_use_gpi: bool = True, losses: Optional[torch.Tensor] = None):
+        """Launch one fused all-task env step (see include/sfx.h: sfx_step_all).  Device tensors
+        must already be float32 / int64 and contiguous (no conversion on this hot path)."""
+        B = 0 if s is None else s.shape[0]
+        check(lib.sfx_step_all(self._h, dptr(s), dptr(a), dptr(phi), dptr(s1), dptr(gamma), B, int(bool(use_gpi)),
+                               int(lms_task), dptr(lms_phi), dptr(lms_r), float(lms_alpha), dptr(s_next),
+                               int(task_index), int(bool(sel_use_gpi)), dptr(losses)), "sfx_step_all")
+
+    def step_finish(self):
+        """Complete the fused step: returns (GPI task c, greedy action, first re-run policy)."""
+        out = (C.c_int64 * 3)()
+        check(lib.sfx_step_finish(self._h, out), "sfx_step_finish")
+        return int(out[0]), int(out[1]), int(out[2])
+
+    def debug_force_rerun(self, first_policy: int):
+        check(lib.sfx_debug_force_rerun(self._h, int(first_policy)), "sfx_debug_force_rerun")
+
+    def set_spec_rounds(self, rounds: int):
+        check(lib.sfx_set_spec_rounds(self._h, int(rounds)), "sfx_set_spec_rounds")
+
+    def step_stats(self):
+        s, f, r, n = C.c_longlong(), C.c_longlong(), C.c_longlong(), C.c_longlong()
+        check(lib.sfx_step_stats(self._h, C.byref(s), C.byref(f), C.byref(r), C.byref(n)), "sfx_step_stats")
+        return {"steps": s.value, "host_round_steps": f.value, "unverified_policies": r.value, "rounds": n.value}
 
     def lms(self, t: int, phi, r, alpha: float):
         phi = self._f(phi, (-1,))

@@ -129,7 +129,12 @@ class EnvLoop:
         self.s = self.task.initialize()
         self.st.h["snext"][0] = self.s
         self.st.upload()
-        self._issue_select()
+        if self.schedule == "all":
+            self.eng.step_all(s_next=self.st.d["snext"], task_index=index, sel_use_gpi=self.use_gpi)
+            c, a, _ = self.eng.step_finish()
+            self.sel = (c, a)
+        else:
+            self._issue_select()
 
     def prefill(self, n: int):
         """Random transitions into the replay (warm-up only; not an env step)."""
@@ -146,10 +151,15 @@ class EnvLoop:
         self.sel_event = torch.cuda.Event()
         self.sel_event.record()
 
-    def step(self):
-        """One env step: GPI action (already in flight), ε-greedy, transition, train."""
+    def _greedy(self):
+        if self.schedule == "all":
+            return self.sel
         self.sel_event.synchronize()
-        c, a_greedy = int(self.sel_host[0]), int(self.sel_host[1])
+        return int(self.sel_host[0]), int(self.sel_host[1])
+
+    def step(self):
+        """One env step: GPI action (computed by the previous step), ε-greedy, transition, train."""
+        c, a_greedy = self._greedy()
         self.gpi_counters[self.task_index, c] += 1
         if self.rng.random() <= self.epsilon:
             a = int(self.rng.integers(self.eng.A))
@@ -171,14 +181,21 @@ class EnvLoop:
         st.upload()
         d, e = st.d, self.eng
         if self.schedule == "all":
-            e.lms(self.task_index, d["phi1"], d["r1"], self.alpha_w)
             if have:
-                e.update_all(d["s"], d["a"], d["phi"], d["s1"], d["gamma"], losses=self.losses)
-        elif have:
-            e.update(self.task_index, d["s"], d["a"], d["r"], d["phi"], d["s1"], d["gamma"], self.use_gpi,
-                     losses=self.losses[0])
+                e.step_all(d["s"], d["a"], d["phi"], d["s1"], d["gamma"], use_gpi=True, lms_task=self.task_index,
+                           lms_phi=d["phi1"], lms_r=d["r1"], lms_alpha=self.alpha_w, s_next=d["snext"],
+                           task_index=self.task_index, sel_use_gpi=self.use_gpi, losses=self.losses)
+            else:
+                e.step_all(lms_task=self.task_index, lms_phi=d["phi1"], lms_r=d["r1"], lms_alpha=self.alpha_w,
+                           s_next=d["snext"], task_index=self.task_index, sel_use_gpi=self.use_gpi)
+            c, a, _ = e.step_finish()
+            self.sel = (c, a)
+        else:
+            if have:
+                e.update(self.task_index, d["s"], d["a"], d["r"], d["phi"], d["s1"], d["gamma"], self.use_gpi,
+                         losses=self.losses[0])
+            self._issue_select()
         self.s = s_next
-        self._issue_select()
 
     def run(self, n: int):
         for _ in range(n):

@@ -126,6 +126,39 @@ int sfx_update(sfx_t h, int policy, const float* S_dev, const int64_t* a_dev, co
 int sfx_update_all(sfx_t h, const float* S_dev, const int64_t* a_dev, const float* phi_dev,
                    const float* S1_dev, const float* gamma_dev, int B, float* losses_dev);
 
+/*
+ * Fused env step of the all-task schedule: the device half of one Agent.next_sample
+ * (agents/agent.py:195-261) with SFDQN.train_agent (agents/sfdqn.py:47-60):
+ *   - LMS reward fit of w[lms_task] on (lms_phi [d], lms_r [1]) when lms_task >= 0
+ *     (SF.update_reward, features/successor.py:164-167);
+ *   - when B > 0, every head updated on the minibatch exactly as the reference's in-order
+ *     loop does.  The update is launched SPECULATIVELY (all policies take their GPI next
+ *     actions from the pre-step heads, the heads update in parallel into their second
+ *     parameter slot); the device then re-derives each policy's next actions with the
+ *     heads before it already updated and flags the first policy whose actions differ;
+ *   - when s_next != NULL, the GPI greedy action for s_next with w[task_index] on the
+ *     updated heads (sfdqn.py:585-594).
+ * sfx_step_all only launches; sfx_step_finish waits, runs further rounds while a policy is
+ * flagged (each round makes at least one more head exact), commits, and writes
+ * out_host[0] = GPI task c, [1] = greedy action, [2] = first policy flagged by the last
+ * device round (T when it held).  losses_dev [T, 3] may be NULL.
+ */
+int sfx_step_all(sfx_t h, const float* S_dev, const int64_t* a_dev, const float* phi_dev, const float* S1_dev,
+                 const float* gamma_dev, int B, int use_gpi, int lms_task, const float* lms_phi_dev,
+                 const float* lms_r_dev, float lms_alpha, const float* s_next_dev, int task_index, int sel_use_gpi,
+                 float* losses_dev);
+int sfx_step_finish(sfx_t h, int64_t* out_host);
+/* Test hook: make every following fused step run one more round as if the speculation had
+ * failed at first_policy (-1: off).  Results must not change. */
+int sfx_debug_force_rerun(sfx_t h, int first_policy);
+/* Speculative rounds launched on the device per fused step (default 2).  Round r > 0
+ * re-derives every policy's next actions from round r-1's updated heads; a step whose
+ * last device round still flags a policy gets further rounds from sfx_step_finish. */
+int sfx_set_spec_rounds(sfx_t h, int rounds);
+/* Counters of fused steps: total, those that needed host-issued rounds, the policies
+ * still unverified after the device rounds, and all rounds run. */
+int sfx_step_stats(sfx_t h, long long* steps, long long* fallbacks, long long* rerun_policies, long long* rounds);
+
 /* LMS reward fit SF.update_reward (features/successor.py:164-167) on w_t:
  * w <- w + alpha (r - φ·w) φ ;  phi_dev [d], r_dev [1]. */
 int sfx_lms(sfx_t h, int t, const float* phi_dev, const float* r_dev, float alpha);
@@ -139,7 +172,7 @@ int sfx_sync_target(sfx_t h, int t);
 /*
  * Event instrumentation for the benchmark's roofline figure: while enabled, graphs are
  * bypassed and every kernel launch is bracketed by a hipEvent pair.  Kinds:
- * 0 forward, 1 TD target, 2 backward+Adam, 3 GPI, 4 LMS.  collect() returns the number of
+ * 0 forward, 1 TD target, 2 backward+Adam, 3 GPI, 4 LMS, 5 speculation check.  collect() returns the number of
  * launches of that kind, their summed event-measured duration (us) and their summed
  * ALGORITHMIC bytes (what the launch must read/write at minimum, fp32).
  */
@@ -148,6 +181,7 @@ int sfx_sync_target(sfx_t h, int t);
 #define SFX_K_BWD 2
 #define SFX_K_GPI 3
 #define SFX_K_LMS 4
+#define SFX_K_VER 5
 int sfx_prof_enable(sfx_t h, int enable);
 int sfx_prof_collect(sfx_t h, int kind, int* count, double* total_us, double* bytes);
 int sfx_prof_reset(sfx_t h);
