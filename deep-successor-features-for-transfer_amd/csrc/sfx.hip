@@ -397,8 +397,10 @@ int run_ver(sfx_handle* h, int M, int npol, bool sel, int post, const GpiArgs& g
   V.spec_next = h->spec_next;
   V.flag = &h->dout->flag;
   V.g = g;
-  launch(h, K_VER, 4.0 * (double)M * npol * h->T * h->O + 4.0 * h->T * h->O, k_ver, dim3(npol + 1), dim3(256),
-         h->G, V);
+  const int TA = h->T * h->A;
+  V.rows = TA >= 256 ? 1 : (256 / TA < M ? 256 / TA : M);
+  launch(h, K_VER, 4.0 * (double)M * npol * h->T * h->O + 4.0 * h->T * h->O, k_ver, dim3(npol + 1, cdiv(M, V.rows)),
+         dim3(256), h->G, V);
   LAUNCHCHK();
   return SFX_OK;
 }

@@ -744,20 +744,25 @@ __global__ __launch_bounds__(256) void k_gpi(Geo G, GpiArgs A) { gpi_row(G, A, b
 // Block npol (when sel): GPI action for s_next (row M of `post`) with w[select_task].
 // -------------------------------------------------------------------------------------
 struct VerArgs {
-  int M, npol, sel, spec_stride, post, pad_;
+  int M, npol, sel, spec_stride, post, rows;  // rows: minibatch rows per workgroup
   const int64_t* spec_next;  // [T][spec_stride]
   int* flag;
   GpiArgs g;                 // action selection for s_next
 };
 
+// Grid (npol + 1, ceil(M / rows)): one workgroup per (policy, `rows` minibatch rows), each
+// thread one q = ψ·w dot product, so every load is issued before the first reduction.
 __global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
   const int i = blockIdx.x, tid = threadIdx.x;
   if (i == V.npol) {
-    if (V.sel) gpi_row(G, V.g, 0);
+    if (V.sel && blockIdx.y == 0) gpi_row(G, V.g, 0);
     return;
   }
   if (i == 0) return;  // policy 0 sees only pre-update heads: always exact
-  const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, M = V.M;
+  const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, TA = T * Aa;
+  const int b0 = blockIdx.y * V.rows;
+  const int nb = V.M - b0 < V.rows ? V.M - b0 : V.rows;
+  if (nb <= 0) return;
   __shared__ float s_w[DMAX];
   __shared__ float s_q[QMAX];
   __shared__ int s_bad;
@@ -765,34 +770,30 @@ __global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
   for (int k = tid; k < d; k += 256) s_w[k] = wrow[k];
   if (tid == 0) s_bad = 0;
   __syncthreads();
-  const int rows = QMAX / (T * Aa) < 1 ? 1 : QMAX / (T * Aa);
-  for (int b0 = 0; b0 < M; b0 += rows) {
-    const int nb = M - b0 < rows ? M - b0 : rows;
-    for (int idx = tid; idx < nb * T * Aa; idx += 256) {
-      const int bl = idx / (T * Aa), rem = idx - bl * T * Aa, t = rem / Aa, a = rem - t * Aa;
-      const float* p = G.actp(t < i ? V.post : R_S1, t, NLm) + (size_t)(b0 + bl) * O + a * d;
-      float q = 0.f;
+  for (int idx = tid; idx < nb * TA; idx += 256) {
+    const int bl = idx / TA, rem = idx - bl * TA, t = rem / Aa, a = rem - t * Aa;
+    const float* p = G.actp(t < i ? V.post : R_S1, t, NLm) + (size_t)(b0 + bl) * O + a * d;
+    float q = 0.f;
 #pragma unroll 8
-      for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
-      s_q[idx] = q;
-    }
-    __syncthreads();
-    for (int bl = tid; bl < nb; bl += 256) {
-      const float* qb = s_q + bl * T * Aa;
-      int am = 0;
-      float best = -INFINITY;
-      for (int a = 0; a < Aa; ++a) {
-        float mx = qb[a];
-        for (int t = 1; t < T; ++t) mx = fmaxf(mx, qb[t * Aa + a]);
-        if (a == 0 || mx > best) {
-          best = mx;
-          am = a;
-        }
-      }
-      if (am != (int)V.spec_next[(size_t)i * V.spec_stride + b0 + bl]) s_bad = 1;
-    }
-    __syncthreads();
+    for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
+    s_q[idx] = q;
   }
+  __syncthreads();
+  for (int bl = tid; bl < nb; bl += 256) {
+    const float* qb = s_q + bl * TA;
+    int am = 0;
+    float best = -INFINITY;
+    for (int a = 0; a < Aa; ++a) {
+      float mx = qb[a];
+      for (int t = 1; t < T; ++t) mx = fmaxf(mx, qb[t * Aa + a]);
+      if (a == 0 || mx > best) {
+        best = mx;
+        am = a;
+      }
+    }
+    if (am != (int)V.spec_next[(size_t)i * V.spec_stride + b0 + bl]) s_bad = 1;
+  }
+  __syncthreads();
   if (tid == 0 && s_bad) atomicMin(V.flag, i);
 }
 
