@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--steps", type=int, default=2000)
     p.add_argument("--warmup", type=int, default=200)
     p.add_argument("--schedule", choices=["all", "active"], default="all")
+    p.add_argument("--loop", choices=["native", "python"], default="native",
+                   help="native: libsfx's C++ env-step runner (pipelined graphs); python: sfx.runner.EnvLoop")
     p.add_argument("--heads", type=int, default=8, help="source tasks (ψ heads) per GPU")
     p.add_argument("--batch", type=int, default=32)
     p.add_argument("--prof-steps", type=int, default=50)
@@ -130,7 +132,7 @@ def main():
 
     from sfx.engine import SFEngine
     from sfx.init import reference_heads
-    from sfx.runner import EnvLoop
+    from sfx.runner import EnvLoop, NativeEnvLoop
 
     T, B = args.heads, args.batch
     eng = SFEngine(T, SHAPE["n_s"], SHAPE["H"], SHAPE["A"], SHAPE["d"], SHAPE["acts"], max_batch=B, device=device)
@@ -141,8 +143,14 @@ def main():
         eng.load_w(t, w[t])
     eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
     eng.set_target_update_ev(1000)
-    loop = EnvLoop(eng, schedule=args.schedule, batch=B, seed=1 + rank)
-    loop.prefill(1000)
+    native = args.loop == "native" and args.schedule == "all"
+    if native:
+        loop = NativeEnvLoop(eng, batch=B, seed=1 + rank)
+        loop.prefill(1000)
+        loop.set_task(0)
+    else:
+        loop = EnvLoop(eng, schedule=args.schedule, batch=B, seed=1 + rank)
+        loop.prefill(1000)
 
     def barrier():
         torch.cuda.synchronize()
@@ -184,6 +192,8 @@ def main():
                     "share_of_gpu_time": round(us / max(sum(v[1] for v in stats.values()), 1e-9), 3),
                     "per_kind_avg_us": {KIND_NAMES[k]: round(v[1] / max(v[0], 1), 3) for k, v in stats.items() if v[0]}}
         spec_stats = eng.step_stats()
+        if native:
+            spec_stats.update(loop.stats())
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, args.cpu_seconds)
@@ -194,7 +204,8 @@ def main():
             "config": {"workload": workload + f" (Reacher-shape |s|=17 |a|=7 d=8, psi MLP 256x2, "
                                                f"{'all heads updated per env step: main_sfdqn_torch.py path' if args.schedule == 'all' else 'active head only: sfdqn.py path'})",
                        "heads_per_gpu": T, "global_batch": B * world, "parallelism": f"replica{world}" if world > 1 else "single",
-                       "loop": "python host loop over libsfx graphs"},
+                       "loop": ("native C++ runner (sfx_runner_run): host env + replay, one pre-launched gated hipGraph per env step"
+                                if native else "python host loop over libsfx graphs")},
             "roofline": roofline,
             "speculation": spec_stats,
             "cpu_baseline": cpu,
@@ -203,6 +214,8 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if native:
+        loop.close()
     eng.close()
 
 

@@ -19,7 +19,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <chrono>
 #include <map>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -89,6 +92,7 @@ struct sfx_handle {
   hipStream_t stream = nullptr;  // caller's stream: everything is ordered on it
   hipStream_t cap = nullptr;     // private stream used only to capture graphs
   bool use_graphs = true;
+  bool fuse_tdg = true;  // SFX_FUSE_TDG=0: K2 as its own launch
   AdamHP hp_psi{1e-3, 0.0, 0.9, 0.999, 1e-8};
   AdamHP hp_w{1e-3, 0.0, 0.9, 0.999, 1e-8};
   int target_update_ev = 1000;
@@ -282,6 +286,27 @@ int run_tdg(sfx_handle* h, int pol0, int npol, int guess, int M, int use_gpi, co
   return SFX_OK;
 }
 
+// K2 inputs for run_bwd: fused into the first backward launch when the 32-row LDS tiles fit,
+// else launched as k_tdg right before it.
+struct TdgSpec {
+  int use_gpi = 1, guess = R_S1, next_stride = 0;
+  const int64_t* a = nullptr;
+  const float* gamma = nullptr;
+  int64_t* next = nullptr;
+  int* flag = nullptr;
+};
+
+// 0: K2 as its own launch; 1: fused, d <= 8; 2: fused, d <= 16 (see tdg_rows)
+int tdg_variant(const sfx_handle* h) {
+  if (!h->fuse_tdg || (h->d & 3) != 0 || h->O > TDG_ROWS_O || h->A > 128) return 0;
+  const long ta = (long)h->T * h->A;
+  if (h->d <= 8 && 32 * ta <= 256 * 8) return 1;
+  if (h->d <= 16 && 32 * ta <= 256 * 4) return 2;
+  return 0;
+}
+
+bool can_fuse_tdg(const sfx_handle* h) { return tdg_variant(h) != 0; }
+
 struct BwdExtra {
   int inc_step = 1;
   bool fuse_v0 = false;  // post-update forward of layer 0 into vRole (rows S1 ++ s_next)
@@ -293,8 +318,22 @@ struct BwdExtra {
 bool can_fuse_v0(const sfx_handle* h) { return h->L[0].K <= KFUSE; }
 
 int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const float* phi, const float* r,
-            float* losses, const BwdExtra& ex = BwdExtra()) {
+            float* losses, const TdgSpec& td, const BwdExtra& ex = BwdExtra()) {
+  const bool fuse = can_fuse_tdg(h) && ((uintptr_t)phi & 15) == 0;  // fused K2 reads φ rows as float4
+  if (!fuse)
+    RC(run_tdg(h, head0, nhead, td.guess, M, td.use_gpi, td.a, phi, td.gamma, td.next, td.next_stride, td.flag));
   BwdArgs A{};
+  A.step_in_tail = fuse ? 0 : 1;
+  A.tdg_use_gpi = td.use_gpi;
+  A.tdg_guess = td.guess;
+  A.tdg_next_stride = td.next_stride;
+  A.tdg_a = td.a;
+  A.tdg_gamma = td.gamma;
+  A.tdg_next = td.next;
+  A.flag = td.flag;
+  A.flag_value = h->T;
+  const int tail_at = fuse ? 1 : 0;  // launch index of the loss tail (needs every row's loss)
+  const double tdg_bytes = 4.0 * nhead * M * ((td.use_gpi ? h->T : 1) * h->O + 2.0 * h->O + 2.0 * h->d + 4);
   A.M = M;
   A.head0 = head0;
   A.mask = h->mask;
@@ -331,7 +370,9 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     return 24.0 * ((double)L.N * L.K + L.N) + 4.0 * ((double)M * L.N + (double)M * L.K);
   };
   for (int l = h->NL - 1; l >= 1; --l) {
-    const double by = nhead * (dx_bytes(l) + (l + 1 <= h->NL - 1 ? dw_bytes(l + 1) : 0.0));
+    const int li = h->NL - 1 - l;
+    A.tdg = fuse && li == 0 ? 1 : 0;
+    const double by = nhead * (dx_bytes(l) + (l + 1 <= h->NL - 1 ? dw_bytes(l + 1) : 0.0)) + (A.tdg ? tdg_bytes : 0.0);
     A.ra = geo(l);
     A.na = cdiv(M, 32) * cdiv(h->L[l].K, 16);
     if (l + 1 <= h->NL - 1) {
@@ -341,15 +382,21 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
       A.nb = 0;
     }
     A.nc = 0;
-    A.tail = l == h->NL - 1 ? 1 : 0;  // loss / w / step in the first launch
-    launch(h, K_BWD, by, k_bwd, dim3(A.na + A.nb + A.nc + A.tail, nhead), dim3(256), h->G, A);
+    A.tail = li == tail_at ? 1 : 0;
+    if (A.tdg && tdg_variant(h) == 1)  // d <= 8
+      launch(h, K_BWD, by, k_bwd_tdg<2, 8>, dim3(A.na, nhead), dim3(256), h->G, A);
+    else if (A.tdg)
+      launch(h, K_BWD, by, k_bwd_tdg<4, 4>, dim3(A.na, nhead), dim3(256), h->G, A);
+    else
+      launch(h, K_BWD, by, k_bwd, dim3(A.na + A.nb + A.nc + A.tail, nhead), dim3(256), h->G, A);
   }
   A.na = 0;
+  A.tdg = 0;
   A.rb = geo(1);
   A.nb = dw_tiles(1);
   A.rc = geo(0);
   A.nc = dw_tiles(0);
-  A.tail = 0;
+  A.tail = h->NL - 1 == tail_at ? 1 : 0;
   A.fuse_v0 = ex.fuse_v0 ? 1 : 0;
   A.vM = M + (ex.v_xn ? 1 : 0);
   A.vOff = h->actOff[0];
@@ -357,7 +404,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.act0 = h->L[0].actOut;
   A.v_x = ex.v_x;
   A.v_xn = ex.v_xn;
-  launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), k_bwd, dim3(A.nb + A.nc, nhead), dim3(256), h->G, A);
+  launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), k_bwd, dim3(A.nb + A.nc + A.tail, nhead), dim3(256), h->G, A);
   LAUNCHCHK();
   return SFX_OK;
 }
@@ -463,20 +510,29 @@ inline int round_role(int r) { return (r & 1) ? R_V2 : R_V; }
 // One speculative round r of the all-task update: every policy takes its GPI next actions
 // with heads t < i seen through role `guess` (round 0: the pre-step heads), every head
 // updates from its read slot into its write slot, the post-update forward of S1 (++ s_next)
-// lands in round_role(r), and k_ver flags the first policy whose actions were wrong.
-int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r) {
+// lands in round_role(r).  Only a final round runs k_ver (flag the first policy whose actions
+// were wrong; action selection): an earlier round's verdict would be overwritten unread.
+int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final) {
   const int T = h->T, B = p.B;
   const int guess = r == 0 ? R_S1 : round_role(r - 1), out = round_role(r);
   const float* wsel = h->w + (size_t)p.task * h->dpad;
-  RC(run_tdg(h, 0, T, guess, B, p.use_gpi, p.a, p.phi, p.gamma, h->spec_next, MMAX, &h->dout->flag));
+  TdgSpec td;
+  td.use_gpi = p.use_gpi;
+  td.guess = guess;
+  td.a = p.a;
+  td.gamma = p.gamma;
+  td.next = h->spec_next;
+  td.next_stride = MMAX;
+  td.flag = &h->dout->flag;
   BwdExtra bx;
   bx.inc_step = r == 0 ? 1 : 0;  // later rounds redo the same optimizer step
   bx.fuse_v0 = can_fuse_v0(h);
   bx.vRole = out;
   bx.v_x = p.S1;
-  bx.v_xn = p.sel ? p.s_next : nullptr;
-  RC(run_bwd(h, 0, T, B, p.S, p.phi, nullptr, p.losses, bx));
-  const int vM = B + (p.sel ? 1 : 0);
+  const bool want_sel = p.sel && final;
+  bx.v_xn = want_sel ? p.s_next : nullptr;
+  RC(run_bwd(h, 0, T, B, p.S, p.phi, nullptr, p.losses, td, bx));
+  const int vM = B + (want_sel ? 1 : 0);
   if (bx.fuse_v0) {
     FwdExtra vx;
     vx.l0 = 1;
@@ -484,6 +540,7 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r) {
   } else {
     RC(run_fwd(h, {{out, P_NEW, 2, 0, T}}, B, p.S1, p.S1));
   }
+  if (!final) return SFX_OK;
   const bool sel = p.sel && bx.fuse_v0;
   const bool verify = p.use_gpi != 0;
   if (verify || sel)
@@ -516,7 +573,7 @@ int launch_step_all(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, c
                                p.sel_use_gpi, 1));
   }
   RC(run_fwd(h, {{R_S, P_ONLINE, 1, 0, T}, {R_S1T, P_TARGET, 2, 0, T}, {R_S1, P_ONLINE, 2, 0, T}}, B, p.S, p.S1, ex));
-  for (int r = 0; r < rounds; ++r) RC(launch_round(h, p, r));
+  for (int r = 0; r < rounds; ++r) RC(launch_round(h, p, r, r == rounds - 1));
   return SFX_OK;
 }
 
@@ -554,6 +611,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->dpad = align4(d);
   const char* eg = std::getenv("SFX_GRAPHS");
   h->use_graphs = !(eg && eg[0] == '0');
+  const char* ef = std::getenv("SFX_FUSE_TDG");
+  h->fuse_tdg = !(ef && ef[0] == '0');
   int off = 0, ptorch = 0;
   for (int l = 0; l < h->NL; ++l) {
     LayerGeo Lr{};
@@ -786,8 +845,13 @@ int sfx_update(sfx_t h, int policy, const float* S, const int64_t* a, const floa
     else
       RC(run_fwd(h, {{R_S, P_ONLINE, 1, policy, 1}, {R_S1T, P_TARGET, 2, policy, 1}, {R_S1, P_ONLINE, 2, policy, 1}},
                  B, S, S1));
-    RC(run_tdg(h, policy, 1, R_S1, B, use_gpi, a, phi, gamma, next, B));
-    return run_bwd(h, policy, 1, B, S, phi, r, losses);
+    TdgSpec td;
+    td.use_gpi = use_gpi;
+    td.a = a;
+    td.gamma = gamma;
+    td.next = next;
+    td.next_stride = B;
+    return run_bwd(h, policy, 1, B, S, phi, r, losses, td);
   }));
   h->mask ^= 1ull << policy;
   after_update(h, policy);
@@ -851,7 +915,7 @@ int sfx_step_finish(sfx_t h, int64_t* out_host) {
     // more rounds until every policy's next actions are verified (each round fixes >= 1 head)
     while (first < h->T) {
       if (r > h->T + 1) SFX_FAIL(SFX_E_STATE, "speculation did not converge");
-      RC(launch_round(h, p, r));
+      RC(launch_round(h, p, r, true));
       HIPCHK(hipMemcpyAsync(h->hout, h->dout, sizeof(StepOut), hipMemcpyDeviceToHost, h->stream));
       HIPCHK(hipStreamSynchronize(h->stream));
       ++r;
@@ -978,3 +1042,5 @@ int sfx_synchronize(sfx_t h) {
 }
 
 }  // extern "C"
+
+#include "sfx_runner.inc"

@@ -32,6 +32,7 @@ constexpr int OMAX = 4096;    // A*d (row of a ψ output) held in LDS
 constexpr int DMAX = 256;     // feature dimension d
 constexpr int MMAX = 1024;    // rows of one update
 constexpr int KFUSE = 64;     // layer-0 fan-in up to which the post-update forward is fused
+constexpr int TQF = 4096;     // 32 rows x (T*A) q values / 32 rows x A*d gradients of the fused TD target
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2 };
 // activation-block roles: ψ(S) online (saved for backward), ψ⁻(S1) target, ψ(S1) online
@@ -405,6 +406,12 @@ struct RoleGeo {
 
 struct BwdArgs {
   int M, na, nb, nc, tail, head0, train_w, inc_step;
+  int step_in_tail;             // 1: the tail bumps the Adam step; 0: dX tile 0 of this launch does
+  int tdg, tdg_use_gpi, tdg_guess, tdg_next_stride, flag_value, pad2_;  // fused TD target (K2)
+  const int64_t* tdg_a;
+  const float* tdg_gamma;
+  int64_t* tdg_next;
+  int* flag;
   int fuse_v0, vM, vOff, act0;  // fused forward: rows (S1 ++ s_next), layer-0 offset, layer-0 act
   int vRole, pad_;              // role block the fused forward writes
   unsigned long long mask;
@@ -422,13 +429,147 @@ __device__ __forceinline__ const float* layer_input(const Geo& G, const BwdArgs&
   return xOff < 0 ? A.x0 : G.actp(R_S, head, xOff);
 }
 
+// K2 fused into the first backward launch: the TD target and output gradient of the 32 rows
+// m0.. of policy `pol` (the arithmetic of k_tdg, in the same order), left in LDS (s.dz, row
+// stride O) for this tile's dX.  The k-tile 0 workgroup of each row tile also publishes dZ,
+// the per-row losses and the next actions for the later launches.
+// Every global load is issued in stage A (one memory latency); stages B-E run from LDS.
+// Shapes (can_fuse_tdg): d = 4V <= 4 VMAX, 32·T·A <= 256 U, A·d <= 128.
+constexpr int TDG_ROWS_O = 128;  // max A*d of a fused row tile
+struct TdgSmem {
+  float w[32], gam[32], ph[32 * 16];
+  int a[32], n[32];
+  float q[2048], m[32 * 128];
+  float tt[32 * TDG_ROWS_O], tc[32 * TDG_ROWS_O];
+  float dz[32 * TDG_ROWS_O];
+};
+
+template <int VMAX, int U>
+__device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pub, TdgSmem& sm) {
+  const int tid = threadIdx.x, T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, M = A.M;
+  const int nb = M - m0 < 32 ? M - m0 : 32;
+  const int t0 = A.tdg_use_gpi ? 0 : pol, nt = A.tdg_use_gpi ? T : 1, TA = nt * Aa, n = nb * TA, V = d >> 2;
+  const int guess = A.tdg_guess;
+  // ---- stage A: all global loads
+  float4 v[U][VMAX];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int idx = tid + u * 256;
+    const bool ok = idx < n;
+    const int bl = idx / TA, rem = idx - bl * TA, t = t0 + rem / Aa, a = rem - (rem / Aa) * Aa;
+    const float4* p = reinterpret_cast<const float4*>(G.actp(t < pol ? guess : R_S1, ok ? t : 0, NLm) +
+                                                      (ok ? (size_t)(m0 + bl) * O + a * d : 0));
+#pragma unroll
+    for (int j = 0; j < VMAX; ++j) v[u][j] = (ok && j < V) ? p[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int n4 = (nb * O) >> 2;  // row tiles are whole float4s (O % 4 == 0)
+  const float4* tg4 = reinterpret_cast<const float4*>(G.actp(R_S1T, pol, NLm) + (size_t)m0 * O);
+  const float4* cu4 = reinterpret_cast<const float4*>(G.actp(R_S, pol, NLm) + (size_t)m0 * O);
+  float4 tt[4], tc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = tid + u * 256;
+    tt[u] = i < n4 ? tg4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    tc[u] = i < n4 ? cu4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int np4 = (nb * d) >> 2;
+  const float4 ph = tid < np4 ? reinterpret_cast<const float4*>(A.phi + (size_t)m0 * d)[tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float wk = tid < d ? G.w[(long long)pol * G.dpad + tid] : 0.f;
+  const int ab_l = tid < nb ? (int)A.tdg_a[m0 + tid] : 0;
+  const float gam_l = tid < nb ? A.tdg_gamma[m0 + tid] : 0.f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = tid + u * 256;
+    if (i < n4) {
+      reinterpret_cast<float4*>(sm.tt)[i] = tt[u];
+      reinterpret_cast<float4*>(sm.tc)[i] = tc[u];
+    }
+  }
+  if (tid < np4) reinterpret_cast<float4*>(sm.ph)[tid] = ph;
+  if (tid < d) sm.w[tid] = wk;
+  if (tid < nb) {
+    sm.a[tid] = ab_l;
+    sm.gam[tid] = gam_l;
+  }
+  __syncthreads();
+  // ---- stage B: q = ψ·w, one fmaf chain per dot in k order
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int idx = tid + u * 256;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < VMAX; ++j) {
+      if (j < V) {
+        q = __builtin_fmaf(v[u][j].x, sm.w[4 * j], q);
+        q = __builtin_fmaf(v[u][j].y, sm.w[4 * j + 1], q);
+        q = __builtin_fmaf(v[u][j].z, sm.w[4 * j + 2], q);
+        q = __builtin_fmaf(v[u][j].w, sm.w[4 * j + 3], q);
+      }
+    }
+    if (idx < n) sm.q[idx] = q;
+  }
+  __syncthreads();
+  // ---- stage C: max over heads per (row, action)   (torch.max(q1, axis=1))
+  for (int i = tid; i < nb * Aa; i += 256) {
+    const int bl = i / Aa, a = i - bl * Aa;
+    const float* qb = sm.q + bl * TA + a;
+    float mx = qb[0];
+    for (int t = 1; t < nt; ++t) mx = fmaxf(mx, qb[t * Aa]);
+    sm.m[i] = mx;
+  }
+  __syncthreads();
+  // ---- stage D: first argmax over actions
+  for (int bl = tid; bl < nb; bl += 256) {
+    const float* mb = sm.m + bl * Aa;
+    int am = 0;
+    float qm = mb[0];
+    for (int a = 1; a < Aa; ++a)
+      if (mb[a] > qm) {
+        qm = mb[a];
+        am = a;
+      }
+    sm.n[bl] = am;
+    if (pub && A.tdg_next) A.tdg_next[(size_t)(pol - A.head0) * A.tdg_next_stride + m0 + bl] = am;
+  }
+  __syncthreads();
+  // ---- stage E: output gradient rows (nonzero only at the taken action) and row losses
+  const float norm = (float)(2.0 / ((double)M * (double)O));
+  float* gout = G.dzp(pol, NLm) + (size_t)m0 * O;
+  for (int i = tid; i < nb * O; i += 256) {
+    const int bl = i / O, o = i - bl * O, ab = sm.a[bl];
+    float gv = 0.f;
+    if (ab >= 0 && ab < Aa && o >= ab * d && o < ab * d + d) {
+      const int k = o - ab * d;
+      const float tg = __fadd_rn(sm.ph[bl * d + k], __fmul_rn(sm.gam[bl], sm.tt[bl * O + sm.n[bl] * d + k]));
+      gv = __fmul_rn(norm, __fsub_rn(sm.tc[i], tg));
+    }
+    sm.dz[i] = gv;
+    if (pub) gout[i] = gv;
+  }
+  if (pub) {
+    for (int bl = tid; bl < nb; bl += 256) {  // row Σ diff^2 in feature order
+      const int ab = sm.a[bl];
+      float sacc = 0.f;
+      if (ab >= 0 && ab < Aa) {
+        for (int k = 0; k < d; ++k) {
+          const float diff = __fsub_rn(sm.tc[bl * O + ab * d + k],
+                                       __fadd_rn(sm.ph[bl * d + k], __fmul_rn(sm.gam[bl], sm.tt[bl * O + sm.n[bl] * d + k])));
+          sacc = __fadd_rn(sacc, __fmul_rn(diff, diff));
+        }
+      }
+      G.rowloss[(long long)pol * MMAX + m0 + bl] = sacc;
+    }
+  }
+  __syncthreads();
+}
+
+template <bool TDG, int VMAX = 2, int U = 8>
 __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floatx4 (*red)[2][64]) {
   const RoleGeo L = A.ra;
   const int N = L.N, K = L.K, M = A.M;
   const int ntk = (K + 15) >> 4;
   const int k0 = (tile % ntk) * 16, m0 = (tile / ntk) * 32;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
-  const float* dZ = G.dzp(head, L.dzOff);
   const float* W = G.online + G.slot_off(rslot(A.mask, head), head) + L.wOff;
   const float* Xin = layer_input(G, A, head, L.xOff);
   float* out = G.dzp(head, L.dzIn);
@@ -445,18 +586,41 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
     }
   }
   floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  const bool vec = (N & 63) == 0;
-  for (int nc = wave * 64; nc < N; nc += 256) {
-    const int nb = nc + g * 16;
-    float a0[16], a1[16], bw[16];
-    load16u(a0, dZ + (size_t)ma * N, nb, N, oka, vec);
-    load16u(a1, dZ + (size_t)mb * N, nb, N, okb, vec);
+  if constexpr (TDG) {
+    // N = A*d <= 128: at most one 64-wide chunk per wave; its W slice is fetched before K2
+    __shared__ TdgSmem sm;
+    if (tile == 0 && A.inc_step && threadIdx.x == 0) G.step[head] += 1;  // no dW reads it in this launch
+    if (A.flag && tile == 0 && blockIdx.y == 0 && threadIdx.x == 0) *A.flag = A.flag_value;
+    const int nb = wave * 64 + g * 16;
+    float bw[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) bw[j] = (okk && nb + j < N) ? W[(size_t)(nb + j) * K + kk] : 0.f;
+    tdg_rows<VMAX, U>(G, A, head, m0, tile % ntk == 0, sm);
+    if (wave * 64 < N) {
+      float a0[16], a1[16];
+      load16u(a0, sm.dz + (size_t)r * N, nb, N, oka, false);
+      load16u(a1, sm.dz + (size_t)(16 + r) * N, nb, N, okb, false);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      acc0 = mfma4(a0[j], bw[j], acc0);
-      acc1 = mfma4(a1[j], bw[j], acc1);
+      for (int j = 0; j < 16; ++j) {
+        acc0 = mfma4(a0[j], bw[j], acc0);
+        acc1 = mfma4(a1[j], bw[j], acc1);
+      }
+    }
+  } else {
+    const float* dZ = G.dzp(head, L.dzOff);
+    const bool vec = (N & 63) == 0;
+    for (int nc = wave * 64; nc < N; nc += 256) {
+      const int nb = nc + g * 16;
+      float a0[16], a1[16], bw[16];
+      load16u(a0, dZ + (size_t)ma * N, nb, N, oka, vec);
+      load16u(a1, dZ + (size_t)mb * N, nb, N, okb, vec);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) bw[j] = (okk && nb + j < N) ? W[(size_t)(nb + j) * K + kk] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        acc0 = mfma4(a0[j], bw[j], acc0);
+        acc1 = mfma4(a1[j], bw[j], acc1);
+      }
     }
   }
   red[wave][0][lane] = acc0;
@@ -598,7 +762,7 @@ __device__ void role_tail(const Geo& G, const BwdArgs& A, int head) {
   const int M = A.M, d = G.d, tid = threadIdx.x;
   __shared__ float s_e[MMAX];
   __shared__ float s_x[1];
-  const int step = A.inc_step ? G.step[head] + 1 : G.step[head];
+  const int step = A.step_in_tail && A.inc_step ? G.step[head] + 1 : G.step[head];
   const float* rl = G.rowloss + (long long)head * MMAX;
   float* w = G.w + (long long)head * G.dpad;
   float l2 = 0.f;
@@ -635,7 +799,7 @@ __device__ void role_tail(const Geo& G, const BwdArgs& A, int head) {
       lo[1] = l1;
       lo[2] = l2;
     }
-    G.step[head] = step;
+    if (A.step_in_tail) G.step[head] = step;
   }
 }
 
@@ -644,7 +808,7 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
   const int head = A.head0 + blockIdx.y;
   int bx = blockIdx.x;
   if (bx < A.na) {
-    role_dx(G, A, head, bx, red);
+    role_dx<false>(G, A, head, bx, red);
     return;
   }
   bx -= A.na;
@@ -658,6 +822,13 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
     return;
   }
   role_tail(G, A, head);
+}
+
+// First backward launch with K2 fused: dX of the last layer only (A.na tiles per head).
+template <int VMAX, int U>
+__global__ __launch_bounds__(256) void k_bwd_tdg(Geo G, BwdArgs A) {
+  __shared__ floatx4 red[4][2][64];
+  role_dx<true, VMAX, U>(G, A, A.head0 + blockIdx.y, blockIdx.x, red);
 }
 
 // -------------------------------------------------------------------------------------
@@ -813,6 +984,66 @@ __global__ void k_lms(float* __restrict__ w, const float* __restrict__ phi, cons
   }
   __syncthreads();
   if (tid < d) w[tid] = __fadd_rn(wk, __fmul_rn(s_e, pk));
+}
+
+}  // namespace sfx
+
+namespace sfx {
+
+// -------------------------------------------------------------------------------------
+// Env-step runner plumbing (sfx_runner_*): the host prepares step j's inputs in pinned,
+// host-coherent memory and bumps `go`; the graph of step j -- launched ahead, while step
+// j-1 still runs -- opens with k_gate, which waits for go >= seq and copies the inputs into
+// device memory, and closes with k_publish, which posts the selected action and the
+// speculation verdict back to host memory.  Every spin is bounded by `timeout` ticks of
+// the 100 MHz wall clock; on expiry the gate records the failure and lets the launch drain.
+// -------------------------------------------------------------------------------------
+struct GateArgs {
+  const uint4* src;  // host-coherent staging
+  uint4* dst;        // device staging
+  int n16;           // 16-byte words
+  int pad_;
+  const long long* go;  // host-coherent: last step whose inputs the host has written
+  long long* dctr;      // device: last step a gate opened (this gate opens dctr + 1)
+  long long timeout;
+  int* err;             // host-coherent
+};
+
+__global__ __launch_bounds__(256) void k_gate(GateArgs g) {
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    ok = 1;
+    const long long want = *g.dctr + 1;
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(g.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+      if (wall_clock64() - t0 > g.timeout) {
+        ok = 0;
+        __hip_atomic_store(g.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    *g.dctr = want;
+  }
+  __syncthreads();
+  if (!ok) return;
+  for (int i = threadIdx.x; i < g.n16; i += 256) g.dst[i] = g.src[i];
+}
+
+struct HostResult {  // host-coherent; seq written last
+  long long sel0, sel1;
+  int flag, err;
+  long long seq;
+};
+
+__global__ void k_publish(const int64_t* sel, const int* flag, HostResult* out, const long long* dctr) {
+  if (threadIdx.x == 0) {
+    out->sel0 = sel[0];
+    out->sel1 = sel[1];
+    out->flag = *flag;
+    __threadfence_system();
+    __hip_atomic_store(&out->seq, *dctr, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 }  // namespace sfx

@@ -51,7 +51,24 @@ SIGNATURES = {
     "sfx_prof_collect": (_I, [_VP, _I, _IP, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "sfx_prof_reset": (_I, [_VP]),
     "sfx_synchronize": (_I, [_VP]),
+    "sfx_runner_create": (_I, [C.POINTER(_VP), _VP, _I, _I, _F, _F, _F, _I, _I, C.c_ulonglong, _VP, _VP, _VP]),
+    "sfx_runner_destroy": (_I, [_VP]),
+    "sfx_runner_layout": (_I, [_VP, C.POINTER(C.c_int64)]),
+    "sfx_runner_set_task": (_I, [_VP, _I]),
+    "sfx_runner_prefill": (_I, [_VP, _I]),
+    "sfx_runner_run": (_I, [_VP, _I]),
+    "sfx_runner_action": (_I, [_VP, C.POINTER(C.c_int64)]),
+    "sfx_runner_stats": (_I, [_VP] + [C.POINTER(C.c_longlong)] * 3 + [C.POINTER(C.c_double)]),
+    "sfx_runner_gpi_counters": (_I, [_VP, C.POINTER(C.c_longlong)]),
+    "sfx_runner_record": (_I, [_VP, _I]),
+    "sfx_runner_recorded": (_I, [_VP]),
+    "sfx_runner_get_record": (_I, [_VP, _I, _VP, C.POINTER(C.c_int64)]),
 }
+
+# env callbacks of sfx_runner_create (include/sfx.h)
+ENV_RESET_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_float))
+ENV_STEP_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                          C.POINTER(C.c_float), C.POINTER(C.c_int))
 
 
 class SFXError(RuntimeError):

@@ -200,3 +200,125 @@ class EnvLoop:
     def run(self, n: int):
         for _ in range(n):
             self.step()
+
+
+class NativeEnvLoop:
+    """The same all-task env-step loop as EnvLoop(schedule="all"), run by libsfx's native
+    runner (include/sfx.h, sfx_runner_*): C++ env + replay ring on the host, one pre-launched
+    hipGraph per env step whose gate kernel waits for the host's inputs.
+
+    env: None for the built-in synthetic Reacher-shape task, or an object with
+    ``reset(task) -> s0`` and ``step(task, a) -> (s1, phi, r, terminal)`` (numpy / floats),
+    called through C callbacks (agents/agent.py's Task interface: tasks/task.py).
+    """
+
+    FIELDS = ("s", "s1", "phi", "a", "gamma", "snext", "phi1", "r1")
+
+    def __init__(self, engine: SFEngine, batch: int = 32, capacity: int = 1_000_000, gamma: float = 0.9,
+                 epsilon: float = 0.1, alpha_w: float = 1e-3, episode_len: int = 500, use_gpi: bool = True,
+                 seed: int = 1, env=None):
+        import ctypes as C
+
+        from ._lib import ENV_RESET_FN, ENV_STEP_FN, check, lib
+
+        self.eng, self.B, self._lib, self._check, self._C = engine, batch, lib, check, C
+        self._cbs = None
+        reset_fn = step_fn = None
+        if env is not None:
+            n_s, d = engine.n_s, engine.d
+
+            def _reset(_ctx, task, s0):
+                try:
+                    v = np.asarray(env.reset(task), dtype=np.float32).reshape(n_s)
+                    np.ctypeslib.as_array(s0, shape=(n_s,))[:] = v
+                    return 0
+                except Exception:  # reported as a failed step by libsfx
+                    return 1
+
+            def _step(_ctx, task, a, s1, phi, r, term):
+                try:
+                    ns, ph, rr, tt = env.step(task, a)
+                    np.ctypeslib.as_array(s1, shape=(n_s,))[:] = np.asarray(ns, np.float32).reshape(n_s)
+                    np.ctypeslib.as_array(phi, shape=(d,))[:] = np.asarray(ph, np.float32).reshape(d)
+                    r[0] = float(rr)
+                    term[0] = 1 if tt else 0
+                    return 0
+                except Exception:
+                    return 1
+
+            self._cbs = (ENV_RESET_FN(_reset), ENV_STEP_FN(_step))
+            reset_fn, step_fn = self._cbs
+        r = C.c_void_p()
+        check(lib.sfx_runner_create(C.byref(r), engine._h, batch, capacity, gamma, epsilon, alpha_w, episode_len,
+                                    1 if use_gpi else 0, seed, C.cast(reset_fn, C.c_void_p) if reset_fn else None,
+                                    C.cast(step_fn, C.c_void_p) if step_fn else None, None), "sfx_runner_create")
+        self._r = r
+        off = (C.c_int64 * 9)()
+        check(lib.sfx_runner_layout(r, off), "sfx_runner_layout")
+        self.layout = {k: int(off[i]) for i, k in enumerate(self.FIELDS)}
+        self.record_bytes = int(off[8])
+        self.task_index = 0
+
+    def close(self):
+        if getattr(self, "_r", None):
+            self._lib.sfx_runner_destroy(self._r)
+            self._r = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_task(self, index: int):
+        self._check(self._lib.sfx_runner_set_task(self._r, index), "sfx_runner_set_task")
+        self.task_index = index
+
+    def prefill(self, n: int):
+        self._check(self._lib.sfx_runner_prefill(self._r, n), "sfx_runner_prefill")
+
+    def run(self, n: int):
+        self._check(self._lib.sfx_runner_run(self._r, n), "sfx_runner_run")
+
+    def action(self):
+        out = (self._C.c_int64 * 3)()
+        self._check(self._lib.sfx_runner_action(self._r, out), "sfx_runner_action")
+        return int(out[0]), int(out[1])
+
+    def stats(self) -> dict:
+        C = self._C
+        a, b, c, w = C.c_longlong(), C.c_longlong(), C.c_longlong(), C.c_double()
+        self._check(self._lib.sfx_runner_stats(self._r, C.byref(a), C.byref(b), C.byref(c), C.byref(w)),
+                    "sfx_runner_stats")
+        return {"env_steps": a.value, "prelaunched": b.value, "host_round_steps": c.value,
+                "host_wait_us": round(w.value, 1)}
+
+    def gpi_counters(self) -> np.ndarray:
+        T = self.eng.T
+        out = np.zeros(T * T, dtype=np.int64)
+        self._check(self._lib.sfx_runner_gpi_counters(self._r, out.ctypes.data_as(self._C.POINTER(self._C.c_longlong))),
+                    "sfx_runner_gpi_counters")
+        return out.reshape(T, T)
+
+    def record(self, capacity: int):
+        self._check(self._lib.sfx_runner_record(self._r, capacity), "sfx_runner_record")
+
+    def records(self) -> list:
+        """Decoded input records: dict of numpy arrays + (task, have, c, a_greedy, a, terminal)."""
+        C, e, B = self._C, self.eng, self.B
+        shapes = {"s": ((B, e.n_s), np.float32), "s1": ((B, e.n_s), np.float32), "phi": ((B, e.d), np.float32),
+                  "a": ((B,), np.int64), "gamma": ((B,), np.float32), "snext": ((e.n_s,), np.float32),
+                  "phi1": ((e.d,), np.float32), "r1": ((1,), np.float32)}
+        out = []
+        for i in range(self._lib.sfx_runner_recorded(self._r)):
+            buf = np.zeros(self.record_bytes, dtype=np.uint8)
+            meta = (C.c_int64 * 6)()
+            self._check(self._lib.sfx_runner_get_record(self._r, i, buf.ctypes.data_as(C.c_void_p), meta),
+                        "sfx_runner_get_record")
+            rec = {}
+            for k, (shape, dt) in shapes.items():
+                n = int(np.prod(shape)) * np.dtype(dt).itemsize
+                rec[k] = buf[self.layout[k]:self.layout[k] + n].view(dt).reshape(shape).copy()
+            rec.update(zip(("task", "have", "c", "a_greedy", "a_taken", "terminal"), (int(m) for m in meta)))
+            out.append(rec)
+        return out

@@ -189,6 +189,48 @@ int sfx_prof_reset(sfx_t h);
 /* Block the host until all work queued on the handle's stream is done. */
 int sfx_synchronize(sfx_t h);
 
+/* ---------------------------------------------------------------------------------------
+ * Native env-step runner (replaces the Python loop of Agent.next_sample + SFDQN.train_agent,
+ * agents/agent.py:195-261 with agents/sfdqn.py:39-60, for the all-task schedule of
+ * main_sfdqn_torch.py).  The env and the replay ring stay on the host; each env step's device
+ * work is one pre-launched hipGraph whose first kernel waits for the host's inputs.
+ * Env callbacks (both or neither; NULL = built-in synthetic Reacher-shape task: s ~ N(0,1),
+ * φ ~ U[0,1), r = φ[task % d], never terminal):
+ *   reset(ctx, task, s0_host[n_s]);  step(ctx, task, action, s1_host[n_s], phi_host[d],
+ *   r_host[1], terminal_host[1]);  return 0 on success.
+ * ------------------------------------------------------------------------------------- */
+typedef struct sfx_runner* sfx_runner_t;
+typedef int (*sfx_env_reset_fn)(void* ctx, int task, float* s0_host);
+typedef int (*sfx_env_step_fn)(void* ctx, int task, int action, float* s1_host, float* phi_host,
+                               float* r_host, int* terminal_host);
+
+/* batch: minibatch rows (buffer n_batch); capacity: replay ring size; gamma: discount of
+ * non-terminal transitions; epsilon: ε-greedy rate; alpha_w: LMS rate of update_reward;
+ * episode_len: T of the env episode; sel_use_gpi: GPI (1) or own-task (0) action choice. */
+int sfx_runner_create(sfx_runner_t* out, sfx_t h, int batch, int capacity, float gamma, float epsilon,
+                      float alpha_w, int episode_len, int sel_use_gpi, unsigned long long seed,
+                      sfx_env_reset_fn reset_fn, sfx_env_step_fn step_fn, void* env_ctx);
+int sfx_runner_destroy(sfx_runner_t r);
+/* byte offsets of one step's input record: s, s1, phi, a(int64), gamma, s_next, phi1, r1, total */
+int sfx_runner_layout(sfx_runner_t r, int64_t* offsets_host /* [9] */);
+/* Agent.set_active_training_task (agents/agent.py:121-139): reset the env, select the first action */
+int sfx_runner_set_task(sfx_runner_t r, int task);
+/* n random transitions into the replay (warm-up; not env steps) */
+int sfx_runner_prefill(sfx_runner_t r, int n);
+/* n env steps; returns with every step finished */
+int sfx_runner_run(sfx_runner_t r, int n);
+/* [GPI task c, greedy action, active task] for the current state */
+int sfx_runner_action(sfx_runner_t r, int64_t* out_host /* [3] */);
+int sfx_runner_stats(sfx_runner_t r, long long* env_steps, long long* prelaunched, long long* host_round_steps,
+                     double* wait_us);
+/* SF.gpi_counters (features/successor.py:270-272): [T][T] counts of the GPI task per active task */
+int sfx_runner_gpi_counters(sfx_runner_t r, long long* out_host /* [T*T] */);
+/* test hooks: keep the input record and (task, have_batch, c, greedy a, taken a, terminal) of
+ * the next `capacity` steps */
+int sfx_runner_record(sfx_runner_t r, int capacity);
+int sfx_runner_recorded(sfx_runner_t r);
+int sfx_runner_get_record(sfx_runner_t r, int i, void* stage_host, int64_t* meta_host /* [6] */);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,133 @@
+"""GPU parity of the native env-step runner (sfx_runner_*, pipelined graphs with gate kernels)
+against the oracle replaying the runner's own recorded inputs.
+
+Each recorded step holds what the host handed the device: the minibatch, the LMS transition
+(φ, r) and the next state.  The oracle applies them in the reference's order (LMS,
+agents/sfdqn.py:51; all-task update, :57-60; GPI action for the next state, :39-45) and must
+reproduce the greedy action the runner recorded at the following step, the final heads,
+the reward weights and the target nets.  Tolerances as in test_gpu_engine.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_cpu as R
+from tests.conftest import gpu_available
+from tests.test_gpu_engine import params_close, rel_close
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if not gpu_available():
+        pytest.skip("no HIP device")
+
+
+def make(spec, T, ev, seed=0, max_batch=16):
+    from sfx.engine import SFEngine
+    from sfx.init import reference_heads
+
+    online, w = reference_heads(T, spec.n_s, spec.H, spec.A, spec.d, spec.acts, seed=seed)
+    eng = SFEngine(T, spec.n_s, spec.H, spec.A, spec.d, spec.acts, max_batch=max_batch)
+    eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
+    eng.set_target_update_ev(ev)
+    for t in range(T):
+        eng.load_head(t, online[t], 0)
+        eng.load_head(t, online[t], 1)
+        eng.load_w(t, w[t])
+    return eng, R.SFState(spec, online.clone(), online.clone(), w.clone())
+
+
+def replay_with_oracle(st, spec, recs, alpha, ev, final_action):
+    for k, rec in enumerate(recs):
+        task = rec["task"]
+        st.w[task] = R.lms_update(st.w[task].view(-1, 1), torch.from_numpy(rec["phi1"]), float(rec["r1"][0]),
+                                  alpha).view(-1)
+        if rec["have"]:
+            batch = (torch.from_numpy(rec["s"]), torch.from_numpy(rec["a"]), torch.from_numpy(rec["phi"]),
+                     torch.from_numpy(rec["s1"]), torch.from_numpy(rec["gamma"]))
+            R.deep_all_task_step(st, batch, lr=1e-3, target_update_ev=ev)
+        q, tk = R.gpi_w(R.psi_all(st.online, spec, torch.from_numpy(rec["snext"]).view(1, -1)), st.w[task])
+        want = (int(tk[0]), R.select_action(q, tk[0], task, True))
+        got = (recs[k + 1]["c"], recs[k + 1]["a_greedy"]) if k + 1 < len(recs) else final_action
+        assert got == want, f"step {k}: runner selected {got}, oracle {want}"
+
+
+def check_state(eng, st, T, k):
+    params_close(torch.stack([eng.get_head(t, 0) for t in range(T)]), st.online, 1e-3 * k)
+    params_close(torch.stack([eng.get_head(t, 1) for t in range(T)]), st.target, 1e-3 * k)
+    rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("pipeline", [True, False])
+def test_runner_matches_oracle(pipeline, monkeypatch):
+    from sfx.runner import NativeEnvLoop
+
+    if not pipeline:
+        monkeypatch.setenv("SFX_RUNNER_PIPELINE", "0")
+    spec = R.Spec(17, 32, 7, 8, ("relu", "relu"))
+    T, ev, alpha, n = 3, 4, 0.05, 24
+    eng, st = make(spec, T, ev)
+    loop = NativeEnvLoop(eng, batch=16, capacity=200, gamma=0.9, epsilon=0.3, alpha_w=alpha, episode_len=7, seed=5)
+    loop.prefill(10)  # first 5 env steps run without a minibatch (replay < batch)
+    loop.set_task(1)
+    first = loop.action()
+    loop.record(n)
+    loop.run(n)
+    recs = loop.records()
+    assert len(recs) == n and (recs[0]["c"], recs[0]["a_greedy"]) == first
+    assert [r["have"] for r in recs[:6]] == [0, 0, 0, 0, 0, 1]
+    replay_with_oracle(st, spec, recs, alpha, ev, loop.action())
+    check_state(eng, st, T, n)
+    stats = loop.stats()
+    assert stats["env_steps"] == n
+    if pipeline:
+        assert stats["prelaunched"] > n // 2
+    else:
+        assert stats["prelaunched"] == 0
+    counts = loop.gpi_counters()
+    assert counts.sum() == n and counts[1].sum() == n
+    loop.close()
+    eng.close()
+
+
+def test_runner_with_python_env_callbacks():
+    """A host env passed as callbacks (tasks/task.py interface) drives the same loop."""
+    from sfx.runner import NativeEnvLoop
+
+    class CountingEnv:
+        def __init__(self, n_s, d):
+            self.n_s, self.d, self.t, self.actions = n_s, d, 0, []
+
+        def reset(self, task):
+            return np.full(self.n_s, 0.1 * task, np.float32)
+
+        def step(self, task, a):
+            self.t += 1
+            self.actions.append(a)
+            s1 = np.linspace(-1, 1, self.n_s).astype(np.float32) * np.float32(self.t % 5)
+            phi = np.full(self.d, 0.01 * (self.t % 7), np.float32)
+            return s1, phi, float(phi.sum()), self.t % 9 == 0
+
+    spec = R.Spec(6, 16, 3, 4, ("relu", "relu"))
+    T, ev, alpha, n = 2, 1000, 0.02, 14
+    eng, st = make(spec, T, ev, max_batch=8)
+    env = CountingEnv(spec.n_s, spec.d)
+    loop = NativeEnvLoop(eng, batch=8, capacity=64, gamma=0.95, epsilon=0.0, alpha_w=alpha, episode_len=100, seed=3,
+                         env=env)
+    loop.prefill(8)
+    loop.set_task(0)
+    env.actions.clear()
+    loop.record(n)
+    loop.run(n)
+    recs = loop.records()
+    assert [r["a_taken"] for r in recs] == env.actions  # ε = 0: the greedy actions went to the env
+    assert [r["terminal"] for r in recs] == [int((8 + i + 1) % 9 == 0) for i in range(n)]
+    for r in recs:
+        if r["have"]:
+            assert set(np.unique(r["gamma"])) <= {np.float32(0.95), np.float32(0.0)}
+    replay_with_oracle(st, spec, recs, alpha, ev, loop.action())
+    check_state(eng, st, T, n)
+    loop.close()
+    eng.close()
