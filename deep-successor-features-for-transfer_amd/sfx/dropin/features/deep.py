@@ -1,0 +1,290 @@
+"""DeepSF on the GPU (the interface of features/deep.py:8-131, the ψ library of
+main_sfdqn_torch.py).
+
+The ψ heads, their target copies, Adam state and the reward weights live in one libsfx
+engine (``sfx.engine.SFEngine``); every ψ forward, GPI reduction, TD target, backward and
+Adam step runs in the hand-written gfx950 kernels.  There is no CPU path: without a HIP
+device the first compute call raises.
+
+The user's ``pytorch_model_handle`` still builds the torch modules (so weight init and the
+optimizer's hyper-parameters are exactly the user's); the engine then owns the values.
+``psi`` returns those modules refreshed from the device on access (read-only views:
+write new weights through ``load_heads``).
+
+``update_successor`` calls are deferred and fused: the all-task loop of
+agents/sfdqn.py:57-60 (policies 0..T-1 on the same minibatch) becomes one speculative
+device step with the exact sequential semantics (sfx_update_all); any other call pattern
+runs head by head (sfx_update).  The deferral is invisible: features/deep.py returns
+nothing from update_successor, and every method that reads state flushes first.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from features.successor import SF
+from utils.torch import get_torch_device, update_models_weights
+
+
+def _geometry(model: torch.nn.Module):
+    """(n_s, H, acts, out) of the reference lambda's Sequential; raises for other shapes."""
+    mods = [m for m in model.modules() if m is not model and not isinstance(m, torch.nn.Sequential)]
+    lin = [m for m in mods if isinstance(m, torch.nn.Linear)]
+    acts = []
+    seq = [m for m in mods if not isinstance(m, (torch.nn.Unflatten, torch.nn.Identity))]
+    ok = len(lin) >= 2 and isinstance(seq[0], torch.nn.Linear) and isinstance(seq[-1], torch.nn.Linear)
+    i = 1
+    while ok and i < len(seq) - 1:
+        if not isinstance(seq[i], torch.nn.Linear) or not isinstance(seq[i + 1], (torch.nn.ReLU, torch.nn.Tanh)):
+            ok = False
+            break
+        acts.append("relu" if isinstance(seq[i + 1], torch.nn.ReLU) else "tanh")
+        i += 2
+    H = lin[0].out_features if lin else 0
+    ok = ok and all(l.in_features == H and l.out_features == H for l in lin[1:-1]) and lin[-1].in_features == H
+    ok = ok and all(l.bias is not None for l in lin)
+    if not ok:
+        raise NotImplementedError(
+            "sfx DeepSF supports the reference ψ architecture only: Linear(n_s,H) -> [Linear(H,H) + ReLU|Tanh]* "
+            f"-> Linear(H, A*d) (-> Unflatten); got {model}")
+    return lin[0].in_features, H, tuple(acts), lin[-1].out_features
+
+
+def _flat(model):
+    return torch.cat([p.detach().reshape(-1).float().cpu() for p in model.parameters()])
+
+
+def _unflat_into(model, flat):
+    off = 0
+    with torch.no_grad():
+        for p in model.parameters():
+            n = p.numel()
+            p.copy_(flat[off:off + n].view_as(p).to(p.device, p.dtype))
+            off += n
+
+
+class _FitW(list):
+    """fit_w whose entries live in the engine once it exists ([d, 1] tensors on read)."""
+
+    def __init__(self, sf):
+        super().__init__()
+        self._sf = sf
+
+    def __getitem__(self, i):
+        sf = self._sf
+        if isinstance(i, int) and sf._eng is not None and sf._eng_T == len(self):
+            sf._flush()
+            w = sf._eng.get_w(i if i >= 0 else len(self) + i)[0].view(-1, 1)
+            return w.to(sf._out_device())
+        return super().__getitem__(i)
+
+    def __setitem__(self, i, v):
+        super().__setitem__(i, v)
+        sf = self._sf
+        if isinstance(i, int) and sf._eng is not None and sf._eng_T == len(self):
+            sf._flush()
+            sf._eng.load_w(i if i >= 0 else len(self) + i, v)
+
+
+class DeepSF(SF):
+    def __init__(self, pytorch_model_handle, *args, target_update_ev=1000, max_batch=256, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.pytorch_model_handle = pytorch_model_handle
+        self.target_update_ev = target_update_ev
+        self.max_batch = max_batch
+        self.device = get_torch_device()
+        self._eng = None
+        self._eng_T = 0
+        self._pending = []
+        self._host_stale = False
+
+    # ------------------------------------------------------------------ library
+    def reset(self):
+        self._close()
+        SF.reset(self)
+        self.fit_w = _FitW(self)
+        self._since = []
+
+    def _close(self):
+        if getattr(self, "_eng", None) is not None:
+            self._pending = []
+            self._eng.close()
+        self._eng, self._eng_T = None, 0
+
+    def build_successor(self, task, source=None):
+        if self.n_tasks == 0:
+            self.n_actions = task.action_count()
+            self.n_features = task.feature_dim()
+            self.inputs = task.encode_dim()
+        A, d = self.n_actions, self.n_features
+        model, loss, optim = self.pytorch_model_handle(self.inputs, A * d, (A, d), 1)
+        if source is not None and self.n_tasks > 0:
+            self._sync_host()
+            update_models_weights(self._psi[source][0][0], model)
+        target, tloss, toptim = self.pytorch_model_handle(self.inputs, A * d, (A, d), 1)
+        update_models_weights(model, target)
+        target.eval()
+        self._since.append(0)
+        return (model, loss, optim), (target, tloss, toptim)
+
+    def add_training_task(self, task, source=None):
+        self._flush()
+        self._sync_host()
+        SF.add_training_task(self, task, source)
+
+    @property
+    def psi(self):
+        self._sync_host()
+        return self._psi
+
+    @property
+    def updates_since_target_updated(self):
+        if self._eng is not None and self._eng_T == self.n_tasks:
+            self._flush()
+            return [self._eng.since_target(t) for t in range(self.n_tasks)]
+        return self._since
+
+    # ------------------------------------------------------------------ engine
+    def _out_device(self):
+        dev = get_torch_device() if self.device is None else self.device
+        return dev if dev is not None else self._eng.device
+
+    def _engine(self, batch: int = 1):
+        """The engine holding every current head (rebuilt when tasks were added)."""
+        if self._eng is not None and self._eng_T == self.n_tasks and batch <= self._eng.max_batch:
+            return self._eng
+        from sfx.engine import SFEngine
+
+        if self.n_tasks == 0:
+            raise RuntimeError("DeepSF has no tasks: call add_training_task first")
+        self._flush()
+        old, old_T = self._eng, self._eng_T
+        if old is not None:  # carry the device state of the heads that already exist
+            self._sync_host()
+            adam = [old.get_adam(t) for t in range(old_T)]
+            ws = [old.get_w(t)[0] for t in range(old_T)]
+            since = [old.since_target(t) for t in range(old_T)]
+        model, loss, optim = self._psi[0][0]
+        n_s, H, acts, out = _geometry(model)
+        if out != self.n_actions * self.n_features:
+            raise ValueError("ψ output width != n_actions * n_features")
+        if not isinstance(loss, torch.nn.MSELoss) or loss.reduction != "mean":
+            raise NotImplementedError("sfx DeepSF trains with MSELoss(reduction='mean') only")
+        g = optim.param_groups[0] if optim is not None else {"lr": 1e-3, "betas": (0.9, 0.999), "eps": 1e-8,
+                                                             "weight_decay": 0.0}
+        if optim is not None and (not isinstance(optim, torch.optim.Adam) or g.get("amsgrad") or g.get("maximize")):
+            raise NotImplementedError("sfx DeepSF trains ψ with torch.optim.Adam (no amsgrad / maximize) only")
+        mb = max(self.max_batch, batch)
+        eng = SFEngine(self.n_tasks, n_s, H, self.n_actions, self.n_features, acts, max_batch=mb)
+        eng.set_adam(g["lr"], g.get("weight_decay", 0.0), g["lr"], 0.0, betas=tuple(g["betas"]), eps=g["eps"])
+        eng.set_target_update_ev(self.target_update_ev)
+        for t, ((m, _, _), (tm, _, _)) in enumerate(self._psi):
+            eng.load_head(t, _flat(m), 0)
+            eng.load_head(t, _flat(tm), 1)
+            if old is not None and t < old_T:
+                eng.load_adam(t, adam[t][0], adam[t][1], adam[t][2])
+                eng.load_w(t, ws[t])
+                eng.set_since_target(t, since[t])
+            else:
+                eng.load_w(t, list.__getitem__(self.fit_w, t))
+                eng.set_since_target(t, self._since[t])
+        if old is not None:
+            old.close()
+        self._eng, self._eng_T = eng, self.n_tasks
+        self.max_batch = mb
+        return eng
+
+    def _sync_host(self):
+        """Refresh the torch modules (online, target) from the device."""
+        if self._eng is None or not self._host_stale:
+            return
+        self._flush()
+        for t in range(self._eng_T):
+            (m, _, _), (tm, _, _) = self._psi[t]
+            _unflat_into(m, self._eng.get_head(t, 0))
+            _unflat_into(tm, self._eng.get_head(t, 1))
+        self._host_stale = False
+
+    def load_heads(self):
+        """Push the torch modules' current weights to the device (after editing ``psi``)."""
+        if self._eng is not None:
+            self._flush()
+            for t, ((m, _, _), (tm, _, _)) in enumerate(self._psi):
+                self._eng.load_head(t, _flat(m), 0)
+                self._eng.load_head(t, _flat(tm), 1)
+            self._host_stale = False
+
+    def _flush(self):
+        """Run deferred update_successor calls."""
+        if not self._pending or self._eng is None:
+            return
+        pend, self._pending = self._pending, []
+        eng = self._eng
+        T = self._eng_T
+        same = all(p[0] is pend[0][0] for p in pend)
+        if same and [p[1] for p in pend] == list(range(T)):
+            s, a, phi, s1, g = pend[0][2]
+            eng.update_all(s, a, phi, s1, g)
+        else:
+            for _, i, (s, a, phi, s1, g) in pend:
+                eng.update(i, s, a, None, phi, s1, g, use_gpi=True)
+        self._host_stale = True
+
+    # ------------------------------------------------------------------ ψ / GPI
+    def _state(self, state):
+        s = torch.as_tensor(state)
+        return s.reshape(1, -1) if s.dim() == 1 else s.reshape(s.shape[0], -1)
+
+    def get_successor(self, state, policy_index):
+        return self.get_successors(state)[:, policy_index]
+
+    def get_successors(self, state):
+        s = self._state(state)
+        eng = self._engine(s.shape[0])
+        self._flush()
+        return eng.successors(s).to(self._out_device())
+
+    def GPI_w(self, state, w):
+        s = self._state(state)
+        eng = self._engine(s.shape[0])
+        self._flush()
+        _, q, task, _ = eng.gpi(s, w=torch.as_tensor(w).reshape(-1))
+        dev = self._out_device()
+        return q.to(dev), torch.squeeze(task).to(dev)
+
+    def GPI(self, state, task_index, update_counters=False):
+        s = self._state(state)
+        eng = self._engine(s.shape[0])
+        self._flush()
+        _, q, task, _ = eng.gpi(s, w_index=task_index)
+        dev = self._out_device()
+        q, task = q.to(dev), torch.squeeze(task).to(dev)
+        if update_counters:
+            self._count(task_index, task)
+        return q, task
+
+    # ------------------------------------------------------------------ training
+    def update_reward(self, phi, r, task_index, exact=False):
+        eng = self._engine()
+        self._flush()
+        eng.lms(task_index, torch.as_tensor(phi).reshape(-1), torch.as_tensor(r, dtype=torch.float32).reshape(1),
+                float(self.alpha_w))
+        if exact:
+            w_true = torch.as_tensor(self.true_w[task_index]).reshape(-1).cpu()
+            r_true = torch.sum(torch.as_tensor(phi).reshape(-1).cpu() * w_true)
+            if not torch.allclose(torch.as_tensor(r).cpu().float(), r_true.float()):
+                raise Exception(f"sampled reward {r} != linear reward {r_true} - please check task {task_index}!")
+
+    def update_successor(self, transitions, policy_index):
+        if transitions is None:
+            return
+        states, actions, phis, next_states, gammas = transitions
+        eng = self._engine(len(gammas))
+        if self._pending and (self._pending[0][0] is not transitions or self._pending[-1][1] + 1 != policy_index):
+            self._flush()
+        self._pending.append((transitions, policy_index, (states, actions, phis, next_states, gammas)))
+        if len(self._pending) == self._eng_T:
+            self._flush()
+        elif self._pending[0][1] != 0:
+            self._flush()
+        del eng

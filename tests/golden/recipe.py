@@ -40,3 +40,103 @@ def full_size_heads(T: int = 8, seed: int = 0):
     gen = torch.Generator().manual_seed(seed + 1)
     w = torch.empty(T, d).uniform_(-0.01, 0.01, generator=gen)
     return torch.stack(heads), w
+
+
+# ---------------------------------------------------------------------------------------
+# End-to-end agent run (agents/sfdqn.py SFDQN over features/deep.py DeepSF, the
+# main_sfdqn_torch.py stack) -- generated with the real reference by tools/gen_golden.py,
+# replayed on the GPU through sfx's drop-in modules by tests/test_gpu_dropin.py.
+# ---------------------------------------------------------------------------------------
+AGENT_RUN = dict(seed=7, n_s=17, H=32, A=7, d=8, acts=("relu", "relu"), T_tasks=3, lr=1e-3, alpha_w=0.05,
+                 target_update_ev=6, n_samples=20, n_test_ev=10, episode_T=9, epsilon=0.2, gamma=0.9,
+                 buffer=dict(n_samples=500, n_batch=8), task_terminal_every=7)
+
+
+class AgentTask:
+    """Reacher-shaped Task (tasks/task.py interface) with its own RNG; records its actions."""
+
+    def __init__(self, n_s, A, d, index, seed, device, terminal_every=0):
+        import numpy as np
+
+        self.n_s, self.A, self.d, self.index, self.device = n_s, A, d, index, device
+        self.rng = np.random.default_rng(seed)
+        self.terminal_every, self.t = terminal_every, 0
+        self.actions, self._phi = [], None
+
+    def initialize(self):
+        import numpy as np
+
+        return torch.from_numpy(self.rng.standard_normal(self.n_s).astype(np.float32)).to(self.device)
+
+    def action_count(self):
+        return self.A
+
+    def transition(self, action):
+        import numpy as np
+
+        a = int(action)
+        self.actions.append(a)
+        self.t += 1
+        s1 = torch.from_numpy(self.rng.standard_normal(self.n_s).astype(np.float32)).to(self.device)
+        phi = (self.rng.random(self.d).astype(np.float32) + np.float32(0.05 * (a % 3))).astype(np.float32)
+        self._phi = torch.from_numpy(phi).to(self.device)
+        r = float(phi[self.index % self.d])
+        done = bool(self.terminal_every) and self.t % self.terminal_every == 0
+        return s1, r, done
+
+    def encode(self, state):
+        return torch.as_tensor(state).detach().reshape((1, -1)).to(self.device)
+
+    def encode_dim(self):
+        return self.n_s
+
+    def features(self, state, action, next_state):
+        return self._phi
+
+    def feature_dim(self):
+        return self.d
+
+    def get_w(self):
+        w = torch.zeros((self.d, 1)).to(self.device)
+        w[self.index % self.d, 0] = 1.0
+        return w
+
+
+def agent_psi_lambda(H, acts, lr, device):
+    """ψ factory with the structure of main_sfdqn_torch.py:44-78 (our code)."""
+    from collections import OrderedDict
+
+    act_cls = {"relu": torch.nn.ReLU, "tanh": torch.nn.Tanh}
+
+    def build(num_inputs, output_dim, reshape_dim, reshape_axis=1):
+        layers = OrderedDict(layer_input=torch.nn.Linear(num_inputs, H))
+        for j, a in enumerate(acts):
+            layers[f"layer_{j}"] = torch.nn.Linear(H, H)
+            layers[f"activation_layer_{j}"] = act_cls[a]()
+        layers["layer_output"] = torch.nn.Linear(H, output_dim)
+        layers["layer_unflatten"] = torch.nn.Unflatten(reshape_axis, reshape_dim)
+        model = torch.nn.Sequential(layers).to(device)
+        return model, torch.nn.MSELoss().to(device), torch.optim.Adam(model.parameters(), lr=lr)
+
+    return build
+
+
+def agent_run(DeepSF, SFDQN, ReplayBuffer, device):
+    """Build and train the agent of AGENT_RUN with the given classes; returns (agent, tasks)."""
+    import random
+
+    import numpy as np
+
+    c = AGENT_RUN
+    random.seed(c["seed"])
+    np.random.seed(c["seed"])
+    torch.manual_seed(c["seed"])
+    tasks = [AgentTask(c["n_s"], c["A"], c["d"], i, 100 + i, device, c["task_terminal_every"])
+             for i in range(c["T_tasks"])]
+    test_tasks = [AgentTask(c["n_s"], c["A"], c["d"], c["T_tasks"], 200, device)]
+    sf = DeepSF(pytorch_model_handle=agent_psi_lambda(c["H"], c["acts"], c["lr"], device),
+                target_update_ev=c["target_update_ev"], hyperparameters={"learning_rate_w": c["alpha_w"]})
+    agent = SFDQN(deep_sf=sf, buffer=ReplayBuffer(**c["buffer"]), gamma=c["gamma"], T=c["episode_T"],
+                  encoding="task", epsilon=c["epsilon"], use_gpi=True, test_epsilon=0.03)
+    returns = agent.train(tasks, c["n_samples"], test_tasks=test_tasks, n_test_ev=c["n_test_ev"])
+    return agent, tasks, test_tasks, returns

@@ -354,6 +354,34 @@ def gen_tsf(name, module, shape, T, k, K):
     np.savez_compressed(os.path.join(OUT, f"upd_{name}.npz"), **rec)
 
 
+def gen_agent_run():
+    """The main_sfdqn_torch.py stack end to end: reference agents/sfdqn.py SFDQN +
+    agents/buffer.py ReplayBuffer + features/deep.py DeepSF on synthetic tasks."""
+    import contextlib
+    import io
+
+    from agents.buffer import ReplayBuffer
+    from agents.sfdqn import SFDQN
+    from tests.golden.recipe import AGENT_RUN, agent_run
+
+    with contextlib.redirect_stdout(io.StringIO()):
+        agent, tasks, test_tasks, returns = agent_run(ref_deep.DeepSF, SFDQN, ReplayBuffer, torch.device("cpu"))
+    sf = agent.sf
+    T = sf.n_tasks
+    rec = dict(online=np_(torch.stack([flat(sf.psi[t][0][0]) for t in range(T)])),
+               target=np_(torch.stack([flat(sf.psi[t][1][0]) for t in range(T)])),
+               w=np_(torch.stack([sf.fit_w[t].reshape(-1).clone() for t in range(T)])),
+               gpi_counters=np.stack([np.asarray(c) for c in sf.gpi_counters]),
+               since_target=np.array(sf.updates_since_target_updated),
+               actions=np.array([a for t in tasks for a in t.actions]),
+               test_actions=np.array(test_tasks[0].actions),
+               test_w=np_(agent.test_tasks_weights[0].weight.detach().reshape(-1)),
+               returns=np.array([float(r) for r in returns]),
+               reward_hist=np.array([float(x) for x in agent.reward_hist]),
+               cum_reward=float(agent.cum_reward), total_steps=agent.total_training_steps)
+    np.savez_compressed(os.path.join(OUT, "run_sfdqn_agent.npz"), **rec)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(4)
@@ -370,8 +398,14 @@ def main():
     gen_deep_alltask(SHAPES["reacher17"], 4, 6, 3)
     gen_tsf("tsf", ref_tsfdqn, SHAPES["hopper11"], 3, 8, 0)
     gen_tsf("tsf_nf", ref_tsfdqn_nf, SHAPES["hopper11"], 3, 6, 3)
+    gen_agent_run()
     print("golden vectors written to", os.path.abspath(OUT))
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1:  # only the named generators, e.g. gen_agent_run
+        os.makedirs(OUT, exist_ok=True)
+        for name in sys.argv[1:]:
+            globals()[name]()
+    else:
+        main()
