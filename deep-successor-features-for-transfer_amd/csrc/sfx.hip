@@ -121,6 +121,14 @@ struct sfx_handle {
   long long steps_spec = 0, steps_fallback = 0, policies_rerun = 0, rounds_total = 0;
   int force_rerun_from = -1;  // test hook: treat the speculation as failed from this policy on
   int spec_rounds = 2;        // speculative rounds launched on the device per fused step
+  // sharded heads (sfx_shard_*): this handle's heads are global [off, off + T) of Tg; w has Tg rows
+  int Tg = 0, off = 0;
+  struct ShardPending {
+    bool active = false;
+    int B = 0;
+    const float *S = nullptr, *S1 = nullptr, *phi = nullptr, *gamma = nullptr, *s_next = nullptr;
+    const int64_t* a = nullptr;
+  } spend;
 
   float *online = nullptr, *target = nullptr, *am = nullptr, *av = nullptr;
   float *w = nullptr, *wm = nullptr, *wv = nullptr;
@@ -265,8 +273,11 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
 }
 
 int run_tdg(sfx_handle* h, int pol0, int npol, int guess, int M, int use_gpi, const int64_t* a, const float* phi,
-            const float* gamma, int64_t* next, int next_stride, int* flag = nullptr) {
+            const float* gamma, int64_t* next, int next_stride, int* flag = nullptr, const float* xmax = nullptr,
+            int poloff = 0) {
   TdgArgs A{};
+  A.xmax = xmax;
+  A.poloff = poloff;
   A.M = M;
   A.use_gpi = use_gpi;
   A.pol0 = pol0;
@@ -294,6 +305,8 @@ struct TdgSpec {
   const float* gamma = nullptr;
   int64_t* next = nullptr;
   int* flag = nullptr;
+  const float* xmax = nullptr;  // sharded heads: all-reduced GPI maxima [T_glob][M][A]
+  int poloff = 0;               // global index of local head 0
 };
 
 // 0: K2 as its own launch; 1: fused, d <= 8; 2: fused, d <= 16 (see tdg_rows)
@@ -319,9 +332,11 @@ bool can_fuse_v0(const sfx_handle* h) { return h->L[0].K <= KFUSE; }
 
 int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const float* phi, const float* r,
             float* losses, const TdgSpec& td, const BwdExtra& ex = BwdExtra()) {
-  const bool fuse = can_fuse_tdg(h) && ((uintptr_t)phi & 15) == 0;  // fused K2 reads φ rows as float4
+  const bool fuse = can_fuse_tdg(h) && ((uintptr_t)phi & 15) == 0 &&  // fused K2 reads φ rows as float4
+                    (!td.xmax || 32 * h->A <= 1024);                     // and up to 4 maxima per thread
   if (!fuse)
-    RC(run_tdg(h, head0, nhead, td.guess, M, td.use_gpi, td.a, phi, td.gamma, td.next, td.next_stride, td.flag));
+    RC(run_tdg(h, head0, nhead, td.guess, M, td.use_gpi, td.a, phi, td.gamma, td.next, td.next_stride, td.flag,
+               td.xmax, td.poloff));
   BwdArgs A{};
   A.step_in_tail = fuse ? 0 : 1;
   A.tdg_use_gpi = td.use_gpi;
@@ -330,6 +345,8 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.tdg_a = td.a;
   A.tdg_gamma = td.gamma;
   A.tdg_next = td.next;
+  A.tdg_xmax = td.xmax;
+  A.tdg_poloff = td.poloff;
   A.flag = td.flag;
   A.flag_value = h->T;
   const int tail_at = fuse ? 1 : 0;  // launch index of the loss tail (needs every row's loss)
@@ -489,6 +506,7 @@ void unpack_head(const sfx_handle* h, const float* src, float* dst) {
 }
 
 bool valid_head(const sfx_handle* h, int t) { return h && t >= 0 && t < h->T; }
+bool valid_w(const sfx_handle* h, int t) { return h && t >= 0 && t < h->Tg; }
 
 void free_all(sfx_handle* h) {
   clear_graphs(h);
@@ -639,6 +657,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
     aoff += align4((max_batch + 1) * h->L[l].N);  // +1 row: the next state of the fused step
   }
   h->actSize = (aoff + 63) & ~63;
+  h->Tg = T;
   h->since_target.assign(T, 0);
   h->host_step.assign(T, 0);
 
@@ -785,7 +804,7 @@ int sfx_get_adam(sfx_t h, int t, float* m_host, float* v_host, int* step) {
 }
 
 int sfx_load_w(sfx_t h, int t, const float* w_host) {
-  if (!valid_head(h, t) || !w_host) SFX_FAIL(SFX_E_ARG, "bad args");
+  if (!valid_w(h, t) || !w_host) SFX_FAIL(SFX_E_ARG, "bad args");
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipMemcpyAsync(h->w + (size_t)t * h->dpad, w_host, sizeof(float) * h->d, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -793,7 +812,7 @@ int sfx_load_w(sfx_t h, int t, const float* w_host) {
 }
 
 int sfx_get_w(sfx_t h, int t, float* w_host, float* wm_host, float* wv_host) {
-  if (!valid_head(h, t)) SFX_FAIL(SFX_E_ARG, "bad head");
+  if (!valid_w(h, t)) SFX_FAIL(SFX_E_ARG, "bad head");
   const size_t o = (size_t)t * h->dpad, n = sizeof(float) * h->d;
   if (w_host) HIPCHK(hipMemcpyAsync(w_host, h->w + o, n, hipMemcpyDeviceToHost, h->stream));
   if (wm_host) HIPCHK(hipMemcpyAsync(wm_host, h->wm + o, n, hipMemcpyDeviceToHost, h->stream));
@@ -803,7 +822,7 @@ int sfx_get_w(sfx_t h, int t, float* w_host, float* wm_host, float* wv_host) {
 }
 
 int sfx_w_ptr(sfx_t h, int t, float** w_dev) {
-  if (!valid_head(h, t) || !w_dev) SFX_FAIL(SFX_E_ARG, "bad args");
+  if (!valid_w(h, t) || !w_dev) SFX_FAIL(SFX_E_ARG, "bad args");
   *w_dev = h->w + (size_t)t * h->dpad;
   return SFX_OK;
 }
@@ -968,7 +987,7 @@ int sfx_update_all(sfx_t h, const float* S, const int64_t* a, const float* phi, 
 }
 
 int sfx_lms(sfx_t h, int t, const float* phi, const float* r, float alpha) {
-  if (!valid_head(h, t) || !phi || !r) SFX_FAIL(SFX_E_ARG, "bad args");
+  if (!valid_w(h, t) || !phi || !r) SFX_FAIL(SFX_E_ARG, "bad args");
   launch(h, K_LMS, 4.0 * (3.0 * h->d + 1), k_lms, dim3(1), dim3(256), h->w + (size_t)t * h->dpad, phi, r, alpha,
          h->d);
   LAUNCHCHK();
@@ -1044,3 +1063,4 @@ int sfx_synchronize(sfx_t h) {
 }  // extern "C"
 
 #include "sfx_runner.inc"
+#include "sfx_shard.inc"

@@ -304,6 +304,10 @@ struct TdgArgs {
   const float* gamma;
   int64_t* next;  // next[(policy - pol0) * next_stride + b] or null
   int* flag;      // reset to flag_value by block (0, 0) when non-null
+  // sharded heads: max over ALL heads of q[b, t, a] (all-reduced across ranks), indexed by the
+  // global policy poloff + pol; replaces the local GPI reduction when non-null
+  const float* xmax;
+  int poloff, pad2_;
 };
 
 __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
@@ -329,20 +333,25 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
     if (aok) cval = G.actp(R_S, pol, NLm)[(size_t)b * O + ab * d + tid];
   }
   __syncthreads();
-  const int t0 = A.use_gpi ? 0 : pol, nt = A.use_gpi ? T : 1;
-  for (int idx = tid; idx < nt * Aa; idx += 256) {
-    const int t = t0 + idx / Aa, a = idx % Aa;
-    const float* p = G.actp(t < pol ? A.guess : R_S1, t, NLm) + (size_t)b * O + a * d;
-    float q = 0.f;
+  if (A.xmax) {
+    const float* xr = A.xmax + ((size_t)(A.poloff + pol) * M + b) * Aa;
+    for (int a = tid; a < Aa; a += 256) s_m[a] = xr[a];
+  } else {
+    const int t0 = A.use_gpi ? 0 : pol, nt = A.use_gpi ? T : 1;
+    for (int idx = tid; idx < nt * Aa; idx += 256) {
+      const int t = t0 + idx / Aa, a = idx % Aa;
+      const float* p = G.actp(t < pol ? A.guess : R_S1, t, NLm) + (size_t)b * O + a * d;
+      float q = 0.f;
 #pragma unroll 8
-    for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
-    s_q[idx] = q;
-  }
-  __syncthreads();
-  for (int a = tid; a < Aa; a += 256) {  // max over heads for each action (torch.max(q1, axis=1))
-    float mx = s_q[a];
-    for (int t = 1; t < nt; ++t) mx = fmaxf(mx, s_q[t * Aa + a]);
-    s_m[a] = mx;
+      for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
+      s_q[idx] = q;
+    }
+    __syncthreads();
+    for (int a = tid; a < Aa; a += 256) {  // max over heads for each action (torch.max(q1, axis=1))
+      float mx = s_q[a];
+      for (int t = 1; t < nt; ++t) mx = fmaxf(mx, s_q[t * Aa + a]);
+      s_m[a] = mx;
+    }
   }
   __syncthreads();
   if (tid == 0) {  // argmax over actions, first index on ties
@@ -411,6 +420,8 @@ struct BwdArgs {
   const int64_t* tdg_a;
   const float* tdg_gamma;
   int64_t* tdg_next;
+  const float* tdg_xmax;  // sharded heads: all-reduced GPI maxima (see TdgArgs::xmax)
+  int tdg_poloff, pad3_;
   int* flag;
   int fuse_v0, vM, vOff, act0;  // fused forward: rows (S1 ++ s_next), layer-0 offset, layer-0 act
   int vRole, pad_;              // role block the fused forward writes
@@ -448,7 +459,8 @@ template <int VMAX, int U>
 __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pub, TdgSmem& sm) {
   const int tid = threadIdx.x, T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, M = A.M;
   const int nb = M - m0 < 32 ? M - m0 : 32;
-  const int t0 = A.tdg_use_gpi ? 0 : pol, nt = A.tdg_use_gpi ? T : 1, TA = nt * Aa, n = nb * TA, V = d >> 2;
+  const bool xm = A.tdg_xmax != nullptr;
+  const int t0 = A.tdg_use_gpi ? 0 : pol, nt = A.tdg_use_gpi ? T : 1, TA = nt * Aa, n = xm ? 0 : nb * TA, V = d >> 2;
   const int guess = A.tdg_guess;
   // ---- stage A: all global loads
   float4 v[U][VMAX];
@@ -477,6 +489,12 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
   const float wk = tid < d ? G.w[(long long)pol * G.dpad + tid] : 0.f;
   const int ab_l = tid < nb ? (int)A.tdg_a[m0 + tid] : 0;
   const float gam_l = tid < nb ? A.tdg_gamma[m0 + tid] : 0.f;
+  float xv[4];
+  if (xm) {  // the all-reduced maxima rows of this policy: stage C's output
+    const float* xr = A.tdg_xmax + ((size_t)(A.tdg_poloff + pol) * M + m0) * Aa;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) xv[u] = tid + u * 256 < nb * Aa ? xr[tid + u * 256] : 0.f;
+  }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int i = tid + u * 256;
@@ -492,6 +510,11 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
     sm.gam[tid] = gam_l;
   }
   __syncthreads();
+  if (xm) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (tid + u * 256 < nb * Aa) sm.m[tid + u * 256] = xv[u];
+  }
   // ---- stage B: q = ψ·w, one fmaf chain per dot in k order
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -510,7 +533,7 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
   }
   __syncthreads();
   // ---- stage C: max over heads per (row, action)   (torch.max(q1, axis=1))
-  for (int i = tid; i < nb * Aa; i += 256) {
+  for (int i = tid; i < (xm ? 0 : nb * Aa); i += 256) {
     const int bl = i / Aa, a = i - bl * Aa;
     const float* qb = sm.q + bl * TA + a;
     float mx = qb[0];
@@ -1044,6 +1067,162 @@ __global__ void k_publish(const int64_t* sel, const int* flag, HostResult* out, 
     __threadfence_system();
     __hip_atomic_store(&out->seq, *dctr, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+}  // namespace sfx
+
+namespace sfx {
+
+// -------------------------------------------------------------------------------------
+// Sharded heads: rank g owns heads [off, off + T) of T_glob; w is replicated
+// ([T_glob][dpad]).  GPI over all heads = all-reduce(MAX) of per-rank maxima, which is exact
+// (max is order-free) and keeps argmax first-index tie-breaking.
+// -------------------------------------------------------------------------------------
+// q[idx] = Σ_k p_idx[k] w[k] for idx < n, one fmaf chain in k order per dot (the order every
+// GPI kernel uses, so argmaxes agree bit for bit).  d = 4V <= 4 VMAX with 16-B aligned rows:
+// U dots per thread with every load issued before the first FMA; other d: scalar loop.
+template <int VMAX, int U, class PF>
+__device__ __forceinline__ void qdots_vec(int n, int d, const float* s_w, float* s_q, PF ptr) {
+  const int V = d >> 2;
+  for (int base = threadIdx.x; base < n; base += 256 * U) {
+    float4 v[U][VMAX];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = base + u * 256;
+      const float4* p = reinterpret_cast<const float4*>(ptr(idx < n ? idx : 0));
+#pragma unroll
+      for (int j = 0; j < VMAX; ++j) v[u][j] = (idx < n && j < V) ? p[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = base + u * 256;
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < VMAX; ++j) {
+        if (j < V) {
+          q = __builtin_fmaf(v[u][j].x, s_w[4 * j], q);
+          q = __builtin_fmaf(v[u][j].y, s_w[4 * j + 1], q);
+          q = __builtin_fmaf(v[u][j].z, s_w[4 * j + 2], q);
+          q = __builtin_fmaf(v[u][j].w, s_w[4 * j + 3], q);
+        }
+      }
+      if (idx < n) s_q[idx] = q;
+    }
+  }
+}
+
+template <class PF>
+__device__ __forceinline__ void qdots(int n, int d, const float* s_w, float* s_q, PF ptr) {
+  if ((d & 3) == 0 && d <= 8) {
+    qdots_vec<2, 8>(n, d, s_w, s_q, ptr);
+  } else if ((d & 3) == 0 && d <= 16) {
+    qdots_vec<4, 4>(n, d, s_w, s_q, ptr);
+  } else {
+    for (int idx = threadIdx.x; idx < n; idx += 256) {
+      const float* p = ptr(idx);
+      float q = 0.f;
+#pragma unroll 8
+      for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
+      s_q[idx] = q;
+    }
+  }
+}
+
+struct QmaxArgs {
+  int M, Tg, off, guess, rows, pad_;
+  float* X;  // [Tg][M][A]: max over this rank's heads of q[b, t, a] with w of policy i
+};
+
+// K5: grid (Tg, ceil(M / rows)).  Head t (global off + t) enters policy i's GPI through role
+// `guess` if off + t < i (already updated in the reference's order) else R_S1.
+__global__ __launch_bounds__(256) void k_qmax(Geo G, QmaxArgs Q) {
+  const int i = blockIdx.x, tid = threadIdx.x;
+  const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, TA = T * Aa;
+  const int b0 = blockIdx.y * Q.rows;
+  const int nb = Q.M - b0 < Q.rows ? Q.M - b0 : Q.rows;
+  if (nb <= 0) return;
+  __shared__ float s_w[DMAX];
+  __shared__ float s_q[QMAX];
+  const float* wrow = G.w + (long long)i * G.dpad;
+  for (int k = tid; k < d; k += 256) s_w[k] = wrow[k];
+  __syncthreads();
+  const int off = Q.off, guess = Q.guess;
+  qdots(nb * TA, d, s_w, s_q, [&](int idx) {
+    const int bl = idx / TA, rem = idx - bl * TA, t = rem / Aa, a = rem - t * Aa;
+    return G.actp(off + t < i ? guess : R_S1, t, NLm) + (size_t)(b0 + bl) * O + a * d;
+  });
+  __syncthreads();
+  for (int j = tid; j < nb * Aa; j += 256) {
+    const int bl = j / Aa, a = j - bl * Aa;
+    const float* qb = s_q + bl * TA + a;
+    float mx = qb[0];
+    for (int t = 1; t < T; ++t) mx = fmaxf(mx, qb[t * Aa]);
+    Q.X[((size_t)i * Q.M + b0 + bl) * Aa + a] = mx;
+  }
+}
+
+// K6: first policy whose next actions differ between the TD maxima X (from the guesses) and
+// the verification maxima Y (from the post-update heads); Tg if none.  One workgroup.
+__global__ __launch_bounds__(256) void k_sverify(const float* X, const float* Y, int Tg, int M, int Aa, int* flag) {
+  __shared__ int s_min;
+  if (threadIdx.x == 0) s_min = Tg;
+  __syncthreads();
+  int mine = Tg;
+  for (int j = threadIdx.x; j < Tg * M; j += 256) {
+    const float* x = X + (size_t)j * Aa;
+    const float* y = Y + (size_t)j * Aa;
+    int ax = 0, ay = 0;
+    float bx = x[0], by = y[0];
+    for (int a = 1; a < Aa; ++a) {
+      if (x[a] > bx) { bx = x[a]; ax = a; }
+      if (y[a] > by) { by = y[a]; ay = a; }
+    }
+    if (ax != ay) mine = min(mine, j / M);
+  }
+  atomicMin(&s_min, mine);
+  __syncthreads();
+  if (threadIdx.x == 0) *flag = s_min;
+}
+
+// K7: this rank's best (q, global t*A + a) for action selection in row `row` of role `role`
+// with w of task `task`, packed into an order-preserving int64 so all-reduce(MAX) returns the
+// reference's pick (argmax_t max_a, then argmax_a; first index on ties).  !use_gpi: only
+// head `task` competes (c = task_index).
+struct KeyArgs {
+  int role, row, task, use_gpi, off, pad_;
+  long long* key;
+};
+
+__device__ __forceinline__ unsigned int orderable(float q) {
+  const unsigned int u = __float_as_uint(q);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__global__ __launch_bounds__(256) void k_skey(Geo G, KeyArgs K) {
+  __shared__ unsigned long long s_best;
+  __shared__ float s_w[DMAX];
+  const int tid = threadIdx.x, T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff;
+  if (tid == 0) s_best = 0ull;
+  const float* wrow = G.w + (long long)K.task * G.dpad;
+  for (int k = tid; k < d; k += 256) s_w[k] = wrow[k];
+  __syncthreads();
+  unsigned long long best = 0ull;
+  for (int j = tid; j < T * Aa; j += 256) {
+    const int t = j / Aa, a = j - t * Aa, tg = K.off + t;
+    if (!K.use_gpi && tg != K.task) continue;
+    const float* p = G.actp(K.role, t, NLm) + (size_t)K.row * O + a * d;
+    float q = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
+    q = __fadd_rn(q, 0.f);  // -0 -> +0: torch's argmax treats them as equal
+    const unsigned long long key =
+        ((unsigned long long)orderable(q) << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)(tg * Aa + a));
+    best = key > best ? key : best;
+  }
+  atomicMax(&s_best, best);
+  __syncthreads();
+  // unsigned order -> signed order (all-reduce MAX runs on int64); 0 (nothing here) -> INT64_MIN
+  if (tid == 0) *K.key = (long long)(s_best ^ 0x8000000000000000ull);
 }
 
 }  // namespace sfx

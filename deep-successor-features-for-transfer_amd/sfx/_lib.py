@@ -63,6 +63,14 @@ SIGNATURES = {
     "sfx_runner_record": (_I, [_VP, _I]),
     "sfx_runner_recorded": (_I, [_VP]),
     "sfx_runner_get_record": (_I, [_VP, _I, _VP, C.POINTER(C.c_int64)]),
+    "sfx_shard_setup": (_I, [_VP, _I, _I]),
+    "sfx_shard_begin": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _F, _VP]),
+    "sfx_shard_td_maxima": (_I, [_VP, _I, _VP]),
+    "sfx_shard_td_update": (_I, [_VP, _I, _VP]),
+    "sfx_shard_ver_maxima": (_I, [_VP, _I, _VP]),
+    "sfx_shard_verify": (_I, [_VP, _VP, _VP, _VP]),
+    "sfx_shard_select": (_I, [_VP, _I, _I, _I, _VP]),
+    "sfx_shard_finish": (_I, [_VP, _I]),
 }
 
 # env callbacks of sfx_runner_create (include/sfx.h)

@@ -45,10 +45,14 @@ class SFEngine:
         self._h = h
         self.P = lib.sfx_head_numel(h)
         self._sel = torch.zeros(2, dtype=torch.long, device=self.device)
+        self._refresh_w_ptrs(T)
+
+    def _refresh_w_ptrs(self, Tw: int):
+        """Device pointers of the w rows (Tw = T, or T_glob after sfx_shard_setup)."""
         self._w_ptrs = []
-        for t in range(T):
+        for t in range(Tw):
             p = C.c_void_p()
-            check(lib.sfx_w_ptr(h, t, C.byref(p)), "sfx_w_ptr")
+            check(lib.sfx_w_ptr(self._h, t, C.byref(p)), "sfx_w_ptr")
             self._w_ptrs.append(p.value)
 
     # ---------------------------------------------------------------- lifecycle

@@ -1,0 +1,164 @@
+"""Source-task heads sharded across ranks (BASELINE config C4).
+
+Rank g owns global heads [g*T_loc, (g+1)*T_loc); the reward weights w, the env and the
+replay are replicated with identical seeds, so every rank sees the same minibatch and the
+same env action.  GPI is the only cross-rank computation: each rank reduces q over its own
+heads and an all-reduce(MAX) finishes the reduction (exact: max is order-free; first-index
+argmax tie-breaking is preserved by the packed selection key).  Backward and Adam stay local.
+
+``ShardedAllTask`` runs one all-task env step (agents/sfdqn.py:47-60 over features/deep.py,
+in-order semantics) as the speculative rounds of DESIGN.md §4 with the GPI split across
+ranks.  It drives a *backend* with the protocol of include/sfx.h's sfx_shard_* calls:
+``LibsfxShardBackend`` (the GPU path) or, in the CPU tests, an oracle backend.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Callable, Optional
+
+import torch
+
+_SIGN = 1 << 63
+
+
+def decode_key(key: int, A: int):
+    """int64 selection key (k_skey) -> (GPI task c, action a)."""
+    u = (int(key) & ((1 << 64) - 1)) ^ _SIGN
+    idx = 0xFFFFFFFF - (u & 0xFFFFFFFF)
+    return idx // A, idx % A
+
+
+def encode_key(q: float, t: int, a: int, A: int) -> int:
+    """The packing k_skey uses (for host-side backends): order-preserving float bits << 32 |
+    ~(t*A + a), shifted into signed int64 order."""
+    import struct
+
+    q = q + 0.0  # -0 -> +0
+    u = struct.unpack("<I", struct.pack("<f", q))[0]
+    o = (~u & 0xFFFFFFFF) if (u & 0x80000000) else (u | 0x80000000)
+    key_u = (o << 32) | (0xFFFFFFFF - (t * A + a))
+    key_s = key_u ^ _SIGN
+    return key_s - (1 << 64) if key_s >= (1 << 63) else key_s
+
+
+def all_reduce_max_fn(group=None, via_host: bool = False) -> Callable[[torch.Tensor], None]:
+    """all-reduce(MAX) in place over the default (or given) process group.  via_host: stage
+    through CPU memory (gloo groups driving device tensors)."""
+    import torch.distributed as dist
+
+    def ar(t: torch.Tensor):
+        if via_host:
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.MAX, group=group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+
+    return ar
+
+
+class ShardedAllTask:
+    def __init__(self, backend, T_glob: int, A: int, all_reduce_max: Callable[[torch.Tensor], None], rounds: int = 2):
+        self.be, self.Tg, self.A, self.ar, self.rounds = backend, T_glob, A, all_reduce_max, rounds
+        self.stats = {"steps": 0, "host_round_steps": 0, "rounds": 0}
+
+    def step(self, batch, lms_task: int, lms_phi, lms_r, alpha: float, s_next, task: int, sel_use_gpi: bool = True):
+        """One env step.  batch = (S, a, phi, S1, gamma) or None (replay not filled yet).
+        Returns (c, a) of the env action for s_next (post-update heads)."""
+        be, ar = self.be, self.ar
+        be.begin(batch, lms_task, lms_phi, lms_r, alpha, s_next)
+        if batch is None:
+            key = be.select(-1, task, sel_use_gpi)
+            ar(key)
+            be.finish(0)
+            return decode_key(int(key.item()), self.A)
+        X, Y = be.X, be.Y
+        for r in range(self.rounds):
+            be.td_maxima(r, X)
+            ar(X)
+            be.td_update(r, X)
+        last = self.rounds - 1
+        be.ver_maxima(last, Y)
+        ar(Y)
+        flag = be.verify(X, Y)
+        if flag < self.Tg:
+            self.stats["host_round_steps"] += 1
+        while flag < self.Tg:  # each extra round fixes at least one more policy
+            last += 1
+            if last > self.Tg + 1:
+                raise RuntimeError("sharded speculation did not converge")
+            be.td_maxima(last, X)
+            ar(X)
+            be.td_update(last, X)
+            be.ver_maxima(last, Y)
+            ar(Y)
+            flag = be.verify(X, Y)
+        key = be.select(last, task, sel_use_gpi)
+        ar(key)
+        be.finish(last + 1)
+        self.stats["steps"] += 1
+        self.stats["rounds"] += last + 1
+        return decode_key(int(key.item()), self.A)
+
+
+class LibsfxShardBackend:
+    """sfx_shard_* on one SFEngine holding this rank's T_loc heads."""
+
+    def __init__(self, engine, T_glob: int, head_offset: int, max_batch: int):
+        from ._lib import check, lib
+
+        self.eng, self.lib, self.check = engine, lib, check
+        self.Tg, self.off = T_glob, head_offset
+        check(lib.sfx_shard_setup(engine.handle, T_glob, head_offset), "sfx_shard_setup")
+        engine._refresh_w_ptrs(T_glob)
+        dev = engine.device
+        self._X = torch.empty(T_glob * max_batch * engine.A, device=dev)
+        self._Y = torch.empty_like(self._X)
+        self.key = torch.empty(1, dtype=torch.long, device=dev)
+        self.flag = torch.empty(1, dtype=torch.int32, device=dev)
+        self.B = 0
+
+    @property
+    def X(self):  # [T_glob][B][A] TD maxima of the current step
+        return self._X[: self.Tg * self.B * self.eng.A]
+
+    @property
+    def Y(self):  # verification maxima
+        return self._Y[: self.Tg * self.B * self.eng.A]
+
+    def begin(self, batch, lms_task, lms_phi, lms_r, alpha, s_next):
+        e = self.eng
+        if batch is None:
+            self.B = 0
+            ptrs = [None] * 5
+        else:
+            S, a, phi, S1, g = batch
+            self.B = S.shape[0]
+            ptrs = [S.data_ptr(), a.data_ptr(), phi.data_ptr(), S1.data_ptr(), g.data_ptr()]
+        self._keep = (batch, lms_phi, lms_r, s_next)
+        self.check(self.lib.sfx_shard_begin(e.handle, *ptrs, self.B, int(lms_task),
+                                            None if lms_phi is None else lms_phi.data_ptr(),
+                                            None if lms_r is None else lms_r.data_ptr(), float(alpha),
+                                            s_next.data_ptr()), "sfx_shard_begin")
+
+    def td_maxima(self, r, X):
+        self.check(self.lib.sfx_shard_td_maxima(self.eng.handle, r, X.data_ptr()), "sfx_shard_td_maxima")
+
+    def td_update(self, r, X):
+        self.check(self.lib.sfx_shard_td_update(self.eng.handle, r, X.data_ptr()), "sfx_shard_td_update")
+
+    def ver_maxima(self, r, Y):
+        self.check(self.lib.sfx_shard_ver_maxima(self.eng.handle, r, Y.data_ptr()), "sfx_shard_ver_maxima")
+
+    def verify(self, X, Y) -> int:
+        self.check(self.lib.sfx_shard_verify(self.eng.handle, X.data_ptr(), Y.data_ptr(), self.flag.data_ptr()),
+                   "sfx_shard_verify")
+        return int(self.flag.item())
+
+    def select(self, r, task, use_gpi) -> torch.Tensor:
+        self.check(self.lib.sfx_shard_select(self.eng.handle, r, int(task), int(bool(use_gpi)), self.key.data_ptr()),
+                   "sfx_shard_select")
+        return self.key
+
+    def finish(self, rounds_run):
+        self.check(self.lib.sfx_shard_finish(self.eng.handle, int(rounds_run)), "sfx_shard_finish")

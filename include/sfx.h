@@ -231,6 +231,32 @@ int sfx_runner_record(sfx_runner_t r, int capacity);
 int sfx_runner_recorded(sfx_runner_t r);
 int sfx_runner_get_record(sfx_runner_t r, int i, void* stage_host, int64_t* meta_host /* [6] */);
 
+/* ---------------------------------------------------------------------------------------
+ * Heads sharded across ranks (BASELINE config C4: 64 tasks, 8 per GPU).
+ * This handle's T heads are the global heads [head_offset, head_offset + T) of T_glob; w has
+ * T_glob rows (replicated: load every task's w on every rank).  One all-task env step
+ * (agents/sfdqn.py:47-60, exact in-order semantics) is the sequence below, with the caller
+ * running all-reduce(MAX) over ranks on X, Y (fp32 [T_glob][B][A]) and key (int64) in between:
+ *   begin; for r < R: td_maxima(r, X), AR(X), td_update(r, X); ver_maxima(R-1, Y), AR(Y);
+ *   verify(X, Y, flag) -> while flag < T_glob: one more round r = R, R+1, ... (td_maxima,
+ *   AR, td_update, ver_maxima, AR, verify);  select(r_last, task, use_gpi, key), AR(key);
+ *   finish(rounds run).
+ * key decodes as idx = 0xFFFFFFFF - ((key ^ 2^63) & 0xFFFFFFFF): c = idx / A, a = idx % A
+ * (SF.GPI + argmax with first-index ties, features/successor.py:223-273).
+ * ------------------------------------------------------------------------------------- */
+int sfx_shard_setup(sfx_t h, int T_glob, int head_offset);
+/* B = 0: no minibatch (LMS + forward of s_next only; then select with round -1) */
+int sfx_shard_begin(sfx_t h, const float* S_dev, const int64_t* a_dev, const float* phi_dev,
+                    const float* S1_dev, const float* gamma_dev, int B, int lms_task,
+                    const float* lms_phi_dev, const float* lms_r_dev, float lms_alpha,
+                    const float* s_next_dev);
+int sfx_shard_td_maxima(sfx_t h, int round, float* X_dev);
+int sfx_shard_td_update(sfx_t h, int round, const float* X_dev);
+int sfx_shard_ver_maxima(sfx_t h, int round, float* Y_dev);
+int sfx_shard_verify(sfx_t h, const float* X_dev, const float* Y_dev, int* flag_dev);
+int sfx_shard_select(sfx_t h, int round, int task, int use_gpi, long long* key_dev);
+int sfx_shard_finish(sfx_t h, int rounds_run);
+
 #ifdef __cplusplus
 }
 #endif
