@@ -49,6 +49,9 @@ def parse():
     p.add_argument("--prof-steps", type=int, default=50)
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--shard-steps", type=int, default=400,
+                   help="also time the north-star sharded mode (heads split over ranks, RCCL all-reduce-max "
+                        "GPI) for this many env steps; 0 skips it")
     return p.parse_args()
 
 
@@ -102,6 +105,51 @@ def cpu_baseline(args, seconds: float):
                       f"oracle/ref_cpu.py on torch CPU with {cores} threads"}
 
 
+def bench_sharded(args, world, rank, device, barrier, dist):
+    """North-star multi-GPU mode: T_loc = --heads heads per rank, T_glob =
+    T_loc * world source tasks, one lock-step env stream replicated on every rank, GPI maxima
+    all-reduced (MAX) over RCCL.  Returns env-steps/s of that one stream (max over ranks)."""
+    from sfx.engine import SFEngine
+    from sfx.init import reference_heads
+    from sfx.runner import ShardedEnvLoop
+    from sfx.shard import all_reduce_max_fn
+
+    T_loc, B = args.heads, args.batch
+    Tg = T_loc * world
+    eng = SFEngine(T_loc, SHAPE["n_s"], SHAPE["H"], SHAPE["A"], SHAPE["d"], SHAPE["acts"], max_batch=B, device=device)
+    online, w = reference_heads(Tg, SHAPE["n_s"], SHAPE["H"], SHAPE["A"], SHAPE["d"], SHAPE["acts"], seed=0)
+    eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
+    eng.set_target_update_ev(1000)
+    ar = all_reduce_max_fn(via_host=args.via_host) if world > 1 else (lambda t: None)
+    loop = ShardedEnvLoop(eng, Tg, rank, ar, batch=B, seed=1)
+    for t in range(T_loc):
+        eng.load_head(t, online[rank * T_loc + t], 0)
+        eng.load_head(t, online[rank * T_loc + t], 1)
+    for t in range(Tg):
+        eng.load_w(t, w[t])
+    loop.prefill(1000)
+    loop.set_task(0)
+    loop.run(max(20, args.shard_steps // 10))
+    barrier()
+    t0 = time.perf_counter()
+    loop.run(args.shard_steps)
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device="cpu" if args.via_host else device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    eng.close()
+    v = args.shard_steps / dt
+    return {"value": round(v, 2), "unit": "env steps/s", "ms_per_step": round(1000.0 * dt / args.shard_steps, 4),
+            "steps": args.shard_steps, "heads_total": Tg, "heads_per_gpu": T_loc,
+            "head_updates_per_s": round(v * Tg, 1), "parallelism": f"heads sharded over {world} GPU(s)",
+            "collective": (("gloo via host (rehearsal)" if args.via_host else "RCCL") +
+                           " all-reduce(MAX) of GPI maxima [T_glob,B,A] per round + int64 action key")
+                          if world > 1 else "none (1 rank)",
+            "rounds": loop.sharded.stats}
+
+
 def traffic_from_profiles(kind: str, workload: str):
     """HBM bytes per launch of `kind` from a committed rocprofv3 --pmc pass (profiles/), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -120,15 +168,24 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # SFX_BENCH_BACKEND=gloo rehearses the multi-rank path on a box with fewer GPUs than ranks
+    # (ranks share GPUs, collectives through host memory); the real run is RCCL ("nccl").
+    backend = os.environ.get("SFX_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1) if backend == "gloo" else local
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     else:
         dist = None
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
+    args.via_host = backend != "nccl"
 
     from sfx.engine import SFEngine
     from sfx.init import reference_heads
@@ -165,7 +222,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        t = torch.tensor([dt], device="cpu" if args.via_host else device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     value = world * args.steps / dt
@@ -177,6 +234,10 @@ def main():
     stats = eng.prof_collect()
     eng.prof_enable(False)
     eng.prof_reset()
+
+    sharded = None
+    if args.shard_steps > 0 and args.schedule == "all":
+        sharded = bench_sharded(args, world, rank, device, barrier, dist)
 
     workload = f"reacher17-{args.schedule}-T{T}-B{B}"
     if rank == 0:
@@ -208,6 +269,7 @@ def main():
                                 if native else "python host loop over libsfx graphs")},
             "roofline": roofline,
             "speculation": spec_stats,
+            "sharded": sharded,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -92,7 +92,8 @@ class Replay:
         np.take(self.s, idx, axis=0, out=st.h["s"])
         np.take(self.s1, idx, axis=0, out=st.h["s1"])
         np.take(self.phi, idx, axis=0, out=st.h["phi"])
-        np.take(self.r, idx, out=st.h["r"])
+        if "r" in st.h:
+            np.take(self.r, idx, out=st.h["r"])
         np.take(self.a, idx, out=st.h["a"])
         np.take(self.gamma, idx, out=st.h["gamma"])
         return True
@@ -322,3 +323,71 @@ class NativeEnvLoop:
             rec.update(zip(("task", "have", "c", "a_greedy", "a_taken", "terminal"), (int(m) for m in meta)))
             out.append(rec)
         return out
+
+
+class ShardedEnvLoop:
+    """The all-task env-step loop with the heads sharded across ranks (sfx.shard): every rank
+    runs the same env / replay stream (same seed), owns T_loc heads, and all-reduces the GPI
+    maxima; the env action is identical on every rank."""
+
+    def __init__(self, engine: SFEngine, T_glob: int, rank: int, all_reduce_max, batch: int = 32,
+                 capacity: int = 1_000_000, gamma: float = 0.9, epsilon: float = 0.1, alpha_w: float = 1e-3,
+                 episode_len: int = 500, use_gpi: bool = True, seed: int = 1, rounds: int = 2):
+        from .shard import LibsfxShardBackend, ShardedAllTask
+
+        e = engine
+        self.eng, self.B, self.Tg = engine, batch, T_glob
+        self.gamma, self.epsilon, self.alpha_w, self.T_ep, self.use_gpi = gamma, epsilon, alpha_w, episode_len, use_gpi
+        self.backend = LibsfxShardBackend(engine, T_glob, rank * engine.T, batch)
+        self.sharded = ShardedAllTask(self.backend, T_glob, e.A, all_reduce_max, rounds=rounds)
+        self.rng = np.random.default_rng(seed)
+        self.tasks = [SynthReacher(e.n_s, e.A, e.d, t, self.rng) for t in range(T_glob)]
+        self.replay = Replay(capacity, e.n_s, e.d, self.rng)
+        self.st = Staging([("s", (batch, e.n_s), torch.float32), ("s1", (batch, e.n_s), torch.float32),
+                           ("phi", (batch, e.d), torch.float32), ("a", (batch,), torch.int64),
+                           ("gamma", (batch,), torch.float32), ("snext", (1, e.n_s), torch.float32),
+                           ("phi1", (e.d,), torch.float32), ("r1", (1,), torch.float32)], e.device)
+        self.gpi_counters = np.zeros((T_glob, T_glob), dtype=np.int64)
+
+    def set_task(self, index: int):
+        self.task_index, self.task = index, self.tasks[index]
+        self.steps_in_episode = 0
+        self.s = self.task.initialize()
+        self.st.h["snext"][0] = self.s
+        self.st.upload()
+        d = self.st.d
+        self.sel = self.sharded.step(None, -1, None, None, 0.0, d["snext"], index, self.use_gpi)
+
+    def prefill(self, n: int):
+        for _ in range(n):
+            s = self.task.initialize() if hasattr(self, "task") else self.tasks[0].initialize()
+            a = int(self.rng.integers(self.eng.A))
+            s1, phi, r, _ = (self.task if hasattr(self, "task") else self.tasks[0]).transition(a)
+            self.replay.append(s, a, r, phi, s1, self.gamma)
+
+    def step(self):
+        c, a_greedy = self.sel
+        self.gpi_counters[self.task_index, c] += 1
+        a = int(self.rng.integers(self.eng.A)) if self.rng.random() <= self.epsilon else a_greedy
+        s1, phi, r, terminal = self.task.transition(a)
+        self.replay.append(self.s, a, r, phi, s1, 0.0 if terminal else self.gamma)
+        st = self.st
+        have = self.replay.sample_into(st, self.B)
+        self.steps_in_episode += 1
+        s_next = s1
+        if terminal or self.steps_in_episode >= self.T_ep:
+            s_next = self.task.initialize()
+            self.steps_in_episode = 0
+        st.h["phi1"][:] = phi
+        st.h["r1"][0] = r
+        st.h["snext"][0] = s_next
+        st.upload()
+        d = st.d
+        batch = (d["s"], d["a"], d["phi"], d["s1"], d["gamma"]) if have else None
+        self.sel = self.sharded.step(batch, self.task_index, d["phi1"], d["r1"], self.alpha_w, d["snext"],
+                                     self.task_index, self.use_gpi)
+        self.s = s_next
+
+    def run(self, n: int):
+        for _ in range(n):
+            self.step()
