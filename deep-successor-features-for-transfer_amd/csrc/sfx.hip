@@ -93,6 +93,7 @@ struct sfx_handle {
   hipStream_t cap = nullptr;     // private stream used only to capture graphs
   bool use_graphs = true;
   bool fuse_tdg = true;  // SFX_FUSE_TDG=0: K2 as its own launch
+  bool fuse_v0 = true;   // SFX_FUSE_V0=0: post-update layer-0 forward as its own launch
   AdamHP hp_psi{1e-3, 0.0, 0.9, 0.999, 1e-8};
   AdamHP hp_w{1e-3, 0.0, 0.9, 0.999, 1e-8};
   int target_update_ev = 1000;
@@ -133,6 +134,7 @@ struct sfx_handle {
   float *online = nullptr, *target = nullptr, *am = nullptr, *av = nullptr;
   float *w = nullptr, *wm = nullptr, *wv = nullptr;
   int* step = nullptr;
+  AdamC* adamc = nullptr;
   float *act = nullptr, *dz = nullptr, *rowloss = nullptr;
   int64_t* spec_next = nullptr;
   StepOut* dout = nullptr;  // device
@@ -328,7 +330,7 @@ struct BwdExtra {
   const float* v_xn = nullptr;
 };
 
-bool can_fuse_v0(const sfx_handle* h) { return h->L[0].K <= KFUSE; }
+bool can_fuse_v0(const sfx_handle* h) { return h->fuse_v0 && h->L[0].K <= KFUSE; }
 
 int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const float* phi, const float* r,
             float* losses, const TdgSpec& td, const BwdExtra& ex = BwdExtra()) {
@@ -516,7 +518,7 @@ void free_all(sfx_handle* h) {
   }
   for (hipEvent_t e : h->prof_pool) (void)hipEventDestroy(e);
   for (void* p : {(void*)h->online, (void*)h->target, (void*)h->am, (void*)h->av, (void*)h->w, (void*)h->wm,
-                  (void*)h->wv, (void*)h->step, (void*)h->act, (void*)h->dz, (void*)h->rowloss, (void*)h->spec_next,
+                  (void*)h->wv, (void*)h->step, (void*)h->adamc, (void*)h->act, (void*)h->dz, (void*)h->rowloss, (void*)h->spec_next,
                   (void*)h->dout})
     if (p) (void)hipFree(p);
   if (h->hout) (void)hipHostFree(h->hout);
@@ -631,6 +633,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->use_graphs = !(eg && eg[0] == '0');
   const char* ef = std::getenv("SFX_FUSE_TDG");
   h->fuse_tdg = !(ef && ef[0] == '0');
+  const char* ev0 = std::getenv("SFX_FUSE_V0");
+  h->fuse_v0 = !(ev0 && ev0[0] == '0');
   int off = 0, ptorch = 0;
   for (int l = 0; l < h->NL; ++l) {
     LayerGeo Lr{};
@@ -679,6 +683,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   alloc((void**)&h->wm, wBytes);
   alloc((void**)&h->wv, wBytes);
   alloc((void**)&h->step, sizeof(int) * T);
+  alloc((void**)&h->adamc, sizeof(AdamC) * T);
   alloc((void**)&h->act, sizeof(float) * (size_t)NROLE * T * h->actSize);
   alloc((void**)&h->dz, sizeof(float) * (size_t)T * h->actSize);
   alloc((void**)&h->rowloss, sizeof(float) * (size_t)T * MMAX);
@@ -714,6 +719,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   G.wm = h->wm;
   G.wv = h->wv;
   G.step = h->step;
+  G.adamc = h->adamc;
   G.act = h->act;
   G.dz = h->dz;
   G.rowloss = h->rowloss;

@@ -85,6 +85,8 @@ struct LayerGeo {
   int N, K, wOff, bOff, actIn, actOut;  // actIn: activation that produced this layer's input
 };
 
+struct AdamC;
+
 struct Geo {
   int T, NL, A, d, O, dpad;
   long long P;        // packed head stride (floats)
@@ -97,6 +99,7 @@ struct Geo {
   float* wm;
   float* wv;
   int* step;          // [T]
+  AdamC* adamc;       // [T] ψ-Adam constants of each head's current step (written where step is bumped)
   float* act;         // [NROLE][T][actSize]
   float* dz;          // [T][actSize]
   float* rowloss;     // [T][MMAX] per-row Σ (c - t)^2 of the last TD target
@@ -612,7 +615,11 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
   if constexpr (TDG) {
     // N = A*d <= 128: at most one 64-wide chunk per wave; its W slice is fetched before K2
     __shared__ TdgSmem sm;
-    if (tile == 0 && A.inc_step && threadIdx.x == 0) G.step[head] += 1;  // no dW reads it in this launch
+    if (tile == 0 && A.inc_step && threadIdx.x == 0) {  // no dW reads them in this launch
+      const int st = G.step[head] + 1;
+      G.step[head] = st;
+      G.adamc[head] = adam_consts(A.hp, st);
+    }
     if (A.flag && tile == 0 && blockIdx.y == 0 && threadIdx.x == 0) *A.flag = A.flag_value;
     const int nb = wave * 64 + g * 16;
     float bw[16];
@@ -696,7 +703,7 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
   float* Pw = G.online + wo;
   float* Mw = G.am + wo;
   float* Vw = G.av + wo;
-  const AdamC c = adam_consts(A.hp, G.step[head]);
+  const AdamC c = G.adamc[head];  // bias corrections of this step (double pow once per head, not per thread)
   const int nn = n0 + r, kb0 = k0 + r, kb1 = k0 + 16 + r;
   // prefetch the optimizer state of the 8 weights this lane will update
   float pp[8], pm[8], pv[8];
@@ -822,7 +829,10 @@ __device__ void role_tail(const Geo& G, const BwdArgs& A, int head) {
       lo[1] = l1;
       lo[2] = l2;
     }
-    if (A.step_in_tail) G.step[head] = step;
+    if (A.step_in_tail) {
+      G.step[head] = step;
+      G.adamc[head] = adam_consts(A.hp, step);
+    }
   }
 }
 
