@@ -94,6 +94,7 @@ struct sfx_handle {
   bool use_graphs = true;
   bool fuse_tdg = true;  // SFX_FUSE_TDG=0: K2 as its own launch
   bool fuse_v0 = true;   // SFX_FUSE_V0=0: post-update layer-0 forward as its own launch
+  bool xcd = true;       // SFX_XCD=0: plain (tile, head) grids instead of XCD-aware ones
   AdamHP hp_psi{1e-3, 0.0, 0.9, 0.999, 1e-8};
   AdamHP hp_w{1e-3, 0.0, 0.9, 0.999, 1e-8};
   int target_update_ev = 1000;
@@ -340,6 +341,8 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     RC(run_tdg(h, head0, nhead, td.guess, M, td.use_gpi, td.a, phi, td.gamma, td.next, td.next_stride, td.flag,
                td.xmax, td.poloff));
   BwdArgs A{};
+  A.xcd = h->xcd && nhead > 1 ? 1 : 0;
+  A.nhead = nhead;
   A.step_in_tail = fuse ? 0 : 1;
   A.tdg_use_gpi = td.use_gpi;
   A.tdg_guess = td.guess;
@@ -402,12 +405,14 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     }
     A.nc = 0;
     A.tail = li == tail_at ? 1 : 0;
+    const int ntile = A.tdg ? A.na : A.na + A.nb + A.nc + A.tail;
+    const dim3 grid = A.xcd ? dim3(8 * cdiv(nhead, 8) * ntile) : dim3(ntile, nhead);
     if (A.tdg && tdg_variant(h) == 1)  // d <= 8
-      launch(h, K_BWD, by, k_bwd_tdg<2, 8>, dim3(A.na, nhead), dim3(256), h->G, A);
+      launch(h, K_BWD, by, k_bwd_tdg<2, 8>, grid, dim3(256), h->G, A);
     else if (A.tdg)
-      launch(h, K_BWD, by, k_bwd_tdg<4, 4>, dim3(A.na, nhead), dim3(256), h->G, A);
+      launch(h, K_BWD, by, k_bwd_tdg<4, 4>, grid, dim3(256), h->G, A);
     else
-      launch(h, K_BWD, by, k_bwd, dim3(A.na + A.nb + A.nc + A.tail, nhead), dim3(256), h->G, A);
+      launch(h, K_BWD, by, k_bwd, grid, dim3(256), h->G, A);
   }
   A.na = 0;
   A.tdg = 0;
@@ -423,7 +428,9 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.act0 = h->L[0].actOut;
   A.v_x = ex.v_x;
   A.v_xn = ex.v_xn;
-  launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), k_bwd, dim3(A.nb + A.nc + A.tail, nhead), dim3(256), h->G, A);
+  const int ntile = A.nb + A.nc + A.tail;
+  launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), k_bwd,
+         A.xcd ? dim3(8 * cdiv(nhead, 8) * ntile) : dim3(ntile, nhead), dim3(256), h->G, A);
   LAUNCHCHK();
   return SFX_OK;
 }
@@ -635,6 +642,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->fuse_tdg = !(ef && ef[0] == '0');
   const char* ev0 = std::getenv("SFX_FUSE_V0");
   h->fuse_v0 = !(ev0 && ev0[0] == '0');
+  const char* ex = std::getenv("SFX_XCD");
+  h->xcd = !(ex && ex[0] == '0');
   int off = 0, ptorch = 0;
   for (int l = 0; l < h->NL; ++l) {
     LayerGeo Lr{};

@@ -119,6 +119,17 @@ struct Geo {
 
 __device__ __forceinline__ int rslot(unsigned long long mask, int head) { return (int)((mask >> head) & 1ull); }
 
+// XCD-aware decode of a 1-D grid of 8 * ceil(nhead / 8) * ntile blocks into (head, tile):
+// workgroups are dealt round-robin over the 8 XCDs, so every tile of head h runs on the XCD
+// of slot h % 8 and the head's parameters, Adam state and activations stay in that XCD's L2
+// from one launch to the next.  Returns false for the padding blocks.
+__device__ __forceinline__ bool xcd_decode(int b, int nhead, int ntile, int& head, int& tile) {
+  const int hp = (nhead + 7) >> 3, k = b >> 3;
+  head = (b & 7) + 8 * (k % hp);
+  tile = k / hp;
+  return head < nhead && tile < ntile;
+}
+
 // -------------------------------------------------------------------------------------
 // Adam, torch 2.10 single-tensor semantics (torch/optim/adam.py:457,476,531-547):
 //   g += wd*p ; m = lerp(m, g, 1-b1) ; v = v*b2 + ((1-b2)*g)*g
@@ -418,6 +429,7 @@ struct RoleGeo {
 
 struct BwdArgs {
   int M, na, nb, nc, tail, head0, train_w, inc_step;
+  int xcd, nhead;               // xcd: 1-D XCD-aware grid (xcd_decode) over nhead heads
   int step_in_tail;             // 1: the tail bumps the Adam step; 0: dX tile 0 of this launch does
   int tdg, tdg_use_gpi, tdg_guess, tdg_next_stride, flag_value, pad2_;  // fused TD target (K2)
   const int64_t* tdg_a;
@@ -620,7 +632,7 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
       G.step[head] = st;
       G.adamc[head] = adam_consts(A.hp, st);
     }
-    if (A.flag && tile == 0 && blockIdx.y == 0 && threadIdx.x == 0) *A.flag = A.flag_value;
+    if (A.flag && tile == 0 && head == A.head0 && threadIdx.x == 0) *A.flag = A.flag_value;
     const int nb = wave * 64 + g * 16;
     float bw[16];
 #pragma unroll
@@ -838,8 +850,11 @@ __device__ void role_tail(const Geo& G, const BwdArgs& A, int head) {
 
 __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
   __shared__ floatx4 red[4][2][64];
-  const int head = A.head0 + blockIdx.y;
-  int bx = blockIdx.x;
+  int head = A.head0 + blockIdx.y, bx = blockIdx.x;
+  if (A.xcd) {
+    if (!xcd_decode(blockIdx.x, A.nhead, A.na + A.nb + A.nc + A.tail, head, bx)) return;
+    head += A.head0;
+  }
   if (bx < A.na) {
     role_dx<false>(G, A, head, bx, red);
     return;
@@ -861,7 +876,12 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
 template <int VMAX, int U>
 __global__ __launch_bounds__(256) void k_bwd_tdg(Geo G, BwdArgs A) {
   __shared__ floatx4 red[4][2][64];
-  role_dx<true, VMAX, U>(G, A, A.head0 + blockIdx.y, blockIdx.x, red);
+  int head = A.head0 + blockIdx.y, bx = blockIdx.x;
+  if (A.xcd) {
+    if (!xcd_decode(blockIdx.x, A.nhead, A.na, head, bx)) return;
+    head += A.head0;
+  }
+  role_dx<true, VMAX, U>(G, A, head, bx, red);
 }
 
 // -------------------------------------------------------------------------------------
