@@ -252,6 +252,10 @@ def main():
                     "bytes_per_launch": round(bpl), "avg_launch_us": round(avg_us, 3),
                     "share_of_gpu_time": round(us / max(sum(v[1] for v in stats.values()), 1e-9), 3),
                     "per_kind_avg_us": {KIND_NAMES[k]: round(v[1] / max(v[0], 1), 3) for k, v in stats.items() if v[0]}}
+        # SURVEY §8(d)'s whole-step figure: algorithmic bytes of every launch of an env step x env-steps/s
+        step_bytes = sum(v[2] for v in stats.values()) / max(args.prof_steps, 1)
+        roofline["per_step"] = {"bytes_per_env_step": round(step_bytes), "achieved": round(step_bytes * value / 1e9, 2),
+                                "frac": round(step_bytes * value / 1e9 / HBM_PEAK_GBS, 5), "unit": "GB/s"}
         spec_stats = eng.step_stats()
         if native:
             spec_stats.update(loop.stats())

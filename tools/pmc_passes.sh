@@ -4,6 +4,7 @@
 cd /tmp && export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${1:-pmc}
+export SFX_RUNNER_PIPELINE=0  # the profiler serialises dispatches: a pre-launched gate would wait on the blocked host
 ARGS="--steps 100 --warmup 10 --prof-steps 20 --no-cpu-baseline --shard-steps 0"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${TAG}_fetch -o run -- python3 bench.py $ARGS > gpurun_out/${TAG}_fetch.log 2>&1 && \
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${TAG}_write -o run -- python3 bench.py $ARGS > gpurun_out/${TAG}_write.log 2>&1
