@@ -95,6 +95,7 @@ struct sfx_handle {
   bool fuse_tdg = true;  // SFX_FUSE_TDG=0: K2 as its own launch
   bool fuse_v0 = true;   // SFX_FUSE_V0=0: post-update layer-0 forward as its own launch
   bool xcd = true;       // SFX_XCD=0: plain (tile, head) grids instead of XCD-aware ones
+  int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
   AdamHP hp_psi{1e-3, 0.0, 0.9, 0.999, 1e-8};
   AdamHP hp_w{1e-3, 0.0, 0.9, 0.999, 1e-8};
   int target_update_ev = 1000;
@@ -244,11 +245,15 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
   F.mask = h->mask;
   F.lms_head = -1;
   int ninst = 0;
+  bool uniform = true;  // every group covers heads 0..T-1: XCD-aware grid possible
   FwdGroup* slots[4] = {&F.g0, &F.g1, &F.g2, &F.g3};
   for (const FwdGroup& g : groups) {
     *slots[F.ngroups++] = g;
     ninst += g.n;
+    uniform = uniform && g.head0 == 0 && g.n == h->T;
   }
+  F.xcd = h->xcd && uniform && h->T > 1 ? 1 : 0;
+  F.nh = h->T;
   for (int l = ex.l0; l < h->NL; ++l) {
     const LayerGeo& L = h->L[l];
     F.N = L.N;
@@ -265,11 +270,19 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     F.lms_alpha = ex.lms_alpha;
     F.flag = first ? ex.flag : nullptr;
     F.flag_value = ex.flag_value;
-    const dim3 grid(cdiv(L.N, 16), ninst, cdiv(M, 32));
+    F.ntN = cdiv(L.N, 16);
+    F.ntM = cdiv(M, 32);
+    const dim3 grid = F.xcd ? dim3(8 * cdiv(h->T, 8) * F.ntN * F.ntM * F.ngroups) : dim3(F.ntN, ninst, F.ntM);
     const double by = 4.0 * ninst * ((double)L.N * L.K + L.N + (double)M * L.K + (double)M * L.N);
     // the vector path needs K % 64 == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
-    const bool vec = (L.K % 64) == 0 && (l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0));
-    launch(h, K_FWD, by, vec ? k_fwd<true> : k_fwd<false>, grid, dim3(256), h->G, F);
+    const bool aligned = l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0);
+    if (h->fwd_waves == 8) {
+      const bool vec = (L.K % 32) == 0 && aligned;
+      launch(h, K_FWD, by, vec ? k_fwd<true, 8> : k_fwd<false, 8>, grid, dim3(512), h->G, F);
+    } else {
+      const bool vec = (L.K % 64) == 0 && aligned;
+      launch(h, K_FWD, by, vec ? k_fwd<true, 4> : k_fwd<false, 4>, grid, dim3(256), h->G, F);
+    }
   }
   LAUNCHCHK();
   return SFX_OK;
@@ -355,6 +368,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.flag = td.flag;
   A.flag_value = h->T;
   const int tail_at = fuse ? 1 : 0;  // launch index of the loss tail (needs every row's loss)
+  const bool need_tail = losses || r || !fuse;  // losses, a w step or the Adam step bump
   const double tdg_bytes = 4.0 * nhead * M * ((td.use_gpi ? h->T : 1) * h->O + 2.0 * h->O + 2.0 * h->d + 4);
   A.M = M;
   A.head0 = head0;
@@ -404,7 +418,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
       A.nb = 0;
     }
     A.nc = 0;
-    A.tail = li == tail_at ? 1 : 0;
+    A.tail = li == tail_at && need_tail ? 1 : 0;
     const int ntile = A.tdg ? A.na : A.na + A.nb + A.nc + A.tail;
     const dim3 grid = A.xcd ? dim3(8 * cdiv(nhead, 8) * ntile) : dim3(ntile, nhead);
     if (A.tdg && tdg_variant(h) == 1)  // d <= 8
@@ -420,7 +434,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.nb = dw_tiles(1);
   A.rc = geo(0);
   A.nc = dw_tiles(0);
-  A.tail = h->NL - 1 == tail_at ? 1 : 0;
+  A.tail = h->NL - 1 == tail_at && need_tail ? 1 : 0;
   A.fuse_v0 = ex.fuse_v0 ? 1 : 0;
   A.vM = M + (ex.v_xn ? 1 : 0);
   A.vOff = h->actOff[0];
@@ -644,6 +658,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->fuse_v0 = !(ev0 && ev0[0] == '0');
   const char* ex = std::getenv("SFX_XCD");
   h->xcd = !(ex && ex[0] == '0');
+  const char* efw = std::getenv("SFX_FWD_WAVES");
+  h->fwd_waves = efw && std::atoi(efw) == 4 ? 4 : 8;
   int off = 0, ptorch = 0;
   for (int l = 0; l < h->NL; ++l) {
     LayerGeo Lr{};

@@ -119,14 +119,29 @@ struct Geo {
 
 __device__ __forceinline__ int rslot(unsigned long long mask, int head) { return (int)((mask >> head) & 1ull); }
 
+// Division by a runtime divisor 1 <= d, for 0 <= x < 2^22: one multiply by a float reciprocal
+// and one correction step (a hardware integer divide is a ~40-instruction sequence, and the
+// index arithmetic of the GPI / TD loops used dozens of them per thread).
+struct FDiv {
+  int d;
+  float inv;
+};
+__device__ __forceinline__ FDiv fdiv(int d) { return FDiv{d, __frcp_rn((float)d)}; }
+__device__ __forceinline__ int operator/(int x, const FDiv& f) {
+  int q = (int)((float)x * f.inv);
+  const int r = x - q * f.d;
+  return q + (r >= f.d) - (r < 0);
+}
+
 // XCD-aware decode of a 1-D grid of 8 * ceil(nhead / 8) * ntile blocks into (head, tile):
 // workgroups are dealt round-robin over the 8 XCDs, so every tile of head h runs on the XCD
 // of slot h % 8 and the head's parameters, Adam state and activations stay in that XCD's L2
 // from one launch to the next.  Returns false for the padding blocks.
 __device__ __forceinline__ bool xcd_decode(int b, int nhead, int ntile, int& head, int& tile) {
   const int hp = (nhead + 7) >> 3, k = b >> 3;
-  head = (b & 7) + 8 * (k % hp);
-  tile = k / hp;
+  const int kq = hp == 1 ? k : k / fdiv(hp);
+  head = (b & 7) + 8 * (k - kq * hp);
+  tile = kq;
   return head < nhead && tile < ntile;
 }
 
@@ -192,7 +207,8 @@ struct FwdGroup {
 
 struct FwdArgs {
   int M, N, K, act, wOff, bOff, xOff, yOff;  // xOff < 0: layer input is xa / xb
-  int ngroups, lms_head, flag_value, pad_;
+  int ngroups, lms_head, flag_value, xcd;  // xcd: 1-D XCD-aware grid (every group has heads 0..nh-1)
+  int nh, ntN, ntM, pad2_;
   unsigned long long mask;
   FwdGroup g0, g1, g2, g3;
   const float* xa;
@@ -220,10 +236,21 @@ __device__ void lms_block(const Geo& G, const FwdArgs& F) {
   if (tid < d) w[tid] = __fadd_rn(wk, __fmul_rn(s_e, pk));
 }
 
-template <bool VEC>
-__global__ __launch_bounds__(256) void k_fwd(Geo G, FwdArgs F) {
+template <bool VEC, int NW>
+__global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
+  constexpr int KW = 256 / NW;  // K chunk of one wave per iteration (NW waves cover 256)
+  constexpr int KL = KW / 4;    // consecutive k per lane (4 lane groups per MFMA k-step)
   // instance -> (group, head) with constant-index selects (no dynamic kernarg indexing)
-  int y = blockIdx.y;
+  int y = blockIdx.y, tN = blockIdx.x, tM = blockIdx.z;
+  if (F.xcd) {  // head h's tiles on the XCD of slot h % 8 (see xcd_decode)
+    const int b = blockIdx.x, hp = (F.nh + 7) >> 3, k = b >> 3;
+    const int r = hp == 1 ? k : k / fdiv(hp), hd = (b & 7) + 8 * (k - r * hp);
+    const int rN = r / fdiv(F.ntN), gi = rN / fdiv(F.ntM);
+    tN = r - rN * F.ntN;
+    tM = rN - gi * F.ntM;
+    if (hd >= F.nh || gi >= F.ngroups) return;
+    y = gi * F.nh + hd;
+  }
   FwdGroup grp = F.g0;
   if (F.ngroups > 1 && y >= grp.n) { y -= grp.n; grp = F.g1; }
   if (F.ngroups > 2 && y >= grp.n) { y -= grp.n; grp = F.g2; }
@@ -234,7 +261,7 @@ __global__ __launch_bounds__(256) void k_fwd(Geo G, FwdArgs F) {
                                          : G.online + G.slot_off(rslot(F.mask, head) ^ (grp.which == P_NEW), head);
   const float* X = F.xOff < 0 ? (grp.xsel == 1 ? F.xa : F.xb) : G.actp(grp.role, head, F.xOff);
   float* Y = G.actp(grp.role, head, F.yOff);
-  const int n0 = blockIdx.x * 16, m0 = blockIdx.z * 32;
+  const int n0 = tN * 16, m0 = tM * 32;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
   const int ma = m0 + r, mb = m0 + 16 + r, n = n0 + r;
   const bool oka = ma < M, okb = mb < M, okn = n < N;
@@ -245,12 +272,12 @@ __global__ __launch_bounds__(256) void k_fwd(Geo G, FwdArgs F) {
   const int Lx = threadIdx.x & 63, col = n0 + (Lx & 15);
   const float bias = (threadIdx.x < 128 && col < N) ? P[F.bOff + col] : 0.f;
   floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  for (int kc = wave * 64; kc < K; kc += 256) {
-    const int kb = kc + g * 16;
-    float a0[16], a1[16], bw[16];
-    if constexpr (VEC) {  // K % 64 == 0, rows 16-B aligned: four float4 per operand row
+  for (int kc = wave * KW; kc < K; kc += 256) {
+    const int kb = kc + g * KL;
+    float a0[KL], a1[KL], bw[KL];
+    if constexpr (VEC) {  // K % KW == 0, rows 16-B aligned: KL/4 float4 per operand row
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < KL / 4; ++q) {
         const float4 ta = oka ? reinterpret_cast<const float4*>(xra + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
         const float4 tb = okb ? reinterpret_cast<const float4*>(xrb + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
         const float4 tw = okn ? reinterpret_cast<const float4*>(wr + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -260,7 +287,7 @@ __global__ __launch_bounds__(256) void k_fwd(Geo G, FwdArgs F) {
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
+      for (int j = 0; j < KL; ++j) {
         const bool kin = kb + j < K;
         a0[j] = (oka && kin) ? xra[kb + j] : 0.f;
         a1[j] = (okb && kin) ? xrb[kb + j] : 0.f;
@@ -268,21 +295,20 @@ __global__ __launch_bounds__(256) void k_fwd(Geo G, FwdArgs F) {
       }
     }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < KL; ++j) {
       acc0 = mfma4(a0[j], bw[j], acc0);
       acc1 = mfma4(a1[j], bw[j], acc1);
     }
   }
-  __shared__ floatx4 red[4][2][64];
+  __shared__ floatx4 red[NW][2][64];
   red[wave][0][lane] = acc0;
   red[wave][1][lane] = acc1;
   __syncthreads();
   if (threadIdx.x < 128) {
     const int s = threadIdx.x >> 6;
     floatx4 v = red[0][s][Lx];
-    v += red[1][s][Lx];
-    v += red[2][s][Lx];
-    v += red[3][s][Lx];
+#pragma unroll
+    for (int w2 = 1; w2 < NW; ++w2) v += red[w2][s][Lx];
     if (col < N) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -291,7 +317,7 @@ __global__ __launch_bounds__(256) void k_fwd(Geo G, FwdArgs F) {
       }
     }
   }
-  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+  if (tN == 0 && tM == 0 && blockIdx.y == 0 && (F.xcd ? blockIdx.x == 0 : true)) {
     if (F.flag && threadIdx.x == 0) *F.flag = F.flag_value;
     if (F.lms_head >= 0) lms_block(G, F);
   }
@@ -352,8 +378,9 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
     for (int a = tid; a < Aa; a += 256) s_m[a] = xr[a];
   } else {
     const int t0 = A.use_gpi ? 0 : pol, nt = A.use_gpi ? T : 1;
+    const FDiv fA = fdiv(Aa);
     for (int idx = tid; idx < nt * Aa; idx += 256) {
-      const int t = t0 + idx / Aa, a = idx % Aa;
+      const int tq = idx / fA, t = t0 + tq, a = idx - tq * Aa;
       const float* p = G.actp(t < pol ? A.guess : R_S1, t, NLm) + (size_t)b * O + a * d;
       float q = 0.f;
 #pragma unroll 8
@@ -477,13 +504,14 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
   const bool xm = A.tdg_xmax != nullptr;
   const int t0 = A.tdg_use_gpi ? 0 : pol, nt = A.tdg_use_gpi ? T : 1, TA = nt * Aa, n = xm ? 0 : nb * TA, V = d >> 2;
   const int guess = A.tdg_guess;
+  const FDiv fTA = fdiv(TA), fA = fdiv(Aa), fO = fdiv(O);
   // ---- stage A: all global loads
   float4 v[U][VMAX];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int idx = tid + u * 256;
     const bool ok = idx < n;
-    const int bl = idx / TA, rem = idx - bl * TA, t = t0 + rem / Aa, a = rem - (rem / Aa) * Aa;
+    const int bl = idx / fTA, rem = idx - bl * TA, tq = rem / fA, t = t0 + tq, a = rem - tq * Aa;
     const float4* p = reinterpret_cast<const float4*>(G.actp(t < pol ? guess : R_S1, ok ? t : 0, NLm) +
                                                       (ok ? (size_t)(m0 + bl) * O + a * d : 0));
 #pragma unroll
@@ -549,7 +577,7 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
   __syncthreads();
   // ---- stage C: max over heads per (row, action)   (torch.max(q1, axis=1))
   for (int i = tid; i < (xm ? 0 : nb * Aa); i += 256) {
-    const int bl = i / Aa, a = i - bl * Aa;
+    const int bl = i / fA, a = i - bl * Aa;
     const float* qb = sm.q + bl * TA + a;
     float mx = qb[0];
     for (int t = 1; t < nt; ++t) mx = fmaxf(mx, qb[t * Aa]);
@@ -574,7 +602,7 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
   const float norm = (float)(2.0 / ((double)M * (double)O));
   float* gout = G.dzp(pol, NLm) + (size_t)m0 * O;
   for (int i = tid; i < nb * O; i += 256) {
-    const int bl = i / O, o = i - bl * O, ab = sm.a[bl];
+    const int bl = i / fO, o = i - bl * O, ab = sm.a[bl];
     float gv = 0.f;
     if (ab >= 0 && ab < Aa && o >= ab * d && o < ab * d + d) {
       const int k = o - ab * d;
@@ -800,40 +828,61 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
 }
 
 // loss finalisation, optional w step, Adam step counter (one workgroup per head)
+// Deterministic block sum (fixed pairwise tree over 256 partials) -- result in every thread.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+#pragma unroll
+  for (int s = 128; s >= 1; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] = __fadd_rn(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  const float r = red[0];
+  __syncthreads();
+  return r;
+}
+
+// loss finalisation, optional w step, Adam step counter (one workgroup per head).  The host
+// drops the tail when it has nothing to do (no losses requested, no w step, step bumped in
+// the fused TD launch).
 __device__ void role_tail(const Geo& G, const BwdArgs& A, int head) {
   const int M = A.M, d = G.d, tid = threadIdx.x;
   __shared__ float s_e[MMAX];
-  __shared__ float s_x[1];
+  __shared__ float s_red[256];
+  __shared__ float s_phi[2048];
   const int step = A.step_in_tail && A.inc_step ? G.step[head] + 1 : G.step[head];
   const float* rl = G.rowloss + (long long)head * MMAX;
   float* w = G.w + (long long)head * G.dpad;
+  float part = 0.f;  // this thread's rows of Σ_b rowloss (b = tid, tid + 256, ...)
+  for (int b = tid; b < M; b += 256) part = __fadd_rn(part, rl[b]);
   float l2 = 0.f;
   if (A.train_w) {
     // r_fit = w·φ_b ; e_b = r_fit - r_b ; dw = Σ_b (2/M) e_b φ_b   (sfdqn.py:340-342)
+    const bool lds_phi = M * d <= 2048;
+    if (lds_phi)
+      for (int j = tid; j < M * d; j += 256) s_phi[j] = A.phi[j];
+    __syncthreads();
+    const float* ph = lds_phi ? s_phi : A.phi;
+    float se = 0.f;
     for (int b = tid; b < M; b += 256) {
       float rf = 0.f;
-      for (int k = 0; k < d; ++k) rf = __builtin_fmaf(w[k], A.phi[(size_t)b * d + k], rf);
+      for (int k = 0; k < d; ++k) rf = __builtin_fmaf(w[k], ph[(size_t)b * d + k], rf);
       s_e[b] = __fsub_rn(rf, A.r[b]);
+      se = __builtin_fmaf(s_e[b], s_e[b], se);
     }
-    __syncthreads();
-    if (tid == 0) {
-      float se = 0.f;
-      for (int b = 0; b < M; ++b) se = __builtin_fmaf(s_e[b], s_e[b], se);
-      s_x[0] = (float)((double)se / (double)M);
-    }
+    se = block_sum(se, s_red);  // also orders s_e for the readers below
     const AdamC c = adam_consts(A.hpw, step);
     const float nrm = (float)(2.0 / (double)M);
     float gw = 0.f;
     if (tid < d) {
-      for (int b = 0; b < M; ++b) gw = __builtin_fmaf(__fmul_rn(nrm, s_e[b]), A.phi[(size_t)b * d + tid], gw);
+      for (int b = 0; b < M; ++b) gw = __builtin_fmaf(__fmul_rn(nrm, s_e[b]), ph[(size_t)b * d + tid], gw);
     }
     __syncthreads();
     if (tid < d) adam_el(w + tid, G.wm + (long long)head * G.dpad + tid, G.wv + (long long)head * G.dpad + tid, gw, c);
-    l2 = s_x[0];
+    l2 = (float)((double)se / (double)M);
   }
+  const float s = A.losses ? block_sum(part, s_red) : 0.f;
   if (tid == 0) {
-    float s = 0.f;
-    for (int b = 0; b < M; ++b) s = __fadd_rn(s, rl[b]);
     const float l1 = (float)((double)s / ((double)M * (double)G.O));
     if (A.losses) {
       float* lo = A.losses + 3 * (head - A.head0);
@@ -899,58 +948,115 @@ struct GpiArgs {
   int64_t* sel_out;  // [2] or null
 };
 
+// argmax helpers: (value, index) packed so that an integer max picks the largest value and,
+// among equal values, the smallest index (torch.argmax's first-index rule); -0 == +0.
+__device__ __forceinline__ unsigned long long argmax_key(float v, int idx) {
+  const unsigned int u = __float_as_uint(__fadd_rn(v, 0.f));
+  const unsigned int o = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)o << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)idx);
+}
+__device__ __forceinline__ int argmax_idx(unsigned long long key) { return (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull)); }
+__device__ __forceinline__ unsigned long long wave_max(unsigned long long k) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const unsigned long long o = __shfl_xor(k, m, 64);
+    k = o > k ? o : k;
+  }
+  return k;
+}
+
 __device__ void gpi_row(const Geo& G, const GpiArgs& A, int b) {
   const int tid = threadIdx.x;
-  const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff;
+  const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, TA = T * Aa;
   __shared__ float s_q[QMAX];
   __shared__ float s_w[DMAX];
   __shared__ float s_mt[256], s_ma[256];
-  for (int k = tid; k < d; k += 256) s_w[k] = A.w[k];
   const long long ob = (long long)(A.row0 + b);
   const int lb = A.rowoff + b;
+  const FDiv fA = fdiv(Aa);
   if (A.psi_out) {
+    const FDiv fO = fdiv(O);
     for (int idx = tid; idx < T * O; idx += 256) {
-      const int t = idx / O, o = idx - t * O;
+      const int t = idx / fO, o = idx - t * O;
       A.psi_out[(ob * T + t) * O + o] = G.actp(A.role, t, NLm)[(size_t)lb * O + o];
     }
   }
-  __syncthreads();
-  for (int idx = tid; idx < T * Aa; idx += 256) {
-    const int t = idx / Aa, a = idx - t * Aa;
-    const float* p = G.actp(A.role, t, NLm) + (size_t)lb * O + a * d;
+  if (TA <= 256 && (d & 3) == 0 && d <= 16 && ((uintptr_t)A.w & 15) == 0) {  // one dot per thread, ψ and w requested together
+    const int V4 = d >> 2, t = tid / fA, a = tid - t * Aa;
+    const bool act = tid < TA;
+    const float4* p4 = reinterpret_cast<const float4*>(G.actp(A.role, act ? t : 0, NLm) + (size_t)lb * O + (act ? a * d : 0));
+    const float4* w4 = reinterpret_cast<const float4*>(A.w);
+    float4 pv[4], wv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pv[j] = (act && j < V4) ? p4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      wv[j] = j < V4 ? w4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j < V4) {
+        q = __builtin_fmaf(pv[j].x, wv[j].x, q);
+        q = __builtin_fmaf(pv[j].y, wv[j].y, q);
+        q = __builtin_fmaf(pv[j].z, wv[j].z, q);
+        q = __builtin_fmaf(pv[j].w, wv[j].w, q);
+      }
+    }
+    if (act) {
+      s_q[tid] = q;
+      if (A.q_out) A.q_out[(ob * T + t) * Aa + a] = q;
+    }
+  } else {
+    for (int k = tid; k < d; k += 256) s_w[k] = A.w[k];
+    __syncthreads();
+    for (int idx = tid; idx < TA; idx += 256) {
+      const int t = idx / fA, a = idx - t * Aa;
+      const float* p = G.actp(A.role, t, NLm) + (size_t)lb * O + a * d;
+      float q = 0.f;
 #pragma unroll 8
-    for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
-    s_q[idx] = q;
-    if (A.q_out) A.q_out[(ob * T + t) * Aa + a] = q;
+      for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
+      s_q[idx] = q;
+      if (A.q_out) A.q_out[(ob * T + t) * Aa + a] = q;
+    }
   }
   __syncthreads();
-  for (int t = tid; t < T; t += 256) {
+  for (int t = tid; t < T; t += 256) {  // max over actions per head (torch.max(q, axis=2))
     float mx = s_q[t * Aa];
     for (int a = 1; a < Aa; ++a) mx = fmaxf(mx, s_q[t * Aa + a]);
     s_mt[t] = mx;
   }
-  for (int a = tid; a < Aa; a += 256) {
+  for (int a = tid; a < Aa; a += 256) {  // max over heads per action (torch.max(q1, axis=1))
     float mx = s_q[a];
     for (int t = 1; t < T; ++t) mx = fmaxf(mx, s_q[t * Aa + a]);
     s_ma[a] = mx;
   }
   __syncthreads();
-  if (tid == 0) {
-    int tb = 0, ab = 0;
-    for (int t = 1; t < T; ++t)
-      if (s_mt[t] > s_mt[tb]) tb = t;
-    for (int a = 1; a < Aa; ++a)
-      if (s_ma[a] > s_ma[ab]) ab = a;
-    if (A.task_out) A.task_out[ob] = tb;
-    if (A.next_out) A.next_out[ob] = ab;
-    if (A.sel_out) {
-      const int c = A.use_gpi ? tb : A.select_task;
-      int act = 0;
-      for (int a = 1; a < Aa; ++a)
-        if (s_q[c * Aa + a] > s_q[c * Aa + act]) act = a;
-      A.sel_out[0] = c;
-      A.sel_out[1] = act;
+  if (tid < 64) {  // first-index argmaxes by one wave
+    unsigned long long kt = 0ull, ka = 0ull;
+    for (int t = tid; t < T; t += 64) {
+      const unsigned long long k = argmax_key(s_mt[t], t);
+      kt = k > kt ? k : kt;
+    }
+    for (int a = tid; a < Aa; a += 64) {
+      const unsigned long long k = argmax_key(s_ma[a], a);
+      ka = k > ka ? k : ka;
+    }
+    const int tb = argmax_idx(wave_max(kt)), ab = argmax_idx(wave_max(ka));
+    const int c = A.use_gpi ? tb : A.select_task;
+    unsigned long long kc = 0ull;
+    if (A.sel_out)
+      for (int a = tid; a < Aa; a += 64) {
+        const unsigned long long k = argmax_key(s_q[c * Aa + a], a);
+        kc = k > kc ? k : kc;
+      }
+    const int act = A.sel_out ? argmax_idx(wave_max(kc)) : 0;
+    if (tid == 0) {
+      if (A.task_out) A.task_out[ob] = tb;
+      if (A.next_out) A.next_out[ob] = ab;
+      if (A.sel_out) {
+        A.sel_out[0] = c;
+        A.sel_out[1] = act;
+      }
     }
   }
 }
@@ -984,38 +1090,74 @@ __global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
   }
   if (i == 0) return;  // policy 0 sees only pre-update heads: always exact
   const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, TA = T * Aa;
+  const FDiv fTA = fdiv(TA), fA = fdiv(Aa);
   const int b0 = blockIdx.y * V.rows;
   const int nb = V.M - b0 < V.rows ? V.M - b0 : V.rows;
   if (nb <= 0) return;
-  __shared__ float s_w[DMAX];
   __shared__ float s_q[QMAX];
+  __shared__ float s_m[QMAX];
+  __shared__ float s_w[DMAX];
   __shared__ int s_bad;
   const float* wrow = G.w + (long long)i * G.dpad;
-  for (int k = tid; k < d; k += 256) s_w[k] = wrow[k];
+  const int n = nb * TA;
+  const int spec = tid < nb ? (int)V.spec_next[(size_t)i * V.spec_stride + b0 + tid] : 0;
   if (tid == 0) s_bad = 0;
-  __syncthreads();
-  for (int idx = tid; idx < nb * TA; idx += 256) {
-    const int bl = idx / TA, rem = idx - bl * TA, t = rem / Aa, a = rem - t * Aa;
-    const float* p = G.actp(t < i ? V.post : R_S1, t, NLm) + (size_t)(b0 + bl) * O + a * d;
+  if (n <= 256 && (d & 3) == 0 && d <= 16) {
+    // one dot per thread; ψ, w and the speculated action all requested before the first wait
+    const int V4 = d >> 2;
+    const int bl = tid / fTA, rem = tid - bl * TA, t = rem / fA, a = rem - t * Aa;
+    const bool act = tid < n;
+    const float4* p4 = reinterpret_cast<const float4*>(
+        G.actp(t < i ? V.post : R_S1, act ? t : 0, NLm) + (act ? (size_t)(b0 + bl) * O + a * d : 0));
+    const float4* w4 = reinterpret_cast<const float4*>(wrow);
+    float4 pv[4], wv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pv[j] = (act && j < V4) ? p4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      wv[j] = j < V4 ? w4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     float q = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
-    s_q[idx] = q;
-  }
-  __syncthreads();
-  for (int bl = tid; bl < nb; bl += 256) {
-    const float* qb = s_q + bl * TA;
-    int am = 0;
-    float best = -INFINITY;
-    for (int a = 0; a < Aa; ++a) {
-      float mx = qb[a];
-      for (int t = 1; t < T; ++t) mx = fmaxf(mx, qb[t * Aa + a]);
-      if (a == 0 || mx > best) {
-        best = mx;
-        am = a;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j < V4) {
+        q = __builtin_fmaf(pv[j].x, wv[j].x, q);
+        q = __builtin_fmaf(pv[j].y, wv[j].y, q);
+        q = __builtin_fmaf(pv[j].z, wv[j].z, q);
+        q = __builtin_fmaf(pv[j].w, wv[j].w, q);
       }
     }
-    if (am != (int)V.spec_next[(size_t)i * V.spec_stride + b0 + bl]) s_bad = 1;
+    if (act) s_q[tid] = q;
+  } else {
+    for (int k = tid; k < d; k += 256) s_w[k] = wrow[k];
+    __syncthreads();
+    for (int idx = tid; idx < n; idx += 256) {
+      const int bl = idx / fTA, rem = idx - bl * TA, t = rem / fA, a = rem - t * Aa;
+      const float* p = G.actp(t < i ? V.post : R_S1, t, NLm) + (size_t)(b0 + bl) * O + a * d;
+      float q = 0.f;
+#pragma unroll 8
+      for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
+      s_q[idx] = q;
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < nb * Aa; j += 256) {  // max over heads per (row, action)
+    const int bl = j / fA, a = j - bl * Aa;
+    const float* qb = s_q + bl * TA + a;
+    float mx = qb[0];
+    for (int t = 1; t < T; ++t) mx = fmaxf(mx, qb[t * Aa]);
+    s_m[j] = mx;
+  }
+  __syncthreads();
+  if (tid < nb) {  // first argmax over actions vs the speculated next action
+    const float* mb = s_m + tid * Aa;
+    int am = 0;
+    float best = mb[0];
+    for (int a = 1; a < Aa; ++a)
+      if (mb[a] > best) {
+        best = mb[a];
+        am = a;
+      }
+    if (am != spec) s_bad = 1;
   }
   __syncthreads();
   if (tid == 0 && s_bad) atomicMin(V.flag, i);
@@ -1168,6 +1310,7 @@ struct QmaxArgs {
 __global__ __launch_bounds__(256) void k_qmax(Geo G, QmaxArgs Q) {
   const int i = blockIdx.x, tid = threadIdx.x;
   const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, TA = T * Aa;
+  const FDiv fTA = fdiv(TA), fA = fdiv(Aa);
   const int b0 = blockIdx.y * Q.rows;
   const int nb = Q.M - b0 < Q.rows ? Q.M - b0 : Q.rows;
   if (nb <= 0) return;
@@ -1178,12 +1321,12 @@ __global__ __launch_bounds__(256) void k_qmax(Geo G, QmaxArgs Q) {
   __syncthreads();
   const int off = Q.off, guess = Q.guess;
   qdots(nb * TA, d, s_w, s_q, [&](int idx) {
-    const int bl = idx / TA, rem = idx - bl * TA, t = rem / Aa, a = rem - t * Aa;
+    const int bl = idx / fTA, rem = idx - bl * TA, t = rem / fA, a = rem - t * Aa;
     return G.actp(off + t < i ? guess : R_S1, t, NLm) + (size_t)(b0 + bl) * O + a * d;
   });
   __syncthreads();
   for (int j = tid; j < nb * Aa; j += 256) {
-    const int bl = j / Aa, a = j - bl * Aa;
+    const int bl = j / fA, a = j - bl * Aa;
     const float* qb = s_q + bl * TA + a;
     float mx = qb[0];
     for (int t = 1; t < T; ++t) mx = fmaxf(mx, qb[t * Aa]);
@@ -1198,6 +1341,7 @@ __global__ __launch_bounds__(256) void k_sverify(const float* X, const float* Y,
   if (threadIdx.x == 0) s_min = Tg;
   __syncthreads();
   int mine = Tg;
+  const FDiv fM = fdiv(M);
   for (int j = threadIdx.x; j < Tg * M; j += 256) {
     const float* x = X + (size_t)j * Aa;
     const float* y = Y + (size_t)j * Aa;
@@ -1207,7 +1351,7 @@ __global__ __launch_bounds__(256) void k_sverify(const float* X, const float* Y,
       if (x[a] > bx) { bx = x[a]; ax = a; }
       if (y[a] > by) { by = y[a]; ay = a; }
     }
-    if (ax != ay) mine = min(mine, j / M);
+    if (ax != ay) mine = min(mine, j / fM);
   }
   atomicMin(&s_min, mine);
   __syncthreads();
@@ -1237,8 +1381,9 @@ __global__ __launch_bounds__(256) void k_skey(Geo G, KeyArgs K) {
   for (int k = tid; k < d; k += 256) s_w[k] = wrow[k];
   __syncthreads();
   unsigned long long best = 0ull;
+  const FDiv fA = fdiv(Aa);
   for (int j = tid; j < T * Aa; j += 256) {
-    const int t = j / Aa, a = j - t * Aa, tg = K.off + t;
+    const int t = j / fA, a = j - t * Aa, tg = K.off + t;
     if (!K.use_gpi && tg != K.task) continue;
     const float* p = G.actp(K.role, t, NLm) + (size_t)K.row * O + a * d;
     float q = 0.f;
