@@ -96,6 +96,7 @@ struct sfx_handle {
   bool fuse_v0 = true;   // SFX_FUSE_V0=0: post-update layer-0 forward as its own launch
   bool xcd = true;       // SFX_XCD=0: plain (tile, head) grids instead of XCD-aware ones
   int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
+  int fwd_nb = 1;        // 16-column blocks per forward tile (SFX_FWD_NB=2: 32x32 tiles, 8 waves only)
   AdamHP hp_psi{1e-3, 0.0, 0.9, 0.999, 1e-8};
   AdamHP hp_w{1e-3, 0.0, 0.9, 0.999, 1e-8};
   int target_update_ev = 1000;
@@ -270,18 +271,25 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     F.lms_alpha = ex.lms_alpha;
     F.flag = first ? ex.flag : nullptr;
     F.flag_value = ex.flag_value;
-    F.ntN = cdiv(L.N, 16);
+    const int NB = h->fwd_nb;
+    F.ntN = cdiv(L.N, 16 * NB);
     F.ntM = cdiv(M, 32);
     const dim3 grid = F.xcd ? dim3(8 * cdiv(h->T, 8) * F.ntN * F.ntM * F.ngroups) : dim3(F.ntN, ninst, F.ntM);
     const double by = 4.0 * ninst * ((double)L.N * L.K + L.N + (double)M * L.K + (double)M * L.N);
     // the vector path needs K % 64 == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
     const bool aligned = l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0);
-    if (h->fwd_waves == 8) {
+    if (h->fwd_waves == 16) {
+      const bool vec = (L.K % 16) == 0 && aligned;
+      launch(h, K_FWD, by, vec ? k_fwd<true, 16, 1> : k_fwd<false, 16, 1>, grid, dim3(1024), h->G, F);
+    } else if (h->fwd_waves == 8) {
       const bool vec = (L.K % 32) == 0 && aligned;
-      launch(h, K_FWD, by, vec ? k_fwd<true, 8> : k_fwd<false, 8>, grid, dim3(512), h->G, F);
+      if (NB == 2)
+        launch(h, K_FWD, by, vec ? k_fwd<true, 8, 2> : k_fwd<false, 8, 2>, grid, dim3(512), h->G, F);
+      else
+        launch(h, K_FWD, by, vec ? k_fwd<true, 8, 1> : k_fwd<false, 8, 1>, grid, dim3(512), h->G, F);
     } else {
       const bool vec = (L.K % 64) == 0 && aligned;
-      launch(h, K_FWD, by, vec ? k_fwd<true, 4> : k_fwd<false, 4>, grid, dim3(256), h->G, F);
+      launch(h, K_FWD, by, vec ? k_fwd<true, 4, 1> : k_fwd<false, 4, 1>, grid, dim3(256), h->G, F);
     }
   }
   LAUNCHCHK();
@@ -659,7 +667,9 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   const char* ex = std::getenv("SFX_XCD");
   h->xcd = !(ex && ex[0] == '0');
   const char* efw = std::getenv("SFX_FWD_WAVES");
-  h->fwd_waves = efw && std::atoi(efw) == 4 ? 4 : 8;
+  h->fwd_waves = efw && (std::atoi(efw) == 4 || std::atoi(efw) == 16) ? std::atoi(efw) : 8;
+  const char* enb = std::getenv("SFX_FWD_NB");
+  h->fwd_nb = enb && std::atoi(enb) == 2 && h->fwd_waves == 8 ? 2 : 1;
   int off = 0, ptorch = 0;
   for (int l = 0; l < h->NL; ++l) {
     LayerGeo Lr{};

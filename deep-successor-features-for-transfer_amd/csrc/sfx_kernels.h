@@ -236,7 +236,7 @@ __device__ void lms_block(const Geo& G, const FwdArgs& F) {
   if (tid < d) w[tid] = __fadd_rn(wk, __fmul_rn(s_e, pk));
 }
 
-template <bool VEC, int NW>
+template <bool VEC, int NW, int NB>
 __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
   constexpr int KW = 256 / NW;  // K chunk of one wave per iteration (NW waves cover 256)
   constexpr int KL = KW / 4;    // consecutive k per lane (4 lane groups per MFMA k-step)
@@ -261,29 +261,42 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
                                          : G.online + G.slot_off(rslot(F.mask, head) ^ (grp.which == P_NEW), head);
   const float* X = F.xOff < 0 ? (grp.xsel == 1 ? F.xa : F.xb) : G.actp(grp.role, head, F.xOff);
   float* Y = G.actp(grp.role, head, F.yOff);
-  const int n0 = tN * 16, m0 = tM * 32;
+  const int n0 = tN * 16 * NB, m0 = tM * 32;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
-  const int ma = m0 + r, mb = m0 + 16 + r, n = n0 + r;
-  const bool oka = ma < M, okb = mb < M, okn = n < N;
+  const int ma = m0 + r, mb = m0 + 16 + r;
+  const bool oka = ma < M, okb = mb < M;
   const float* xra = X + (size_t)ma * K;
   const float* xrb = X + (size_t)mb * K;
-  const float* wr = P + F.wOff + (size_t)n * K;
+  const float* wr[NB];
+  bool okn[NB];
+#pragma unroll
+  for (int c = 0; c < NB; ++c) {
+    const int n = n0 + 16 * c + r;
+    okn[c] = n < N;
+    wr[c] = P + F.wOff + (size_t)n * K;
+  }
   // the reducing threads fetch their bias early
-  const int Lx = threadIdx.x & 63, col = n0 + (Lx & 15);
-  const float bias = (threadIdx.x < 128 && col < N) ? P[F.bOff + col] : 0.f;
-  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const int Lx = threadIdx.x & 63, sr = threadIdx.x >> 6;  // sr: (row block sr & 1, col block sr >> 1)
+  const int col = n0 + 16 * (sr >> 1) + (Lx & 15);
+  const float bias = (threadIdx.x < 128 * NB && col < N) ? P[F.bOff + col] : 0.f;
+  floatx4 acc[2][NB];
+#pragma unroll
+  for (int c = 0; c < NB; ++c) acc[0][c] = acc[1][c] = floatx4{0.f, 0.f, 0.f, 0.f};
   for (int kc = wave * KW; kc < K; kc += 256) {
     const int kb = kc + g * KL;
-    float a0[KL], a1[KL], bw[KL];
+    float a0[KL], a1[KL], bw[NB][KL];
     if constexpr (VEC) {  // K % KW == 0, rows 16-B aligned: KL/4 float4 per operand row
 #pragma unroll
       for (int q = 0; q < KL / 4; ++q) {
         const float4 ta = oka ? reinterpret_cast<const float4*>(xra + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
         const float4 tb = okb ? reinterpret_cast<const float4*>(xrb + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 tw = okn ? reinterpret_cast<const float4*>(wr + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
         a0[4 * q] = ta.x; a0[4 * q + 1] = ta.y; a0[4 * q + 2] = ta.z; a0[4 * q + 3] = ta.w;
         a1[4 * q] = tb.x; a1[4 * q + 1] = tb.y; a1[4 * q + 2] = tb.z; a1[4 * q + 3] = tb.w;
-        bw[4 * q] = tw.x; bw[4 * q + 1] = tw.y; bw[4 * q + 2] = tw.z; bw[4 * q + 3] = tw.w;
+#pragma unroll
+        for (int c = 0; c < NB; ++c) {
+          const float4 tw = okn[c] ? reinterpret_cast<const float4*>(wr[c] + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+          bw[c][4 * q] = tw.x; bw[c][4 * q + 1] = tw.y; bw[c][4 * q + 2] = tw.z; bw[c][4 * q + 3] = tw.w;
+        }
       }
     } else {
 #pragma unroll
@@ -291,28 +304,34 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
         const bool kin = kb + j < K;
         a0[j] = (oka && kin) ? xra[kb + j] : 0.f;
         a1[j] = (okb && kin) ? xrb[kb + j] : 0.f;
-        bw[j] = (okn && kin) ? wr[kb + j] : 0.f;
+#pragma unroll
+        for (int c = 0; c < NB; ++c) bw[c][j] = (okn[c] && kin) ? wr[c][kb + j] : 0.f;
       }
     }
 #pragma unroll
     for (int j = 0; j < KL; ++j) {
-      acc0 = mfma4(a0[j], bw[j], acc0);
-      acc1 = mfma4(a1[j], bw[j], acc1);
+#pragma unroll
+      for (int c = 0; c < NB; ++c) {
+        acc[0][c] = mfma4(a0[j], bw[c][j], acc[0][c]);
+        acc[1][c] = mfma4(a1[j], bw[c][j], acc[1][c]);
+      }
     }
   }
-  __shared__ floatx4 red[NW][2][64];
-  red[wave][0][lane] = acc0;
-  red[wave][1][lane] = acc1;
-  __syncthreads();
-  if (threadIdx.x < 128) {
-    const int s = threadIdx.x >> 6;
-    floatx4 v = red[0][s][Lx];
+  __shared__ floatx4 red[NW][2 * NB][64];
 #pragma unroll
-    for (int w2 = 1; w2 < NW; ++w2) v += red[w2][s][Lx];
+  for (int c = 0; c < NB; ++c) {
+    red[wave][2 * c][lane] = acc[0][c];
+    red[wave][2 * c + 1][lane] = acc[1][c];
+  }
+  __syncthreads();
+  if (threadIdx.x < 128 * NB) {
+    floatx4 v = red[0][sr][Lx];
+#pragma unroll
+    for (int w2 = 1; w2 < NW; ++w2) v += red[w2][sr][Lx];
     if (col < N) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int row = m0 + 16 * s + (Lx >> 4) * 4 + i;
+        const int row = m0 + 16 * (sr & 1) + (Lx >> 4) * 4 + i;
         if (row < M) Y[(size_t)row * N + col] = act_fwd(__fadd_rn(v[i], bias), F.act);
       }
     }
