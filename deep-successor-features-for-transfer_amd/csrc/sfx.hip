@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "sfx_kernels.h"
+#include "sfx_tsf.h"
 #include "../../include/sfx.h"
 
 using namespace sfx;
@@ -127,6 +128,7 @@ struct sfx_handle {
   int spec_rounds = 2;        // speculative rounds launched on the device per fused step
   // sharded heads (sfx_shard_*): this handle's heads are global [off, off + T) of Tg; w has Tg rows
   int Tg = 0, off = 0;
+  struct sfx_tsf_state* tsf = nullptr;  // TSF-DQN state (sfx_tsf_setup)
   struct ShardPending {
     bool active = false;
     int B = 0;
@@ -763,9 +765,12 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   return SFX_OK;
 }
 
+void tsf_release(sfx_handle* h);
+
 int sfx_destroy(sfx_t h) {
   if (!h) return SFX_OK;
   (void)hipStreamSynchronize(h->stream);
+  tsf_release(h);
   free_all(h);
   delete h;
   return SFX_OK;
@@ -1105,3 +1110,4 @@ int sfx_synchronize(sfx_t h) {
 
 #include "sfx_runner.inc"
 #include "sfx_shard.inc"
+#include "sfx_tsf.inc"

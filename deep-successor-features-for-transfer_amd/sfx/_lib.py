@@ -71,6 +71,12 @@ SIGNATURES = {
     "sfx_shard_verify": (_I, [_VP, _VP, _VP, _VP]),
     "sfx_shard_select": (_I, [_VP, _I, _I, _I, _VP]),
     "sfx_shard_finish": (_I, [_VP, _I]),
+    "sfx_tsf_setup": (_I, [_VP, _I, _I, _F, _D, _D, _D, _D]),
+    "sfx_tsf_load_g": (_I, [_VP, _I, _FP]),
+    "sfx_tsf_get_g": (_I, [_VP, _I, _FP, _FP, _FP]),
+    "sfx_tsf_load_h": (_I, [_VP, _FP]),
+    "sfx_tsf_get_h": (_I, [_VP, _FP]),
+    "sfx_tsf_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP]),
 }
 
 # env callbacks of sfx_runner_create (include/sfx.h)

@@ -251,3 +251,52 @@ class SFEngine:
         phi = self._f(phi, (-1,))
         r = self._f(r, (1,))
         check(lib.sfx_lms(self._h, int(t), phi.data_ptr(), r.data_ptr(), float(alpha)), "sfx_lms")
+
+    # ---------------------------------------------------------------- TSF-DQN (tsfdqn.py / tsfdqn_nf.py)
+    def tsf_setup(self, G: int, K: int = 0, beta: float = 1.0, lr_g: float = 1e-3, wd_g: float = 0.0,
+                  lr_h: float = 1e-3, wd_h: float = 0.0):
+        """Transformed features: g_i = K planar flows + Linear(n_s, G) per task, h = Linear(G, d) shared."""
+        check(lib.sfx_tsf_setup(self._h, int(G), int(K), float(beta), float(lr_g), float(wd_g), float(lr_h),
+                                float(wd_h)), "sfx_tsf_setup")
+        self.tsf_G, self.tsf_K = G, K
+        self.tsf_Pg = K * (2 * self.n_s + 1) + G * self.n_s + G
+        self.tsf_Ph = self.d * G + self.d
+
+    def tsf_load_g(self, t: int, g):
+        a = np.ascontiguousarray(torch.as_tensor(g).detach().cpu().reshape(-1).numpy(), dtype=np.float32)
+        if a.size != self.tsf_Pg:
+            raise ValueError(f"g has {a.size} parameters, expected {self.tsf_Pg}")
+        check(lib.sfx_tsf_load_g(self._h, t, fptr(a)), "sfx_tsf_load_g")
+
+    def tsf_get_g(self, t: int):
+        g, m, v = (np.empty(self.tsf_Pg, dtype=np.float32) for _ in range(3))
+        check(lib.sfx_tsf_get_g(self._h, t, fptr(g), fptr(m), fptr(v)), "sfx_tsf_get_g")
+        return torch.from_numpy(g), torch.from_numpy(m), torch.from_numpy(v)
+
+    def tsf_load_h(self, h):
+        a = np.ascontiguousarray(torch.as_tensor(h).detach().cpu().reshape(-1).numpy(), dtype=np.float32)
+        if a.size != self.tsf_Ph:
+            raise ValueError(f"h has {a.size} parameters, expected {self.tsf_Ph}")
+        check(lib.sfx_tsf_load_h(self._h, fptr(a)), "sfx_tsf_load_h")
+
+    def tsf_get_h(self):
+        a = np.empty(self.tsf_Ph, dtype=np.float32)
+        check(lib.sfx_tsf_get_h(self._h, fptr(a)), "sfx_tsf_get_h")
+        return torch.from_numpy(a)
+
+    def tsf_update(self, policy: int, s, a, r, phi, s1, gamma, use_gpi: bool = True,
+                   losses: Optional[torch.Tensor] = None, next_actions: Optional[torch.Tensor] = None):
+        """TSFDQN.update_successor (tsfdqn.py:588-709): returns losses [3] = (l1 + beta l2, l1, l2)."""
+        s, s1 = self._f(s), self._f(s1)
+        B = s.shape[0]
+        a = self._l(a)
+        phi = self._f(phi, (B, self.d))
+        gamma = self._f(gamma, (B,))
+        r = self._f(r, (B,))
+        if losses is None:
+            losses = torch.empty(3, device=self.device)
+        check(lib.sfx_tsf_update(self._h, int(policy), s.data_ptr(), a.data_ptr(), r.data_ptr(), phi.data_ptr(),
+                                 s1.data_ptr(), gamma.data_ptr(), B, int(bool(use_gpi)), losses.data_ptr(),
+                                 dptr(next_actions)), "sfx_tsf_update")
+        return losses
+

@@ -257,6 +257,24 @@ int sfx_shard_verify(sfx_t h, const float* X_dev, const float* Y_dev, int* flag_
 int sfx_shard_select(sfx_t h, int round, int task, int use_gpi, long long* key_dev);
 int sfx_shard_finish(sfx_t h, int rounds_run);
 
+/* ---------------------------------------------------------------------------------------
+ * TSF-DQN (tsfdqn.py:588-709; tsfdqn_nf.py with planar-flow g): transformed features
+ *   φ̃ = (h(g_i(s)) + h(g_i(s1))) ⊙ φ,  g_i = K planar flows + Linear(n_s, G), h = Linear(G, d)
+ * shared by all tasks; TD target φ̃ + γ ψ⁻_i(s1)[a'], loss = l1 + β MSE(w_i·φ̃, r), one Adam step
+ * over {ψ_i, w_i, g_i, h} (h's moments per task).  g packing per task: for each flow k
+ * weight[n_s], bias, scale[n_s] (tsfdqn_nf.py:335-337 registration order), then Linear
+ * weight[G][n_s], bias[G].  h packing: weight[d][G], bias[d].  K = 0: tsfdqn.py's g.
+ * ------------------------------------------------------------------------------------- */
+int sfx_tsf_setup(sfx_t h, int G, int K, float beta, double lr_g, double wd_g, double lr_h, double wd_h);
+int sfx_tsf_load_g(sfx_t h, int t, const float* g_host);
+int sfx_tsf_get_g(sfx_t h, int t, float* g_host, float* gm_host, float* gv_host);
+int sfx_tsf_load_h(sfx_t h, const float* h_host);
+int sfx_tsf_get_h(sfx_t h, float* h_host);
+/* TSFDQN.update_successor(transitions, policy, use_gpi): losses_dev [3] = (l1 + β l2, l1, l2) */
+int sfx_tsf_update(sfx_t h, int policy, const float* S_dev, const int64_t* a_dev, const float* r_dev,
+                   const float* phi_dev, const float* S1_dev, const float* gamma_dev, int B, int use_gpi,
+                   float* losses_dev, int64_t* next_dev);
+
 #ifdef __cplusplus
 }
 #endif
