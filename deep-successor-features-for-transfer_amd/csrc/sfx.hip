@@ -97,7 +97,7 @@ struct sfx_handle {
   bool fuse_v0 = true;   // SFX_FUSE_V0=0: post-update layer-0 forward as its own launch
   bool xcd = true;       // SFX_XCD=0: plain (tile, head) grids instead of XCD-aware ones
   int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
-  int fwd_nb = 1;        // 16-column blocks per forward tile (SFX_FWD_NB=2: 32x32 tiles, 8 waves only)
+  bool fuse_l0 = true;   // SFX_FUSE_L0=0: layer 0 of a forward from the states as its own launch
   AdamHP hp_psi{1e-3, 0.0, 0.9, 0.999, 1e-8};
   AdamHP hp_w{1e-3, 0.0, 0.9, 0.999, 1e-8};
   int target_update_ev = 1000;
@@ -257,41 +257,45 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
   }
   F.xcd = h->xcd && uniform && h->T > 1 ? 1 : 0;
   F.nh = h->T;
-  for (int l = ex.l0; l < h->NL; ++l) {
+  // layers 0 and 1 in one launch when layer 0 is small (its rows recomputed per tile in LDS)
+  const bool fuse01 = h->fuse_l0 && ex.l0 == 0 && h->NL >= 3 && h->L[0].K <= L0_KMAX && h->L[0].N <= L0_NMAX &&
+                      h->L[1].K % 32 == 0 && h->fwd_waves == 8;
+  for (int l = fuse01 ? 1 : ex.l0; l < h->NL; ++l) {
     const LayerGeo& L = h->L[l];
+    const bool l0 = fuse01 && l == 1;
     F.N = L.N;
     F.K = L.K;
     F.act = L.actOut;
     F.wOff = L.wOff;
     F.bOff = L.bOff;
-    F.xOff = l == 0 ? -1 : h->actOff[l - 1];
+    F.xOff = l == 0 || l0 ? -1 : h->actOff[l - 1];
     F.yOff = h->actOff[l];
-    const bool first = l == ex.l0;
+    F.w0Off = h->L[0].wOff;
+    F.b0Off = h->L[0].bOff;
+    F.K0 = h->L[0].K;
+    F.y0Off = h->actOff[0];
+    const bool first = l == ex.l0 || l0;
     F.lms_head = first ? ex.lms_head : -1;
     F.lms_phi = ex.lms_phi;
     F.lms_r = ex.lms_r;
     F.lms_alpha = ex.lms_alpha;
     F.flag = first ? ex.flag : nullptr;
     F.flag_value = ex.flag_value;
-    const int NB = h->fwd_nb;
-    F.ntN = cdiv(L.N, 16 * NB);
+    F.ntN = cdiv(L.N, 16);
     F.ntM = cdiv(M, 32);
     const dim3 grid = F.xcd ? dim3(8 * cdiv(h->T, 8) * F.ntN * F.ntM * F.ngroups) : dim3(F.ntN, ninst, F.ntM);
-    const double by = 4.0 * ninst * ((double)L.N * L.K + L.N + (double)M * L.K + (double)M * L.N);
-    // the vector path needs K % 64 == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
+    double by = 4.0 * ninst * ((double)L.N * L.K + L.N + (double)M * L.K + (double)M * L.N);
+    if (l0) by += 4.0 * ninst * ((double)h->L[0].N * h->L[0].K + h->L[0].N + (double)M * h->L[0].K);
+    // the vector path needs K % (256/NW) == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
     const bool aligned = l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0);
-    if (h->fwd_waves == 16) {
-      const bool vec = (L.K % 16) == 0 && aligned;
-      launch(h, K_FWD, by, vec ? k_fwd<true, 16, 1> : k_fwd<false, 16, 1>, grid, dim3(1024), h->G, F);
+    if (l0) {
+      launch(h, K_FWD, by, k_fwd<true, 8, true>, grid, dim3(512), h->G, F);
     } else if (h->fwd_waves == 8) {
       const bool vec = (L.K % 32) == 0 && aligned;
-      if (NB == 2)
-        launch(h, K_FWD, by, vec ? k_fwd<true, 8, 2> : k_fwd<false, 8, 2>, grid, dim3(512), h->G, F);
-      else
-        launch(h, K_FWD, by, vec ? k_fwd<true, 8, 1> : k_fwd<false, 8, 1>, grid, dim3(512), h->G, F);
+      launch(h, K_FWD, by, vec ? k_fwd<true, 8, false> : k_fwd<false, 8, false>, grid, dim3(512), h->G, F);
     } else {
       const bool vec = (L.K % 64) == 0 && aligned;
-      launch(h, K_FWD, by, vec ? k_fwd<true, 4, 1> : k_fwd<false, 4, 1>, grid, dim3(256), h->G, F);
+      launch(h, K_FWD, by, vec ? k_fwd<true, 4, false> : k_fwd<false, 4, false>, grid, dim3(256), h->G, F);
     }
   }
   LAUNCHCHK();
@@ -669,9 +673,9 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   const char* ex = std::getenv("SFX_XCD");
   h->xcd = !(ex && ex[0] == '0');
   const char* efw = std::getenv("SFX_FWD_WAVES");
-  h->fwd_waves = efw && (std::atoi(efw) == 4 || std::atoi(efw) == 16) ? std::atoi(efw) : 8;
-  const char* enb = std::getenv("SFX_FWD_NB");
-  h->fwd_nb = enb && std::atoi(enb) == 2 && h->fwd_waves == 8 ? 2 : 1;
+  h->fwd_waves = efw && std::atoi(efw) == 4 ? 4 : 8;
+  const char* el0 = std::getenv("SFX_FUSE_L0");
+  h->fuse_l0 = !(el0 && el0[0] == '0');
   int off = 0, ptorch = 0;
   for (int l = 0; l < h->NL; ++l) {
     LayerGeo Lr{};

@@ -209,6 +209,7 @@ struct FwdArgs {
   int M, N, K, act, wOff, bOff, xOff, yOff;  // xOff < 0: layer input is xa / xb
   int ngroups, lms_head, flag_value, xcd;  // xcd: 1-D XCD-aware grid (every group has heads 0..nh-1)
   int nh, ntN, ntM, pad2_;
+  int w0Off, b0Off, K0, y0Off;  // L0 launches: layer 0 (K0 -> K, identity) computed in-tile, stored at y0Off
   unsigned long long mask;
   FwdGroup g0, g1, g2, g3;
   const float* xa;
@@ -236,7 +237,13 @@ __device__ void lms_block(const Geo& G, const FwdArgs& F) {
   if (tid < d) w[tid] = __fadd_rn(wk, __fmul_rn(s_e, pk));
 }
 
-template <bool VEC, int NW, int NB>
+// L0 = true (layer-1 launches of a forward from the states): the workgroup first computes the
+// 32 x K layer-0 rows it needs, a0 = X W0ᵀ + b0 (layer 0 has no activation), into LDS -- each
+// column tile recomputes them (K0 is the small state width), the tile-0 workgroups publish
+// them for the backward -- and feeds them to the layer-1 MFMAs from LDS: one launch less.
+constexpr int L0_KMAX = 64, L0_NMAX = 256;  // layer-0 fan-in / width handled in-tile
+
+template <bool VEC, int NW, bool L0>
 __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
   constexpr int KW = 256 / NW;  // K chunk of one wave per iteration (NW waves cover 256)
   constexpr int KL = KW / 4;    // consecutive k per lane (4 lane groups per MFMA k-step)
@@ -261,42 +268,75 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
                                          : G.online + G.slot_off(rslot(F.mask, head) ^ (grp.which == P_NEW), head);
   const float* X = F.xOff < 0 ? (grp.xsel == 1 ? F.xa : F.xb) : G.actp(grp.role, head, F.xOff);
   float* Y = G.actp(grp.role, head, F.yOff);
-  const int n0 = tN * 16 * NB, m0 = tM * 32;
+  const int n0 = tN * 16, m0 = tM * 32;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
-  const int ma = m0 + r, mb = m0 + 16 + r;
-  const bool oka = ma < M, okb = mb < M;
-  const float* xra = X + (size_t)ma * K;
-  const float* xrb = X + (size_t)mb * K;
-  const float* wr[NB];
-  bool okn[NB];
-#pragma unroll
-  for (int c = 0; c < NB; ++c) {
-    const int n = n0 + 16 * c + r;
-    okn[c] = n < N;
-    wr[c] = P + F.wOff + (size_t)n * K;
-  }
+  const int ma = m0 + r, mb = m0 + 16 + r, n = n0 + r;
+  const bool oka = ma < M, okb = mb < M, okn = n < N;
+  const float* wr = P + F.wOff + (size_t)n * K;
   // the reducing threads fetch their bias early
-  const int Lx = threadIdx.x & 63, sr = threadIdx.x >> 6;  // sr: (row block sr & 1, col block sr >> 1)
-  const int col = n0 + 16 * (sr >> 1) + (Lx & 15);
-  const float bias = (threadIdx.x < 128 * NB && col < N) ? P[F.bOff + col] : 0.f;
-  floatx4 acc[2][NB];
+  const int Lx = threadIdx.x & 63, col = n0 + (Lx & 15);
+  const float bias = (threadIdx.x < 128 && col < N) ? P[F.bOff + col] : 0.f;
+  constexpr int AS = L0 ? L0_NMAX + 4 : 4;  // LDS row stride of a0 (padded against bank conflicts)
+  __shared__ __align__(16) float sA[L0 ? 32 * AS : 4];
+  if constexpr (L0) {
+    __shared__ float sX[32 * L0_KMAX];
+    const int K0 = F.K0;
+    for (int j = threadIdx.x; j < 32 * K0; j += 64 * NW) {
+      const int rr = j / fdiv(K0), kk = j - rr * K0;
+      sX[j] = m0 + rr < M ? X[(size_t)(m0 + rr) * K0 + kk] : 0.f;
+    }
+    __syncthreads();
+    // a0 = X W0ᵀ + b0 by MFMA: wave w owns layer-0 columns [32w, 32w + 32), K0 in k-steps of 4
+    const float* W0 = P + F.w0Off;
+    const float* b0 = P + F.b0Off;
+    float* Y0 = G.actp(grp.role, head, F.y0Off);
+    for (int cb = wave * 32; cb < K; cb += 32 * NW) {
+      floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c10 = c00, c11 = c00;
+      const int nA = cb + r, nB = cb + 16 + r;
+      for (int k4 = 0; k4 < K0; k4 += 4) {
+        const int kk = k4 + g;
+        const bool okk = kk < K0;
+        const float x0 = okk ? sX[r * K0 + kk] : 0.f, x1 = okk ? sX[(16 + r) * K0 + kk] : 0.f;
+        const float wA = okk && nA < K ? W0[(size_t)nA * K0 + kk] : 0.f;
+        const float wB = okk && nB < K ? W0[(size_t)nB * K0 + kk] : 0.f;
+        c00 = mfma4(x0, wA, c00);
+        c01 = mfma4(x0, wB, c01);
+        c10 = mfma4(x1, wA, c10);
+        c11 = mfma4(x1, wB, c11);
+      }
+      const floatx4* cs[4] = {&c00, &c01, &c10, &c11};
 #pragma unroll
-  for (int c = 0; c < NB; ++c) acc[0][c] = acc[1][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < 4; ++q) {
+        const int cc = cb + (q & 1) * 16 + r;
+        if (cc < K) {
+          const float bb = b0[cc];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int rr = (q >> 1) * 16 + g * 4 + i;
+            const float v = __fadd_rn((*cs[q])[i], bb);
+            sA[rr * AS + cc] = v;
+            if (tN == 0 && m0 + rr < M) Y0[(size_t)(m0 + rr) * K + cc] = v;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const float* xra = L0 ? sA + r * AS : X + (size_t)ma * K;
+  const float* xrb = L0 ? sA + (16 + r) * AS : X + (size_t)mb * K;
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   for (int kc = wave * KW; kc < K; kc += 256) {
     const int kb = kc + g * KL;
-    float a0[KL], a1[KL], bw[NB][KL];
+    float a0[KL], a1[KL], bw[KL];
     if constexpr (VEC) {  // K % KW == 0, rows 16-B aligned: KL/4 float4 per operand row
 #pragma unroll
       for (int q = 0; q < KL / 4; ++q) {
         const float4 ta = oka ? reinterpret_cast<const float4*>(xra + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
         const float4 tb = okb ? reinterpret_cast<const float4*>(xrb + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 tw = okn ? reinterpret_cast<const float4*>(wr + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
         a0[4 * q] = ta.x; a0[4 * q + 1] = ta.y; a0[4 * q + 2] = ta.z; a0[4 * q + 3] = ta.w;
         a1[4 * q] = tb.x; a1[4 * q + 1] = tb.y; a1[4 * q + 2] = tb.z; a1[4 * q + 3] = tb.w;
-#pragma unroll
-        for (int c = 0; c < NB; ++c) {
-          const float4 tw = okn[c] ? reinterpret_cast<const float4*>(wr[c] + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-          bw[c][4 * q] = tw.x; bw[c][4 * q + 1] = tw.y; bw[c][4 * q + 2] = tw.z; bw[c][4 * q + 3] = tw.w;
-        }
+        bw[4 * q] = tw.x; bw[4 * q + 1] = tw.y; bw[4 * q + 2] = tw.z; bw[4 * q + 3] = tw.w;
       }
     } else {
 #pragma unroll
@@ -304,34 +344,28 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
         const bool kin = kb + j < K;
         a0[j] = (oka && kin) ? xra[kb + j] : 0.f;
         a1[j] = (okb && kin) ? xrb[kb + j] : 0.f;
-#pragma unroll
-        for (int c = 0; c < NB; ++c) bw[c][j] = (okn[c] && kin) ? wr[c][kb + j] : 0.f;
+        bw[j] = (okn && kin) ? wr[kb + j] : 0.f;
       }
     }
 #pragma unroll
     for (int j = 0; j < KL; ++j) {
-#pragma unroll
-      for (int c = 0; c < NB; ++c) {
-        acc[0][c] = mfma4(a0[j], bw[c][j], acc[0][c]);
-        acc[1][c] = mfma4(a1[j], bw[c][j], acc[1][c]);
-      }
+      acc0 = mfma4(a0[j], bw[j], acc0);
+      acc1 = mfma4(a1[j], bw[j], acc1);
     }
   }
-  __shared__ floatx4 red[NW][2 * NB][64];
-#pragma unroll
-  for (int c = 0; c < NB; ++c) {
-    red[wave][2 * c][lane] = acc[0][c];
-    red[wave][2 * c + 1][lane] = acc[1][c];
-  }
+  __shared__ floatx4 red[NW][2][64];
+  red[wave][0][lane] = acc0;
+  red[wave][1][lane] = acc1;
   __syncthreads();
-  if (threadIdx.x < 128 * NB) {
-    floatx4 v = red[0][sr][Lx];
+  if (threadIdx.x < 128) {
+    const int s = threadIdx.x >> 6;
+    floatx4 v = red[0][s][Lx];
 #pragma unroll
-    for (int w2 = 1; w2 < NW; ++w2) v += red[w2][sr][Lx];
+    for (int w2 = 1; w2 < NW; ++w2) v += red[w2][s][Lx];
     if (col < N) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int row = m0 + 16 * (sr & 1) + (Lx >> 4) * 4 + i;
+        const int row = m0 + 16 * s + (Lx >> 4) * 4 + i;
         if (row < M) Y[(size_t)row * N + col] = act_fwd(__fadd_rn(v[i], bias), F.act);
       }
     }
