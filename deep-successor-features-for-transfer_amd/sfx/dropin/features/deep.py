@@ -176,7 +176,8 @@ class DeepSF(SF):
             raise NotImplementedError("sfx DeepSF trains ψ with torch.optim.Adam (no amsgrad / maximize) only")
         mb = max(self.max_batch, batch)
         eng = SFEngine(self.n_tasks, n_s, H, self.n_actions, self.n_features, acts, max_batch=mb)
-        eng.set_adam(g["lr"], g.get("weight_decay", 0.0), g["lr"], 0.0, betas=tuple(g["betas"]), eps=g["eps"])
+        (lr_sf, wd_sf), (lr_w, wd_w) = self._adam_groups(optim) if optim is not None else ((1e-3, 0.0), (1e-3, 0.0))
+        eng.set_adam(lr_sf, wd_sf, lr_w, wd_w, betas=tuple(g["betas"]), eps=g["eps"])
         eng.set_target_update_ev(self.target_update_ev)
         for t, ((m, _, _), (tm, _, _)) in enumerate(self._psi):
             eng.load_head(t, _flat(m), 0)
@@ -186,13 +187,22 @@ class DeepSF(SF):
                 eng.load_w(t, ws[t])
                 eng.set_since_target(t, since[t])
             else:
-                eng.load_w(t, list.__getitem__(self.fit_w, t))
+                eng.load_w(t, self._w_host(t))
                 eng.set_since_target(t, self._since[t])
         if old is not None:
             old.close()
         self._eng, self._eng_T = eng, self.n_tasks
         self.max_batch = mb
         return eng
+
+    def _w_host(self, t):
+        """Host value of fit_w[t] before the engine owns it ([d, 1] tensor here)."""
+        return list.__getitem__(self.fit_w, t)
+
+    def _adam_groups(self, optim):
+        """(lr, weight_decay) of the ψ group and of the w group of a task's optimizer."""
+        g = optim.param_groups[0]
+        return (g["lr"], g.get("weight_decay", 0.0)), (g["lr"], 0.0)
 
     def _sync_host(self):
         """Refresh the torch modules (online, target) from the device."""

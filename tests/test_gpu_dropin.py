@@ -61,3 +61,52 @@ def test_dropin_reproduces_reference_agent_run(golden):
                               for t in range(T)]), g["target"], 1e-3 * 60)
     rel_close(torch.stack([sf.fit_w[t].reshape(-1).cpu() for t in range(T)]), g["w"], rtol=1e-4, atol=1e-6)
     rel_close(agent.test_tasks_weights[0].weight.detach().reshape(-1).cpu(), g["test_w"], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("case", ["sfdqn_gpi", "sfdqn_nogpi", "sfdqn_tanh"])
+def test_dropin_sequential_deepsf_vs_reference_updates(golden, case):
+    """features.deep_sequential.DeepSF (main_sfdqn_sequential_torch.py's library) driven through its
+    public API reproduces the reference's update_successor sequence (tests/golden/upd_sfdqn_*)."""
+    from sfx import dropin
+
+    dropin.install()
+    import utils.torch as ut
+
+    ut.set_torch_device(True)
+    from features.deep_sequential import DeepSF
+
+    from tests.golden.recipe import AgentTask, agent_psi_lambda
+    from tests.test_gpu_engine import batches_of, spec_of
+
+    g = golden("upd_" + case)
+    spec, T = spec_of(g), int(g["T"])
+    hp = {"learning_rate_sf": 1e-3, "learning_rate_w": 1e-3, "weight_decay_sf": 0.0, "weight_decay_w": 0.0}
+    sf = DeepSF(pytorch_model_handle=agent_psi_lambda(spec.H, spec.acts, 1e-3, ut.device),
+                target_update_ev=int(g["target_update_ev"]), hyperparameters=hp)
+    sf.reset()
+    for t in range(T):
+        sf.add_training_task(AgentTask(spec.n_s, spec.A, spec.d, t, t, ut.device))
+    # the fixture's initial weights into the library's modules (before the engine exists)
+    for t in range(T):
+        (m, _, _), (tm, _, _) = sf.psi[t]
+        for mod in (m, tm):
+            off = 0
+            with torch.no_grad():
+                for p in mod.parameters():
+                    p.copy_(torch.from_numpy(g["online0"][t][off:off + p.numel()]).view_as(p))
+                    off += p.numel()
+        with torch.no_grad():
+            list.__getitem__(sf.fit_w, t).weight.copy_(torch.from_numpy(g["w0"][t]).view(1, -1))
+    for j, (s, a, r, phi, s1, gamma) in enumerate(batches_of(g)):
+        i = int(g["policies"][j])
+        dev = ut.device
+        loss, l1, l2 = sf.update_successor((s.to(dev), a.to(dev), r.to(dev), phi.to(dev), s1.to(dev), gamma.to(dev)),
+                                           i, use_gpi=bool(g["use_gpi"]))
+        rel_close(torch.stack([loss, l1, l2]).cpu(), g["losses"][j], rtol=2e-4, atol=1e-7)
+    k = int(g["k"])
+    online = torch.stack([torch.cat([p.detach().reshape(-1).cpu() for p in sf.psi[t][0][0].parameters()])
+                          for t in range(T)])
+    params_close(online, g["online"], 1e-3 * k)
+    rel_close(torch.stack([sf.fit_w[t].weight.detach().reshape(-1).cpu() for t in range(T)]), g["w"], rtol=1e-4,
+              atol=1e-5)
+    assert list(sf.updates_since_target_updated) == [int(x) for x in g["since_target"]]
