@@ -358,7 +358,7 @@ struct BwdExtra {
   const float* v_xn = nullptr;
 };
 
-bool can_fuse_v0(const sfx_handle* h) { return h->fuse_v0 && h->L[0].K <= KFUSE; }
+bool can_fuse_v0(const sfx_handle* h, int vM) { return h->fuse_v0 && h->L[0].K <= KFUSE && vM * h->L[0].K <= VFUSE; }
 
 int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const float* phi, const float* r,
             float* losses, const TdgSpec& td, const BwdExtra& ex = BwdExtra()) {
@@ -581,10 +581,10 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
   td.flag = &h->dout->flag;
   BwdExtra bx;
   bx.inc_step = r == 0 ? 1 : 0;  // later rounds redo the same optimizer step
-  bx.fuse_v0 = can_fuse_v0(h);
+  const bool want_sel = p.sel && final;
+  bx.fuse_v0 = can_fuse_v0(h, B + 1);
   bx.vRole = out;
   bx.v_x = p.S1;
-  const bool want_sel = p.sel && final;
   bx.v_xn = want_sel ? p.s_next : nullptr;
   RC(run_bwd(h, 0, T, B, p.S, p.phi, nullptr, p.losses, td, bx));
   const int vM = B + (want_sel ? 1 : 0);
@@ -638,6 +638,21 @@ extern "C" {
 
 const char* sfx_version(void) { return "sfx 0.3 gfx950 fp32-mfma graphs speculative-gpi"; }
 const char* sfx_last_error(void) { return g_err.c_str(); }
+
+#ifdef SFX_PROBE
+// Debug builds: copy out (and reset) the kernel timing probe records; returns the count.
+int sfx_probe_dump(void* out_host, int max_recs) {
+  unsigned n = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(sfx::g_probe_n), sizeof(n)) != hipSuccess) return -1;
+  if (n > sfx::PROBE_N) n = sfx::PROBE_N;
+  if ((int)n > max_recs) n = (unsigned)max_recs;
+  if (n && hipMemcpyFromSymbol(out_host, HIP_SYMBOL(sfx::g_probe), n * sizeof(sfx::ProbeRec)) != hipSuccess) return -1;
+  const unsigned z = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(sfx::g_probe_n), &z, sizeof(z)) != hipSuccess) return -1;
+  return (int)n;
+}
+#endif
 
 int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts, int A, int d, int max_batch,
                int device, void* stream) {

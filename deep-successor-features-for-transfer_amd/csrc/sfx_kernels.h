@@ -32,6 +32,7 @@ constexpr int OMAX = 4096;    // A*d (row of a ψ output) held in LDS
 constexpr int DMAX = 256;     // feature dimension d
 constexpr int MMAX = 1024;    // rows of one update
 constexpr int KFUSE = 64;     // layer-0 fan-in up to which the post-update forward is fused
+constexpr int VFUSE = 4096;   // (rows x fan-in) of that forward's input, staged in LDS
 constexpr int TQF = 4096;     // 32 rows x (T*A) q values / 32 rows x A*d gradients of the fused TD target
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2 };
@@ -55,6 +56,46 @@ __device__ __forceinline__ float act_bwd(float gy, float y, int code) {
   if (code == ACT_TANH) return __fmul_rn(gy, __fsub_rn(1.f, __fmul_rn(y, y)));
   return gy;
 }
+
+// Timing probe (debug builds with -DSFX_PROBE only): wave 0 of each workgroup logs
+// s_memrealtime (100 MHz) at entry (t[0]), at up to four marks (t[1] kernel arguments
+// landed, t[2] operands landed / MFMA done, t[3], t[4] free) and after its stores completed
+// (t[5]), for tools/probe_run.py.
+#ifdef SFX_PROBE
+struct ProbeRec {
+  unsigned kid, blk;
+  unsigned long long t[6];
+};
+constexpr unsigned PROBE_N = 1u << 17;
+__device__ ProbeRec g_probe[PROBE_N];
+__device__ unsigned g_probe_n;
+__shared__ unsigned long long s_probe_t[6];
+#define PROBE_T(v)                                                                 \
+  const unsigned long long v = __builtin_amdgcn_s_memrealtime();                   \
+  if (threadIdx.x == 0) s_probe_t[1] = s_probe_t[2] = s_probe_t[3] = s_probe_t[4] = 0
+#define PROBE_AT(i) \
+  do { if (threadIdx.x == 0) s_probe_t[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define PROBE_MARKA() \
+  do { __builtin_amdgcn_s_waitcnt(0); PROBE_AT(1); } while (0)
+#define PROBE_MARK() PROBE_AT(2)
+#define PROBE_REC(kid, t0)                                                         \
+  do {                                                                             \
+    __builtin_amdgcn_s_waitcnt(0);                                                 \
+    const unsigned long long t5_ = __builtin_amdgcn_s_memrealtime();               \
+    if (threadIdx.x == 0) {                                                        \
+      const unsigned i_ = atomicAdd(&g_probe_n, 1u);                               \
+      if (i_ < PROBE_N)                                                            \
+        g_probe[i_] = ProbeRec{(unsigned)(kid), blockIdx.x + 65536u * blockIdx.y,  \
+                               {t0, s_probe_t[1], s_probe_t[2], s_probe_t[3], s_probe_t[4], t5_}}; \
+    }                                                                              \
+  } while (0)
+#else
+#define PROBE_T(v)
+#define PROBE_AT(i)
+#define PROBE_MARK()
+#define PROBE_MARKA()
+#define PROBE_REC(kid, t0)
+#endif
 
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -248,6 +289,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
   constexpr int KW = 256 / NW;  // K chunk of one wave per iteration (NW waves cover 256)
   constexpr int KL = KW / 4;    // consecutive k per lane (4 lane groups per MFMA k-step)
   // instance -> (group, head) with constant-index selects (no dynamic kernarg indexing)
+  PROBE_T(pt0);
   int y = blockIdx.y, tN = blockIdx.x, tM = blockIdx.z;
   if (F.xcd) {  // head h's tiles on the XCD of slot h % 8 (see xcd_decode)
     const int b = blockIdx.x, hp = (F.nh + 7) >> 3, k = b >> 3;
@@ -264,6 +306,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
   if (F.ngroups > 3 && y >= grp.n) { y -= grp.n; grp = F.g3; }
   const int head = grp.head0 + y;
   const int M = F.M, N = F.N, K = F.K;
+  PROBE_MARKA();
   const float* P = grp.which == P_TARGET ? G.target + (long long)head * G.P
                                          : G.online + G.slot_off(rslot(F.mask, head) ^ (grp.which == P_NEW), head);
   const float* X = F.xOff < 0 ? (grp.xsel == 1 ? F.xa : F.xb) : G.actp(grp.role, head, F.xOff);
@@ -353,6 +396,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
       acc1 = mfma4(a1[j], bw[j], acc1);
     }
   }
+  PROBE_MARK();
   __shared__ floatx4 red[NW][2][64];
   red[wave][0][lane] = acc0;
   red[wave][1][lane] = acc1;
@@ -374,6 +418,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
     if (F.flag && threadIdx.x == 0) *F.flag = F.flag_value;
     if (F.lms_head >= 0) lms_block(G, F);
   }
+  PROBE_REC(L0 ? 2 : 1, pt0);
 }
 
 // -------------------------------------------------------------------------------------
@@ -606,6 +651,7 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
     sm.gam[tid] = gam_l;
   }
   __syncthreads();
+  PROBE_AT(3);
   if (xm) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
@@ -651,6 +697,7 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
     if (pub && A.tdg_next) A.tdg_next[(size_t)(pol - A.head0) * A.tdg_next_stride + m0 + bl] = am;
   }
   __syncthreads();
+  PROBE_AT(4);
   // ---- stage E: output gradient rows (nonzero only at the taken action) and row losses
   const float norm = (float)(2.0 / ((double)M * (double)O));
   float* gout = G.dzp(pol, NLm) + (size_t)m0 * O;
@@ -746,6 +793,7 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
       }
     }
   }
+  PROBE_MARK();
   red[wave][0][lane] = acc0;
   red[wave][1][lane] = acc1;
   __syncthreads();
@@ -765,18 +813,34 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
 }
 
 // post-update forward of layer 0 for the 32 output rows this tile just optimised
-__device__ void fused_v0(const Geo& G, const BwdArgs& A, const RoleGeo& L, int head, int nbase, float* sW,
-                         float* sB) {
+// (input rows staged in LDS by role_dw: sX[m * K + k], m < vM)
+__device__ void fused_v0(const Geo& G, const BwdArgs& A, const RoleGeo& L, int head, int nbase, const float* sW,
+                         const float* sB, const float* sX) {
   __syncthreads();
+  PROBE_AT(3);
   const int K = L.K, N = L.N, VM = A.vM;
   float* Y = G.actp(A.vRole, head, A.vOff);
-  for (int idx = threadIdx.x; idx < VM * 32; idx += 256) {
-    const int m = idx >> 5, nl = idx & 31, n = nbase + nl;
-    if (n >= N) continue;
-    const float* x = m < A.M ? A.v_x + (size_t)m * K : A.v_xn;
-    float acc = 0.f;
-    for (int k = 0; k < K; ++k) acc = __builtin_fmaf(x[k], sW[nl * KFUSE + k], acc);
-    Y[(size_t)m * N + n] = act_fwd(__fadd_rn(acc, sB[nl]), A.act0);
+  // MFMA from LDS (the same k-ordered accumulation as k_fwd's layer-0 path): wave w owns
+  // column half (w & 1) and row tiles (w >> 1), (w >> 1) + 2, ...
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  const int nl = (wave & 1) * 16 + r, n = nbase + nl;
+  const float bias = sB[nl];
+  for (int mt = wave >> 1; mt * 16 < VM; mt += 2) {
+    floatx4 c = {0.f, 0.f, 0.f, 0.f};
+    const int ma = mt * 16 + r;
+    for (int k4 = 0; k4 < K; k4 += 4) {
+      const int k = k4 + g;
+      const float a = (k < K && ma < VM) ? sX[ma * K + k] : 0.f;
+      const float b = k < K ? sW[nl * KFUSE + k] : 0.f;
+      c = mfma4(a, b, c);
+    }
+    if (n < N) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = mt * 16 + g * 4 + i;
+        if (m < VM) Y[(size_t)m * N + n] = act_fwd(__fadd_rn(c[i], bias), A.act0);
+      }
+    }
   }
 }
 
@@ -815,15 +879,30 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
       pv[e] = ok[e] ? Vr[off] : 0.f;
     }
   }
-  // bias state (threads 0..31 of the kt == 0 tiles)
-  const bool dob = kt == 0 && threadIdx.x < 32 && nbase + (int)threadIdx.x < N;
-  const int nbias = nbase + threadIdx.x;
+  // bias of column n0 + r: lane r of waves 0/1 (k-half 0) of the kt == 0 tiles.  Its gradient
+  // Σ_m dZ[m][n] comes from the dZ operands already in registers (no extra loads: a lane
+  // stays under the 63 outstanding loads the vmcnt counter tracks).
+  const bool dob = kt == 0 && wave < 2 && g == 0 && nn < N;
+  const int nbias = nn;
   float bp = 0.f, bm = 0.f, bv = 0.f;
   if (dob) {
     bp = Pr[L.bOff + nbias];
     bm = Mr[L.bOff + nbias];
     bv = Vr[L.bOff + nbias];
   }
+  // fused forward input (S1 rows ++ s_next), requested with the rest, parked in LDS below
+  constexpr int XQ = VFUSE / 256;
+  float xs[XQ];
+  const int nxs = fuse ? A.vM * K : 0;
+  if (fuse) {
+#pragma unroll
+    for (int q = 0; q < XQ; ++q) {
+      const int j = threadIdx.x + 256 * q;
+      const float* src = j < M * K ? A.v_x + j : A.v_xn + (j - M * K);
+      xs[q] = j < nxs ? *src : 0.f;
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep those loads ahead of the MFMA operands
   floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
   for (int mc = 0; mc < M; mc += MT) {
@@ -836,23 +915,28 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
       bv0[j] = (okm && kb0 < K) ? X[(size_t)m * K + kb0] : 0.f;
       bv1[j] = (okm && kb1 < K) ? X[(size_t)m * K + kb1] : 0.f;
     }
-    float db[MT];
-    if (dob) {
-#pragma unroll
-      for (int m = 0; m < MT; ++m) db[m] = (mc + m < M) ? dZ[(size_t)(mc + m) * N + nbias] : 0.f;
-    }
 #pragma unroll
     for (int j = 0; j < MT / 4; ++j) {
       acc0 = mfma4(av[j], bv0[j], acc0);
       acc1 = mfma4(av[j], bv1[j], acc1);
     }
-    if (dob) {
 #pragma unroll
-      for (int m = 0; m < MT; ++m) bsum = __fadd_rn(bsum, db[m]);
-    }
+    for (int j = 0; j < MT / 4; ++j) bsum = __fadd_rn(bsum, av[j]);  // rows mc + 4j + g
   }
+  // + the other three row classes (lanes r + 16, r + 32, r + 48), fixed order
+  bsum = __fadd_rn(bsum, __shfl_xor(bsum, 16));
+  bsum = __fadd_rn(bsum, __shfl_xor(bsum, 32));
+  PROBE_MARK();
   __shared__ float sW[32 * KFUSE];
   __shared__ float sB[32];
+  __shared__ float sX[VFUSE];
+  if (fuse) {
+#pragma unroll
+    for (int q = 0; q < XQ; ++q) {
+      const int j = threadIdx.x + 256 * q;
+      if (j < nxs) sX[j] = xs[q];
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int n = n0 + g * 4 + i;
@@ -875,9 +959,9 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
     Pw[L.bOff + nbias] = bp;
     Mw[L.bOff + nbias] = bm;
     Vw[L.bOff + nbias] = bv;
-    if (fuse) sB[threadIdx.x] = bp;
+    if (fuse) sB[nbias - nbase] = bp;
   }
-  if (fuse) fused_v0(G, A, L, head, nbase, sW, sB);
+  if (fuse) fused_v0(G, A, L, head, nbase, sW, sB, sX);
 }
 
 // loss finalisation, optional w step, Adam step counter (one workgroup per head)
@@ -952,23 +1036,28 @@ __device__ void role_tail(const Geo& G, const BwdArgs& A, int head) {
 
 __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
   __shared__ floatx4 red[4][2][64];
+  PROBE_T(pt0);
   int head = A.head0 + blockIdx.y, bx = blockIdx.x;
   if (A.xcd) {
     if (!xcd_decode(blockIdx.x, A.nhead, A.na + A.nb + A.nc + A.tail, head, bx)) return;
     head += A.head0;
   }
+  PROBE_MARKA();
   if (bx < A.na) {
     role_dx<false>(G, A, head, bx, red);
+    PROBE_REC(4, pt0);
     return;
   }
   bx -= A.na;
   if (bx < A.nb) {
     role_dw(G, A, head, A.rb, bx, false);
+    PROBE_REC(5, pt0);
     return;
   }
   bx -= A.nb;
   if (bx < A.nc) {
     role_dw(G, A, head, A.rc, bx, A.fuse_v0 != 0);
+    PROBE_REC(6, pt0);
     return;
   }
   role_tail(G, A, head);
@@ -978,12 +1067,15 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
 template <int VMAX, int U>
 __global__ __launch_bounds__(256) void k_bwd_tdg(Geo G, BwdArgs A) {
   __shared__ floatx4 red[4][2][64];
+  PROBE_T(pt0);
   int head = A.head0 + blockIdx.y, bx = blockIdx.x;
   if (A.xcd) {
     if (!xcd_decode(blockIdx.x, A.nhead, A.na, head, bx)) return;
     head += A.head0;
   }
+  PROBE_MARKA();
   role_dx<true, VMAX, U>(G, A, head, bx, red);
+  PROBE_REC(3, pt0);
 }
 
 // -------------------------------------------------------------------------------------
@@ -1137,6 +1229,7 @@ struct VerArgs {
 // thread one q = ψ·w dot product, so every load is issued before the first reduction.
 __global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
   const int i = blockIdx.x, tid = threadIdx.x;
+  PROBE_T(pt0);
   if (i == V.npol) {
     if (V.sel && blockIdx.y == 0) gpi_row(G, V.g, 0);
     return;
@@ -1151,6 +1244,7 @@ __global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
   __shared__ float s_m[QMAX];
   __shared__ float s_w[DMAX];
   __shared__ int s_bad;
+  PROBE_MARKA();
   const float* wrow = G.w + (long long)i * G.dpad;
   const int n = nb * TA;
   const int spec = tid < nb ? (int)V.spec_next[(size_t)i * V.spec_stride + b0 + tid] : 0;
@@ -1192,6 +1286,7 @@ __global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
       s_q[idx] = q;
     }
   }
+  PROBE_MARK();
   __syncthreads();
   for (int j = tid; j < nb * Aa; j += 256) {  // max over heads per (row, action)
     const int bl = j / fA, a = j - bl * Aa;
@@ -1214,6 +1309,7 @@ __global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
   }
   __syncthreads();
   if (tid == 0 && s_bad) atomicMin(V.flag, i);
+  PROBE_REC(8, pt0);
 }
 
 // LMS reward fit (features/successor.py:164-167): w += α (r - Σ φ⊙w) φ
@@ -1259,6 +1355,7 @@ struct GateArgs {
 
 __global__ __launch_bounds__(256) void k_gate(GateArgs g) {
   __shared__ int ok;
+  PROBE_T(pt0);
   if (threadIdx.x == 0) {
     ok = 1;
     const long long want = *g.dctr + 1;
@@ -1275,7 +1372,9 @@ __global__ __launch_bounds__(256) void k_gate(GateArgs g) {
   }
   __syncthreads();
   if (!ok) return;
+  PROBE_MARK();
   for (int i = threadIdx.x; i < g.n16; i += 256) g.dst[i] = g.src[i];
+  PROBE_REC(9, pt0);
 }
 
 struct HostResult {  // host-coherent; seq written last
