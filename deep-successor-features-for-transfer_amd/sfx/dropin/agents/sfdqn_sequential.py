@@ -1,10 +1,12 @@
-"""SFDQN agent over a DeepSF library (the interface of agents/sfdqn.py:10-217).
+"""Sequential SFDQN agent over a DeepSF library (the interface of agents/sfdqn_sequential.py:11-245,
+main_sfdqn_sequential_torch.py).
 
-Per env step (``train_agent``): LMS reward fit for the active task, replay append, then every
-source task's ψ is updated on the same minibatch in index order -- with ``features.deep.DeepSF``
-those T calls run as one fused, exact device step.  Test tasks (``test_agent``) use GPI with
-a per-test-task reward model ``w`` (nn.Linear(d, 1)) trained by SGD on the observed rewards
-(agents/sfdqn.py:140-200).
+One replay buffer per training task (``buffer_handle()``); each env step appends
+(s, a, r, φ, s', γ) to the active task's buffer and runs ONE ``update_successor`` on the active
+task (l1 + l2 with the Adam-trained reward model, features.deep_sequential -> libsfx).  Test
+tasks (agents/sfdqn_sequential.py:177-234, the same as sfdqn.py:681-738): actions by GPI over the
+source heads with the test task's own reward model ``w`` (one B=1 GPI launch in libsfx), and
+``w`` trained by Adam on the observed rewards (d parameters, torch on the configured device).
 """
 from __future__ import annotations
 
@@ -18,15 +20,21 @@ from utils.torch import get_torch_device
 
 
 class SFDQN(Agent):
-    def __init__(self, deep_sf, buffer, *args, use_gpi=True, test_epsilon=0.03, **kwargs):
+    def __init__(self, deep_sf, buffer_handle, *args, use_gpi=True, test_epsilon=0.03, **kwargs):
         super().__init__(*args, **kwargs)
         self.sf = deep_sf
-        self.buffer = buffer
+        self.buffer_handle = buffer_handle
         self.use_gpi = use_gpi
         self.test_epsilon = test_epsilon
         self.logger = get_logger_level() or set_logger_level(False, quiet=True)
         self.device = get_torch_device()
         self.test_tasks_weights = []
+        self.hyperparameters = kwargs.get("hyperparameters", {})
+        self.buffers = []
+
+    def set_active_training_task(self, index):
+        super().set_active_training_task(index)
+        self.buffer = self.buffers[index]
 
     def get_Q_values(self, s, s_enc):
         with torch.no_grad():
@@ -38,25 +46,38 @@ class SFDQN(Agent):
 
     def train_agent(self, s, s_enc, a, r, s1, s1_enc, gamma):
         phi = self.phi(s, a, s1)
-        self.sf.update_reward(phi, r, self.task_index)
-        self.buffer.append(s_enc, a, phi, s1_enc, gamma)
+        self.buffer.append(s_enc, a, r, phi, s1_enc, gamma)
         transitions = self.buffer.replay()
-        for index in range(self.n_tasks):
-            self.sf.update_successor(transitions, index)
+        losses = self.sf.update_successor(transitions, self.task_index, self.use_gpi)
+        if isinstance(losses, tuple):
+            total_loss, psi_loss, phi_loss = losses
+            self.logger.log_losses(total_loss.item(), psi_loss.item(), phi_loss.item(), [1], self.total_training_steps)
+        if self.total_training_steps % 1000 == 0:
+            print(f"Current task {self.task_index} Reward Mapper {self.sf.fit_w[self.task_index].weight}")
 
     def reset(self):
         super().reset()
         self.sf.reset()
-        self.buffer.reset()
+        for buffer in self.buffers:
+            buffer.reset()
 
     def add_training_task(self, task):
         super().add_training_task(task)
         self.sf.add_training_task(task, source=None)
+        self.buffers.append(self.buffer_handle())
+
+    def get_progress_dict(self):
+        gpi = self.sf.GPI_usage_percent(self.task_index)
+        w_err = torch.linalg.norm(self.sf.fit_w[self.task_index].weight.T - self.sf.true_w[self.task_index])
+        return {"task": self.task_index, "steps": self.total_training_steps, "episodes": self.episode,
+                "eps": self.epsilon, "ep_reward": self.episode_reward, "reward": self.reward,
+                "reward_hist": self.reward_hist, "cum_reward": self.cum_reward,
+                "cum_reward_hist": self.cum_reward_hist, "GPI%": gpi, "w_err": w_err}
 
     def get_progress_strings(self):
         sample, reward = super().get_progress_strings()
         gpi = self.sf.GPI_usage_percent(self.task_index)
-        w_err = torch.linalg.norm(self.sf.fit_w[self.task_index] - self.sf.true_w[self.task_index])
+        w_err = torch.linalg.norm(self.sf.fit_w[self.task_index].weight.T - self.sf.true_w[self.task_index])
         return sample, reward, "GPI% \t {:.4f} \t w_err \t {:.4f}".format(gpi, w_err)
 
     def train(self, train_tasks, n_samples, viewers=None, n_view_ev=None, test_tasks=[], n_test_ev=1000,
@@ -65,12 +86,16 @@ class SFDQN(Agent):
         self.reset()
         for task in train_tasks:
             self.add_training_task(task)
+        hp = self.hyperparameters
         for test_task in test_tasks:
             fit_w = torch.Tensor(1, test_task.feature_dim()).uniform_(-0.01, 0.01).to(self.device)
-            w_approx = torch.nn.Linear(test_task.feature_dim(), 1, bias=False).to(self.device)  # CPU init draw
+            # CPU init draw (see features.deep_sequential.add_training_task)
+            w_approx = torch.nn.Linear(test_task.feature_dim(), 1, bias=False).to(self.device)
             with torch.no_grad():
                 w_approx.weight = torch.nn.Parameter(fit_w)
-            self.test_tasks_weights.append(w_approx)
+            optim = torch.optim.Adam([{"params": w_approx.parameters(), "lr": hp["learning_rate_w"],
+                                       "weight_decay": hp["weight_decay_w"]}])
+            self.test_tasks_weights.append((w_approx, optim))
         returns = []
         for _ in range(cycles_per_task):
             for index, (task, viewer) in enumerate(zip(train_tasks, viewers)):
@@ -86,19 +111,19 @@ class SFDQN(Agent):
                         self.logger.log_accumulative_reward(torch.sum(torch.Tensor(returns).to(self.device)),
                                                             self.total_training_steps)
                     self.total_training_steps += 1
-            return returns
+        return returns
 
-    # ---- test tasks (agents/sfdqn.py:140-200)
+    # ---- test tasks (agents/sfdqn_sequential.py:177-245)
     def get_test_action(self, s_enc, w):
         with torch.no_grad():
             if random.random() <= self.test_epsilon:
                 return torch.tensor(random.randrange(self.n_actions)).to(self.device)
-            q, c = self.sf.GPI_w(s_enc, w.weight.detach().reshape(-1, 1))
+            q, c = self.sf.GPI_w(s_enc, w)
             return torch.argmax(q[:, c, :])
 
     def test_agent(self, task, test_index):
         R = 0.0
-        w = self.test_tasks_weights[test_index]
+        w, optim = self.test_tasks_weights[test_index]
         s = task.initialize()
         s_enc = self.encoding(s)
         accum_loss = 0
@@ -106,7 +131,7 @@ class SFDQN(Agent):
             a = self.get_test_action(s_enc, w)
             s1, r, done = task.transition(a)
             s1_enc = self.encoding(s1)
-            accum_loss += self.update_test_reward_mapper(w, task, r, s_enc, a, s1_enc).item()
+            accum_loss += self.update_test_reward_mapper(w, optim, task, r, s_enc, a, s1_enc).item()
             s, s_enc = s1, s1_enc
             R += r
             if done:
@@ -114,10 +139,9 @@ class SFDQN(Agent):
         self.logger.log_target_error_progress(self.get_target_reward_mapper_error(R, accum_loss, test_index, self.T))
         return R
 
-    def update_test_reward_mapper(self, w_approx, task, r, s, a, s1):
+    def update_test_reward_mapper(self, w_approx, optim, task, r, s, a, s1):
         phi = task.features(s, a, s1)
-        optim = torch.optim.SGD(w_approx.parameters(), lr=0.005, weight_decay=0.01)
-        r_t = torch.tensor(r).detach().float().unsqueeze(0).requires_grad_(False).to(self.device)
+        r_t = torch.as_tensor(r).detach().float().reshape(1).to(self.device)
         optim.zero_grad()
         loss = torch.nn.MSELoss()(w_approx(phi), r_t)
         loss.backward()

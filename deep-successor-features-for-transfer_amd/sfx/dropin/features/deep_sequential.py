@@ -60,7 +60,9 @@ class DeepSF(_deep.DeepSF):
         true_w = task.get_w()
         n_features = task.feature_dim()
         fit_w = torch.Tensor(1, n_features).uniform_(-0.01, 0.01).to(self.device)
-        w_approx = torch.nn.Linear(n_features, 1, bias=False, device=self.device)
+        # built on the CPU and moved: its (overwritten) init draw comes from the CPU generator, as
+        # in a CPU run of the reference, so seeded runs follow the reference's trajectory
+        w_approx = torch.nn.Linear(n_features, 1, bias=False).to(self.device)
         with torch.no_grad():
             w_approx.weight = torch.nn.Parameter(fit_w)
         self.true_w.append(true_w)

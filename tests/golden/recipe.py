@@ -55,10 +55,11 @@ AGENT_RUN = dict(seed=7, n_s=17, H=32, A=7, d=8, acts=("relu", "relu"), T_tasks=
 class AgentTask:
     """Reacher-shaped Task (tasks/task.py interface) with its own RNG; records its actions."""
 
-    def __init__(self, n_s, A, d, index, seed, device, terminal_every=0):
+    def __init__(self, n_s, A, d, index, seed, device, terminal_every=0, tensor_reward=False):
         import numpy as np
 
         self.n_s, self.A, self.d, self.index, self.device = n_s, A, d, index, device
+        self.tensor_reward = tensor_reward  # tasks/reacher.py returns r as a 0-d tensor
         self.rng = np.random.default_rng(seed)
         self.terminal_every, self.t = terminal_every, 0
         self.actions, self._phi = [], None
@@ -82,6 +83,8 @@ class AgentTask:
         self._phi = torch.from_numpy(phi).to(self.device)
         r = float(phi[self.index % self.d])
         done = bool(self.terminal_every) and self.t % self.terminal_every == 0
+        if self.tensor_reward:
+            r = torch.tensor(r).to(self.device)
         return s1, r, done
 
     def encode(self, state):
@@ -138,5 +141,35 @@ def agent_run(DeepSF, SFDQN, ReplayBuffer, device):
                 target_update_ev=c["target_update_ev"], hyperparameters={"learning_rate_w": c["alpha_w"]})
     agent = SFDQN(deep_sf=sf, buffer=ReplayBuffer(**c["buffer"]), gamma=c["gamma"], T=c["episode_T"],
                   encoding="task", epsilon=c["epsilon"], use_gpi=True, test_epsilon=0.03)
+    returns = agent.train(tasks, c["n_samples"], test_tasks=test_tasks, n_test_ev=c["n_test_ev"])
+    return agent, tasks, test_tasks, returns
+
+
+# The main_sfdqn_sequential_torch.py stack: agents/sfdqn_sequential.py SFDQN (one buffer per
+# task, active-task updates, l1 + l2 with Adam-trained reward models, Adam-trained test-task
+# reward models) + agents/buffer_sequential.py + features/deep_sequential.py.
+AGENT_RUN_SEQ = dict(seed=11, n_s=17, H=32, A=7, d=8, acts=("relu", "relu"), T_tasks=3, lr=1e-3,
+                     hp=dict(learning_rate_sf=1e-3, weight_decay_sf=0.0, learning_rate_w=5e-3, weight_decay_w=1e-2),
+                     target_update_ev=5, n_samples=24, n_test_ev=8, episode_T=9, epsilon=0.2, gamma=0.9,
+                     buffer=dict(n_samples=500, n_batch=8), task_terminal_every=7)
+
+
+def agent_run_sequential(DeepSF, SFDQN, ReplayBuffer, device):
+    """Build and train the sequential agent of AGENT_RUN_SEQ; returns (agent, tasks, test_tasks, returns)."""
+    import random
+
+    import numpy as np
+
+    c = AGENT_RUN_SEQ
+    random.seed(c["seed"])
+    np.random.seed(c["seed"])
+    torch.manual_seed(c["seed"])
+    tasks = [AgentTask(c["n_s"], c["A"], c["d"], i, 300 + i, device, c["task_terminal_every"], tensor_reward=True)
+             for i in range(c["T_tasks"])]
+    test_tasks = [AgentTask(c["n_s"], c["A"], c["d"], c["T_tasks"], 400, device, tensor_reward=True)]
+    sf = DeepSF(pytorch_model_handle=agent_psi_lambda(c["H"], c["acts"], c["lr"], device),
+                target_update_ev=c["target_update_ev"], hyperparameters=c["hp"])
+    agent = SFDQN(deep_sf=sf, buffer_handle=lambda: ReplayBuffer(**c["buffer"]), gamma=c["gamma"], T=c["episode_T"],
+                  encoding="task", epsilon=c["epsilon"], use_gpi=True, test_epsilon=0.03, hyperparameters=c["hp"])
     returns = agent.train(tasks, c["n_samples"], test_tasks=test_tasks, n_test_ev=c["n_test_ev"])
     return agent, tasks, test_tasks, returns

@@ -61,3 +61,35 @@ def test_replay_buffer_semantics(mods):
     assert b.size == 4 and b.index == 2
     s, a, phi, s1, g = b.replay()
     assert s.shape == (2, 3) and a.shape == (2,) and phi.shape == (2, 2) and g.dtype == torch.float32
+
+
+def test_sequential_modules_and_buffer(mods):
+    """main_sfdqn_sequential_torch.py's imports resolve to the drop-in tree; the per-task buffer
+    keeps agents/buffer_sequential.py's 6-tuples, ring order and np.random sampling."""
+    import numpy as np
+
+    from sfx import dropin
+
+    root = dropin.install()
+    import agents.buffer_sequential as bs
+    import agents.sfdqn_sequential as ss
+    import features.deep_sequential as ds
+
+    for m in (bs, ss, ds):
+        assert m.__file__.startswith(root)
+    b = bs.ReplayBuffer(n_samples=4, n_batch=3)
+    assert b.replay() is None
+    for i in range(6):
+        b.append(torch.full((1, 3), float(i)), i % 2, torch.tensor(0.5 * i), torch.ones(1, 2) * i,
+                 torch.zeros(1, 3), 0.9)
+    assert b.size == 4 and b.index == 2
+    np.random.seed(3)
+    idx = np.random.randint(low=0, high=4, size=(3,))
+    np.random.seed(3)
+    s, a, r, phi, s1, g = b.replay()
+    # ring slots: 0 <- sample 4, 1 <- sample 5, 2 <- sample 2, 3 <- sample 3
+    src = np.array([4, 5, 2, 3])[idx]
+    assert torch.equal(s[:, 0], torch.tensor(src, dtype=torch.float32))
+    assert torch.equal(r[:, 0], torch.tensor(0.5 * src, dtype=torch.float32))
+    assert r.shape == (3, 1) and phi.shape == (3, 2) and a.tolist() == [int(x) % 2 for x in src]
+    assert g.dtype == torch.float32

@@ -1,4 +1,5 @@
-"""The main_sfdqn_torch.py stack on sfx's drop-in modules reproduces the REAL reference run.
+"""The main_sfdqn_torch.py (and main_sfdqn_sequential_torch.py) stacks on sfx's drop-in modules
+reproduce the REAL reference runs.
 
 tests/golden/run_sfdqn_agent.npz was produced by tools/gen_golden.py with the reference's own
 agents/sfdqn.py SFDQN, agents/buffer.py ReplayBuffer and features/deep.py DeepSF (CPU, torch
@@ -61,6 +62,48 @@ def test_dropin_reproduces_reference_agent_run(golden):
                               for t in range(T)]), g["target"], 1e-3 * 60)
     rel_close(torch.stack([sf.fit_w[t].reshape(-1).cpu() for t in range(T)]), g["w"], rtol=1e-4, atol=1e-6)
     rel_close(agent.test_tasks_weights[0].weight.detach().reshape(-1).cpu(), g["test_w"], rtol=1e-4, atol=1e-6)
+
+
+def test_dropin_reproduces_reference_sequential_run(golden):
+    """main_sfdqn_sequential_torch.py's stack (agents.sfdqn_sequential + agents.buffer_sequential +
+    features.deep_sequential) on the drop-in reproduces the real reference's seeded run
+    (tests/golden/run_sfdqn_sequential_agent.npz): training actions (active-task l1 + l2 updates),
+    test-task actions (GPI with the test task's Adam-trained reward model), GPI counters."""
+    from sfx import dropin
+
+    dropin.install()
+    import utils.torch as ut
+    from utils.logger import set_logger_level
+
+    ut.set_torch_device(True)
+    set_logger_level(False, quiet=True)
+    from agents.buffer_sequential import ReplayBuffer
+    from agents.sfdqn_sequential import SFDQN
+    from features.deep_sequential import DeepSF
+
+    from tests.golden.recipe import agent_run_sequential
+
+    assert "dropin" in __import__("agents.sfdqn_sequential").sfdqn_sequential.__file__
+    with contextlib.redirect_stdout(io.StringIO()):
+        agent, tasks, test_tasks, returns = agent_run_sequential(DeepSF, SFDQN, ReplayBuffer, ut.device)
+    g = golden("run_sfdqn_sequential_agent")
+    sf = agent.sf
+    assert sf._eng is not None, "the libsfx engine did not run"
+    got = np.array([a for t in tasks for a in t.actions])
+    assert np.array_equal(got, g["actions"]), f"training actions diverge at {np.argmax(got != g['actions'])}"
+    tg = np.array(test_tasks[0].actions)
+    assert np.array_equal(tg, g["test_actions"]), f"test actions diverge at {np.argmax(tg != g['test_actions'])}"
+    assert np.array_equal(np.stack([np.asarray(c) for c in sf.gpi_counters]), g["gpi_counters"])
+    assert list(sf.updates_since_target_updated) == list(g["since_target"])
+    assert agent.total_training_steps == int(g["total_steps"])
+    rel_close(torch.tensor([float(r) for r in returns]), g["returns"], rtol=1e-5, atol=1e-6)
+    T = sf.n_tasks
+    k = int(g["total_steps"])
+    params_close(torch.stack([torch.cat([p.detach().reshape(-1).cpu() for p in sf.psi[t][0][0].parameters()])
+                              for t in range(T)]), g["online"], 1e-3 * k)
+    rel_close(torch.stack([sf.fit_w[t].weight.detach().reshape(-1).cpu() for t in range(T)]), g["w"], rtol=1e-4,
+              atol=1e-5)
+    rel_close(agent.test_tasks_weights[0][0].weight.detach().reshape(-1).cpu(), g["test_w"], rtol=1e-4, atol=1e-6)
 
 
 @pytest.mark.parametrize("case", ["sfdqn_gpi", "sfdqn_nogpi", "sfdqn_tanh"])

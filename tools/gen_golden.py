@@ -382,6 +382,36 @@ def gen_agent_run():
     np.savez_compressed(os.path.join(OUT, "run_sfdqn_agent.npz"), **rec)
 
 
+def gen_agent_run_sequential():
+    """The main_sfdqn_sequential_torch.py stack end to end: reference agents/sfdqn_sequential.py
+    SFDQN + agents/buffer_sequential.py + features/deep_sequential.py DeepSF."""
+    import contextlib
+    import io
+
+    from agents.buffer_sequential import ReplayBuffer
+    from agents.sfdqn_sequential import SFDQN
+    from features.deep_sequential import DeepSF
+    from tests.golden.recipe import agent_run_sequential
+
+    with contextlib.redirect_stdout(io.StringIO()):
+        agent, tasks, test_tasks, returns = agent_run_sequential(DeepSF, SFDQN, ReplayBuffer, torch.device("cpu"))
+    sf = agent.sf
+    T = sf.n_tasks
+    tw, _ = agent.test_tasks_weights[0]
+    rec = dict(online=np_(torch.stack([flat(sf.psi[t][0][0]) for t in range(T)])),
+               target=np_(torch.stack([flat(sf.psi[t][1][0]) for t in range(T)])),
+               w=np_(torch.stack([sf.fit_w[t].weight.detach().reshape(-1).clone() for t in range(T)])),
+               gpi_counters=np.stack([np.asarray(c) for c in sf.gpi_counters]),
+               since_target=np.array(sf.updates_since_target_updated),
+               actions=np.array([a for t in tasks for a in t.actions]),
+               test_actions=np.array(test_tasks[0].actions),
+               test_w=np_(tw.weight.detach().reshape(-1)),
+               returns=np.array([float(r) for r in returns]),
+               reward_hist=np.array([float(x) for x in agent.reward_hist]),
+               cum_reward=float(agent.cum_reward), total_steps=agent.total_training_steps)
+    np.savez_compressed(os.path.join(OUT, "run_sfdqn_sequential_agent.npz"), **rec)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(4)
@@ -399,6 +429,7 @@ def main():
     gen_tsf("tsf", ref_tsfdqn, SHAPES["hopper11"], 3, 8, 0)
     gen_tsf("tsf_nf", ref_tsfdqn_nf, SHAPES["hopper11"], 3, 6, 3)
     gen_agent_run()
+    gen_agent_run_sequential()
     print("golden vectors written to", os.path.abspath(OUT))
 
 
