@@ -80,7 +80,7 @@ struct GraphKey {
 struct StepOut {
   int64_t sel[2];
   int flag;
-  int pad;
+  unsigned done;  // k_ver arrivals when it publishes (reset by the last arrival)
 };
 
 }  // namespace
@@ -143,6 +143,12 @@ struct sfx_handle {
   float *act = nullptr, *dz = nullptr, *rowloss = nullptr;
   int64_t* spec_next = nullptr;
   StepOut* dout = nullptr;  // device
+  // set by the runner while it captures a step: the final k_ver (with action selection)
+  // publishes to pub_res instead of a separate k_publish; pub_folded reports that it did
+  HostResult* pub_res = nullptr;
+  const long long* pub_dctr = nullptr;
+  bool pub_folded = false;
+  bool fold_publish = true;  // SFX_FOLD_PUBLISH=0: always a separate k_publish
   StepOut* hout = nullptr;  // pinned host
 
   int slot(int head) const { return (int)((mask >> head) & 1ull); }
@@ -500,8 +506,15 @@ int run_ver(sfx_handle* h, int M, int npol, bool sel, int post, const GpiArgs& g
   V.g = g;
   const int TA = h->T * h->A;
   V.rows = TA >= 256 ? 1 : (256 / TA < M ? 256 / TA : M);
-  launch(h, K_VER, 4.0 * (double)M * npol * h->T * h->O + 4.0 * h->T * h->O, k_ver, dim3(npol + 1, cdiv(M, V.rows)),
-         dim3(256), h->G, V);
+  const dim3 grid(npol + 1, cdiv(M, V.rows));
+  if (sel && h->pub_res && h->fold_publish) {
+    V.pub = h->pub_res;
+    V.pub_dctr = h->pub_dctr;
+    V.done = &h->dout->done;
+    V.nblocks = (int)(grid.x * grid.y);
+    h->pub_folded = true;
+  }
+  launch(h, K_VER, 4.0 * (double)M * npol * h->T * h->O + 4.0 * h->T * h->O, k_ver, grid, dim3(256), h->G, V);
   LAUNCHCHK();
   return SFX_OK;
 }
@@ -685,6 +698,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->fuse_tdg = !(ef && ef[0] == '0');
   const char* ev0 = std::getenv("SFX_FUSE_V0");
   h->fuse_v0 = !(ev0 && ev0[0] == '0');
+  const char* efp = std::getenv("SFX_FOLD_PUBLISH");
+  h->fold_publish = !(efp && efp[0] == '0');
   const char* ex = std::getenv("SFX_XCD");
   h->xcd = !(ex && ex[0] == '0');
   const char* efw = std::getenv("SFX_FWD_WAVES");

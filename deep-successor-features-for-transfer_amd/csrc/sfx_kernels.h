@@ -324,35 +324,54 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
   if constexpr (L0) {
     __shared__ float sX[32 * L0_KMAX];
     const int K0 = F.K0;
+    // a0 = X W0ᵀ + b0 by MFMA: wave w owns layer-0 columns [32w, 32w + 32) (+32·NW ...), K0 in
+    // k-steps of 4.  The W0 / b0 operands of the first column block are requested together
+    // with the X rows, before the barrier (one memory latency, not one per k-step).
+    const float* W0 = P + F.w0Off;
+    const float* b0 = P + F.b0Off;
+    float* Y0 = G.actp(grp.role, head, F.y0Off);
+    constexpr int KS = L0_KMAX / 4;
+    float wA[KS], wB[KS], bA, bB;
+    auto load_w0 = [&](int cb) {
+      const int nA = cb + r, nB = cb + 16 + r;
+#pragma unroll
+      for (int q = 0; q < KS; ++q) {
+        const int kk = 4 * q + g;
+        const bool okk = kk < K0;
+        wA[q] = okk && nA < K ? W0[(size_t)nA * K0 + kk] : 0.f;
+        wB[q] = okk && nB < K ? W0[(size_t)nB * K0 + kk] : 0.f;
+      }
+      bA = nA < K ? b0[nA] : 0.f;
+      bB = nB < K ? b0[nB] : 0.f;
+    };
+    int cb = wave * 32;
+    load_w0(cb);
     for (int j = threadIdx.x; j < 32 * K0; j += 64 * NW) {
       const int rr = j / fdiv(K0), kk = j - rr * K0;
       sX[j] = m0 + rr < M ? X[(size_t)(m0 + rr) * K0 + kk] : 0.f;
     }
     __syncthreads();
-    // a0 = X W0ᵀ + b0 by MFMA: wave w owns layer-0 columns [32w, 32w + 32), K0 in k-steps of 4
-    const float* W0 = P + F.w0Off;
-    const float* b0 = P + F.b0Off;
-    float* Y0 = G.actp(grp.role, head, F.y0Off);
-    for (int cb = wave * 32; cb < K; cb += 32 * NW) {
+    PROBE_AT(3);
+    for (; cb < K; cb += 32 * NW) {
       floatx4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c10 = c00, c11 = c00;
-      const int nA = cb + r, nB = cb + 16 + r;
-      for (int k4 = 0; k4 < K0; k4 += 4) {
-        const int kk = k4 + g;
-        const bool okk = kk < K0;
-        const float x0 = okk ? sX[r * K0 + kk] : 0.f, x1 = okk ? sX[(16 + r) * K0 + kk] : 0.f;
-        const float wA = okk && nA < K ? W0[(size_t)nA * K0 + kk] : 0.f;
-        const float wB = okk && nB < K ? W0[(size_t)nB * K0 + kk] : 0.f;
-        c00 = mfma4(x0, wA, c00);
-        c01 = mfma4(x0, wB, c01);
-        c10 = mfma4(x1, wA, c10);
-        c11 = mfma4(x1, wB, c11);
+#pragma unroll
+      for (int q = 0; q < KS; ++q) {
+        if (4 * q < K0) {
+          const int kk = 4 * q + g;
+          const bool okk = kk < K0;
+          const float x0 = okk ? sX[r * K0 + kk] : 0.f, x1 = okk ? sX[(16 + r) * K0 + kk] : 0.f;
+          c00 = mfma4(x0, wA[q], c00);
+          c01 = mfma4(x0, wB[q], c01);
+          c10 = mfma4(x1, wA[q], c10);
+          c11 = mfma4(x1, wB[q], c11);
+        }
       }
       const floatx4* cs[4] = {&c00, &c01, &c10, &c11};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int cc = cb + (q & 1) * 16 + r;
         if (cc < K) {
-          const float bb = b0[cc];
+          const float bb = (q & 1) ? bB : bA;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int rr = (q >> 1) * 16 + g * 4 + i;
@@ -362,8 +381,10 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
           }
         }
       }
+      if (cb + 32 * NW < K) load_w0(cb + 32 * NW);
     }
     __syncthreads();
+    PROBE_AT(4);
   }
   const float* xra = L0 ? sA + r * AS : X + (size_t)ma * K;
   const float* xrb = L0 ? sA + (16 + r) * AS : X + (size_t)mb * K;
@@ -602,7 +623,7 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
   const bool xm = A.tdg_xmax != nullptr;
   const int t0 = A.tdg_use_gpi ? 0 : pol, nt = A.tdg_use_gpi ? T : 1, TA = nt * Aa, n = xm ? 0 : nb * TA, V = d >> 2;
   const int guess = A.tdg_guess;
-  const FDiv fTA = fdiv(TA), fA = fdiv(Aa), fO = fdiv(O);
+  const FDiv fTA = fdiv(TA), fA = fdiv(Aa);
   // ---- stage A: all global loads
   float4 v[U][VMAX];
 #pragma unroll
@@ -642,6 +663,7 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
     if (i < n4) {
       reinterpret_cast<float4*>(sm.tt)[i] = tt[u];
       reinterpret_cast<float4*>(sm.tc)[i] = tc[u];
+      reinterpret_cast<float4*>(sm.dz)[i] = make_float4(0.f, 0.f, 0.f, 0.f);  // stage E fills the taken actions
     }
   }
   if (tid < np4) reinterpret_cast<float4*>(sm.ph)[tid] = ph;
@@ -698,35 +720,32 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
   }
   __syncthreads();
   PROBE_AT(4);
-  // ---- stage E: output gradient rows (nonzero only at the taken action) and row losses
+  // ---- stage E: output gradient rows -- nonzero only at the taken action: one thread per
+  // (row, feature) of it -- and the rows' squared errors (into sm.q, free after stage C)
   const float norm = (float)(2.0 / ((double)M * (double)O));
-  float* gout = G.dzp(pol, NLm) + (size_t)m0 * O;
-  for (int i = tid; i < nb * O; i += 256) {
-    const int bl = i / fO, o = i - bl * O, ab = sm.a[bl];
-    float gv = 0.f;
-    if (ab >= 0 && ab < Aa && o >= ab * d && o < ab * d + d) {
-      const int k = o - ab * d;
+  const FDiv fd = fdiv(d);
+  float* sq = sm.q;
+  for (int i = tid; i < nb * d; i += 256) {
+    const int bl = i / fd, k = i - bl * d, ab = sm.a[bl];
+    float e2 = 0.f;
+    if (ab >= 0 && ab < Aa) {
       const float tg = __fadd_rn(sm.ph[bl * d + k], __fmul_rn(sm.gam[bl], sm.tt[bl * O + sm.n[bl] * d + k]));
-      gv = __fmul_rn(norm, __fsub_rn(sm.tc[i], tg));
+      const float diff = __fsub_rn(sm.tc[bl * O + ab * d + k], tg);
+      sm.dz[bl * O + ab * d + k] = __fmul_rn(norm, diff);
+      e2 = __fmul_rn(diff, diff);
     }
-    sm.dz[i] = gv;
-    if (pub) gout[i] = gv;
+    sq[i] = e2;
   }
+  __syncthreads();
   if (pub) {
+    float4* gout4 = reinterpret_cast<float4*>(G.dzp(pol, NLm) + (size_t)m0 * O);
+    for (int i = tid; i < n4; i += 256) gout4[i] = reinterpret_cast<const float4*>(sm.dz)[i];
     for (int bl = tid; bl < nb; bl += 256) {  // row Σ diff^2 in feature order
-      const int ab = sm.a[bl];
       float sacc = 0.f;
-      if (ab >= 0 && ab < Aa) {
-        for (int k = 0; k < d; ++k) {
-          const float diff = __fsub_rn(sm.tc[bl * O + ab * d + k],
-                                       __fadd_rn(sm.ph[bl * d + k], __fmul_rn(sm.gam[bl], sm.tt[bl * O + sm.n[bl] * d + k])));
-          sacc = __fadd_rn(sacc, __fmul_rn(diff, diff));
-        }
-      }
+      for (int k = 0; k < d; ++k) sacc = __fadd_rn(sacc, sq[bl * d + k]);
       G.rowloss[(long long)pol * MMAX + m0 + bl] = sacc;
     }
   }
-  __syncthreads();
 }
 
 template <bool TDG, int VMAX = 2, int U = 8>
@@ -761,19 +780,23 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
       G.adamc[head] = adam_consts(A.hp, st);
     }
     if (A.flag && tile == 0 && head == A.head0 && threadIdx.x == 0) *A.flag = A.flag_value;
-    const int nb = wave * 64 + g * 16;
+    // the 16 k-steps of each 64-wide chunk are split over the waves (4 or 8 steps each); the
+    // partial sums meet in the reduction below
+    const int wpc = N > 64 ? 2 : 4, jw = 16 / wpc, j0 = (wave % wpc) * jw;
+    const int nb = (wave / wpc) * 64 + g * 16;
     float bw[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) bw[j] = (okk && nb + j < N) ? W[(size_t)(nb + j) * K + kk] : 0.f;
+    for (int j = 0; j < 16; ++j)
+      bw[j] = (j >= j0 && j < j0 + jw && okk && nb + j < N) ? W[(size_t)(nb + j) * K + kk] : 0.f;
     tdg_rows<VMAX, U>(G, A, head, m0, tile % ntk == 0, sm);
-    if (wave * 64 < N) {
-      float a0[16], a1[16];
-      load16u(a0, sm.dz + (size_t)r * N, nb, N, oka, false);
-      load16u(a1, sm.dz + (size_t)(16 + r) * N, nb, N, okb, false);
+    const float* da = sm.dz + (size_t)r * N + nb;
+    const float* db = sm.dz + (size_t)(16 + r) * N + nb;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        acc0 = mfma4(a0[j], bw[j], acc0);
-        acc1 = mfma4(a1[j], bw[j], acc1);
+    for (int j = 0; j < 16; ++j) {
+      if (j >= j0 && j < j0 + jw) {
+        const bool okj = nb + j < N;
+        acc0 = mfma4(oka && okj ? da[j] : 0.f, bw[j], acc0);
+        acc1 = mfma4(okb && okj ? db[j] : 0.f, bw[j], acc1);
       }
     }
   } else {
@@ -1198,9 +1221,9 @@ __device__ void gpi_row(const Geo& G, const GpiArgs& A, int b) {
     if (tid == 0) {
       if (A.task_out) A.task_out[ob] = tb;
       if (A.next_out) A.next_out[ob] = ab;
-      if (A.sel_out) {
-        A.sel_out[0] = c;
-        A.sel_out[1] = act;
+      if (A.sel_out) {  // sc1 stores: k_ver's last workgroup may publish them in this launch
+        __hip_atomic_store(A.sel_out, (int64_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(A.sel_out + 1, (int64_t)act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -1218,18 +1241,43 @@ __global__ __launch_bounds__(256) void k_gpi(Geo G, GpiArgs A) { gpi_row(G, A, b
 // policy's actions from this round's post-update values and fixes at least one more head.
 // Block npol (when sel): GPI action for s_next (row M of `post`) with w[select_task].
 // -------------------------------------------------------------------------------------
+struct HostResult {  // host-coherent; seq written last
+  long long sel0, sel1;
+  int flag, err;
+  long long seq;
+};
+
+// Post the step's result (selected action, speculation verdict) to host-coherent memory;
+// seq is written last (system release).  The inputs are read with coherent (sc1) loads.
+__device__ __forceinline__ void publish_result(const int64_t* sel, const int* flag, HostResult* out,
+                                               const long long* dctr) {
+  const long long s0 = __hip_atomic_load(sel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long long s1 = __hip_atomic_load(sel + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  out->sel0 = s0;
+  out->sel1 = s1;
+  out->flag = f;
+  __threadfence_system();
+  __hip_atomic_store(&out->seq, *dctr, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct VerArgs {
   int M, npol, sel, spec_stride, post, rows;  // rows: minibatch rows per workgroup
   const int64_t* spec_next;  // [T][spec_stride]
   int* flag;
   GpiArgs g;                 // action selection for s_next
+  // k_publish folded in (runner steps): every workgroup arrives on `done`; the last one to
+  // arrive (told by the value its add returns) publishes.  Null: no publication.
+  HostResult* pub;
+  const long long* pub_dctr;
+  unsigned* done;
+  int nblocks, pad_;
 };
 
 // Grid (npol + 1, ceil(M / rows)): one workgroup per (policy, `rows` minibatch rows), each
 // thread one q = ψ·w dot product, so every load is issued before the first reduction.
-__global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
+__device__ void ver_block(const Geo& G, const VerArgs& V) {
   const int i = blockIdx.x, tid = threadIdx.x;
-  PROBE_T(pt0);
   if (i == V.npol) {
     if (V.sel && blockIdx.y == 0) gpi_row(G, V.g, 0);
     return;
@@ -1309,6 +1357,26 @@ __global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
   }
   __syncthreads();
   if (tid == 0 && s_bad) atomicMin(V.flag, i);
+}
+
+__global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
+  PROBE_T(pt0);
+  ver_block(G, V);
+  if (V.pub) {
+    // this workgroup's sel stores / flag atomic are sc1 (coherent) and issued by wave 0:
+    // wait for them, then arrive; the last arrival publishes
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_s_waitcnt(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned prev = __hip_atomic_fetch_add(V.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("" ::: "memory");
+      if (prev == (unsigned)V.nblocks - 1) {
+        publish_result(V.g.sel_out, V.flag, V.pub, V.pub_dctr);
+        __hip_atomic_store(V.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
   PROBE_REC(8, pt0);
 }
 
@@ -1377,20 +1445,9 @@ __global__ __launch_bounds__(256) void k_gate(GateArgs g) {
   PROBE_REC(9, pt0);
 }
 
-struct HostResult {  // host-coherent; seq written last
-  long long sel0, sel1;
-  int flag, err;
-  long long seq;
-};
 
 __global__ void k_publish(const int64_t* sel, const int* flag, HostResult* out, const long long* dctr) {
-  if (threadIdx.x == 0) {
-    out->sel0 = sel[0];
-    out->sel1 = sel[1];
-    out->flag = *flag;
-    __threadfence_system();
-    __hip_atomic_store(&out->seq, *dctr, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  if (threadIdx.x == 0) publish_result(sel, flag, out, dctr);
 }
 
 }  // namespace sfx
