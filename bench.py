@@ -33,7 +33,8 @@ import torch  # noqa: E402
 METRIC = "env steps/sec (whole node), Reacher 8-task SF-DQN at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SHAPE = dict(n_s=17, H=256, A=7, d=8, acts=("relu", "relu"))
-KIND_NAMES = {"fwd": "k_fwd", "tdg": "k_tdg", "bwd": "k_bwd", "gpi": "k_gpi", "lms": "k_lms", "ver": "k_ver"}
+KIND_NAMES = {"fwd": "k_fwd", "tdg": "k_tdg", "bwd": "k_bwd", "gpi": "k_gpi", "lms": "k_lms", "ver": "k_ver",
+              "round": "k_round"}
 
 
 def parse():

@@ -149,6 +149,17 @@ struct sfx_handle {
   const long long* pub_dctr = nullptr;
   bool pub_folded = false;
   bool fold_publish = true;  // SFX_FOLD_PUBLISH=0: always a separate k_publish
+  // k_round (one launch per speculative round, see sfx_kernels.h); SFX_ROUND=1 turns it on
+  bool use_round = false;
+  unsigned* round_ctr = nullptr;  // [T] per-head arrival counters
+  struct RoundRec {               // launch arguments recorded instead of launched
+    std::vector<BwdArgs> b;
+    std::vector<FwdArgs> f;
+    std::vector<double> bytes;
+    bool fvec = true;
+    int tdg = 0;
+  };
+  RoundRec* rec = nullptr;
   StepOut* hout = nullptr;  // pinned host
 
   int slot(int head) const { return (int)((mask >> head) & 1ull); }
@@ -166,7 +177,7 @@ void clear_graphs(sfx_handle* h) {
   h->graphs.clear();
 }
 
-enum { K_FWD = 0, K_TDG = 1, K_BWD = 2, K_GPI = 3, K_LMS = 4, K_VER = 5, K_NKIND = 6 };
+enum { K_FWD = 0, K_TDG = 1, K_BWD = 2, K_GPI = 3, K_LMS = 4, K_VER = 5, K_ROUND = 6, K_NKIND = 7 };
 
 hipEvent_t prof_event(sfx_handle* h) {
   if (!h->prof_pool.empty()) {
@@ -294,7 +305,11 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     if (l0) by += 4.0 * ninst * ((double)h->L[0].N * h->L[0].K + h->L[0].N + (double)M * h->L[0].K);
     // the vector path needs K % (256/NW) == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
     const bool aligned = l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0);
-    if (l0) {
+    if (h->rec) {  // k_round's post-update forward runs 4-wave tiles
+      h->rec->f.push_back(F);
+      h->rec->bytes.push_back(by);
+      h->rec->fvec = h->rec->fvec && (L.K % 64) == 0 && aligned && !l0;
+    } else if (l0) {
       launch(h, K_FWD, by, k_fwd<true, 8, true>, grid, dim3(512), h->G, F);
     } else if (h->fwd_waves == 8) {
       const bool vec = (L.K % 32) == 0 && aligned;
@@ -441,7 +456,11 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     A.tail = li == tail_at && need_tail ? 1 : 0;
     const int ntile = A.tdg ? A.na : A.na + A.nb + A.nc + A.tail;
     const dim3 grid = A.xcd ? dim3(8 * cdiv(nhead, 8) * ntile) : dim3(ntile, nhead);
-    if (A.tdg && tdg_variant(h) == 1)  // d <= 8
+    if (h->rec) {
+      h->rec->b.push_back(A);
+      h->rec->bytes.push_back(by);
+      if (A.tdg) h->rec->tdg = tdg_variant(h);
+    } else if (A.tdg && tdg_variant(h) == 1)  // d <= 8
       launch(h, K_BWD, by, k_bwd_tdg<2, 8>, grid, dim3(256), h->G, A);
     else if (A.tdg)
       launch(h, K_BWD, by, k_bwd_tdg<4, 4>, grid, dim3(256), h->G, A);
@@ -463,6 +482,11 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.v_x = ex.v_x;
   A.v_xn = ex.v_xn;
   const int ntile = A.nb + A.nc + A.tail;
+  if (h->rec) {
+    h->rec->b.push_back(A);
+    h->rec->bytes.push_back(nhead * (dw_bytes(1) + dw_bytes(0)));
+    return SFX_OK;
+  }
   launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), k_bwd,
          A.xcd ? dim3(8 * cdiv(nhead, 8) * ntile) : dim3(ntile, nhead), dim3(256), h->G, A);
   LAUNCHCHK();
@@ -566,7 +590,7 @@ void free_all(sfx_handle* h) {
   }
   for (hipEvent_t e : h->prof_pool) (void)hipEventDestroy(e);
   for (void* p : {(void*)h->online, (void*)h->target, (void*)h->am, (void*)h->av, (void*)h->w, (void*)h->wm,
-                  (void*)h->wv, (void*)h->step, (void*)h->adamc, (void*)h->act, (void*)h->dz, (void*)h->rowloss, (void*)h->spec_next,
+                  (void*)h->wv, (void*)h->step, (void*)h->adamc, (void*)h->round_ctr, (void*)h->act, (void*)h->dz, (void*)h->rowloss, (void*)h->spec_next,
                   (void*)h->dout})
     if (p) (void)hipFree(p);
   if (h->hout) (void)hipHostFree(h->hout);
@@ -599,9 +623,43 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
   bx.vRole = out;
   bx.v_x = p.S1;
   bx.v_xn = want_sel ? p.s_next : nullptr;
-  RC(run_bwd(h, 0, T, B, p.S, p.phi, nullptr, p.losses, td, bx));
   const int vM = B + (want_sel ? 1 : 0);
-  if (bx.fuse_v0) {
+  // the whole round as one k_round launch when its preconditions hold (see RoundArgs)
+  const bool round1 = h->use_round && T <= 8 && bx.fuse_v0 && !p.losses && can_fuse_tdg(h) &&
+                      ((uintptr_t)p.phi & 15) == 0 && h->NL >= 3 && h->NL - 1 <= RF_MAX && h->NL <= RB_MAX;
+  if (round1) {
+    sfx_handle::RoundRec rec;
+    h->rec = &rec;
+    int rc = run_bwd(h, 0, T, B, p.S, p.phi, nullptr, nullptr, td, bx);
+    FwdExtra vx;
+    vx.l0 = 1;
+    if (rc == SFX_OK) rc = run_fwd(h, {{out, P_NEW, 0, 0, T}}, vM, nullptr, nullptr, vx);
+    h->rec = nullptr;
+    RC(rc);
+    if ((int)rec.b.size() != h->NL || (int)rec.f.size() != h->NL - 1 || !rec.b[0].tdg || rec.b.back().tail)
+      SFX_FAIL(SFX_E_STATE, "k_round: unexpected launch sequence");
+    RoundArgs R{};
+    for (size_t i = 0; i < rec.b.size(); ++i) R.b[i] = rec.b[i];
+    for (size_t i = 0; i < rec.f.size(); ++i) R.f[i] = rec.f[i];
+    R.nb = (int)rec.b.size();
+    R.nf = (int)rec.f.size();
+    R.wph = 256 / T < 32 ? 256 / T : 32;
+    R.ctr = h->round_ctr;
+    R.err = &h->dout->flag;
+    R.timeout = 200000000LL;  // 2 s of the 100 MHz clock
+    double by = 0.0;
+    for (double x : rec.bytes) by += x;
+    const dim3 grid(T * R.wph);
+    if (rec.tdg == 1)
+      launch(h, K_ROUND, by, rec.fvec ? k_round<2, 8, true> : k_round<2, 8, false>, grid, dim3(256), h->G, R);
+    else
+      launch(h, K_ROUND, by, rec.fvec ? k_round<4, 4, true> : k_round<4, 4, false>, grid, dim3(256), h->G, R);
+    LAUNCHCHK();
+  } else {
+    RC(run_bwd(h, 0, T, B, p.S, p.phi, nullptr, p.losses, td, bx));
+  }
+  if (round1) {
+  } else if (bx.fuse_v0) {
     FwdExtra vx;
     vx.l0 = 1;
     RC(run_fwd(h, {{out, P_NEW, 0, 0, T}}, vM, nullptr, nullptr, vx));
@@ -700,6 +758,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->fuse_v0 = !(ev0 && ev0[0] == '0');
   const char* efp = std::getenv("SFX_FOLD_PUBLISH");
   h->fold_publish = !(efp && efp[0] == '0');
+  const char* erd = std::getenv("SFX_ROUND");  // opt-in: measured slower than the launches
+  h->use_round = erd && erd[0] == '1';
   const char* ex = std::getenv("SFX_XCD");
   h->xcd = !(ex && ex[0] == '0');
   const char* efw = std::getenv("SFX_FWD_WAVES");
@@ -755,6 +815,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   alloc((void**)&h->wv, wBytes);
   alloc((void**)&h->step, sizeof(int) * T);
   alloc((void**)&h->adamc, sizeof(AdamC) * T);
+  alloc((void**)&h->round_ctr, sizeof(unsigned) * T);
   alloc((void**)&h->act, sizeof(float) * (size_t)NROLE * T * h->actSize);
   alloc((void**)&h->dz, sizeof(float) * (size_t)T * h->actSize);
   alloc((void**)&h->rowloss, sizeof(float) * (size_t)T * MMAX);

@@ -64,15 +64,16 @@ __device__ __forceinline__ float act_bwd(float gy, float y, int code) {
 #ifdef SFX_PROBE
 struct ProbeRec {
   unsigned kid, blk;
-  unsigned long long t[6];
+  unsigned long long t[10];
 };
-constexpr unsigned PROBE_N = 1u << 17;
+constexpr unsigned PROBE_N = 1u << 16;
 __device__ ProbeRec g_probe[PROBE_N];
 __device__ unsigned g_probe_n;
-__shared__ unsigned long long s_probe_t[6];
+__shared__ unsigned long long s_probe_t[10];
 #define PROBE_T(v)                                                                 \
   const unsigned long long v = __builtin_amdgcn_s_memrealtime();                   \
-  if (threadIdx.x == 0) s_probe_t[1] = s_probe_t[2] = s_probe_t[3] = s_probe_t[4] = 0
+  if (threadIdx.x == 0)                                                            \
+    for (int i_ = 1; i_ < 9; ++i_) s_probe_t[i_] = 0
 #define PROBE_AT(i) \
   do { if (threadIdx.x == 0) s_probe_t[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define PROBE_MARKA() \
@@ -86,7 +87,8 @@ __shared__ unsigned long long s_probe_t[6];
       const unsigned i_ = atomicAdd(&g_probe_n, 1u);                               \
       if (i_ < PROBE_N)                                                            \
         g_probe[i_] = ProbeRec{(unsigned)(kid), blockIdx.x + 65536u * blockIdx.y,  \
-                               {t0, s_probe_t[1], s_probe_t[2], s_probe_t[3], s_probe_t[4], t5_}}; \
+                               {t0, s_probe_t[1], s_probe_t[2], s_probe_t[3], s_probe_t[4],   \
+                                s_probe_t[5], s_probe_t[6], s_probe_t[7], s_probe_t[8], t5_}}; \
     }                                                                              \
   } while (0)
 #else
@@ -101,13 +103,35 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Loads / stores of data handed between workgroups INSIDE one launch (the round kernel,
+// k_round): C = true makes them coherent -- sc1 (L1-bypassing) dword loads and write-through
+// stores, the hand-off form of MI355X_MICROARCH.md's validated table (sc1 stores, every storing
+// wave's vmcnt(0), one agent-scope arrival per workgroup, sc1 poll, barrier, sc1 loads).
+// C = false: plain accesses (data from an earlier launch; the kernel boundary orders it).
+template <bool C>
+__device__ __forceinline__ float ldc(const float* p) {
+  if constexpr (C) return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <bool C>
+__device__ __forceinline__ void stc(float* p, float v) {
+  if constexpr (C) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <bool C>
+__device__ __forceinline__ float4 ldc4(const float* p) {  // 16-B aligned
+  if constexpr (C) return make_float4(ldc<true>(p), ldc<true>(p + 1), ldc<true>(p + 2), ldc<true>(p + 3));
+  else return *reinterpret_cast<const float4*>(p);
+}
+
 // 16 consecutive floats row[kb .. kb+15] (zero where !ok / outside [0, K)).  `vec` must be
 // wave-uniform (K % 64 == 0 with 16-B aligned rows): then four predicated float4 loads.
+template <bool C = false>
 __device__ __forceinline__ void load16u(float (&v)[16], const float* row, int kb, int K, bool ok, bool vec) {
   if (vec) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float4 t = ok ? reinterpret_cast<const float4*>(row + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 t = ok ? ldc4<C>(row + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
       v[4 * q] = t.x;
       v[4 * q + 1] = t.y;
       v[4 * q + 2] = t.z;
@@ -115,7 +139,7 @@ __device__ __forceinline__ void load16u(float (&v)[16], const float* row, int kb
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = (ok && kb + j < K) ? row[kb + j] : 0.f;
+    for (int j = 0; j < 16; ++j) v[j] = (ok && kb + j < K) ? ldc<C>(row + kb + j) : 0.f;
   }
 }
 
@@ -201,6 +225,24 @@ struct AdamC {
   float omb1, b2, omb2, eps, wd, bc2s, nss;
 };
 
+template <bool C>
+__device__ __forceinline__ AdamC load_adamc(const AdamC* p) {
+  if constexpr (!C) {
+    return *p;
+  } else {
+    const float* f = reinterpret_cast<const float*>(p);
+    AdamC c;
+    c.omb1 = ldc<true>(f);
+    c.b2 = ldc<true>(f + 1);
+    c.omb2 = ldc<true>(f + 2);
+    c.eps = ldc<true>(f + 3);
+    c.wd = ldc<true>(f + 4);
+    c.bc2s = ldc<true>(f + 5);
+    c.nss = ldc<true>(f + 6);
+    return c;
+  }
+}
+
 __device__ __forceinline__ AdamC adam_consts(const AdamHP& hp, int step) {
   AdamC c;
   const double bc1 = 1.0 - pow(hp.b1, (double)step);
@@ -284,29 +326,21 @@ __device__ void lms_block(const Geo& G, const FwdArgs& F) {
 // them for the backward -- and feeds them to the layer-1 MFMAs from LDS: one launch less.
 constexpr int L0_KMAX = 64, L0_NMAX = 256;  // layer-0 fan-in / width handled in-tile
 
-template <bool VEC, int NW, bool L0>
-__global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
+// One 32-row x 16-column output tile of instance y (flattened over the groups).  C: the layer
+// input X, the parameters and the output are handed between workgroups inside the launch
+// (k_round's post-update forward) -- coherent accesses.
+template <bool VEC, int NW, bool L0, bool C>
+__device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, int tN, int tM) {
+  static_assert(!(L0 && C), "the in-tile layer 0 reads only inputs of earlier launches");
   constexpr int KW = 256 / NW;  // K chunk of one wave per iteration (NW waves cover 256)
   constexpr int KL = KW / 4;    // consecutive k per lane (4 lane groups per MFMA k-step)
   // instance -> (group, head) with constant-index selects (no dynamic kernarg indexing)
-  PROBE_T(pt0);
-  int y = blockIdx.y, tN = blockIdx.x, tM = blockIdx.z;
-  if (F.xcd) {  // head h's tiles on the XCD of slot h % 8 (see xcd_decode)
-    const int b = blockIdx.x, hp = (F.nh + 7) >> 3, k = b >> 3;
-    const int r = hp == 1 ? k : k / fdiv(hp), hd = (b & 7) + 8 * (k - r * hp);
-    const int rN = r / fdiv(F.ntN), gi = rN / fdiv(F.ntM);
-    tN = r - rN * F.ntN;
-    tM = rN - gi * F.ntM;
-    if (hd >= F.nh || gi >= F.ngroups) return;
-    y = gi * F.nh + hd;
-  }
   FwdGroup grp = F.g0;
   if (F.ngroups > 1 && y >= grp.n) { y -= grp.n; grp = F.g1; }
   if (F.ngroups > 2 && y >= grp.n) { y -= grp.n; grp = F.g2; }
   if (F.ngroups > 3 && y >= grp.n) { y -= grp.n; grp = F.g3; }
   const int head = grp.head0 + y;
   const int M = F.M, N = F.N, K = F.K;
-  PROBE_MARKA();
   const float* P = grp.which == P_TARGET ? G.target + (long long)head * G.P
                                          : G.online + G.slot_off(rslot(F.mask, head) ^ (grp.which == P_NEW), head);
   const float* X = F.xOff < 0 ? (grp.xsel == 1 ? F.xa : F.xb) : G.actp(grp.role, head, F.xOff);
@@ -318,7 +352,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
   const float* wr = P + F.wOff + (size_t)n * K;
   // the reducing threads fetch their bias early
   const int Lx = threadIdx.x & 63, col = n0 + (Lx & 15);
-  const float bias = (threadIdx.x < 128 && col < N) ? P[F.bOff + col] : 0.f;
+  const float bias = (threadIdx.x < 128 && col < N) ? ldc<C>(P + F.bOff + col) : 0.f;
   constexpr int AS = L0 ? L0_NMAX + 4 : 4;  // LDS row stride of a0 (padded against bank conflicts)
   __shared__ __align__(16) float sA[L0 ? 32 * AS : 4];
   if constexpr (L0) {
@@ -395,9 +429,15 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
     if constexpr (VEC) {  // K % KW == 0, rows 16-B aligned: KL/4 float4 per operand row
 #pragma unroll
       for (int q = 0; q < KL / 4; ++q) {
-        const float4 ta = oka ? reinterpret_cast<const float4*>(xra + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 tb = okb ? reinterpret_cast<const float4*>(xrb + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 tw = okn ? reinterpret_cast<const float4*>(wr + kb)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 ta, tb;
+        if constexpr (L0) {  // a0 from LDS
+          ta = reinterpret_cast<const float4*>(xra + kb)[q];
+          tb = reinterpret_cast<const float4*>(xrb + kb)[q];
+        } else {
+          ta = oka ? ldc4<C>(xra + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+          tb = okb ? ldc4<C>(xrb + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        const float4 tw = okn ? ldc4<C>(wr + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
         a0[4 * q] = ta.x; a0[4 * q + 1] = ta.y; a0[4 * q + 2] = ta.z; a0[4 * q + 3] = ta.w;
         a1[4 * q] = tb.x; a1[4 * q + 1] = tb.y; a1[4 * q + 2] = tb.z; a1[4 * q + 3] = tb.w;
         bw[4 * q] = tw.x; bw[4 * q + 1] = tw.y; bw[4 * q + 2] = tw.z; bw[4 * q + 3] = tw.w;
@@ -406,9 +446,14 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
 #pragma unroll
       for (int j = 0; j < KL; ++j) {
         const bool kin = kb + j < K;
-        a0[j] = (oka && kin) ? xra[kb + j] : 0.f;
-        a1[j] = (okb && kin) ? xrb[kb + j] : 0.f;
-        bw[j] = (okn && kin) ? wr[kb + j] : 0.f;
+        if constexpr (L0) {
+          a0[j] = (oka && kin) ? xra[kb + j] : 0.f;
+          a1[j] = (okb && kin) ? xrb[kb + j] : 0.f;
+        } else {
+          a0[j] = (oka && kin) ? ldc<C>(xra + kb + j) : 0.f;
+          a1[j] = (okb && kin) ? ldc<C>(xrb + kb + j) : 0.f;
+        }
+        bw[j] = (okn && kin) ? ldc<C>(wr + kb + j) : 0.f;
       }
     }
 #pragma unroll
@@ -431,10 +476,26 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = m0 + 16 * s + (Lx >> 4) * 4 + i;
-        if (row < M) Y[(size_t)row * N + col] = act_fwd(__fadd_rn(v[i], bias), F.act);
+        if (row < M) stc<C>(Y + (size_t)row * N + col, act_fwd(__fadd_rn(v[i], bias), F.act));
       }
     }
   }
+}
+
+template <bool VEC, int NW, bool L0>
+__global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
+  PROBE_T(pt0);
+  int y = blockIdx.y, tN = blockIdx.x, tM = blockIdx.z;
+  if (F.xcd) {  // head h's tiles on the XCD of slot h % 8 (see xcd_decode)
+    const int b = blockIdx.x, hp = (F.nh + 7) >> 3, k = b >> 3;
+    const int r = hp == 1 ? k : k / fdiv(hp), hd = (b & 7) + 8 * (k - r * hp);
+    const int rN = r / fdiv(F.ntN), gi = rN / fdiv(F.ntM);
+    tN = r - rN * F.ntN;
+    tM = rN - gi * F.ntM;
+    if (hd >= F.nh || gi >= F.ngroups) return;
+    y = gi * F.nh + hd;
+  }
+  fwd_tile<VEC, NW, L0, false>(G, F, y, tN, tM);
   if (tN == 0 && tM == 0 && blockIdx.y == 0 && (F.xcd ? blockIdx.x == 0 : true)) {
     if (F.flag && threadIdx.x == 0) *F.flag = F.flag_value;
     if (F.lms_head >= 0) lms_block(G, F);
@@ -616,7 +677,7 @@ struct TdgSmem {
   float dz[32 * TDG_ROWS_O];
 };
 
-template <int VMAX, int U>
+template <int VMAX, int U, bool C>
 __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pub, TdgSmem& sm) {
   const int tid = threadIdx.x, T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, M = A.M;
   const int nb = M - m0 < 32 ? M - m0 : 32;
@@ -739,7 +800,18 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
   __syncthreads();
   if (pub) {
     float4* gout4 = reinterpret_cast<float4*>(G.dzp(pol, NLm) + (size_t)m0 * O);
-    for (int i = tid; i < n4; i += 256) gout4[i] = reinterpret_cast<const float4*>(sm.dz)[i];
+    for (int i = tid; i < n4; i += 256) {
+      const float4 v = reinterpret_cast<const float4*>(sm.dz)[i];
+      if constexpr (C) {
+        float* o = reinterpret_cast<float*>(gout4 + i);
+        stc<true>(o, v.x);
+        stc<true>(o + 1, v.y);
+        stc<true>(o + 2, v.z);
+        stc<true>(o + 3, v.w);
+      } else {
+        gout4[i] = v;
+      }
+    }
     for (int bl = tid; bl < nb; bl += 256) {  // row Σ diff^2 in feature order
       float sacc = 0.f;
       for (int k = 0; k < d; ++k) sacc = __fadd_rn(sacc, sq[bl * d + k]);
@@ -748,7 +820,7 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
   }
 }
 
-template <bool TDG, int VMAX = 2, int U = 8>
+template <bool TDG, int VMAX = 2, int U = 8, bool C = false>
 __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floatx4 (*red)[2][64]) {
   const RoleGeo L = A.ra;
   const int N = L.N, K = L.K, M = A.M;
@@ -776,8 +848,21 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
     __shared__ TdgSmem sm;
     if (tile == 0 && A.inc_step && threadIdx.x == 0) {  // no dW reads them in this launch
       const int st = G.step[head] + 1;
-      G.step[head] = st;
-      G.adamc[head] = adam_consts(A.hp, st);
+      const AdamC ac = adam_consts(A.hp, st);
+      if constexpr (C) {  // read by this launch's dW tiles
+        __hip_atomic_store(G.step + head, st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        float* f = reinterpret_cast<float*>(G.adamc + head);
+        stc<true>(f, ac.omb1);
+        stc<true>(f + 1, ac.b2);
+        stc<true>(f + 2, ac.omb2);
+        stc<true>(f + 3, ac.eps);
+        stc<true>(f + 4, ac.wd);
+        stc<true>(f + 5, ac.bc2s);
+        stc<true>(f + 6, ac.nss);
+      } else {
+        G.step[head] = st;
+        G.adamc[head] = ac;
+      }
     }
     if (A.flag && tile == 0 && head == A.head0 && threadIdx.x == 0) *A.flag = A.flag_value;
     // the 16 k-steps of each 64-wide chunk are split over the waves (4 or 8 steps each); the
@@ -788,7 +873,7 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       bw[j] = (j >= j0 && j < j0 + jw && okk && nb + j < N) ? W[(size_t)(nb + j) * K + kk] : 0.f;
-    tdg_rows<VMAX, U>(G, A, head, m0, tile % ntk == 0, sm);
+    tdg_rows<VMAX, U, C>(G, A, head, m0, tile % ntk == 0, sm);
     const float* da = sm.dz + (size_t)r * N + nb;
     const float* db = sm.dz + (size_t)(16 + r) * N + nb;
 #pragma unroll
@@ -805,8 +890,8 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
     for (int nc = wave * 64; nc < N; nc += 256) {
       const int nb = nc + g * 16;
       float a0[16], a1[16], bw[16];
-      load16u(a0, dZ + (size_t)ma * N, nb, N, oka, vec);
-      load16u(a1, dZ + (size_t)mb * N, nb, N, okb, vec);
+      load16u<C>(a0, dZ + (size_t)ma * N, nb, N, oka, vec);
+      load16u<C>(a1, dZ + (size_t)mb * N, nb, N, okb, vec);
 #pragma unroll
       for (int j = 0; j < 16; ++j) bw[j] = (okk && nb + j < N) ? W[(size_t)(nb + j) * K + kk] : 0.f;
 #pragma unroll
@@ -829,7 +914,7 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = m0 + 16 * s + (Lx >> 4) * 4 + i;
-        if (row < M) out[(size_t)row * K + col] = act_bwd(v[i], xin[i], L.actIn);
+        if (row < M) stc<C>(out + (size_t)row * K + col, act_bwd(v[i], xin[i], L.actIn));
       }
     }
   }
@@ -837,6 +922,7 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
 
 // post-update forward of layer 0 for the 32 output rows this tile just optimised
 // (input rows staged in LDS by role_dw: sX[m * K + k], m < vM)
+template <bool C>
 __device__ void fused_v0(const Geo& G, const BwdArgs& A, const RoleGeo& L, int head, int nbase, const float* sW,
                          const float* sB, const float* sX) {
   __syncthreads();
@@ -861,12 +947,13 @@ __device__ void fused_v0(const Geo& G, const BwdArgs& A, const RoleGeo& L, int h
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = mt * 16 + g * 4 + i;
-        if (m < VM) Y[(size_t)m * N + n] = act_fwd(__fadd_rn(c[i], bias), A.act0);
+        if (m < VM) stc<C>(Y + (size_t)m * N + n, act_fwd(__fadd_rn(c[i], bias), A.act0));
       }
     }
   }
 }
 
+template <bool C = false>
 __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile, bool fuse) {
   const int N = L.N, K = L.K, M = A.M;
   const int ntk = (K + 63) >> 6;
@@ -883,7 +970,7 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
   float* Pw = G.online + wo;
   float* Mw = G.am + wo;
   float* Vw = G.av + wo;
-  const AdamC c = G.adamc[head];  // bias corrections of this step (double pow once per head, not per thread)
+  const AdamC c = load_adamc<C>(G.adamc + head);  // bias corrections of this step (double pow once per head)
   const int nn = n0 + r, kb0 = k0 + r, kb1 = k0 + 16 + r;
   // prefetch the optimizer state of the 8 weights this lane will update
   float pp[8], pm[8], pv[8];
@@ -934,7 +1021,7 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
     for (int j = 0; j < MT / 4; ++j) {
       const int m = mc + 4 * j + g;
       const bool okm = m < M;
-      av[j] = (okm && nn < N) ? dZ[(size_t)m * N + nn] : 0.f;
+      av[j] = (okm && nn < N) ? ldc<C>(dZ + (size_t)m * N + nn) : 0.f;
       bv0[j] = (okm && kb0 < K) ? X[(size_t)m * K + kb0] : 0.f;
       bv1[j] = (okm && kb1 < K) ? X[(size_t)m * K + kb1] : 0.f;
     }
@@ -970,7 +1057,7 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
         const int k = h ? kb1 : kb0;
         const size_t off = (size_t)L.wOff + (size_t)n * K + k;
         adam_apply(pp[e], pm[e], pv[e], h ? acc1[i] : acc0[i], c);
-        Pw[off] = pp[e];
+        stc<C>(Pw + off, pp[e]);
         Mw[off] = pm[e];
         Vw[off] = pv[e];
         if (fuse) sW[(n - nbase) * KFUSE + k] = pp[e];
@@ -979,12 +1066,12 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
   }
   if (dob) {
     adam_apply(bp, bm, bv, bsum, c);
-    Pw[L.bOff + nbias] = bp;
+    stc<C>(Pw + L.bOff + nbias, bp);
     Mw[L.bOff + nbias] = bm;
     Vw[L.bOff + nbias] = bv;
     if (fuse) sB[nbias - nbase] = bp;
   }
-  if (fuse) fused_v0(G, A, L, head, nbase, sW, sB, sX);
+  if (fuse) fused_v0<C>(G, A, L, head, nbase, sW, sB, sX);
 }
 
 // loss finalisation, optional w step, Adam step counter (one workgroup per head)
@@ -1099,6 +1186,105 @@ __global__ __launch_bounds__(256) void k_bwd_tdg(Geo G, BwdArgs A) {
   PROBE_MARKA();
   role_dx<true, VMAX, U>(G, A, head, bx, red);
   PROBE_REC(3, pt0);
+}
+
+// -------------------------------------------------------------------------------------
+// K3+K1' as ONE launch per speculative round (k_round): the whole per-head chain of a round
+//   fused TD target + last dX -> dX ∥ dW ... -> dW1 ∥ dW0 (+ post-update layer 0)
+//   -> post-update forward layers 1 .. NL-1
+// with the arguments the separate launches would get (b[], f[]).  Workgroup w serves head
+// w % T (blocks b and b + 8 share an XCD, so a head's workgroups share an L2) as slot w / T of
+// wph; a head's phases are separated by a per-head arrival counter instead of a kernel
+// boundary.  Every hand-off inside the launch is coherent: producers store sc1 and wait
+// vmcnt(0) in every wave, one lane per workgroup adds to the head's counter, consumers poll
+// it sc1 and read sc1 (ldc/stc, C = true).  Heads never wait on each other inside a round.
+// Residency: T·wph <= 256 workgroups of 256 threads and > 80 KB LDS, one per CU.  Every wait
+// is bounded (timeout ticks of the 100 MHz clock); on expiry *err is set, the launch drains.
+// -------------------------------------------------------------------------------------
+constexpr int RB_MAX = 5, RF_MAX = 4;  // up to 4 hidden Linear layers
+struct RoundArgs {
+  BwdArgs b[RB_MAX];  // b[0]: fused TD + last dX; b[1..nb-2]: dX ∥ dW; b[nb-1]: dW1 ∥ dW0 (+ v0)
+  FwdArgs f[RF_MAX];  // post-update forward of layers 1 .. NL-1
+  int nb, nf, wph, pad_;
+  unsigned* ctr;  // [T] per-head arrivals; zero at launch, returned to zero by each head's last arrival
+  int* err;       // the speculation flag word: set to -1 when a wait times out (the host fails loudly)
+  long long timeout;
+};
+
+__device__ __forceinline__ void head_sync(const RoundArgs& R, unsigned* ctr, unsigned target, bool probe = false) {
+  if (probe) PROBE_AT(6);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have landed
+  __syncthreads();
+  if (probe) PROBE_AT(7);
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const long long t0 = wall_clock64();
+    unsigned it = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if ((++it & 63) == 0 && (wall_clock64() - t0 > R.timeout ||
+                               __hip_atomic_load(R.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0)) {
+        atomicMin(R.err, -1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+
+template <int VMAX, int U, bool FVEC>
+__global__ __launch_bounds__(256) void k_round(Geo G, RoundArgs R) {
+  __shared__ floatx4 red[4][2][64];
+  PROBE_T(pt0);
+  const int T = G.T, head = blockIdx.x % T, slot = blockIdx.x / T, wph = R.wph;
+  unsigned* ctr = R.ctr + head;
+  unsigned target = 0;
+  // phase 0: TD target + output gradient + dX of the last layer
+  for (int t = slot; t < R.b[0].na; t += wph) {
+    role_dx<true, VMAX, U, true>(G, R.b[0], head, t, red);
+    __syncthreads();
+  }
+  target += wph;
+  head_sync(R, ctr, target, true);
+  PROBE_AT(1);
+  // backward phases
+  for (int p = 1; p < R.nb; ++p) {
+    const BwdArgs& A = R.b[p];
+    const int n = A.na + A.nb + A.nc;
+    for (int t = slot; t < n; t += wph) {
+      if (t < A.na)
+        role_dx<false, 2, 8, true>(G, A, head, t, red);
+      else if (t < A.na + A.nb)
+        role_dw<true>(G, A, head, A.rb, t - A.na, false);
+      else
+        role_dw<true>(G, A, head, A.rc, t - A.na - A.nb, A.fuse_v0 != 0);
+      __syncthreads();
+    }
+    target += wph;
+    head_sync(R, ctr, target);
+    if (p < 4) PROBE_AT(1 + p);
+  }
+  // post-update forward (instance = head: one group covering heads 0..T-1)
+  for (int p = 0; p < R.nf; ++p) {
+    const FwdArgs& F = R.f[p];
+    const int n = F.ntN * F.ntM;
+    for (int t = slot; t < n; t += wph) {
+      const int tM = t / F.ntN;
+      fwd_tile<FVEC, 4, false, true>(G, F, head, t - tM * F.ntN, tM);
+      __syncthreads();
+    }
+    if (p + 1 < R.nf) {
+      target += wph;
+      head_sync(R, ctr, target);
+      if (p < 1) PROBE_AT(5 + p);
+    }
+  }
+  // the head's last workgroup to finish returns its counter to zero for the next round
+  __syncthreads();
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == target + wph - 1)
+    __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  PROBE_REC(7, pt0);
 }
 
 // -------------------------------------------------------------------------------------

@@ -18,7 +18,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "deep-successor-features-for-transfer_a
 import numpy as np
 import torch
 
-KIDS = {1: "fwd", 2: "fwdL0", 3: "bwd_tdg", 4: "dx", 5: "dw", 6: "dw_v0", 8: "ver", 9: "gate"}
+KIDS = {1: "fwd", 2: "fwdL0", 3: "bwd_tdg", 4: "dx", 5: "dw", 6: "dw_v0", 7: "round", 8: "ver", 9: "gate"}
 
 
 def main():
@@ -43,8 +43,8 @@ def main():
     loop = NativeEnvLoop(eng, batch=B, seed=1)
     loop.prefill(1000)
     loop.set_task(0)
-    dt = np.dtype([("kid", "<u4"), ("blk", "<u4"), ("t", "<u8", (6,))])
-    buf = np.zeros(1 << 17, dtype=dt)
+    dt = np.dtype([("kid", "<u4"), ("blk", "<u4"), ("t", "<u8", (10,))])
+    buf = np.zeros(1 << 16, dtype=dt)
     loop.run(60)
     torch.cuda.synchronize()
     lib.sfx_probe_dump(buf.ctypes.data, len(buf))
@@ -52,6 +52,8 @@ def main():
     torch.cuda.synchronize()
     n = lib.sfx_probe_dump(buf.ctypes.data, len(buf))
     rec = buf[:n][np.argsort(buf[:n]["t"][:, 0], kind="stable")]
+    if os.environ.get("SFX_PROBE_RAW"):
+        np.save(os.environ["SFX_PROBE_RAW"], rec)
     # cluster into launches (a stream's launches do not overlap)
     launches, start, cur_end = [], 0, 0
     for i in range(len(rec)):
@@ -59,14 +61,14 @@ def main():
         if i > start and t[0] > cur_end:
             launches.append(rec[start:i])
             start, cur_end = i, 0
-        cur_end = max(cur_end, int(t[5]))
+        cur_end = max(cur_end, int(t[9]))
     launches.append(rec[start:])
 
     def marks(L):
         t = L["t"].astype(np.int64)
         rel = (t - t[:, :1]) * 10e-3
-        out = [np.median(rel[:, 5]), rel[:, 5].max()]
-        for j in (1, 2, 3, 4):
+        out = [np.median(rel[:, 9]), rel[:, 9].max()]
+        for j in (1, 2, 3, 4, 5, 6, 7, 8):
             ok = t[:, j] > 0
             out.append(np.median(rel[ok, j]) if ok.any() else np.nan)
         return out
@@ -81,8 +83,8 @@ def main():
         pos += 1
         t = L["t"].astype(np.int64)
         gap = (t[:, 0].min() - prev_end) * 10e-3 if prev_end is not None else np.nan
-        prev_end = t[:, 5].max()
-        row = [(t[:, 0].max() - t[:, 0].min()) * 10e-3, (t[:, 5].max() - t[:, 0].min()) * 10e-3, gap] + marks(L)
+        prev_end = t[:, 9].max()
+        row = [(t[:, 0].max() - t[:, 0].min()) * 10e-3, (t[:, 9].max() - t[:, 0].min()) * 10e-3, gap] + marks(L)
         if key not in agg:
             agg[key], sub[key] = [], {k: [] for k in kinds}
             order.append(key)
@@ -91,9 +93,9 @@ def main():
             for k in kinds:
                 sub[key][k].append([int((L["kid"] == k).sum())] + marks(L[L["kid"] == k]))
     print(f"{n} records, {len(launches)} launches over {steps} steps (us; marks relative to workgroup entry:"
-          " karg = kernel arguments landed, mark = operands landed / MFMA done, m3 / m4 kernel specific)")
+          " m1 = kernel arguments landed, m2 = operands landed / MFMA done, m3 / m4 kernel specific; k_round: m1..m6 after each phase)")
     print(f"{'pos':>3} {'kernel':16s} {'WGs':>5} {'spread':>6} {'span':>6} {'gap':>5} | {'body50':>6} {'bodymx':>6}"
-          f" {'karg':>5} {'mark':>5} {'m3':>5} {'m4':>5}")
+          f" {'m1':>5} {'m2':>5} {'m3':>5} {'m4':>5} {'m5':>5} {'m6':>5} {'m7':>5} {'m8':>5}")
     tot_span = tot_gap = 0.0
     f = lambda x: "    -" if np.isnan(x) else f"{x:5.2f}"
     for key in order:
@@ -105,13 +107,13 @@ def main():
         tot_span += m[1]
         tot_gap += 0 if np.isnan(m[2]) else m[2]
         name = "+".join(KIDS.get(k, str(k)) for k in kinds)
-        print(f"{pos:3d} {name:16s} {nwg:5d} {m[0]:6.2f} {m[1]:6.2f} {f(m[2])} | {m[3]:6.2f} {m[4]:6.2f}"
-              f" {f(m[5])} {f(m[6])} {f(m[7])} {f(m[8])}")
+        print(f"{pos:3d} {name:16s} {nwg:5d} {m[0]:6.2f} {m[1]:6.2f} {f(m[2])} | {m[3]:6.2f} {m[4]:6.2f} "
+              + " ".join(f(x) for x in m[5:13]))
         for k, v in sub[key].items():
             if v:
                 u = np.nanmedian(np.array(v, dtype=float), axis=0)
-                print(f"    {'- ' + KIDS.get(k, str(k)):16s} {int(u[0]):5d} {'':6s} {'':6s} {'':5s} | {u[1]:6.2f} {u[2]:6.2f}"
-                      f" {f(u[3])} {f(u[4])} {f(u[5])} {f(u[6])}")
+                print(f"    {'- ' + KIDS.get(k, str(k)):16s} {int(u[0]):5d} {'':6s} {'':6s} {'':5s} | {u[1]:6.2f} {u[2]:6.2f} "
+                      + " ".join(f(x) for x in u[3:11]))
     print(f"sum span {tot_span:.1f} us, sum gap {tot_gap:.1f} us")
 
 
