@@ -47,6 +47,8 @@ def parse():
                    help="native: libsfx's C++ env-step runner (pipelined graphs); python: sfx.runner.EnvLoop")
     p.add_argument("--heads", type=int, default=8, help="source tasks (ψ heads) per GPU")
     p.add_argument("--batch", type=int, default=32)
+    p.add_argument("--spec-rounds", type=int, default=2,
+                   help="speculative rounds of the all-task step launched on the device (more run from the host)")
     p.add_argument("--prof-steps", type=int, default=50)
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -201,6 +203,7 @@ def main():
         eng.load_w(t, w[t])
     eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
     eng.set_target_update_ev(1000)
+    eng.set_spec_rounds(args.spec_rounds)
     native = args.loop == "native" and args.schedule == "all"
     if native:
         loop = NativeEnvLoop(eng, batch=B, seed=1 + rank)

@@ -981,6 +981,19 @@ int sfx_gpi(sfx_t h, const float* S, int B, const float* w, float* psi, float* q
   });
 }
 
+int sfx_successors(sfx_t h, const float* S, int B, int which, float* psi) {
+  if (!h || !S || !psi || B < 1 || (which != 0 && which != 1)) SFX_FAIL(SFX_E_ARG, "bad args");
+  const GraphKey key = make_key(21, {B, which}, h->mask, {S, psi});
+  return run_graph(h, key, [&]() -> int {
+    for (int row0 = 0; row0 < B; row0 += h->Mmax) {
+      const int m = B - row0 < h->Mmax ? B - row0 : h->Mmax;
+      RC(run_fwd(h, {{R_G, which ? P_TARGET : P_ONLINE, 1, 0, h->T}}, m, S + (size_t)row0 * h->n_s, nullptr));
+      RC(run_gpi(h, gpi_args(R_G, 0, row0, h->w, psi, nullptr, nullptr, nullptr, nullptr, 0, 0, m)));
+    }
+    return SFX_OK;
+  });
+}
+
 int sfx_select_action(sfx_t h, const float* s, int task_index, int use_gpi, float* q, int64_t* out) {
   if (!h || !s || !out || task_index < 0 || task_index >= h->T) SFX_FAIL(SFX_E_ARG, "bad args");
   use_gpi = use_gpi ? 1 : 0;

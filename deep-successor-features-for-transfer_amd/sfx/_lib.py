@@ -34,6 +34,7 @@ SIGNATURES = {
     "sfx_get_w": (_I, [_VP, _I, _FP, _FP, _FP]),
     "sfx_w_ptr": (_I, [_VP, _I, C.POINTER(_VP)]),
     "sfx_gpi": (_I, [_VP, _VP, _I, _VP, _VP, _VP, _VP, _VP]),
+    "sfx_successors": (_I, [_VP, _VP, _I, _I, _VP]),
     "sfx_select_action": (_I, [_VP, _VP, _I, _I, _VP, _VP]),
     "sfx_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP]),
     "sfx_update_all": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _VP]),

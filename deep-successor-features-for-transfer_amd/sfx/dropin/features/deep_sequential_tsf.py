@@ -1,0 +1,146 @@
+"""DeepTSF on the GPU (the interface of features/deep_sequential_tsf.py:9-185, the library of
+main_tsfdqn_sequential_torch.py).
+
+The library of the transformed-successor-feature scripts: per-task ψ heads with an
+Adam-trained reward model ``fit_w[i]`` (nn.Linear(d, 1, bias=False)), per-task g_i and the
+shared h handed in by the agent (agents/tsfdqn_sequential.py), and one optimizer per task over
+{ψ_i, w_i, g_i, h} (build_successor).  The update itself is the agent's
+(TSFDQN.update_successor); here it runs as one libsfx call (sfx_tsf_update: GPI next
+actions, φ̃ = (h(g_i(s)) + h(g_i(s'))) ⊙ φ, TD target on φ̃, l1 + β l2, backward through ψ_i,
+w_i, g_i and h, Adam on all four, target sync).  ``get_next_successors`` (target heads) is
+sfx_successors(which = 1).  g_i / h modules are refreshed from the device by
+``sync_tsf_modules`` (the agent does it before its test episodes).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from features import deep_sequential as _seq
+from utils.torch import update_models_weights
+
+
+def _linear_flat(lin: torch.nn.Linear):
+    return torch.cat([lin.weight.detach().reshape(-1), lin.bias.detach().reshape(-1)]).float().cpu()
+
+
+def _linear_load(lin: torch.nn.Linear, flat):
+    n = lin.weight.numel()
+    with torch.no_grad():
+        lin.weight.copy_(flat[:n].view_as(lin.weight).to(lin.weight.device))
+        lin.bias.copy_(flat[n:n + lin.bias.numel()].view_as(lin.bias).to(lin.bias.device))
+
+
+class DeepTSF(_seq.DeepSF):
+    TSF_MAX_BATCH = 64  # minibatch rows of the TSF kernels (sfx_tsf.h)
+
+    def __init__(self, pytorch_model_handle, *args, target_update_ev=1000, **kwargs):
+        super().__init__(pytorch_model_handle, *args, target_update_ev=target_update_ev, **kwargs)
+        self.max_batch = min(self.max_batch, self.TSF_MAX_BATCH)
+
+    def reset(self):
+        super().reset()
+        self._g = []
+        self._h = None
+        self._tsf_stale = False
+
+    def add_training_task(self, task, source=None, g_function_model={}, h_function_model={}):
+        """features/deep_sequential_tsf.py:40-73 (w first, then the ψ networks and the optimizer)."""
+        self._flush()
+        self._sync_host()
+        if self._eng is not None:
+            raise NotImplementedError("sfx DeepTSF: add every training task before the first update")
+        true_w = task.get_w()
+        n_features = task.feature_dim()
+        fit_w = torch.Tensor(1, n_features).uniform_(-0.01, 0.01).to(self.device)
+        # built on the CPU and moved (see features.deep_sequential.add_training_task)
+        w_approx = torch.nn.Linear(n_features, 1, bias=False).to(self.device)
+        with torch.no_grad():
+            w_approx.weight = torch.nn.Parameter(fit_w)
+        self.true_w.append(true_w)
+        list.append(self.fit_w, w_approx)
+        self._psi.append(self.build_successor(task, source, w_approx, g_function_model, h_function_model))
+        self.n_tasks = len(self._psi)
+        self.gpi_counters = [np.append(c, 0) for c in self.gpi_counters]
+        self.gpi_counters.append(np.zeros((self.n_tasks,), dtype=int))
+        self._g.append(g_function_model)
+        self._h = h_function_model
+
+    def build_successor(self, task, source=None, task_w={}, g_function={}, h_function={}):
+        if self.n_tasks == 0:
+            self.n_actions = task.action_count()
+            self.n_features = task.feature_dim()
+            self.inputs = task.encode_dim()
+        A, d = self.n_actions, self.n_features
+        model, loss, _ = self.pytorch_model_handle(self.inputs, A * d, (A, d), 1)
+        if source is not None and self.n_tasks > 0:
+            self._sync_host()
+            update_models_weights(self._psi[source][0][0], model)
+        hp = self.hyperparameters
+        optim = torch.optim.Adam([
+            {"params": model.parameters(), "lr": hp["learning_rate_sf"], "weight_decay": hp["weight_decay_sf"]},
+            {"params": task_w.parameters(), "lr": hp["learning_rate_w"], "weight_decay": hp["weight_decay_w"]},
+            {"params": g_function.parameters(), "lr": hp["learning_rate_g"], "weight_decay": hp["weight_decay_g"]},
+            {"params": h_function.parameters(), "lr": hp["learning_rate_h"], "weight_decay": hp["weight_decay_h"]},
+        ])
+        target, _, _ = self.pytorch_model_handle(self.inputs, A * d, (A, d), 1)
+        update_models_weights(model, target)
+        self._since.append(0)
+        target.eval()
+        return (model, loss, optim), (target, None, None)
+
+    # ------------------------------------------------------------------ engine
+    def _engine(self, batch: int = 1):
+        fresh = self._eng is None or self._eng_T != self.n_tasks or batch > self._eng.max_batch
+        if fresh and self._eng is not None and self._eng_T > 0:
+            raise NotImplementedError("sfx DeepTSF: the engine cannot be rebuilt once TSF training started")
+        eng = super()._engine(batch)
+        if fresh:
+            g0, h = self._g[0], self._h
+            for g in self._g:
+                if not isinstance(g, torch.nn.Linear) or g.bias is None:
+                    raise NotImplementedError("sfx DeepTSF: g_i must be nn.Linear(n_s, G) with bias")
+            if not isinstance(h, torch.nn.Linear) or h.bias is None or h.out_features != self.n_features:
+                raise NotImplementedError("sfx DeepTSF: h must be nn.Linear(G, d) with bias")
+            hp = self.hyperparameters
+            eng.tsf_setup(g0.out_features, 0, float(hp.get("beta_loss_coefficient", 1.0)), hp["learning_rate_g"],
+                          hp["weight_decay_g"], hp["learning_rate_h"], hp["weight_decay_h"])
+            for t, g in enumerate(self._g):
+                eng.tsf_load_g(t, _linear_flat(g))
+            eng.tsf_load_h(_linear_flat(h))
+        return eng
+
+    def sync_tsf_modules(self):
+        """Copy the device's g_i and h into the agent's modules."""
+        if self._eng is None or not self._tsf_stale:
+            return
+        for t, g in enumerate(self._g):
+            _linear_load(g, self._eng.tsf_get_g(t)[0])
+        _linear_load(self._h, self._eng.tsf_get_h())
+        self._tsf_stale = False
+
+    def tsf_update(self, transitions, policy_index, use_gpi=True, beta=None):
+        """agents/tsfdqn_sequential.py:123-252 (TSFDQN.update_successor) -> (loss, l1, l2)."""
+        states, actions, rs, phis, next_states, gammas = transitions
+        eng = self._engine(len(gammas))
+        if beta is not None and float(beta) != float(self.hyperparameters.get("beta_loss_coefficient", 1.0)):
+            raise NotImplementedError("sfx DeepTSF: the agent's beta_loss_coefficient differs from the library's")
+        self._flush()
+        losses = eng.tsf_update(policy_index, states, actions, rs, phis, next_states, gammas, use_gpi=use_gpi)
+        self._host_stale = True
+        self._tsf_stale = True
+        loss, l1, l2 = (x.to(self._out_device()) for x in losses)
+        return loss, l1, l2
+
+    # ------------------------------------------------------------------ ψ
+    def get_next_successor(self, state, policy_index):
+        return self.get_next_successors(state)[:, policy_index]
+
+    def get_next_successors(self, state):
+        s = self._state(state)
+        eng = self._engine(s.shape[0])
+        self._flush()
+        return eng.successors(s, which=1).to(self._out_device())
+
+    def update_successor(self, transitions, policy_index, use_gpi=True):
+        raise Exception("This function should not be called")

@@ -179,9 +179,14 @@ class SFEngine:
                           nxt.data_ptr()), "sfx_gpi")
         return psi, q, task, nxt
 
-    def successors(self, S) -> torch.Tensor:
-        """get_successors: [B, T, A, d]."""
-        psi, _, _, _ = self.gpi(S, w_index=0, want_psi=True, want_q=False)
+    def successors(self, S, which: int = 0) -> torch.Tensor:
+        """get_successors (which=0, online heads) / get_next_successors (which=1, target heads):
+        [B, T, A, d]."""
+        S = self._f(S)
+        if S.dim() == 1:
+            S = S.reshape(1, -1)
+        psi = torch.empty(S.shape[0], self.T, self.A, self.d, device=self.device)
+        check(lib.sfx_successors(self._h, S.data_ptr(), S.shape[0], int(which), psi.data_ptr()), "sfx_successors")
         return psi
 
     def select_action(self, s, task_index: int, use_gpi: bool = True, q_out: Optional[torch.Tensor] = None):

@@ -98,6 +98,14 @@ int sfx_gpi(sfx_t h, const float* S_dev, int B, const float* w_dev, float* psi_d
             int64_t* task_dev, int64_t* next_dev);
 
 /*
+ * Successor features of every head, online (which = 0: DeepSF.get_successors,
+ * features/deep.py:85-91; features/deep_sequential_tsf.py:150-158) or target (which = 1:
+ * DeepTSF.get_next_successors, features/deep_sequential_tsf.py:160-174; tsfdqn.py:296-307):
+ * psi_dev[b,t,:,:] = ψ_t(S[b]) (ψ⁻_t for which = 1), [B,T,A,d].
+ */
+int sfx_successors(sfx_t h, const float* S_dev, int B, int which, float* psi_dev);
+
+/*
  * Greedy action of Agent.next_sample for one encoded state (sfdqn.py:585-594;
  * agents/sfdqn.py:39-45 + agents/agent.py:144-157 greedy branch):
  *   (q, c) = GPI(s, task_index); c = task_index unless use_gpi; a = argmax_a q[0,c,:].

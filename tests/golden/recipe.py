@@ -173,3 +173,36 @@ def agent_run_sequential(DeepSF, SFDQN, ReplayBuffer, device):
                   encoding="task", epsilon=c["epsilon"], use_gpi=True, test_epsilon=0.03, hyperparameters=c["hp"])
     returns = agent.train(tasks, c["n_samples"], test_tasks=test_tasks, n_test_ev=c["n_test_ev"])
     return agent, tasks, test_tasks, returns
+
+
+# The main_tsfdqn_sequential_torch.py stack: agents/tsfdqn_sequential.py TSFDQN (per-task g_i =
+# Linear(n_s, G), shared h = Linear(G, d), loss l1 + beta l2, ω-weighted test tasks) +
+# agents/buffer_tsf_sequential.py + features/deep_sequential_tsf.py DeepTSF.
+AGENT_RUN_TSF = dict(seed=13, n_s=17, H=32, A=7, d=8, acts=("relu", "relu"), T_tasks=3, lr=1e-3,
+                     hp=dict(learning_rate_sf=1e-3, learning_rate_w=1e-3, learning_rate_g=1e-3, learning_rate_h=1e-3,
+                             learning_rate_omega=1e-3, learning_rate_omega_decay=0.0, weight_decay_sf=0.0,
+                             weight_decay_w=0.0, weight_decay_g=0.0, weight_decay_h=0.0, weight_decay_omega=0.0,
+                             g_h_function_dims=16, beta_loss_coefficient=1.0, omegas_l1_coefficient=0.0),
+                     target_update_ev=5, n_samples=24, n_test_ev=8, episode_T=9, epsilon=0.2, gamma=0.9,
+                     buffer=dict(n_samples=500, n_batch=8), task_terminal_every=7)
+
+
+def agent_run_tsf(DeepTSF, TSFDQN, ReplayBuffer, device):
+    """Build and train the TSF agent of AGENT_RUN_TSF; returns (agent, tasks, test_tasks, returns)."""
+    import random
+
+    import numpy as np
+
+    c = AGENT_RUN_TSF
+    random.seed(c["seed"])
+    np.random.seed(c["seed"])
+    torch.manual_seed(c["seed"])
+    tasks = [AgentTask(c["n_s"], c["A"], c["d"], i, 500 + i, device, c["task_terminal_every"], tensor_reward=True)
+             for i in range(c["T_tasks"])]
+    test_tasks = [AgentTask(c["n_s"], c["A"], c["d"], c["T_tasks"], 600, device, tensor_reward=True)]
+    sf = DeepTSF(pytorch_model_handle=agent_psi_lambda(c["H"], c["acts"], c["lr"], device),
+                 target_update_ev=c["target_update_ev"], hyperparameters=c["hp"])
+    agent = TSFDQN(deep_sf=sf, buffer_handle=lambda: ReplayBuffer(**c["buffer"]), gamma=c["gamma"], T=c["episode_T"],
+                   encoding="task", epsilon=c["epsilon"], use_gpi=True, test_epsilon=0.03, hyperparameters=c["hp"])
+    returns = agent.train(tasks, c["n_samples"], test_tasks=test_tasks, n_test_ev=c["n_test_ev"])
+    return agent, tasks, test_tasks, returns

@@ -72,10 +72,13 @@ def test_sequential_modules_and_buffer(mods):
 
     root = dropin.install()
     import agents.buffer_sequential as bs
+    import agents.buffer_tsf_sequential as bts
     import agents.sfdqn_sequential as ss
+    import agents.tsfdqn_sequential as ts
     import features.deep_sequential as ds
+    import features.deep_sequential_tsf as dts
 
-    for m in (bs, ss, ds):
+    for m in (bs, ss, ds, bts, ts, dts):
         assert m.__file__.startswith(root)
     b = bs.ReplayBuffer(n_samples=4, n_batch=3)
     assert b.replay() is None

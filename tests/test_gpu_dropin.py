@@ -106,6 +106,51 @@ def test_dropin_reproduces_reference_sequential_run(golden):
     rel_close(agent.test_tasks_weights[0][0].weight.detach().reshape(-1).cpu(), g["test_w"], rtol=1e-4, atol=1e-6)
 
 
+def test_dropin_reproduces_reference_tsf_run(golden):
+    """main_tsfdqn_sequential_torch.py's stack (agents.tsfdqn_sequential + agents.buffer_tsf_sequential
+    + features.deep_sequential_tsf) on the drop-in reproduces the real reference's seeded run
+    (tests/golden/run_tsfdqn_sequential_agent.npz): training actions (TSF updates of ψ_i, w_i, g_i
+    and the shared h on the device), ω-weighted test-task actions, GPI counters; ψ / w / g / h
+    within the Adam tolerance."""
+    from sfx import dropin
+
+    dropin.install()
+    import utils.torch as ut
+    from utils.logger import set_logger_level
+
+    ut.set_torch_device(True)
+    set_logger_level(False, quiet=True)
+    from agents.buffer_tsf_sequential import ReplayBuffer
+    from agents.tsfdqn_sequential import TSFDQN
+    from features.deep_sequential_tsf import DeepTSF
+
+    from tests.golden.recipe import agent_run_tsf
+
+    with contextlib.redirect_stdout(io.StringIO()):
+        agent, tasks, test_tasks, returns = agent_run_tsf(DeepTSF, TSFDQN, ReplayBuffer, ut.device)
+    g = golden("run_tsfdqn_sequential_agent")
+    sf = agent.sf
+    assert sf._eng is not None, "the libsfx engine did not run"
+    got = np.array([a for t in tasks for a in t.actions])
+    assert np.array_equal(got, g["actions"]), f"training actions diverge at {np.argmax(got != g['actions'])}"
+    tg = np.array(test_tasks[0].actions)
+    assert np.array_equal(tg, g["test_actions"]), f"test actions diverge at {np.argmax(tg != g['test_actions'])}"
+    assert np.array_equal(np.stack([np.asarray(c) for c in sf.gpi_counters]), g["gpi_counters"])
+    assert list(sf.updates_since_target_updated) == list(g["since_target"])
+    rel_close(torch.tensor([float(r) for r in returns]), g["returns"], rtol=1e-5, atol=1e-6)
+    T = sf.n_tasks
+    k = int(g["total_steps"])
+    params_close(torch.stack([torch.cat([p.detach().reshape(-1).cpu() for p in sf.psi[t][0][0].parameters()])
+                              for t in range(T)]), g["online"], 1e-3 * k)
+    rel_close(torch.stack([sf.fit_w[t].weight.detach().reshape(-1).cpu() for t in range(T)]), g["w"], rtol=1e-3,
+              atol=1e-5)
+    sf.sync_tsf_modules()
+    params_close(torch.stack([torch.cat([p.detach().reshape(-1).cpu() for p in agent.g_functions[t].parameters()])
+                              for t in range(T)]), g["g"], 1e-3 * k)
+    params_close(torch.cat([p.detach().reshape(-1).cpu() for p in agent.h_function.parameters()]), g["h"], 1e-3 * k)
+    rel_close(agent.omegas[0].detach().reshape(-1).cpu(), g["omegas"], rtol=1e-4, atol=1e-6)
+
+
 @pytest.mark.parametrize("case", ["sfdqn_gpi", "sfdqn_nogpi", "sfdqn_tanh"])
 def test_dropin_sequential_deepsf_vs_reference_updates(golden, case):
     """features.deep_sequential.DeepSF (main_sfdqn_sequential_torch.py's library) driven through its

@@ -412,6 +412,38 @@ def gen_agent_run_sequential():
     np.savez_compressed(os.path.join(OUT, "run_sfdqn_sequential_agent.npz"), **rec)
 
 
+def gen_agent_run_tsf():
+    """The main_tsfdqn_sequential_torch.py stack end to end: reference agents/tsfdqn_sequential.py
+    TSFDQN + agents/buffer_tsf_sequential.py + features/deep_sequential_tsf.py DeepTSF."""
+    import contextlib
+    import io
+
+    from agents.buffer_tsf_sequential import ReplayBuffer
+    from agents.tsfdqn_sequential import TSFDQN
+    from features.deep_sequential_tsf import DeepTSF
+    from tests.golden.recipe import agent_run_tsf
+
+    with contextlib.redirect_stdout(io.StringIO()):
+        agent, tasks, test_tasks, returns = agent_run_tsf(DeepTSF, TSFDQN, ReplayBuffer, torch.device("cpu"))
+    sf = agent.sf
+    T = sf.n_tasks
+    tw, _, _ = agent.test_tasks_weights[0]
+    rec = dict(online=np_(torch.stack([flat(sf.psi[t][0][0]) for t in range(T)])),
+               target=np_(torch.stack([flat(sf.psi[t][1][0]) for t in range(T)])),
+               w=np_(torch.stack([sf.fit_w[t].weight.detach().reshape(-1).clone() for t in range(T)])),
+               g=np_(torch.stack([flat(agent.g_functions[t]) for t in range(T)])),
+               h=np_(flat(agent.h_function)),
+               gpi_counters=np.stack([np.asarray(c) for c in sf.gpi_counters]),
+               since_target=np.array(sf.updates_since_target_updated),
+               actions=np.array([a for t in tasks for a in t.actions]),
+               test_actions=np.array(test_tasks[0].actions),
+               test_w=np_(tw.weight.detach().reshape(-1)),
+               omegas=np_(agent.omegas[0].detach().reshape(-1)),
+               returns=np.array([float(r) for r in returns]),
+               cum_reward=float(agent.cum_reward), total_steps=agent.total_training_steps)
+    np.savez_compressed(os.path.join(OUT, "run_tsfdqn_sequential_agent.npz"), **rec)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(4)
@@ -430,6 +462,7 @@ def main():
     gen_tsf("tsf_nf", ref_tsfdqn_nf, SHAPES["hopper11"], 3, 6, 3)
     gen_agent_run()
     gen_agent_run_sequential()
+    gen_agent_run_tsf()
     print("golden vectors written to", os.path.abspath(OUT))
 
 
