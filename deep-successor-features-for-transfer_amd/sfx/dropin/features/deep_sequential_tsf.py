@@ -20,15 +20,33 @@ from features import deep_sequential as _seq
 from utils.torch import update_models_weights
 
 
-def _linear_flat(lin: torch.nn.Linear):
-    return torch.cat([lin.weight.detach().reshape(-1), lin.bias.detach().reshape(-1)]).float().cpu()
+def _g_geometry(g, n_s):
+    """(K, G) of a g_i: nn.Linear(n_s, G) (tsfdqn.py, agents/tsfdqn_sequential.py) or K planar flows
+    (modules with weight [1, n_s], bias [1], scale [1, n_s]) followed by nn.Linear(n_s, G)
+    (tsfdqn_nf.py:331-358); raises for anything else."""
+    mods = list(g) if isinstance(g, torch.nn.Sequential) else [g]
+    *flows, lin = mods
+    ok = isinstance(lin, torch.nn.Linear) and lin.bias is not None and lin.in_features == n_s
+    for f in flows:
+        names = [n for n, _ in f.named_parameters()]
+        ok = ok and names == ["weight", "bias", "scale"] and f.weight.shape == (1, n_s) and f.scale.shape == (1, n_s)
+    if not ok:
+        raise NotImplementedError("sfx DeepTSF: g_i must be nn.Linear(n_s, G) with bias, optionally after planar "
+                                  f"flows (weight, bias, scale); got {g}")
+    return len(flows), lin.out_features
 
 
-def _linear_load(lin: torch.nn.Linear, flat):
-    n = lin.weight.numel()
+def _params_flat(m: torch.nn.Module):
+    """Parameters in registration order (the engine's packing, include/sfx.h sfx_tsf_load_g)."""
+    return torch.cat([p.detach().reshape(-1).float().cpu() for p in m.parameters()])
+
+
+def _params_load(m: torch.nn.Module, flat):
+    off = 0
     with torch.no_grad():
-        lin.weight.copy_(flat[:n].view_as(lin.weight).to(lin.weight.device))
-        lin.bias.copy_(flat[n:n + lin.bias.numel()].view_as(lin.bias).to(lin.bias.device))
+        for p in m.parameters():
+            p.copy_(flat[off:off + p.numel()].view_as(p).to(p.device, p.dtype))
+            off += p.numel()
 
 
 class DeepTSF(_seq.DeepSF):
@@ -96,18 +114,20 @@ class DeepTSF(_seq.DeepSF):
             raise NotImplementedError("sfx DeepTSF: the engine cannot be rebuilt once TSF training started")
         eng = super()._engine(batch)
         if fresh:
-            g0, h = self._g[0], self._h
-            for g in self._g:
-                if not isinstance(g, torch.nn.Linear) or g.bias is None:
-                    raise NotImplementedError("sfx DeepTSF: g_i must be nn.Linear(n_s, G) with bias")
-            if not isinstance(h, torch.nn.Linear) or h.bias is None or h.out_features != self.n_features:
+            h = self._h
+            geos = {_g_geometry(g, self.inputs) for g in self._g}
+            if len(geos) != 1:
+                raise NotImplementedError("sfx DeepTSF: every g_i must have the same shape")
+            (K, G), = geos
+            if not isinstance(h, torch.nn.Linear) or h.bias is None or h.out_features != self.n_features or \
+                    h.in_features != G:
                 raise NotImplementedError("sfx DeepTSF: h must be nn.Linear(G, d) with bias")
             hp = self.hyperparameters
-            eng.tsf_setup(g0.out_features, 0, float(hp.get("beta_loss_coefficient", 1.0)), hp["learning_rate_g"],
+            eng.tsf_setup(G, K, float(hp.get("beta_loss_coefficient", 1.0)), hp["learning_rate_g"],
                           hp["weight_decay_g"], hp["learning_rate_h"], hp["weight_decay_h"])
             for t, g in enumerate(self._g):
-                eng.tsf_load_g(t, _linear_flat(g))
-            eng.tsf_load_h(_linear_flat(h))
+                eng.tsf_load_g(t, _params_flat(g))
+            eng.tsf_load_h(_params_flat(h))
         return eng
 
     def sync_tsf_modules(self):
@@ -115,8 +135,8 @@ class DeepTSF(_seq.DeepSF):
         if self._eng is None or not self._tsf_stale:
             return
         for t, g in enumerate(self._g):
-            _linear_load(g, self._eng.tsf_get_g(t)[0])
-        _linear_load(self._h, self._eng.tsf_get_h())
+            _params_load(g, self._eng.tsf_get_g(t)[0])
+        _params_load(self._h, self._eng.tsf_get_h())
         self._tsf_stale = False
 
     def tsf_update(self, transitions, policy_index, use_gpi=True, beta=None):

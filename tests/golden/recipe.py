@@ -187,20 +187,24 @@ AGENT_RUN_TSF = dict(seed=13, n_s=17, H=32, A=7, d=8, acts=("relu", "relu"), T_t
                      buffer=dict(n_samples=500, n_batch=8), task_terminal_every=7)
 
 
-def agent_run_tsf(DeepTSF, TSFDQN, ReplayBuffer, device):
-    """Build and train the TSF agent of AGENT_RUN_TSF; returns (agent, tasks, test_tasks, returns)."""
+def agent_run_tsf(DeepTSF, TSFDQN, ReplayBuffer, device, nf=False):
+    """Build and train the TSF agent of AGENT_RUN_TSF (nf: tsfdqn_nf.py's planar-flow g_i with
+    n_coupling_layers = 3); returns (agent, tasks, test_tasks, returns)."""
     import random
 
     import numpy as np
 
-    c = AGENT_RUN_TSF
+    c = dict(AGENT_RUN_TSF)
+    if nf:
+        c["hp"] = dict(c["hp"], n_coupling_layers=3)
+        c["seed"] = 17
     random.seed(c["seed"])
     np.random.seed(c["seed"])
     torch.manual_seed(c["seed"])
     tasks = [AgentTask(c["n_s"], c["A"], c["d"], i, 500 + i, device, c["task_terminal_every"], tensor_reward=True)
              for i in range(c["T_tasks"])]
     test_tasks = [AgentTask(c["n_s"], c["A"], c["d"], c["T_tasks"], 600, device, tensor_reward=True)]
-    sf = DeepTSF(pytorch_model_handle=agent_psi_lambda(c["H"], c["acts"], c["lr"], device),
+    sf = DeepTSF(pytorch_model_handle=agent_psi_lambda(c["H"], c["acts"], c["lr"], device), use_true_reward=False,
                  target_update_ev=c["target_update_ev"], hyperparameters=c["hp"])
     agent = TSFDQN(deep_sf=sf, buffer_handle=lambda: ReplayBuffer(**c["buffer"]), gamma=c["gamma"], T=c["episode_T"],
                    encoding="task", epsilon=c["epsilon"], use_gpi=True, test_epsilon=0.03, hyperparameters=c["hp"])

@@ -106,12 +106,14 @@ def test_dropin_reproduces_reference_sequential_run(golden):
     rel_close(agent.test_tasks_weights[0][0].weight.detach().reshape(-1).cpu(), g["test_w"], rtol=1e-4, atol=1e-6)
 
 
-def test_dropin_reproduces_reference_tsf_run(golden):
+@pytest.mark.parametrize("nf", [False, True])
+def test_dropin_reproduces_reference_tsf_run(golden, nf):
     """main_tsfdqn_sequential_torch.py's stack (agents.tsfdqn_sequential + agents.buffer_tsf_sequential
-    + features.deep_sequential_tsf) on the drop-in reproduces the real reference's seeded run
-    (tests/golden/run_tsfdqn_sequential_agent.npz): training actions (TSF updates of ψ_i, w_i, g_i
-    and the shared h on the device), ω-weighted test-task actions, GPI counters; ψ / w / g / h
-    within the Adam tolerance."""
+    + features.deep_sequential_tsf) -- nf: main_tsfdqn_sequential_torch_nf.py's single-file
+    tsfdqn_nf (planar-flow g_i, 3 flows) -- on the drop-in reproduces the real reference's seeded
+    run (tests/golden/run_tsfdqn_sequential_agent.npz / run_tsfdqn_nf_agent.npz): training
+    actions (TSF updates of ψ_i, w_i, g_i and the shared h on the device), ω-weighted test-task
+    actions, GPI counters; ψ / w / g / h within the Adam tolerance."""
     from sfx import dropin
 
     dropin.install()
@@ -120,15 +122,20 @@ def test_dropin_reproduces_reference_tsf_run(golden):
 
     ut.set_torch_device(True)
     set_logger_level(False, quiet=True)
-    from agents.buffer_tsf_sequential import ReplayBuffer
-    from agents.tsfdqn_sequential import TSFDQN
-    from features.deep_sequential_tsf import DeepTSF
+    if nf:
+        from tsfdqn_nf import DeepTSF, ReplayBuffer, TSFDQN
+
+        assert "dropin" in __import__("tsfdqn_nf").__file__
+    else:
+        from agents.buffer_tsf_sequential import ReplayBuffer
+        from agents.tsfdqn_sequential import TSFDQN
+        from features.deep_sequential_tsf import DeepTSF
 
     from tests.golden.recipe import agent_run_tsf
 
     with contextlib.redirect_stdout(io.StringIO()):
-        agent, tasks, test_tasks, returns = agent_run_tsf(DeepTSF, TSFDQN, ReplayBuffer, ut.device)
-    g = golden("run_tsfdqn_sequential_agent")
+        agent, tasks, test_tasks, returns = agent_run_tsf(DeepTSF, TSFDQN, ReplayBuffer, ut.device, nf=nf)
+    g = golden("run_tsfdqn_nf_agent" if nf else "run_tsfdqn_sequential_agent")
     sf = agent.sf
     assert sf._eng is not None, "the libsfx engine did not run"
     got = np.array([a for t in tasks for a in t.actions])

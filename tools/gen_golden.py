@@ -412,19 +412,23 @@ def gen_agent_run_sequential():
     np.savez_compressed(os.path.join(OUT, "run_sfdqn_sequential_agent.npz"), **rec)
 
 
-def gen_agent_run_tsf():
+def gen_agent_run_tsf(nf=False):
     """The main_tsfdqn_sequential_torch.py stack end to end: reference agents/tsfdqn_sequential.py
-    TSFDQN + agents/buffer_tsf_sequential.py + features/deep_sequential_tsf.py DeepTSF."""
+    TSFDQN + agents/buffer_tsf_sequential.py + features/deep_sequential_tsf.py DeepTSF; nf: the
+    single-file tsfdqn_nf.py of main_tsfdqn_sequential_torch_nf.py (planar-flow g_i)."""
     import contextlib
     import io
 
-    from agents.buffer_tsf_sequential import ReplayBuffer
-    from agents.tsfdqn_sequential import TSFDQN
-    from features.deep_sequential_tsf import DeepTSF
     from tests.golden.recipe import agent_run_tsf
 
+    if nf:
+        DeepTSF, TSFDQN, ReplayBuffer = ref_tsfdqn_nf.DeepTSF, ref_tsfdqn_nf.TSFDQN, ref_tsfdqn_nf.ReplayBuffer
+    else:
+        from agents.buffer_tsf_sequential import ReplayBuffer
+        from agents.tsfdqn_sequential import TSFDQN
+        from features.deep_sequential_tsf import DeepTSF
     with contextlib.redirect_stdout(io.StringIO()):
-        agent, tasks, test_tasks, returns = agent_run_tsf(DeepTSF, TSFDQN, ReplayBuffer, torch.device("cpu"))
+        agent, tasks, test_tasks, returns = agent_run_tsf(DeepTSF, TSFDQN, ReplayBuffer, torch.device("cpu"), nf=nf)
     sf = agent.sf
     T = sf.n_tasks
     tw, _, _ = agent.test_tasks_weights[0]
@@ -441,7 +445,12 @@ def gen_agent_run_tsf():
                omegas=np_(agent.omegas[0].detach().reshape(-1)),
                returns=np.array([float(r) for r in returns]),
                cum_reward=float(agent.cum_reward), total_steps=agent.total_training_steps)
-    np.savez_compressed(os.path.join(OUT, "run_tsfdqn_sequential_agent.npz"), **rec)
+    np.savez_compressed(os.path.join(OUT, "run_tsfdqn_nf_agent.npz" if nf else "run_tsfdqn_sequential_agent.npz"),
+                        **rec)
+
+
+def gen_agent_run_tsf_nf():
+    gen_agent_run_tsf(nf=True)
 
 
 def main():
@@ -463,6 +472,7 @@ def main():
     gen_agent_run()
     gen_agent_run_sequential()
     gen_agent_run_tsf()
+    gen_agent_run_tsf_nf()
     print("golden vectors written to", os.path.abspath(OUT))
 
 
