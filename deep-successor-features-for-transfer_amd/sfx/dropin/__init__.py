@@ -3,7 +3,7 @@
 ``install()`` puts this directory first on ``sys.path`` so that the imports of
 main_sfdqn_torch.py -- ``features.deep``, ``agents.sfdqn``, ``agents.buffer``,
 ``utils.torch``, ``utils.config``, ``utils.logger``, ``utils.types``, ``tasks.reacher``; those
-of the sequential SF / TSF scripts and the single-file ``tsfdqn_nf`` --
+of the sequential SF / TSF scripts and the single-file ``sfdqn``, ``tsfdqn``, ``tsfdqn_nf`` --
 resolve to this package's modules, whose ``DeepSF`` runs every ψ / GPI / TD / Adam
 computation in libsfx.so (hand-written gfx950 kernels).  The modules are written for sfx;
 they reproduce the reference's public names, argument meanings, return conventions and
@@ -24,7 +24,7 @@ def install() -> str:
         sys.path.insert(0, ROOT)
     for name in list(sys.modules):
         top = name.split(".")[0]
-        if top in ("features", "agents", "utils", "tasks", "tsfdqn_nf"):
+        if top in ("features", "agents", "utils", "tasks", "sfdqn", "tsfdqn", "tsfdqn_nf"):
             mod = sys.modules[name]
             if not (getattr(mod, "__file__", "") or "").startswith(ROOT):
                 del sys.modules[name]

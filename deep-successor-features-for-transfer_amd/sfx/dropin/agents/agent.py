@@ -92,6 +92,10 @@ class Agent:
                 "cum_reward_hist": self.cum_reward_hist, "GPI%": gpi, "w_err": w_err}
 
     # ---- one env step (agents/agent.py:195-261)
+    def _select_action(self):
+        """Q-values of the current state (GPI), then ε-greedy (agents/agent.py:221-225)."""
+        return self._epsilon_greedy(self.get_Q_values(self.s, self.s_enc))
+
     def next_sample(self, viewer=None, n_view_ev=None):
         if self.new_episode:
             self.s = self.active_task.initialize()
@@ -103,8 +107,7 @@ class Agent:
             self.reward_since_last_episode = 0.0
             if self.episode > 1:
                 self.episode_reward_hist.append(self.episode_reward)
-        q = self.get_Q_values(self.s, self.s_enc)
-        a = self._epsilon_greedy(q)
+        a = self._select_action()
         s1, r, terminal = self.active_task.transition(a)
         s1_enc = self.encoding(s1)
         gamma = 0.0 if terminal else self.gamma

@@ -78,9 +78,11 @@ def test_sequential_modules_and_buffer(mods):
     import features.deep_sequential as ds
     import features.deep_sequential_tsf as dts
 
+    import sfdqn
+    import tsfdqn
     import tsfdqn_nf
 
-    for m in (bs, ss, ds, bts, ts, dts, tsfdqn_nf):
+    for m in (bs, ss, ds, bts, ts, dts, sfdqn, tsfdqn, tsfdqn_nf):
         assert m.__file__.startswith(root)
     b = bs.ReplayBuffer(n_samples=4, n_batch=3)
     assert b.replay() is None

@@ -64,7 +64,8 @@ def test_dropin_reproduces_reference_agent_run(golden):
     rel_close(agent.test_tasks_weights[0].weight.detach().reshape(-1).cpu(), g["test_w"], rtol=1e-4, atol=1e-6)
 
 
-def test_dropin_reproduces_reference_sequential_run(golden):
+@pytest.mark.parametrize("single_file", [False, True])
+def test_dropin_reproduces_reference_sequential_run(golden, single_file):
     """main_sfdqn_sequential_torch.py's stack (agents.sfdqn_sequential + agents.buffer_sequential +
     features.deep_sequential) on the drop-in reproduces the real reference's seeded run
     (tests/golden/run_sfdqn_sequential_agent.npz): training actions (active-task l1 + l2 updates),
@@ -77,16 +78,22 @@ def test_dropin_reproduces_reference_sequential_run(golden):
 
     ut.set_torch_device(True)
     set_logger_level(False, quiet=True)
-    from agents.buffer_sequential import ReplayBuffer
-    from agents.sfdqn_sequential import SFDQN
-    from features.deep_sequential import DeepSF
+    if single_file:  # sfdqn.py: the same stack in one module, ε drawn before GPI
+        from sfdqn import DeepSF, ReplayBuffer, SFDQN
+
+        assert "dropin" in __import__("sfdqn").__file__
+    else:
+        from agents.buffer_sequential import ReplayBuffer
+        from agents.sfdqn_sequential import SFDQN
+        from features.deep_sequential import DeepSF
+
+        assert "dropin" in __import__("agents.sfdqn_sequential").sfdqn_sequential.__file__
 
     from tests.golden.recipe import agent_run_sequential
 
-    assert "dropin" in __import__("agents.sfdqn_sequential").sfdqn_sequential.__file__
     with contextlib.redirect_stdout(io.StringIO()):
         agent, tasks, test_tasks, returns = agent_run_sequential(DeepSF, SFDQN, ReplayBuffer, ut.device)
-    g = golden("run_sfdqn_sequential_agent")
+    g = golden("run_sfdqn_singlefile_agent" if single_file else "run_sfdqn_sequential_agent")
     sf = agent.sf
     assert sf._eng is not None, "the libsfx engine did not run"
     got = np.array([a for t in tasks for a in t.actions])
@@ -106,8 +113,8 @@ def test_dropin_reproduces_reference_sequential_run(golden):
     rel_close(agent.test_tasks_weights[0][0].weight.detach().reshape(-1).cpu(), g["test_w"], rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("nf", [False, True])
-def test_dropin_reproduces_reference_tsf_run(golden, nf):
+@pytest.mark.parametrize("variant", ["sequential", "nf", "singlefile"])
+def test_dropin_reproduces_reference_tsf_run(golden, variant):
     """main_tsfdqn_sequential_torch.py's stack (agents.tsfdqn_sequential + agents.buffer_tsf_sequential
     + features.deep_sequential_tsf) -- nf: main_tsfdqn_sequential_torch_nf.py's single-file
     tsfdqn_nf (planar-flow g_i, 3 flows) -- on the drop-in reproduces the real reference's seeded
@@ -122,10 +129,15 @@ def test_dropin_reproduces_reference_tsf_run(golden, nf):
 
     ut.set_torch_device(True)
     set_logger_level(False, quiet=True)
+    nf = variant == "nf"
     if nf:
         from tsfdqn_nf import DeepTSF, ReplayBuffer, TSFDQN
 
         assert "dropin" in __import__("tsfdqn_nf").__file__
+    elif variant == "singlefile":
+        from tsfdqn import DeepTSF, ReplayBuffer, TSFDQN
+
+        assert "dropin" in __import__("tsfdqn").__file__
     else:
         from agents.buffer_tsf_sequential import ReplayBuffer
         from agents.tsfdqn_sequential import TSFDQN
@@ -135,7 +147,7 @@ def test_dropin_reproduces_reference_tsf_run(golden, nf):
 
     with contextlib.redirect_stdout(io.StringIO()):
         agent, tasks, test_tasks, returns = agent_run_tsf(DeepTSF, TSFDQN, ReplayBuffer, ut.device, nf=nf)
-    g = golden("run_tsfdqn_nf_agent" if nf else "run_tsfdqn_sequential_agent")
+    g = golden(f"run_tsfdqn_{variant}_agent")
     sf = agent.sf
     assert sf._eng is not None, "the libsfx engine did not run"
     got = np.array([a for t in tasks for a in t.actions])

@@ -382,16 +382,21 @@ def gen_agent_run():
     np.savez_compressed(os.path.join(OUT, "run_sfdqn_agent.npz"), **rec)
 
 
-def gen_agent_run_sequential():
+def gen_agent_run_sequential(single_file=False):
     """The main_sfdqn_sequential_torch.py stack end to end: reference agents/sfdqn_sequential.py
-    SFDQN + agents/buffer_sequential.py + features/deep_sequential.py DeepSF."""
+    SFDQN + agents/buffer_sequential.py + features/deep_sequential.py DeepSF; single_file: the
+    same agent from sfdqn.py (its SFDQN, ReplayBuffer and DeepSF)."""
     import contextlib
     import io
 
-    from agents.buffer_sequential import ReplayBuffer
-    from agents.sfdqn_sequential import SFDQN
-    from features.deep_sequential import DeepSF
     from tests.golden.recipe import agent_run_sequential
+
+    if single_file:
+        DeepSF, SFDQN, ReplayBuffer = ref_sfdqn.DeepSF, ref_sfdqn.SFDQN, ref_sfdqn.ReplayBuffer
+    else:
+        from agents.buffer_sequential import ReplayBuffer
+        from agents.sfdqn_sequential import SFDQN
+        from features.deep_sequential import DeepSF
 
     with contextlib.redirect_stdout(io.StringIO()):
         agent, tasks, test_tasks, returns = agent_run_sequential(DeepSF, SFDQN, ReplayBuffer, torch.device("cpu"))
@@ -409,10 +414,15 @@ def gen_agent_run_sequential():
                returns=np.array([float(r) for r in returns]),
                reward_hist=np.array([float(x) for x in agent.reward_hist]),
                cum_reward=float(agent.cum_reward), total_steps=agent.total_training_steps)
-    np.savez_compressed(os.path.join(OUT, "run_sfdqn_sequential_agent.npz"), **rec)
+    np.savez_compressed(os.path.join(OUT, "run_sfdqn_singlefile_agent.npz" if single_file
+                                     else "run_sfdqn_sequential_agent.npz"), **rec)
 
 
-def gen_agent_run_tsf(nf=False):
+def gen_agent_run_singlefile():
+    gen_agent_run_sequential(single_file=True)
+
+
+def gen_agent_run_tsf(nf=False, single_file=False):
     """The main_tsfdqn_sequential_torch.py stack end to end: reference agents/tsfdqn_sequential.py
     TSFDQN + agents/buffer_tsf_sequential.py + features/deep_sequential_tsf.py DeepTSF; nf: the
     single-file tsfdqn_nf.py of main_tsfdqn_sequential_torch_nf.py (planar-flow g_i)."""
@@ -423,6 +433,8 @@ def gen_agent_run_tsf(nf=False):
 
     if nf:
         DeepTSF, TSFDQN, ReplayBuffer = ref_tsfdqn_nf.DeepTSF, ref_tsfdqn_nf.TSFDQN, ref_tsfdqn_nf.ReplayBuffer
+    elif single_file:
+        DeepTSF, TSFDQN, ReplayBuffer = ref_tsfdqn.DeepTSF, ref_tsfdqn.TSFDQN, ref_tsfdqn.ReplayBuffer
     else:
         from agents.buffer_tsf_sequential import ReplayBuffer
         from agents.tsfdqn_sequential import TSFDQN
@@ -445,8 +457,12 @@ def gen_agent_run_tsf(nf=False):
                omegas=np_(agent.omegas[0].detach().reshape(-1)),
                returns=np.array([float(r) for r in returns]),
                cum_reward=float(agent.cum_reward), total_steps=agent.total_training_steps)
-    np.savez_compressed(os.path.join(OUT, "run_tsfdqn_nf_agent.npz" if nf else "run_tsfdqn_sequential_agent.npz"),
-                        **rec)
+    name = "run_tsfdqn_nf_agent" if nf else "run_tsfdqn_singlefile_agent" if single_file else "run_tsfdqn_sequential_agent"
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **rec)
+
+
+def gen_agent_run_tsf_singlefile():
+    gen_agent_run_tsf(single_file=True)
 
 
 def gen_agent_run_tsf_nf():
@@ -471,8 +487,10 @@ def main():
     gen_tsf("tsf_nf", ref_tsfdqn_nf, SHAPES["hopper11"], 3, 6, 3)
     gen_agent_run()
     gen_agent_run_sequential()
+    gen_agent_run_singlefile()
     gen_agent_run_tsf()
     gen_agent_run_tsf_nf()
+    gen_agent_run_tsf_singlefile()
     print("golden vectors written to", os.path.abspath(OUT))
 
 
