@@ -33,8 +33,12 @@ import torch  # noqa: E402
 METRIC = "env steps/sec (whole node), Reacher 8-task SF-DQN at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SHAPE = dict(n_s=17, H=256, A=7, d=8, acts=("relu", "relu"))
+# BASELINE.json configs C3 / C5 (one GPU): Hopper-shape TSF-DQN, |s|=11, 27 actions, d=50, 16 source
+# tasks, g_i / h width 100; K planar layers in g_i for tsfdqn_nf.py (reacher.cfg n_coupling_layers=100)
+TSF_SHAPE = dict(n_s=11, H=256, A=27, d=50, acts=("relu", "relu"), G=100)
+WORKLOADS = {"reacher-sf": None, "hopper-tsf": 0, "hopper-tsf-nf": 100}
 KIND_NAMES = {"fwd": "k_fwd", "tdg": "k_tdg", "bwd": "k_bwd", "gpi": "k_gpi", "lms": "k_lms", "ver": "k_ver",
-              "round": "k_round"}
+              "round": "k_round", "tsf": "k_tsf"}
 
 
 def parse():
@@ -45,7 +49,10 @@ def parse():
     p.add_argument("--schedule", choices=["all", "active"], default="all")
     p.add_argument("--loop", choices=["native", "python"], default="native",
                    help="native: libsfx's C++ env-step runner (pipelined graphs); python: sfx.runner.EnvLoop")
-    p.add_argument("--heads", type=int, default=8, help="source tasks (ψ heads) per GPU")
+    p.add_argument("--workload", choices=list(WORKLOADS), default="reacher-sf",
+                   help="reacher-sf: the metric's workload (C2, default); hopper-tsf / hopper-tsf-nf: BASELINE "
+                        "configs C3 / C5 on one GPU (TSF-DQN, active-task schedule, python host loop)")
+    p.add_argument("--heads", type=int, default=None, help="source tasks (ψ heads) per GPU (8; 16 for hopper-tsf*)")
     p.add_argument("--batch", type=int, default=32)
     p.add_argument("--spec-rounds", type=int, default=2,
                    help="speculative rounds of the all-task step launched on the device (more run from the host)")
@@ -55,7 +62,36 @@ def parse():
     p.add_argument("--shard-steps", type=int, default=400,
                    help="also time the north-star sharded mode (heads split over ranks, RCCL all-reduce-max "
                         "GPI) for this many env steps; 0 skips it")
-    return p.parse_args()
+    args = p.parse_args()
+    args.tsf_K = WORKLOADS[args.workload]
+    if args.heads is None:
+        args.heads = 8 if args.tsf_K is None else 16
+    if args.tsf_K is not None:
+        args.schedule = "tsf"
+    return args
+
+
+def shape_of(args):
+    return SHAPE if args.tsf_K is None else TSF_SHAPE
+
+
+def tsf_problem(T: int, K: int, seed: int):
+    """ψ heads as the reference lambda builds them; g_i = K planar layers (PlanarFlow.reset_parameters,
+    tsfdqn_nf.py:341-345: weight, bias, scale ~ U(-0.01, 0.01)) + nn.Linear(n_s, G); h = nn.Linear(G, d)."""
+    from sfx.init import reference_heads
+
+    sh = TSF_SHAPE
+    online, w = reference_heads(T, sh["n_s"], sh["H"], sh["A"], sh["d"], sh["acts"], seed=seed)
+    gs = []
+    for _ in range(T):
+        parts = []
+        for _k in range(K):
+            parts += [torch.empty(sh["n_s"] + 1 + sh["n_s"]).uniform_(-0.01, 0.01)]
+        lin = torch.nn.Linear(sh["n_s"], sh["G"])
+        parts += [lin.weight.detach().reshape(-1), lin.bias.detach()]
+        gs.append(torch.cat(parts))
+    hl = torch.nn.Linear(sh["G"], sh["d"])
+    return online, w, torch.stack(gs), torch.cat([hl.weight.detach().reshape(-1), hl.bias.detach()])
 
 
 def cpu_baseline(args, seconds: float):
@@ -63,16 +99,23 @@ def cpu_baseline(args, seconds: float):
     oracle/ref_cpu.py) running the same env-step loop on the host cores."""
     from oracle import ref_cpu as R
     from sfx.init import reference_heads
-    from sfx.runner import Replay, SynthReacher
+    from sfx.runner import Replay, SynthHopper, SynthReacher
 
     cores = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count(), os.cpu_count())
     torch.set_num_threads(cores)
     T, B = args.heads, args.batch
-    spec = R.Spec(SHAPE["n_s"], SHAPE["H"], SHAPE["A"], SHAPE["d"], SHAPE["acts"])
-    online, w = reference_heads(T, spec.n_s, spec.H, spec.A, spec.d, spec.acts, seed=0)
-    st = R.SFState(spec, online.clone(), online.clone(), w.clone())
-    rng = np.random.default_rng(1)
-    task = SynthReacher(spec.n_s, spec.A, spec.d, 0, rng)
+    sh = shape_of(args)
+    spec = R.Spec(sh["n_s"], sh["H"], sh["A"], sh["d"], sh["acts"])
+    if args.tsf_K is None:
+        online, w = reference_heads(T, spec.n_s, spec.H, spec.A, spec.d, spec.acts, seed=0)
+        st = R.SFState(spec, online.clone(), online.clone(), w.clone())
+        task = SynthReacher(spec.n_s, spec.A, spec.d, 0, np.random.default_rng(1))
+    else:
+        online, w, g, h = tsf_problem(T, args.tsf_K, seed=0)
+        st = R.TSFState(spec, online.clone(), online.clone(), w.clone(), gspec=R.GSpec(spec.n_s, sh["G"], args.tsf_K),
+                        g=g.clone(), h=h.clone())
+        task = SynthHopper(spec.n_s, spec.A, spec.d, 0, np.random.default_rng(1))
+    rng = task.rng
     rep = Replay(100_000, spec.n_s, spec.d, rng)
     for _ in range(1000):
         s0 = task.initialize()
@@ -87,9 +130,10 @@ def cpu_baseline(args, seconds: float):
             a = R.select_action(q, c[0], 0, True)
             if rng.random() <= 0.1:
                 a = int(rng.integers(spec.A))
-            s1, phi, r, _ = task.transition(a)
-            st.w[0] = R.lms_update(st.w[0].view(-1, 1), torch.from_numpy(phi), torch.tensor(r), 1e-3).view(-1)
-            rep.append(s, a, r, phi, s1, 0.9)
+            s1, phi, r, term = task.transition(a)
+            if args.schedule == "all":
+                st.w[0] = R.lms_update(st.w[0].view(-1, 1), torch.from_numpy(phi), torch.tensor(r), 1e-3).view(-1)
+            rep.append(s, a, r, phi, s1, 0.0 if term else 0.9)
             idx = rng.integers(0, rep.size, B)
             batch = (torch.from_numpy(rep.s[idx]), torch.from_numpy(rep.a[idx]), torch.from_numpy(rep.phi[idx]),
                      torch.from_numpy(rep.s1[idx]), torch.from_numpy(rep.gamma[idx]))
@@ -97,8 +141,11 @@ def cpu_baseline(args, seconds: float):
                 R.deep_all_task_step(st, batch)
             else:
                 b6 = (batch[0], batch[1], torch.from_numpy(rep.r[idx]).view(-1, 1), batch[2], batch[3], batch[4])
-                R.sf_update(st, b6, 0, use_gpi=True)
-            s = s1
+                if args.schedule == "tsf":
+                    R.tsf_update(st, b6, 0, use_gpi=True)
+                else:
+                    R.sf_update(st, b6, 0, use_gpi=True)
+            s = task.initialize() if term else s1
             steps += 1
             el = time.perf_counter() - t0
             if el >= seconds:
@@ -192,11 +239,19 @@ def main():
 
     from sfx.engine import SFEngine
     from sfx.init import reference_heads
-    from sfx.runner import EnvLoop, NativeEnvLoop
+    from sfx.runner import EnvLoop, NativeEnvLoop, SynthHopper, SynthReacher
 
     T, B = args.heads, args.batch
-    eng = SFEngine(T, SHAPE["n_s"], SHAPE["H"], SHAPE["A"], SHAPE["d"], SHAPE["acts"], max_batch=B, device=device)
-    online, w = reference_heads(T, SHAPE["n_s"], SHAPE["H"], SHAPE["A"], SHAPE["d"], SHAPE["acts"], seed=rank)
+    sh = shape_of(args)
+    eng = SFEngine(T, sh["n_s"], sh["H"], sh["A"], sh["d"], sh["acts"], max_batch=B, device=device)
+    if args.tsf_K is None:
+        online, w = reference_heads(T, sh["n_s"], sh["H"], sh["A"], sh["d"], sh["acts"], seed=rank)
+    else:
+        online, w, g, h = tsf_problem(T, args.tsf_K, seed=rank)
+        eng.tsf_setup(sh["G"], args.tsf_K, 1.0, 1e-3, 0.0, 1e-3, 0.0)
+        for t in range(T):
+            eng.tsf_load_g(t, g[t])
+        eng.tsf_load_h(h)
     for t in range(T):
         eng.load_head(t, online[t], 0)
         eng.load_head(t, online[t], 1)
@@ -210,7 +265,8 @@ def main():
         loop.prefill(1000)
         loop.set_task(0)
     else:
-        loop = EnvLoop(eng, schedule=args.schedule, batch=B, seed=1 + rank)
+        task_cls = SynthReacher if args.tsf_K is None else SynthHopper
+        loop = EnvLoop(eng, schedule=args.schedule, batch=B, seed=1 + rank, task_cls=task_cls)
         loop.prefill(1000)
 
     def barrier():
@@ -243,7 +299,8 @@ def main():
     if args.shard_steps > 0 and args.schedule == "all":
         sharded = bench_sharded(args, world, rank, device, barrier, dist)
 
-    workload = f"reacher17-{args.schedule}-T{T}-B{B}"
+    workload = (f"reacher17-{args.schedule}-T{T}-B{B}" if args.tsf_K is None else
+                f"hopper11-tsf{'-nf' + str(args.tsf_K) if args.tsf_K else ''}-T{T}-B{B}")
     if rank == 0:
         kind = max(stats, key=lambda k: stats[k][1])
         n, us, by = stats[kind]
@@ -267,11 +324,17 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, args.cpu_seconds)
         out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "env steps/s", "n_gpus": world, "steps": args.steps,
+            "metric": METRIC if args.tsf_K is None else
+                      f"env steps/sec, Hopper 16-task TSF-DQN{' + planar-flow g' if args.tsf_K else ''} (BASELINE config "
+                      f"{'C5' if args.tsf_K else 'C3'}, one GPU)", "value": round(value, 2), "unit": "env steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000.0 * dt / args.steps, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-            "config": {"workload": workload + f" (Reacher-shape |s|=17 |a|=7 d=8, psi MLP 256x2, "
-                                               f"{'all heads updated per env step: main_sfdqn_torch.py path' if args.schedule == 'all' else 'active head only: sfdqn.py path'})",
+            "config": {"workload": workload + (f" (Reacher-shape |s|=17 |a|=7 d=8, psi MLP 256x2, "
+                                               f"{'all heads updated per env step: main_sfdqn_torch.py path' if args.schedule == 'all' else 'active head only: sfdqn.py path'})"
+                                               if args.tsf_K is None else
+                                               f" (Hopper-shape |s|=11 |a|=27 d=50, psi MLP 256x2, g/h width 100, "
+                                               f"{args.tsf_K} planar layers, active head only: "
+                                               f"{'tsfdqn_nf.py' if args.tsf_K else 'tsfdqn.py'} path)"),
                        "heads_per_gpu": T, "global_batch": B * world, "parallelism": f"replica{world}" if world > 1 else "single",
                        "loop": ("native C++ runner (sfx_runner_run): host env + replay, one pre-launched gated hipGraph per env step"
                                 if native else "python host loop over libsfx graphs")},

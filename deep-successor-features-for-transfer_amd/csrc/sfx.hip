@@ -177,7 +177,7 @@ void clear_graphs(sfx_handle* h) {
   h->graphs.clear();
 }
 
-enum { K_FWD = 0, K_TDG = 1, K_BWD = 2, K_GPI = 3, K_LMS = 4, K_VER = 5, K_ROUND = 6, K_NKIND = 7 };
+enum { K_FWD = 0, K_TDG = 1, K_BWD = 2, K_GPI = 3, K_LMS = 4, K_VER = 5, K_ROUND = 6, K_TSF = 7, K_NKIND = 8 };
 
 hipEvent_t prof_event(sfx_handle* h) {
   if (!h->prof_pool.empty()) {

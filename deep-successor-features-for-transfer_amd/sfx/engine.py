@@ -138,7 +138,7 @@ class SFEngine:
     def sync_target(self, t: int):
         check(lib.sfx_sync_target(self._h, t), "sfx_sync_target")
 
-    KINDS = {"fwd": 0, "tdg": 1, "bwd": 2, "gpi": 3, "lms": 4, "ver": 5, "round": 6}
+    KINDS = {"fwd": 0, "tdg": 1, "bwd": 2, "gpi": 3, "lms": 4, "ver": 5, "round": 6, "tsf": 7}
 
     def prof_enable(self, on: bool):
         check(lib.sfx_prof_enable(self._h, int(bool(on))), "sfx_prof_enable")

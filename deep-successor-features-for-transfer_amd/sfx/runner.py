@@ -8,6 +8,9 @@ schedules the reference has:
               actions, loss = l1.
   * "active": sfdqn.py:462-471 / agents/sfdqn_sequential.py:63-76: only the active head is
               updated (with l2 + Adam-trained w), next actions by GPI or own ψ (use_gpi).
+  * "tsf":    tsfdqn.py:566-580 / tsfdqn_nf.py:598-612: only the active head is updated, by
+              TSFDQN.update_successor (φ̃ from g_i and the shared h; the engine must have
+              been set up with SFEngine.tsf_setup).
 
 The environment is a synthetic Reacher-shape task: s ~ N(0,1)^n_s,
 φ ~ U[0,1)^d, r = φ·w_true with one-hot w_true (tasks/reacher.py:85-88), γ constant,
@@ -39,6 +42,20 @@ class SynthReacher:
         phi = self.rng.random(self.d, dtype=np.float32)
         r = float(phi @ self.w_true)
         return s1, phi, r, False
+
+
+class SynthHopper(SynthReacher):
+    """Synthetic Hopper-shape task (BASELINE config C3: |s|=11, 27 actions, d=50): like
+    SynthReacher, but an episode ends with probability `p_end` per step (γ = 0 then), the
+    way tasks/hopper_phi.py's falls do."""
+
+    def __init__(self, n_s: int, A: int, d: int, task_index: int, rng: np.random.Generator, p_end: float = 0.01):
+        super().__init__(n_s, A, d, task_index, rng)
+        self.p_end = p_end
+
+    def transition(self, a: int):
+        s1, phi, r, _ = super().transition(a)
+        return s1, phi, r, bool(self.rng.random() < self.p_end)
 
 
 class Staging:
@@ -104,13 +121,13 @@ class EnvLoop:
 
     def __init__(self, engine: SFEngine, schedule: str = "all", batch: int = 32, capacity: int = 1_000_000,
                  gamma: float = 0.9, epsilon: float = 0.1, alpha_w: float = 1e-3, episode_len: int = 500,
-                 use_gpi: bool = True, seed: int = 1):
-        assert schedule in ("all", "active")
+                 use_gpi: bool = True, seed: int = 1, task_cls=SynthReacher):
+        assert schedule in ("all", "active", "tsf")
         self.eng, self.schedule, self.B = engine, schedule, batch
         self.gamma, self.epsilon, self.alpha_w, self.T_ep, self.use_gpi = gamma, epsilon, alpha_w, episode_len, use_gpi
         e = engine
         self.rng = np.random.default_rng(seed)
-        self.tasks = [SynthReacher(e.n_s, e.A, e.d, t, self.rng) for t in range(e.T)]
+        self.tasks = [task_cls(e.n_s, e.A, e.d, t, self.rng) for t in range(e.T)]
         self.replay = Replay(capacity, e.n_s, e.d, self.rng)
         self.st = Staging([("s", (batch, e.n_s), torch.float32), ("s1", (batch, e.n_s), torch.float32),
                            ("phi", (batch, e.d), torch.float32), ("r", (batch,), torch.float32),
@@ -192,9 +209,10 @@ class EnvLoop:
             c, a, _ = e.step_finish()
             self.sel = (c, a)
         else:
+            upd = e.tsf_update if self.schedule == "tsf" else e.update
             if have:
-                e.update(self.task_index, d["s"], d["a"], d["r"], d["phi"], d["s1"], d["gamma"], self.use_gpi,
-                         losses=self.losses[0])
+                upd(self.task_index, d["s"], d["a"], d["r"], d["phi"], d["s1"], d["gamma"], self.use_gpi,
+                    losses=self.losses[0])
             self._issue_select()
         self.s = s_next
 

@@ -180,7 +180,8 @@ int sfx_sync_target(sfx_t h, int t);
 /*
  * Event instrumentation for the benchmark's roofline figure: while enabled, graphs are
  * bypassed and every kernel launch is bracketed by a hipEvent pair.  Kinds:
- * 0 forward, 1 TD target, 2 backward+Adam, 3 GPI, 4 LMS, 5 speculation check.  collect() returns the number of
+ * 0 forward, 1 TD target, 2 backward+Adam, 3 GPI, 4 LMS, 5 speculation check, 6 persistent
+ * round (k_round), 7 TSF transform (k_tsf_fwd / k_tsf_bwd).  collect() returns the number of
  * launches of that kind, their summed event-measured duration (us) and their summed
  * ALGORITHMIC bytes (what the launch must read/write at minimum, fp32).
  */
@@ -190,6 +191,8 @@ int sfx_sync_target(sfx_t h, int t);
 #define SFX_K_GPI 3
 #define SFX_K_LMS 4
 #define SFX_K_VER 5
+#define SFX_K_ROUND 6
+#define SFX_K_TSF 7
 int sfx_prof_enable(sfx_t h, int enable);
 int sfx_prof_collect(sfx_t h, int kind, int* count, double* total_us, double* bytes);
 int sfx_prof_reset(sfx_t h);

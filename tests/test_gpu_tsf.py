@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 import torch
 
+from oracle import ref_cpu as R
 from tests.conftest import gpu_available
 from tests.test_gpu_engine import batches_of, params_close, rel_close, spec_of
 
@@ -44,4 +45,58 @@ def test_tsf_update_vs_golden(golden, case):
     rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), g["w"], rtol=1e-3, atol=1e-6)
     params_close(torch.stack([eng.tsf_get_g(t)[0] for t in range(T)]), g["g"], 1e-3 * k)
     params_close(eng.tsf_get_h(), g["h"], 1e-3 * k)
+    eng.close()
+
+
+def tsf_c3_problem(T, K, seed=0):
+    """Full BASELINE config C3 shape (Hopper: |s|=11, 27 actions, d=50, ψ 256x2, g/h width 100)
+    with reference-initialised ψ heads (sfx.init) and random g_i / h; weights are seeded."""
+    from sfx.init import reference_heads
+
+    spec = R.Spec(11, 256, 27, 50, ("relu", "relu"))
+    gs = R.GSpec(spec.n_s, 100, K)
+    online, w = reference_heads(T, spec.n_s, spec.H, spec.A, spec.d, spec.acts, seed=seed)
+    gen = torch.Generator().manual_seed(seed + 7)
+    g = torch.empty(T, gs.P).uniform_(-0.3, 0.3, generator=gen)
+    h = torch.empty(spec.d * gs.G + spec.d).uniform_(-0.1, 0.1, generator=gen)
+    st = R.TSFState(spec, online.clone(), online.clone(), w.clone(), gspec=gs, g=g.clone(), h=h.clone())
+    return spec, gs, st
+
+
+@pytest.mark.parametrize("K", [0, 100])
+def test_tsf_full_c3_vs_oracle(K):
+    """Config C3/C5 geometry at full size (T=16 heads, H=256, A=27, d=50, G=100; K=100 planar
+    layers for the NF variant): losses, GPI next actions (exact) and every parameter group
+    after 4 updates of different policies vs the CPU oracle's tsf_update."""
+    from sfx.engine import SFEngine
+
+    T, B = 16, 32
+    spec, gs, st = tsf_c3_problem(T, K)
+    eng = SFEngine(T, spec.n_s, spec.H, spec.A, spec.d, spec.acts, max_batch=B)
+    eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
+    eng.set_target_update_ev(1000)
+    eng.tsf_setup(gs.G, K, 1.0, 1e-3, 0.0, 1e-3, 0.0)
+    for t in range(T):
+        eng.load_head(t, st.online[t], 0)
+        eng.load_head(t, st.target[t], 1)
+        eng.load_w(t, st.w[t])
+        eng.tsf_load_g(t, st.g[t])
+    eng.tsf_load_h(st.h)
+    gen = torch.Generator().manual_seed(3)
+    nxt = torch.empty(B, dtype=torch.int64, device="cuda")
+    for j, i in enumerate((0, 5, 15, 5)):
+        s, s1 = torch.randn(B, spec.n_s, generator=gen), torch.randn(B, spec.n_s, generator=gen)
+        a = torch.randint(0, spec.A, (B,), generator=gen)
+        phi = torch.rand(B, spec.d, generator=gen)
+        r = torch.rand(B, 1, generator=gen)
+        gamma = torch.where(torch.rand(B, generator=gen) < 0.01, 0.0, 0.9)
+        loss, l1, l2, na = R.tsf_update(st, (s, a, r, phi, s1, gamma), i, use_gpi=True)
+        lo = eng.tsf_update(i, s, a, r, phi, s1, gamma, use_gpi=True, next_actions=nxt)
+        assert torch.equal(nxt.cpu(), na), f"update {j}: GPI next actions differ"
+        rel_close(lo, [float(loss), float(l1), float(l2)], rtol=2e-4, atol=1e-7)
+    for t in (0, 5, 15):
+        params_close(eng.get_head(t, 0), st.online[t], 4e-3)
+        params_close(eng.tsf_get_g(t)[0], st.g[t], 4e-3)
+        rel_close(eng.get_w(t)[0], st.w[t], rtol=1e-3, atol=1e-6)
+    params_close(eng.tsf_get_h(), st.h, 4e-3)
     eng.close()
