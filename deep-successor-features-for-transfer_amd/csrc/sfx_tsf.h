@@ -7,21 +7,43 @@
 // which replace φ in the TD target (t = φ̃ + γ ψ⁻_i(s1)[a'], so l1 trains g_i and h too) and in
 // l2 = MSE(w_i·φ̃, r); loss = l1 + β l2 and one Adam step over {ψ_i, w_i, g_i, h}.
 //
-// The ψ part runs through the SF-DQN kernels with φ̃ as the features; these two single-
-// workgroup kernels do the rest: k_tsf_fwd (φ̃ and the saved activations) before the TD
-// target, k_tsf_bwd (w_i, g_i, h gradients + Adam, l2) after the ψ backward.
-// Limits (checked by sfx_tsf_setup): n_s <= 32, B <= 64, d*G <= 8192, 2B*G <= 8192,
-// B*d <= 4096, B*G <= 4096, K(2 n_s + 1) + G(n_s + 1) <= 4096.
+// The ψ part runs through the SF-DQN kernels with φ̃ as the features; these kernels do the rest:
+//   k_tsf_fwd<LPR>  before the TD target: φ̃, the saved flow states / tanh outputs / g features,
+//                   and a snapshot of g_i, h, w_i as they were before the step.  A workgroup
+//                   owns PB batch indices (their s and s1 rows); a row's planar-flow chain runs
+//                   on LPR lanes (one state component per lane, butterfly reduction of w_k·z).
+//   k_tsf_bwd<LPR>  after the ψ backward, one launch of four workgroup roles that all read the
+//                   snapshot (so no role sees another's Adam writes):
+//                     flow rows  FR rows each: dg, then the reverse flow chain on LPR lanes per
+//                                row with the flow states staged in LDS; each row's terms of the
+//                                flow-parameter gradients into `part`
+//                     h          256 parameters of the shared h each: gradient + Adam
+//                     g-Linear   TSF_QS output columns of g_i's Linear each: dg, gradient + Adam
+//                     w          l2, the w_i gradient + Adam, the loss row
+//   k_tsf_flow      flow parameters: sum of the per-row terms (fixed order) + Adam (K > 0).
+// Limits (checked by sfx_tsf_setup, see tsf_geometry_ok): n_s <= 32, B <= 64, d*G <= 8192,
+// 2B*G <= 8192, B*d <= 4096, K(2 n_s + 1) + G(n_s + 1) <= 4096, and the flow-row staging
+// FR*(K+1)*n_s <= TSF_ZS, FR*K <= TSF_TS, FR*G <= 2048, FR*d <= 2048.
 #pragma once
 
 namespace sfx {
 
-constexpr int TSF_NS = 32;     // max n_s (flow state in registers)
+constexpr int TSF_NS = 32;     // max n_s (one lane per state component, LPR <= 32)
 constexpr int TSF_LDS = 8192;  // floats per staged operand (flows, W_h, g features)
+constexpr int TSF_ZS = 12288;  // flow states staged per flow-row workgroup: FR x (K+1) x n_s
+constexpr int TSF_TS = 1024;   // tanh outputs staged per flow-row workgroup: FR x K
+constexpr int TSF_QS = 16;     // g-Linear output columns per backward workgroup
+constexpr int TSF_SM = TSF_ZS + TSF_TS + TSF_LDS / 2 + TSF_LDS + 2048 + 2048;  // k_tsf_bwd LDS (floats)
+
+// lanes per flow row and the row groups they imply (256-thread workgroups)
+__host__ __device__ constexpr int tsf_lpr(int n_s) { return n_s <= 16 ? 16 : 32; }
+__host__ __device__ constexpr int tsf_rpw(int lpr) { return 256 / lpr; }  // forward rows per WG
+__host__ __device__ constexpr int tsf_fr(int lpr) { return 128 / lpr; }   // backward flow rows per WG
 
 struct TsfArgs {
   int pol, B, n_s, G, K, d, Pg, Ph, O, lastOff;
   float beta;
+  int nflow, nh, nlin, pad_;  // k_tsf_bwd roles: flow-row / h / g-Linear workgroups, then one w workgroup
   const float* S;
   const float* S1;
   const float* phi;
@@ -37,11 +59,12 @@ struct TsfArgs {
   float* ts;     // [K][2B] tanh outputs
   float* gfeat;  // [2B][G]
   float* tphi;   // [B][d]
-  float* part;   // [K][2B][2n_s+1] per-row flow-parameter gradients
+  float* part;   // [K][2B][2n_s+1] per-row flow-parameter gradient terms
+  float* snap;   // [Pg + Ph + d]: g_i, h, w_i before this step (written by k_tsf_fwd)
   float* losses; // [3]: [1] = l1 (written by the ψ tail); [0], [2] written here
   const float* dzlast;  // output gradient of the policy's ψ head [B][O] (written by K2)
   const int* step;      // Adam step of the policy (already bumped by the ψ path)
-  float* w;             // [d] reward weights of the policy (+ moments)
+  float* w;             // [d] reward weights of the policy (+ moments; its global row when sharded)
   float* wm;
   float* wv;
   AdamHP hpw, hpg, hph;
@@ -49,222 +72,378 @@ struct TsfArgs {
 
 __device__ __forceinline__ int tsf_flow_stride(int n_s) { return 2 * n_s + 1; }
 
-__global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A) {
-  __shared__ float s_fl[TSF_LDS];  // flow parameters, then the Linear of g
-  __shared__ float s_wh[TSF_LDS];  // W_h
-  __shared__ float s_gf[TSF_LDS];  // g features of the 2B rows
-  __shared__ float s_z[4 * TSF_NS * 32];
-  const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
-  const int fs = tsf_flow_stride(n_s), nfl = K * fs, nlin = G * n_s + G;
-  const float* gp = A.g + (long long)A.pol * A.Pg;
-  for (int j = tid; j < nfl + nlin; j += 256) s_fl[j] = gp[j];
-  for (int j = tid; j < d * G; j += 256) s_wh[j] = A.hp[j];
-  __syncthreads();
-  // planar flows, one thread per row (state in registers); save z_k and t_k for the backward
-  for (int row = tid; row < R2; row += 256) {
-    const float* x = row < B ? A.S + (size_t)row * n_s : A.S1 + (size_t)(row - B) * n_s;
-    float z[TSF_NS];
-#pragma unroll
-    for (int i = 0; i < TSF_NS; ++i) z[i] = i < n_s ? x[i] : 0.f;
-    for (int k = 0; k < K; ++k) {
-      const float* f = s_fl + k * fs;
-      float acc = 0.f;
-#pragma unroll
-      for (int i = 0; i < TSF_NS; ++i)
-        if (i < n_s) acc = __builtin_fmaf(z[i], f[i], acc);
-      const float t = tanhf(__fadd_rn(acc, f[n_s]));
-      float* zk = A.zs + ((size_t)k * R2 + row) * n_s;
-#pragma unroll
-      for (int i = 0; i < TSF_NS; ++i)
-        if (i < n_s) {
-          zk[i] = z[i];
-          z[i] = __fadd_rn(z[i], __fmul_rn(f[n_s + 1 + i], t));
-        }
-      A.ts[(size_t)k * R2 + row] = t;
-    }
-    float* zK = A.zs + ((size_t)K * R2 + row) * n_s;
-#pragma unroll
-    for (int i = 0; i < TSF_NS; ++i)
-      if (i < n_s) {
-        zK[i] = z[i];
-        s_z[row * n_s + i] = z[i];
-      }
+// Sum over a flow row's LPR lanes, the same value in every lane: quad_perm xor 1, xor 2,
+// row_half_mirror, row_mirror (DPP, no LDS round trip; each step pairs lanes symmetrically so
+// every lane adds the same two partials), then xor 16 across the two DPP rows when LPR = 32.
+template <int LPR>
+__device__ __forceinline__ float tsf_row_sum(float v) {
+#define SFX_DPP_ADD(ctrl) \
+  v = __fadd_rn(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xF, 0xF, false)))
+  SFX_DPP_ADD(0xB1);   // quad_perm [1,0,3,2]
+  SFX_DPP_ADD(0x4E);   // quad_perm [2,3,0,1]
+  SFX_DPP_ADD(0x141);  // row_half_mirror
+  SFX_DPP_ADD(0x140);  // row_mirror
+#undef SFX_DPP_ADD
+  if (LPR == 32) v = __fadd_rn(v, __shfl_xor(v, 16, 32));
+  return v;
+}
+
+// Rows [r0, r0 + n) of the minibatch, staged in LDS for the backward roles (every global read
+// is issued here, before any dependent arithmetic): φ̃ and φ rows, the taken action's row of the
+// ψ output gradient, r and the pre-step w_i; then dr_b = β (2/B) (w·φ̃_b − r_b) and
+//   daff[b][c] = (−∂l1/∂t[b][c] + dr_b w_c) φ[b][c]
+// (the gradient reaching h's output through the TD targets and through w·φ̃).  Returns this
+// thread's share of Σ_b (w·φ̃_b − r_b)² (l2 numerator; rows r0.. only).  Rows are batch indices
+// (`bmap` maps a local row to its batch index).  Ends with a barrier.
+template <class BMap>
+__device__ float tsf_stage_daff(const TsfArgs& A, int n, BMap bmap, float* s_tp, float* s_da, float* s_dr,
+                                float* s_w, float* s_r, int* s_ab) {
+  const int tid = threadIdx.x, d = A.d, O = A.O;
+  const float* wold = A.snap + A.Pg + A.Ph;
+  const FDiv fd = fdiv(d);
+  if (tid < d) s_w[tid] = wold[tid];
+  if (tid < n) {
+    const int b = bmap(tid);
+    s_r[tid] = A.r[b];
+    s_ab[tid] = (int)A.a[b];
+  }
+  for (int j = tid; j < n * d; j += 256) {
+    const int rl = j / fd, c = j - rl * d, b = bmap(rl);
+    s_tp[j] = A.tphi[(size_t)b * d + c];
+    s_da[j] = A.phi[(size_t)b * d + c];
   }
   __syncthreads();
-  // Linear(n_s, G) of g
+  float se = 0.f;
+  const float bnorm = __fmul_rn(A.beta, (float)(2.0 / (double)A.B));
+  if (tid < n) {
+    float rf = 0.f;
+    for (int j = 0; j < d; ++j) rf = __builtin_fmaf(s_tp[tid * d + j], s_w[j], rf);
+    const float e = __fsub_rn(rf, s_r[tid]);
+    se = __fmul_rn(e, e);
+    s_dr[tid] = __fmul_rn(bnorm, e);
+  }
+  __syncthreads();
+  for (int j = tid; j < n * d; j += 256) {
+    const int rl = j / fd, c = j - rl * d, b = bmap(rl), ab = s_ab[rl];
+    const float gc = (ab >= 0 && ab * d < O) ? A.dzlast[(size_t)b * O + ab * d + c] : 0.f;
+    const float dt = __fadd_rn(-gc, __fmul_rn(s_dr[rl], s_w[c]));
+    s_da[j] = __fmul_rn(dt, s_da[j]);
+  }
+  __syncthreads();
+  return se;
+}
+
+// grid cdiv(B, PB), 256 threads; PB = RPW / 2 batch indices (their s rows and s1 rows) per WG.
+template <int LPR>
+__global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A) {
+  constexpr int RPW = tsf_rpw(LPR), PB = RPW / 2;
+  __shared__ float s_fl[TSF_LDS / 2];  // flows, then the Linear of g
+  __shared__ float s_wh[TSF_LDS];      // W_h
+  __shared__ float s_gf[TSF_LDS / 2];  // g features of this workgroup's rows [RPW][G]
+  __shared__ float s_z[RPW * TSF_NS];  // z_K of this workgroup's rows
+  const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
+  const int fs = tsf_flow_stride(n_s), nfl = K * fs, nlin = G * n_s + G;
+  const int b0 = blockIdx.x * PB;
+  PROBE_T(t0_);
+  const float* gp = A.g + (long long)A.pol * A.Pg;
+  {  // this workgroup's slice of the pre-step snapshot of g_i, h, w_i (read by k_tsf_bwd)
+    const int S = A.Pg + A.Ph + d, per = (S + gridDim.x - 1) / gridDim.x;
+    const int lo = blockIdx.x * per, hi = min(S, lo + per);
+    for (int j = lo + tid; j < hi; j += 256)
+      A.snap[j] = j < A.Pg ? gp[j] : (j < A.Pg + A.Ph ? A.hp[j - A.Pg] : A.w[j - A.Pg - A.Ph]);
+  }
+  for (int j = tid; j < nfl + nlin; j += 256) s_fl[j] = gp[j];
+  for (int j = tid; j < d * G; j += 256) s_wh[j] = A.hp[j];
+  const int rl = tid / LPR, li = tid - rl * LPR;
+  const bool s1row = rl >= PB;
+  const int b = b0 + (s1row ? rl - PB : rl);
+  const bool valid = b < B;
+  const int row = s1row ? B + b : b;
+  float z = 0.f;
+  if (valid && li < n_s) z = (s1row ? A.S1 : A.S)[(size_t)b * n_s + li];
+  __syncthreads();
+  // planar flows: lane li carries z[li]; w_k·z by a butterfly over the row's LPR lanes
+  const int lc = li < n_s ? li : 0;  // lanes past n_s carry z = 0 and weight 0
+  const float lm = li < n_s ? 1.f : 0.f;
+  float fw = K > 0 ? __fmul_rn(lm, s_fl[lc]) : 0.f, fb = K > 0 ? s_fl[n_s] : 0.f;
+  float fu = K > 0 ? __fmul_rn(lm, s_fl[n_s + 1 + lc]) : 0.f;
+  float* zp = A.zs + (size_t)row * n_s + lc;
+  float* tp = A.ts + row;
+  PROBE_AT(1);
+  // z·w_k is formed one step ahead, so z's load is waited for before the loop and the loop body
+  // holds no wait on global memory (its stores stay in flight)
+  float zw = __fmul_rn(z, fw);
+  for (int k = 0; k < K; ++k) {
+    const float b_k = fb, u_k = fu;
+    if (k + 1 < K) {  // next flow's parameters, off the chain
+      const float* f = s_fl + (k + 1) * fs;
+      fw = __fmul_rn(lm, f[lc]);
+      fb = f[n_s];
+      fu = __fmul_rn(lm, f[n_s + 1 + lc]);
+    }
+    const float p = tsf_row_sum<LPR>(zw);
+    const float t = tanhf(__fadd_rn(p, b_k));
+    if (valid) {
+      if (li < n_s) zp[(size_t)k * R2 * n_s] = z;
+      if (li == 0) tp[(size_t)k * R2] = t;
+    }
+    z = __fadd_rn(z, __fmul_rn(u_k, t));
+    zw = __fmul_rn(z, fw);
+  }
+  if (valid && li < n_s) A.zs[((size_t)K * R2 + row) * n_s + li] = z;
+  s_z[rl * TSF_NS + li] = z;
+  __syncthreads();
+  PROBE_AT(2);
+  // Linear(n_s, G) of g for this workgroup's rows
   const float* Wl = s_fl + nfl;
   const float* bl = Wl + G * n_s;
-  for (int j = tid; j < R2 * G; j += 256) {
-    const int row = j / fdiv(G), c = j - row * G;
+  const FDiv fG = fdiv(G), fd = fdiv(d);
+  for (int j = tid; j < RPW * G; j += 256) {
+    const int r = j / fG, c = j - r * G;
     float acc = 0.f;
-    for (int i = 0; i < n_s; ++i) acc = __builtin_fmaf(s_z[row * n_s + i], Wl[c * n_s + i], acc);
+    for (int i = 0; i < n_s; ++i) acc = __builtin_fmaf(s_z[r * TSF_NS + i], Wl[c * n_s + i], acc);
     const float v = __fadd_rn(acc, bl[c]);
     s_gf[j] = v;
-    A.gfeat[j] = v;
+    const int bb = b0 + (r >= PB ? r - PB : r);
+    if (bb < B) A.gfeat[(size_t)(r >= PB ? B + bb : bb) * G + c] = v;
   }
   __syncthreads();
   // φ̃ = (h(g(s)) + h(g(s1))) ⊙ φ
   const float* bh = A.hp + d * G;
-  for (int j = tid; j < B * d; j += 256) {
-    const int b = j / fdiv(d), c = j - b * d;
+  for (int j = tid; j < PB * d; j += 256) {
+    const int r = j / fd, c = j - r * d, bb = b0 + r;
+    if (bb >= B) continue;
     float h0 = 0.f, h1 = 0.f;
     for (int q = 0; q < G; ++q) {
-      h0 = __builtin_fmaf(s_gf[b * G + q], s_wh[c * G + q], h0);
-      h1 = __builtin_fmaf(s_gf[(B + b) * G + q], s_wh[c * G + q], h1);
+      h0 = __builtin_fmaf(s_gf[r * G + q], s_wh[c * G + q], h0);
+      h1 = __builtin_fmaf(s_gf[(PB + r) * G + q], s_wh[c * G + q], h1);
     }
-    const float bb = bh[c];
-    const float aff = __fadd_rn(__fadd_rn(h0, bb), __fadd_rn(h1, bb));
-    A.tphi[j] = __fmul_rn(aff, A.phi[j]);
+    const float hb = bh[c];
+    const float aff = __fadd_rn(__fadd_rn(h0, hb), __fadd_rn(h1, hb));
+    A.tphi[(size_t)bb * d + c] = __fmul_rn(aff, A.phi[(size_t)bb * d + c]);
   }
+  PROBE_REC(10, t0_);
 }
 
-__global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A) {
-  __shared__ float s_wh[TSF_LDS];      // W_h before its update (+ dg [B][G] when it fits)
-  __shared__ float s_gf[TSF_LDS];      // g features [2B][G]
-  __shared__ float s_da[TSF_LDS / 2];  // daff [B][d]
-  __shared__ float s_tp[TSF_LDS / 2];  // φ̃ [B][d], then dg [B][G] when it does not fit after W_h
-  __shared__ float s_fl[TSF_LDS / 2];  // g parameters (flows + Linear) before the update
-  __shared__ float s_w[256], s_gw[256], s_dr[64], s_red[256];
-  const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B, O = A.O;
+// flow-row role: rows [f FR, (f+1) FR) of the 2B rows; waves 0-1 run the reverse flow chains
+template <int LPR>
+__device__ void tsf_bwd_flows(const TsfArgs& A, float* sm, float* s_dr, float* s_w, float* s_r, int* s_ab, int f) {
+  constexpr int FR = tsf_fr(LPR);
+  const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
   const int fs = tsf_flow_stride(n_s), nfl = K * fs, nlin = G * n_s + G;
-  const FDiv fd = fdiv(d), fG = fdiv(G);
-  float* gp = A.g + (long long)A.pol * A.Pg;
-  for (int j = tid; j < d * G; j += 256) s_wh[j] = A.hp[j];
-  for (int j = tid; j < R2 * G; j += 256) s_gf[j] = A.gfeat[j];
-  for (int j = tid; j < B * d; j += 256) s_tp[j] = A.tphi[j];
-  for (int j = tid; j < nfl + nlin; j += 256) s_fl[j] = gp[j];
-  if (tid < d) s_w[tid] = A.w[tid];
+  float* s_z = sm;                                  // [K+1][FR][n_s]
+  float* s_t = sm + TSF_ZS;                         // [K][FR]
+  float* s_fl = s_t + TSF_TS;                       // flows + Linear of g (pre-step)
+  float* s_wh = s_fl + TSF_LDS / 2;                 // W_h (pre-step)
+  float* s_dg = s_wh + TSF_LDS;                     // [FR][G] (φ̃ rows while staging)
+  float* s_da = s_dg + 2048;                        // [FR][d]
+  const float* snap = A.snap;
+  PROBE_T(t0_);
+  const int r0 = f * FR;
+  const int nr = min(FR, R2 - r0);
+  // stage everything up front (independent loads)
+  const int zr = FR * n_s;
+  const FDiv fzr = fdiv(zr);
+  for (int j = tid; j < (K + 1) * zr; j += 256) {
+    const int k = j / fzr, e = j - k * zr;
+    s_z[j] = e < nr * n_s ? A.zs[((size_t)k * R2 + r0) * n_s + e] : 0.f;
+  }
+  for (int j = tid; j < K * FR; j += 256) {
+    const int k = j / FR, e = j - k * FR;
+    s_t[j] = e < nr ? A.ts[(size_t)k * R2 + r0 + e] : 0.f;
+  }
+  for (int j = tid; j < nfl + nlin; j += 256) s_fl[j] = snap[j];
+  for (int j = tid; j < d * G; j += 256) s_wh[j] = snap[A.Pg + j];
+  (void)tsf_stage_daff(A, nr, [&](int rl) { const int row = r0 + rl; return row < B ? row : row - B; }, s_dg, s_da,
+                       s_dr, s_w, s_r, s_ab);
+  PROBE_AT(1);
+  const FDiv fG = fdiv(G);
+  // dg = daff W_h (the same for a batch index's s row and s1 row); rows past nr are zero
+  for (int j = tid; j < FR * G; j += 256) {
+    const int rl = j / fG, q = j - rl * G;
+    float acc = 0.f;
+    if (rl < nr)
+      for (int c = 0; c < d; ++c) acc = __builtin_fmaf(s_da[rl * d + c], s_wh[c * G + q], acc);
+    s_dg[j] = acc;
+  }
   __syncthreads();
-  // l2 = MSE(w·φ̃, r): dr_b = β (2/B) (r_fit_b - r_b)
-  float se = 0.f;
-  const float bnorm = __fmul_rn(A.beta, (float)(2.0 / (double)B));
-  for (int b = tid; b < B; b += 256) {
-    float rf = 0.f;
-    for (int j = 0; j < d; ++j) rf = __builtin_fmaf(s_tp[b * d + j], s_w[j], rf);
-    const float e = __fsub_rn(rf, A.r[b]);
-    se = __builtin_fmaf(e, e, se);
-    s_dr[b] = __fmul_rn(bnorm, e);
+  PROBE_AT(2);
+  if (tid >= 128) return;
+  const int rl = tid / LPR, li = tid - rl * LPR;
+  const float* Wl = s_fl + nfl;
+  float dz = 0.f;
+  if (li < n_s)
+    for (int q = 0; q < G; ++q) dz = __builtin_fmaf(s_dg[rl * G + q], Wl[q * n_s + li], dz);
+  // reverse chain; each row stores its own parameter-gradient terms (summed in k_tsf_flow).  The
+  // next step's operands are read from LDS one step ahead, off the chain.
+  const int row = r0 + rl;
+  const bool valid = row < R2;
+  const int lc = li < n_s ? li : 0;
+  const float lm = li < n_s ? 1.f : 0.f;
+  float* pr = A.part + (size_t)row * fs;
+  auto ld = [&](int k, float& t, float& zk, float& uk, float& wk) {
+    const float* fp = s_fl + k * fs;
+    t = s_t[k * FR + rl];
+    zk = __fmul_rn(lm, s_z[(k * FR + rl) * n_s + lc]);
+    uk = __fmul_rn(lm, fp[n_s + 1 + lc]);
+    wk = __fmul_rn(lm, fp[lc]);
+  };
+  PROBE_AT(3);
+  float nt = 0.f, nz = 0.f, nu = 0.f, nw = 0.f;
+  if (K > 0) ld(K - 1, nt, nz, nu, nw);
+  for (int k = K - 1; k >= 0; --k) {
+    const float t = nt, zk = nz, uk = nu, wk = nw;
+    if (k > 0) ld(k - 1, nt, nz, nu, nw);
+    const float su = tsf_row_sum<LPR>(__fmul_rn(dz, uk));
+    const float da = __fmul_rn(su, __fsub_rn(1.f, __fmul_rn(t, t)));
+    if (valid) {
+      float* pk = pr + (size_t)k * R2 * fs;
+      if (li < n_s) {
+        pk[li] = __fmul_rn(da, zk);
+        pk[n_s + 1 + li] = __fmul_rn(dz, t);
+      }
+      if (li == 0) pk[n_s] = da;
+    }
+    dz = __fadd_rn(dz, __fmul_rn(da, wk));
   }
-  se = block_sum(se, s_red);
-  // g_w = drᵀ φ̃ ; dφ̃ = -g_l1[b, a_b, :] + dr w ; daff = dφ̃ ⊙ φ
-  if (tid < d) {
-    float gw = 0.f;
-    for (int b = 0; b < B; ++b) gw = __builtin_fmaf(s_dr[b], s_tp[b * d + tid], gw);
-    s_gw[tid] = gw;
+  PROBE_REC(11, t0_);
+}
+
+// grid nflow + nh + nlin + 1, 256 threads (roles: see the header comment)
+template <int LPR>
+__global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A) {
+  __shared__ float sm[TSF_SM];
+  __shared__ float s_dr[64], s_r[64], s_w[256], s_red[256];
+  __shared__ int s_ab[64];
+  const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
+  const int fs = tsf_flow_stride(n_s), nfl = K * fs;
+  int role = blockIdx.x;
+  if (role < A.nflow) {
+    tsf_bwd_flows<LPR>(A, sm, s_dr, s_w, s_r, s_ab, role);
+    return;
   }
-  for (int j = tid; j < B * d; j += 256) {
-    const int b = j / fd, c = j - b * d;
-    const int ab = (int)A.a[b];
-    const float gc = (ab >= 0 && ab * d < O) ? A.dzlast[(size_t)b * O + ab * d + c] : 0.f;
-    const float dt = __fadd_rn(-gc, __fmul_rn(s_dr[b], s_w[c]));
-    s_da[j] = __fmul_rn(dt, A.phi[j]);
-  }
-  __syncthreads();
+  role -= A.nflow;
+  PROBE_T(t0_);
+  const float* snap = A.snap;
   const int step = *A.step;
-  // h: g_Wh = daffᵀ g(s) + daffᵀ g(s1) ; g_bh = 2 Σ_b daff   (Adam with this task's moments)
-  {
-    const AdamC c = adam_consts(A.hph, step);
-    float* hm = A.hm + (long long)A.pol * A.Ph;
-    float* hv = A.hv + (long long)A.pol * A.Ph;
-    for (int j = tid; j < d * G; j += 256) {
-      const int c0 = j / fG, q = j - c0 * G;
+  const FDiv fG = fdiv(G);
+  // LDS: daff [0, 4096) | role operands [4096, 12288) | φ̃ rows [12288, 16384)
+  float* s_da = sm;
+  float* s_tp = sm + 3 * (TSF_LDS / 2);
+  const bool wrole = role == A.nh + A.nlin;
+  float* s_gf = sm + TSF_LDS / 2;       // h role: [2B][G]
+  float* s_whs = sm + TSF_LDS / 2;      // g-Linear role: [d][TSF_QS] pre-step W_h columns
+  float* s_zk = s_whs + TSF_LDS / 2;    // g-Linear role: [2B][n_s] z_K
+  float* s_dg = s_zk + 2048;            // g-Linear role: [B][TSF_QS]
+  const int q0 = (role - A.nh) * TSF_QS, nq = min(TSF_QS, G - q0);
+  if (!wrole && role < A.nh) {
+    for (int j = tid; j < R2 * G; j += 256) s_gf[j] = A.gfeat[j];
+  } else if (!wrole) {
+    for (int j = tid; j < d * TSF_QS; j += 256) {
+      const int c = j / TSF_QS, qq = j - c * TSF_QS;
+      s_whs[j] = qq < nq ? snap[A.Pg + c * G + q0 + qq] : 0.f;
+    }
+    for (int j = tid; j < R2 * n_s; j += 256) s_zk[j] = A.zs[(size_t)K * R2 * n_s + j];
+  }
+  const float se = tsf_stage_daff(A, B, [](int rl) { return rl; }, s_tp, s_da, s_dr, s_w, s_r, s_ab);
+  PROBE_AT(1);
+  if (wrole) {  // l2, g_w = drᵀ φ̃, Adam on w_i, the loss row
+    const float sse = block_sum(se, s_red);
+    if (tid < d) {
+      float gw = 0.f;
+      for (int b = 0; b < B; ++b) gw = __builtin_fmaf(s_dr[b], s_tp[b * d + tid], gw);
+      adam_el(A.w + tid, A.wm + tid, A.wv + tid, gw, adam_consts(A.hpw, step));
+    }
+    if (tid == 0 && A.losses) {
+      const float l2 = (float)((double)sse / (double)B);
+      A.losses[2] = l2;
+      A.losses[0] = __fadd_rn(A.losses[1], __fmul_rn(A.beta, l2));
+    }
+    PROBE_REC(14, t0_);
+    return;
+  }
+  if (role < A.nh) {  // h role: g_Wh = daffᵀ g(s) + daffᵀ g(s1), g_bh = 2 Σ_b daff
+    const int j = role * 256 + tid;
+    float g = 0.f;
+    if (j >= A.Ph) {
+    } else if (j < d * G) {
+      const int c = j / fG, q = j - c * G;
       float g0 = 0.f, g1 = 0.f;
       for (int b = 0; b < B; ++b) {
-        g0 = __builtin_fmaf(s_da[b * d + c0], s_gf[b * G + q], g0);
-        g1 = __builtin_fmaf(s_da[b * d + c0], s_gf[(B + b) * G + q], g1);
+        g0 = __builtin_fmaf(s_da[b * d + c], s_gf[b * G + q], g0);
+        g1 = __builtin_fmaf(s_da[b * d + c], s_gf[(B + b) * G + q], g1);
       }
-      adam_el(A.hp + j, hm + j, hv + j, __fadd_rn(g0, g1), c);
-    }
-    for (int c0 = tid; c0 < d; c0 += 256) {
+      g = __fadd_rn(g0, g1);
+    } else {
+      const int c = j - d * G;
       float sb = 0.f;
-      for (int b = 0; b < B; ++b) sb = __fadd_rn(sb, s_da[b * d + c0]);
-      adam_el(A.hp + d * G + c0, hm + d * G + c0, hv + d * G + c0, __fmul_rn(2.f, sb), c);
+      for (int b = 0; b < B; ++b) sb = __fadd_rn(sb, s_da[b * d + c]);
+      g = __fmul_rn(2.f, sb);
     }
+    const long long ho = (long long)A.pol * A.Ph;
+    if (j < A.Ph) adam_el(A.hp + j, A.hm + ho + j, A.hv + ho + j, g, adam_consts(A.hph, step));
+    PROBE_REC(12, t0_);
+    return;
   }
-  // w
-  if (tid < d) adam_el(A.w + tid, A.wm + tid, A.wv + tid, s_gw[tid], adam_consts(A.hpw, step));
-  // dg = daff W_h (identical for the s and s1 rows)
-  __syncthreads();
-  float* s_dg = s_wh + d * G;  // after W_h in the same buffer when it fits, else reuse s_tp
-  const bool dg_in_wh = d * G + B * G <= TSF_LDS;
-  if (!dg_in_wh) s_dg = s_tp;
-  for (int j = tid; j < B * G; j += 256) {
-    const int b = j / fG, q = j - b * G;
+  // g-Linear role: columns [q0, q0 + nq) of g_i's Linear(n_s, G)
+  for (int j = tid; j < B * TSF_QS; j += 256) {
+    const int b = j / TSF_QS, qq = j - b * TSF_QS;
     float acc = 0.f;
-    for (int c0 = 0; c0 < d; ++c0) acc = __builtin_fmaf(s_da[b * d + c0], s_wh[c0 * G + q], acc);
+    for (int c = 0; c < d; ++c) acc = __builtin_fmaf(s_da[b * d + c], s_whs[c * TSF_QS + qq], acc);
     s_dg[j] = acc;
   }
   __syncthreads();
   const AdamC cg = adam_consts(A.hpg, step);
+  float* gp = A.g + (long long)A.pol * A.Pg;
   float* gm = A.gm + (long long)A.pol * A.Pg;
   float* gv = A.gv + (long long)A.pol * A.Pg;
-  const float* Wl = s_fl + nfl;
-  // Linear of g: dW = dgᵀ z_K(s) + dgᵀ z_K(s1) ; db = Σ dg + Σ dg
-  for (int j = tid; j < G * n_s; j += 256) {
-    const int q = j / fdiv(n_s), i = j - q * n_s;
-    float g0 = 0.f, g1 = 0.f;
-    for (int b = 0; b < B; ++b) {
-      g0 = __builtin_fmaf(s_dg[b * G + q], A.zs[((size_t)K * R2 + b) * n_s + i], g0);
-      g1 = __builtin_fmaf(s_dg[b * G + q], A.zs[((size_t)K * R2 + B + b) * n_s + i], g1);
+  for (int j = tid; j < nq * (n_s + 1); j += 256) {
+    const int qq = j / (n_s + 1), i = j - qq * (n_s + 1);
+    int o;
+    float g;
+    if (i < n_s) {  // dW = dgᵀ z_K(s) + dgᵀ z_K(s1)
+      float g0 = 0.f, g1 = 0.f;
+      for (int b = 0; b < B; ++b) {
+        g0 = __builtin_fmaf(s_dg[b * TSF_QS + qq], s_zk[b * n_s + i], g0);
+        g1 = __builtin_fmaf(s_dg[b * TSF_QS + qq], s_zk[(B + b) * n_s + i], g1);
+      }
+      g = __fadd_rn(g0, g1);
+      o = nfl + (q0 + qq) * n_s + i;
+    } else {  // db = Σ dg + Σ dg
+      float sb = 0.f;
+      for (int b = 0; b < B; ++b) sb = __fadd_rn(sb, s_dg[b * TSF_QS + qq]);
+      g = __fadd_rn(sb, sb);
+      o = nfl + G * n_s + q0 + qq;
     }
-    adam_el(gp + nfl + j, gm + nfl + j, gv + nfl + j, __fadd_rn(g0, g1), cg);
+    adam_el(gp + o, gm + o, gv + o, g, cg);
   }
-  for (int q = tid; q < G; q += 256) {
-    float sb = 0.f;
-    for (int b = 0; b < B; ++b) sb = __fadd_rn(sb, s_dg[b * G + q]);
-    const int o = nfl + G * n_s + q;
-    adam_el(gp + o, gm + o, gv + o, __fadd_rn(sb, sb), cg);
-  }
-  // planar flows, backward per row: dz = dg W ; for k = K-1..0: t = t_k, da = (dz·u_k)(1 - t²),
-  // per-row parts du_k = dz t, dw_k = da z_k, db_k = da ; dz += da w_k
-  for (int row = tid; row < R2 && K > 0; row += 256) {
-    const int b = row < B ? row : row - B;
-    float dz[TSF_NS];
+  PROBE_REC(13, t0_);
+}
+
+// flow parameters: Σ over the s rows + Σ over the s1 rows of the per-row terms (the two
+// g_backward calls of the reference), then Adam.  grid cdiv(K (2 n_s + 1), 256).  All 2B loads
+// of a thread are issued before the first add.
+__global__ __launch_bounds__(256) void k_tsf_flow(TsfArgs A) {
+  const int fs = tsf_flow_stride(A.n_s), nfl = A.K * fs, B = A.B, R2 = 2 * B;
+  PROBE_T(t0_);
+  const int j0 = blockIdx.x * 256 + threadIdx.x, j = j0 < nfl ? j0 : nfl - 1;
+  const int k = j / fs, e = j - k * fs;
+  const float* pk = A.part + (size_t)k * R2 * fs + e;
+  float v[128];
 #pragma unroll
-    for (int i = 0; i < TSF_NS; ++i) {
-      float acc = 0.f;
-      if (i < n_s)
-        for (int q = 0; q < G; ++q) acc = __builtin_fmaf(s_dg[b * G + q], Wl[q * n_s + i], acc);
-      dz[i] = acc;
-    }
-    for (int k = K - 1; k >= 0; --k) {
-      const float* f = s_fl + k * fs;
-      const float t = A.ts[(size_t)k * R2 + row];
-      const float* zk = A.zs + ((size_t)k * R2 + row) * n_s;
-      float* pr = A.part + ((size_t)k * R2 + row) * fs;
-      float su = 0.f;
+  for (int r = 0; r < 128; ++r) v[r] = r < R2 ? pk[(size_t)r * fs] : 0.f;
+  float g0 = 0.f, g1 = 0.f;
 #pragma unroll
-      for (int i = 0; i < TSF_NS; ++i)
-        if (i < n_s) {
-          su = __builtin_fmaf(dz[i], f[n_s + 1 + i], su);
-          pr[n_s + 1 + i] = __fmul_rn(dz[i], t);
-        }
-      const float da = __fmul_rn(su, __fsub_rn(1.f, __fmul_rn(t, t)));
-#pragma unroll
-      for (int i = 0; i < TSF_NS; ++i)
-        if (i < n_s) {
-          pr[i] = __fmul_rn(da, zk[i]);
-          dz[i] = __fadd_rn(dz[i], __fmul_rn(da, f[i]));
-        }
-      pr[n_s] = da;
-    }
+  for (int r = 0; r < 128; ++r) {
+    if (r < B)
+      g0 = __fadd_rn(g0, v[r]);
+    else if (r < R2)
+      g1 = __fadd_rn(g1, v[r]);
   }
-  __syncthreads();
-  // flow parameter gradients: Σ over the s rows + Σ over the s1 rows, then Adam
-  for (int j = tid; j < nfl; j += 256) {
-    const int k = j / fdiv(fs), e = j - k * fs;
-    float g0 = 0.f, g1 = 0.f;
-    for (int b = 0; b < B; ++b) {
-      g0 = __fadd_rn(g0, A.part[((size_t)k * R2 + b) * fs + e]);
-      g1 = __fadd_rn(g1, A.part[((size_t)k * R2 + B + b) * fs + e]);
-    }
-    adam_el(gp + j, gm + j, gv + j, __fadd_rn(g0, g1), cg);
-  }
-  if (tid == 0 && A.losses) {
-    const float l2 = (float)((double)se / (double)B);
-    A.losses[2] = l2;
-    A.losses[0] = __fadd_rn(A.losses[1], __fmul_rn(A.beta, l2));
-  }
+  const float g = __fadd_rn(g0, g1);
+  const long long go = (long long)A.pol * A.Pg;
+  if (j0 < nfl) adam_el(A.g + go + j, A.gm + go + j, A.gv + go + j, g, adam_consts(A.hpg, *A.step));
+  PROBE_REC(15, t0_);
 }
 
 }  // namespace sfx
