@@ -259,9 +259,10 @@ def main():
     eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
     eng.set_target_update_ev(1000)
     eng.set_spec_rounds(args.spec_rounds)
-    native = args.loop == "native" and args.schedule == "all"
+    native = args.loop == "native"
     if native:
-        loop = NativeEnvLoop(eng, batch=B, seed=1 + rank)
+        loop = NativeEnvLoop(eng, batch=B, seed=1 + rank, schedule=args.schedule,
+                             p_end=0.0 if args.tsf_K is None else 0.01)
         loop.prefill(1000)
         loop.set_task(0)
     else:
@@ -336,8 +337,8 @@ def main():
                                                f"{args.tsf_K} planar layers, active head only: "
                                                f"{'tsfdqn_nf.py' if args.tsf_K else 'tsfdqn.py'} path)"),
                        "heads_per_gpu": T, "global_batch": B * world, "parallelism": f"replica{world}" if world > 1 else "single",
-                       "loop": ("native C++ runner (sfx_runner_run): host env + replay, one pre-launched gated hipGraph per env step"
-                                if native else "python host loop over libsfx graphs")},
+                       "loop": (f"native C++ runner (sfx_runner_run, {args.schedule} schedule): host env + replay, one "
+                                "pre-launched gated hipGraph per env step" if native else "python host loop over libsfx graphs")},
             "roofline": roofline,
             "speculation": spec_stats,
             "sharded": sharded,

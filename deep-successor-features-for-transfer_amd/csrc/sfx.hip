@@ -682,6 +682,37 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
 
 // The fused step: LMS + forward of the minibatch, then `rounds` speculative rounds (or just
 // LMS + action selection when there is no minibatch yet).
+// SFDQN.get_Q_values + action choice for one state (sfdqn.py:577-596; agents/sfdqn.py:39-45):
+// forward of every head on s, GPI with w of `task`, selection into out[2] = (c, a).
+int select_body(sfx_handle* h, const float* s, int task, int use_gpi, float* q, int64_t* out) {
+  RC(run_fwd(h, {{R_A, P_ONLINE, 1, 0, h->T}}, 1, s, nullptr));
+  return run_gpi(h, gpi_args(R_A, 0, 0, h->w + (size_t)task * h->dpad, nullptr, q, nullptr, nullptr, out, task,
+                             use_gpi, 1));
+}
+
+// DeepSF.update_successor of one head (sfdqn.py:303-371): forwards, GPI / own-ψ next actions,
+// TD target, backward + Adam (+ l2 and the w step when r is given).  Launches only.
+int update_body(sfx_handle* h, int policy, const float* S, const int64_t* a, const float* r, const float* phi,
+                const float* S1, const float* gamma, int B, int use_gpi, float* losses, int64_t* next) {
+  if (use_gpi)
+    RC(run_fwd(h, {{R_S, P_ONLINE, 1, policy, 1}, {R_S1T, P_TARGET, 2, policy, 1}, {R_S1, P_ONLINE, 2, 0, h->T}}, B,
+               S, S1));
+  else
+    RC(run_fwd(h, {{R_S, P_ONLINE, 1, policy, 1}, {R_S1T, P_TARGET, 2, policy, 1}, {R_S1, P_ONLINE, 2, policy, 1}},
+               B, S, S1));
+  TdgSpec td;
+  td.use_gpi = use_gpi;
+  td.a = a;
+  td.gamma = gamma;
+  td.next = next;
+  td.next_stride = B;
+  return run_bwd(h, policy, 1, B, S, phi, r, losses, td);
+}
+
+// TSFDQN.update_successor (sfx_tsf.inc)
+int tsf_body(sfx_handle* h, int policy, const float* S, const int64_t* a, const float* r, const float* phi,
+             const float* S1, const float* gamma, int B, int use_gpi, float* losses, int64_t* next);
+
 int launch_step_all(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, const float* lms_phi, const float* lms_r,
                     float lms_alpha, int rounds) {
   const int T = h->T, B = p.B;
@@ -998,11 +1029,7 @@ int sfx_select_action(sfx_t h, const float* s, int task_index, int use_gpi, floa
   if (!h || !s || !out || task_index < 0 || task_index >= h->T) SFX_FAIL(SFX_E_ARG, "bad args");
   use_gpi = use_gpi ? 1 : 0;
   const GraphKey key = make_key(2, {task_index, use_gpi}, h->mask, {s, q, out});
-  return run_graph(h, key, [&]() -> int {
-    RC(run_fwd(h, {{R_A, P_ONLINE, 1, 0, h->T}}, 1, s, nullptr));
-    return run_gpi(h, gpi_args(R_A, 0, 0, h->w + (size_t)task_index * h->dpad, nullptr, q, nullptr, nullptr, out,
-                               task_index, use_gpi, 1));
-  });
+  return run_graph(h, key, [&]() -> int { return select_body(h, s, task_index, use_gpi, q, out); });
 }
 
 int sfx_update(sfx_t h, int policy, const float* S, const int64_t* a, const float* r, const float* phi,
@@ -1011,21 +1038,7 @@ int sfx_update(sfx_t h, int policy, const float* S, const int64_t* a, const floa
   if (B < 1 || B > h->Mmax) SFX_FAIL(SFX_E_ARG, "batch exceeds max_batch");
   use_gpi = use_gpi ? 1 : 0;
   const GraphKey key = make_key(3, {policy, use_gpi, B}, h->mask, {S, a, r, phi, S1, gamma, losses, next});
-  RC(run_graph(h, key, [&]() -> int {
-    if (use_gpi)
-      RC(run_fwd(h, {{R_S, P_ONLINE, 1, policy, 1}, {R_S1T, P_TARGET, 2, policy, 1}, {R_S1, P_ONLINE, 2, 0, h->T}}, B,
-                 S, S1));
-    else
-      RC(run_fwd(h, {{R_S, P_ONLINE, 1, policy, 1}, {R_S1T, P_TARGET, 2, policy, 1}, {R_S1, P_ONLINE, 2, policy, 1}},
-                 B, S, S1));
-    TdgSpec td;
-    td.use_gpi = use_gpi;
-    td.a = a;
-    td.gamma = gamma;
-    td.next = next;
-    td.next_stride = B;
-    return run_bwd(h, policy, 1, B, S, phi, r, losses, td);
-  }));
+  RC(run_graph(h, key, [&]() -> int { return update_body(h, policy, S, a, r, phi, S1, gamma, B, use_gpi, losses, next); }));
   h->mask ^= 1ull << policy;
   after_update(h, policy);
   return maybe_sync_target(h, policy);

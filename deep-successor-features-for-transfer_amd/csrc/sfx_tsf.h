@@ -33,7 +33,7 @@ constexpr int TSF_LDS = 8192;  // floats per staged operand (flows, W_h, g featu
 constexpr int TSF_ZS = 12288;  // flow states staged per flow-row workgroup: FR x (K+1) x n_s
 constexpr int TSF_TS = 1024;   // tanh outputs staged per flow-row workgroup: FR x K
 constexpr int TSF_QS = 16;     // g-Linear output columns per backward workgroup
-constexpr int TSF_SM = TSF_ZS + TSF_TS + TSF_LDS / 2 + TSF_LDS + 2048 + 2048;  // k_tsf_bwd LDS (floats)
+constexpr int TSF_SM = TSF_ZS + TSF_TS + TSF_LDS / 2 + TSF_LDS + 3 * 2048;  // k_tsf_bwd LDS (floats)
 
 // lanes per flow row and the row groups they imply (256-thread workgroups)
 __host__ __device__ constexpr int tsf_lpr(int n_s) { return n_s <= 16 ? 16 : 32; }
@@ -61,6 +61,7 @@ struct TsfArgs {
   float* tphi;   // [B][d]
   float* part;   // [K][2B][2n_s+1] per-row flow-parameter gradient terms
   float* snap;   // [Pg + Ph + d]: g_i, h, w_i before this step (written by k_tsf_fwd)
+  float* trash;  // one word written by lanes whose store is unused (branch-free store loops)
   float* losses; // [3]: [1] = l1 (written by the ψ tail); [0], [2] written here
   const float* dzlast;  // output gradient of the policy's ψ head [B][O] (written by K2)
   const int* step;      // Adam step of the policy (already bumped by the ψ path)
@@ -71,6 +72,21 @@ struct TsfArgs {
 };
 
 __device__ __forceinline__ int tsf_flow_stride(int n_s) { return 2 * n_s + 1; }
+
+// tanh without branches: for |x| < 0.625 the same odd minimax polynomial (same coefficients,
+// same operation order) as the device library's tanhf, else 1 − 2 / (e^{2|x|} + 1) by v_exp /
+// v_rcp; both are evaluated and selected, so a flow step's chain has no exec-mask branches.
+__device__ __forceinline__ float tsf_tanh(float x) {
+  const float ax = fabsf(x), x2 = __fmul_rn(x, x);
+  float p = __builtin_fmaf(x2, __int_as_float(0xbbbac73d), __int_as_float(0x3ca908c9));
+  p = __builtin_fmaf(x2, p, __int_as_float(0xbd5c1c4e));
+  p = __builtin_fmaf(x2, p, __int_as_float(0x3e088382));
+  p = __builtin_fmaf(x2, p, __int_as_float(0xbeaaaa99));
+  const float small = __builtin_fmaf(x2, __fmul_rn(ax, p), ax);
+  const float e = __expf(__fadd_rn(ax, ax));
+  const float large = __builtin_fmaf(__builtin_amdgcn_rcpf(__fadd_rn(e, 1.f)), -2.f, 1.f);
+  return copysignf(ax < 0.625f ? small : large, x);
+}
 
 // Sum over a flow row's LPR lanes, the same value in every lane: quad_perm xor 1, xor 2,
 // row_half_mirror, row_mirror (DPP, no LDS round trip; each step pairs lanes symmetrically so
@@ -88,31 +104,52 @@ __device__ __forceinline__ float tsf_row_sum(float v) {
   return v;
 }
 
-// Rows [r0, r0 + n) of the minibatch, staged in LDS for the backward roles (every global read
-// is issued here, before any dependent arithmetic): φ̃ and φ rows, the taken action's row of the
-// ψ output gradient, r and the pre-step w_i; then dr_b = β (2/B) (w·φ̃_b − r_b) and
+typedef __attribute__((address_space(3))) void* tsf_lds_t;
+
+// LDS-DMA staging: dst[j] = *src(j) for j < n (global_load_lds_dword; wave-uniform LDS base +
+// lane * 4, per-lane global address, no VGPR destination).  Nothing waits here: the loads of
+// every staging call stay in flight together until the caller's next __syncthreads().
+template <class F>
+__device__ __forceinline__ void glds(float* dst, int n, F src) {
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  for (int c = threadIdx.x >> 6; c * 64 < n; c += nw) {
+    const int j = c * 64 + lane;
+    if (j < n) __builtin_amdgcn_global_load_lds((const void*)src(j), (tsf_lds_t)(dst + c * 64), 4, 0, 0);
+  }
+}
+
+// Rows [0, n) of the minibatch (row rl is batch index bmap(rl)), staged for the backward roles:
+// φ̃ and φ rows, r, the taken actions, the pre-step w_i, then (second round trip) the taken
+// action's row of the ψ output gradient; dr_b = β (2/B) (w·φ̃_b − r_b) and
 //   daff[b][c] = (−∂l1/∂t[b][c] + dr_b w_c) φ[b][c]
 // (the gradient reaching h's output through the TD targets and through w·φ̃).  Returns this
-// thread's share of Σ_b (w·φ̃_b − r_b)² (l2 numerator; rows r0.. only).  Rows are batch indices
-// (`bmap` maps a local row to its batch index).  Ends with a barrier.
+// thread's share of Σ_b (w·φ̃_b − r_b)² (l2 numerator).  Callers may have staging loads of their
+// own in flight; the first barrier here retires them too.  Ends with a barrier.
 template <class BMap>
-__device__ float tsf_stage_daff(const TsfArgs& A, int n, BMap bmap, float* s_tp, float* s_da, float* s_dr,
-                                float* s_w, float* s_r, int* s_ab) {
+__device__ float tsf_stage_daff(const TsfArgs& A, int n, BMap bmap, float* s_tp, float* s_da, float* s_gc,
+                                float* s_dr, float* s_w, float* s_r, int* s_ab) {
   const int tid = threadIdx.x, d = A.d, O = A.O;
   const float* wold = A.snap + A.Pg + A.Ph;
   const FDiv fd = fdiv(d);
-  if (tid < d) s_w[tid] = wold[tid];
+  float rv = 0.f;
+  int av = 0;
   if (tid < n) {
     const int b = bmap(tid);
-    s_r[tid] = A.r[b];
-    s_ab[tid] = (int)A.a[b];
+    rv = A.r[b];
+    av = (int)A.a[b];
   }
-  for (int j = tid; j < n * d; j += 256) {
-    const int rl = j / fd, c = j - rl * d, b = bmap(rl);
-    s_tp[j] = A.tphi[(size_t)b * d + c];
-    s_da[j] = A.phi[(size_t)b * d + c];
+  glds(s_w, d, [&](int j) { return wold + j; });
+  glds(s_tp, n * d, [&](int j) { const int rl = j / fd; return A.tphi + (size_t)bmap(rl) * d + (j - rl * d); });
+  glds(s_da, n * d, [&](int j) { const int rl = j / fd; return A.phi + (size_t)bmap(rl) * d + (j - rl * d); });
+  if (tid < n) {
+    s_r[tid] = rv;
+    s_ab[tid] = av;
   }
   __syncthreads();
+  glds(s_gc, n * d, [&](int j) {
+    const int rl = j / fd, ab = s_ab[rl];
+    return (ab >= 0 && ab * d < O) ? A.dzlast + (size_t)bmap(rl) * O + ab * d + (j - rl * d) : A.dzlast;
+  });
   float se = 0.f;
   const float bnorm = __fmul_rn(A.beta, (float)(2.0 / (double)A.B));
   if (tid < n) {
@@ -124,8 +161,8 @@ __device__ float tsf_stage_daff(const TsfArgs& A, int n, BMap bmap, float* s_tp,
   }
   __syncthreads();
   for (int j = tid; j < n * d; j += 256) {
-    const int rl = j / fd, c = j - rl * d, b = bmap(rl), ab = s_ab[rl];
-    const float gc = (ab >= 0 && ab * d < O) ? A.dzlast[(size_t)b * O + ab * d + c] : 0.f;
+    const int rl = j / fd, c = j - rl * d, ab = s_ab[rl];
+    const float gc = (ab >= 0 && ab * d < O) ? s_gc[j] : 0.f;
     const float dt = __fadd_rn(-gc, __fmul_rn(s_dr[rl], s_w[c]));
     s_da[j] = __fmul_rn(dt, s_da[j]);
   }
@@ -138,22 +175,16 @@ template <int LPR>
 __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A) {
   constexpr int RPW = tsf_rpw(LPR), PB = RPW / 2;
   __shared__ float s_fl[TSF_LDS / 2];  // flows, then the Linear of g
-  __shared__ float s_wh[TSF_LDS];      // W_h
+  __shared__ float s_whT[TSF_LDS];     // W_h transposed: [G][d]
   __shared__ float s_gf[TSF_LDS / 2];  // g features of this workgroup's rows [RPW][G]
+  __shared__ float s_ph[1024];         // φ rows of this workgroup's batch indices [PB][d]
   __shared__ float s_z[RPW * TSF_NS];  // z_K of this workgroup's rows
+  __shared__ float s_bh[256], s_wv[256];
   const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
   const int fs = tsf_flow_stride(n_s), nfl = K * fs, nlin = G * n_s + G;
-  const int b0 = blockIdx.x * PB;
+  const int b0 = blockIdx.x * PB, nb = min(PB, B - b0);
   PROBE_T(t0_);
   const float* gp = A.g + (long long)A.pol * A.Pg;
-  {  // this workgroup's slice of the pre-step snapshot of g_i, h, w_i (read by k_tsf_bwd)
-    const int S = A.Pg + A.Ph + d, per = (S + gridDim.x - 1) / gridDim.x;
-    const int lo = blockIdx.x * per, hi = min(S, lo + per);
-    for (int j = lo + tid; j < hi; j += 256)
-      A.snap[j] = j < A.Pg ? gp[j] : (j < A.Pg + A.Ph ? A.hp[j - A.Pg] : A.w[j - A.Pg - A.Ph]);
-  }
-  for (int j = tid; j < nfl + nlin; j += 256) s_fl[j] = gp[j];
-  for (int j = tid; j < d * G; j += 256) s_wh[j] = A.hp[j];
   const int rl = tid / LPR, li = tid - rl * LPR;
   const bool s1row = rl >= PB;
   const int b = b0 + (s1row ? rl - PB : rl);
@@ -161,7 +192,31 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A) {
   const int row = s1row ? B + b : b;
   float z = 0.f;
   if (valid && li < n_s) z = (s1row ? A.S1 : A.S)[(size_t)b * n_s + li];
+  const FDiv fd = fdiv(d), fG = fdiv(G);
+  glds(s_fl, nfl + nlin, [&](int j) { return gp + j; });
+  glds(s_whT, d * G, [&](int j) { const int q = j / fd; return A.hp + (j - q * d) * G + q; });
+  glds(s_bh, d, [&](int j) { return A.hp + d * G + j; });
+  glds(s_wv, d, [&](int j) { return A.w + j; });
+  glds(s_ph, nb * d, [&](int j) { return A.phi + (size_t)b0 * d + j; });
   __syncthreads();
+  {  // this workgroup's slice of the pre-step snapshot of g_i, h, w_i (read by k_tsf_bwd)
+    const int S = A.Pg + A.Ph + d, per = (S + gridDim.x - 1) / gridDim.x;
+    const int lo = blockIdx.x * per, hi = min(S, lo + per);
+    for (int j = lo + tid; j < hi; j += 256) {
+      float v;
+      if (j < A.Pg) {
+        v = s_fl[j];
+      } else if (j < A.Pg + d * G) {
+        const int jj = j - A.Pg, c = jj / fG, q = jj - c * G;
+        v = s_whT[q * d + c];
+      } else if (j < A.Pg + A.Ph) {
+        v = s_bh[j - A.Pg - d * G];
+      } else {
+        v = s_wv[j - A.Pg - A.Ph];
+      }
+      A.snap[j] = v;
+    }
+  }
   // planar flows: lane li carries z[li]; w_k·z by a butterfly over the row's LPR lanes
   const int lc = li < n_s ? li : 0;  // lanes past n_s carry z = 0 and weight 0
   const float lm = li < n_s ? 1.f : 0.f;
@@ -173,6 +228,7 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A) {
   // z·w_k is formed one step ahead, so z's load is waited for before the loop and the loop body
   // holds no wait on global memory (its stores stay in flight)
   float zw = __fmul_rn(z, fw);
+  const bool zok = valid && li < n_s, tok = valid && li == 0;
   for (int k = 0; k < K; ++k) {
     const float b_k = fb, u_k = fu;
     if (k + 1 < K) {  // next flow's parameters, off the chain
@@ -182,11 +238,9 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A) {
       fu = __fmul_rn(lm, f[n_s + 1 + lc]);
     }
     const float p = tsf_row_sum<LPR>(zw);
-    const float t = tanhf(__fadd_rn(p, b_k));
-    if (valid) {
-      if (li < n_s) zp[(size_t)k * R2 * n_s] = z;
-      if (li == 0) tp[(size_t)k * R2] = t;
-    }
+    const float t = tsf_tanh(__fadd_rn(p, b_k));
+    *(zok ? zp + (size_t)k * R2 * n_s : A.trash) = z;  // lanes with nothing to save write the trash word
+    *(tok ? tp + (size_t)k * R2 : A.trash) = t;
     z = __fadd_rn(z, __fmul_rn(u_k, t));
     zw = __fmul_rn(z, fw);
   }
@@ -197,7 +251,6 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A) {
   // Linear(n_s, G) of g for this workgroup's rows
   const float* Wl = s_fl + nfl;
   const float* bl = Wl + G * n_s;
-  const FDiv fG = fdiv(G), fd = fdiv(d);
   for (int j = tid; j < RPW * G; j += 256) {
     const int r = j / fG, c = j - r * G;
     float acc = 0.f;
@@ -208,19 +261,17 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A) {
     if (bb < B) A.gfeat[(size_t)(r >= PB ? B + bb : bb) * G + c] = v;
   }
   __syncthreads();
-  // φ̃ = (h(g(s)) + h(g(s1))) ⊙ φ
-  const float* bh = A.hp + d * G;
-  for (int j = tid; j < PB * d; j += 256) {
+  // φ̃ = (h(g(s)) + h(g(s1))) ⊙ φ  (lanes over c read W_hᵀ rows: conflict-free)
+  for (int j = tid; j < nb * d; j += 256) {
     const int r = j / fd, c = j - r * d, bb = b0 + r;
-    if (bb >= B) continue;
     float h0 = 0.f, h1 = 0.f;
     for (int q = 0; q < G; ++q) {
-      h0 = __builtin_fmaf(s_gf[r * G + q], s_wh[c * G + q], h0);
-      h1 = __builtin_fmaf(s_gf[(PB + r) * G + q], s_wh[c * G + q], h1);
+      h0 = __builtin_fmaf(s_gf[r * G + q], s_whT[q * d + c], h0);
+      h1 = __builtin_fmaf(s_gf[(PB + r) * G + q], s_whT[q * d + c], h1);
     }
-    const float hb = bh[c];
+    const float hb = s_bh[c];
     const float aff = __fadd_rn(__fadd_rn(h0, hb), __fadd_rn(h1, hb));
-    A.tphi[(size_t)bb * d + c] = __fmul_rn(aff, A.phi[(size_t)bb * d + c]);
+    A.tphi[(size_t)bb * d + c] = __fmul_rn(aff, s_ph[j]);
   }
   PROBE_REC(10, t0_);
 }
@@ -237,25 +288,27 @@ __device__ void tsf_bwd_flows(const TsfArgs& A, float* sm, float* s_dr, float* s
   float* s_wh = s_fl + TSF_LDS / 2;                 // W_h (pre-step)
   float* s_dg = s_wh + TSF_LDS;                     // [FR][G] (φ̃ rows while staging)
   float* s_da = s_dg + 2048;                        // [FR][d]
+  float* s_gc = s_da + 2048;                        // [FR][d] ψ output gradient rows
   const float* snap = A.snap;
   PROBE_T(t0_);
   const int r0 = f * FR;
   const int nr = min(FR, R2 - r0);
-  // stage everything up front (independent loads)
+  // stage everything up front (LDS-DMA, all in flight together)
   const int zr = FR * n_s;
   const FDiv fzr = fdiv(zr);
-  for (int j = tid; j < (K + 1) * zr; j += 256) {
+  const int nzv = nr * n_s;
+  glds(s_z, (K + 1) * zr, [&](int j) {
     const int k = j / fzr, e = j - k * zr;
-    s_z[j] = e < nr * n_s ? A.zs[((size_t)k * R2 + r0) * n_s + e] : 0.f;
-  }
-  for (int j = tid; j < K * FR; j += 256) {
+    return A.zs + ((size_t)k * R2 + r0) * n_s + (e < nzv ? e : 0);  // rows past 2B: finite copies, zero dg
+  });
+  glds(s_t, K * FR, [&](int j) {
     const int k = j / FR, e = j - k * FR;
-    s_t[j] = e < nr ? A.ts[(size_t)k * R2 + r0 + e] : 0.f;
-  }
-  for (int j = tid; j < nfl + nlin; j += 256) s_fl[j] = snap[j];
-  for (int j = tid; j < d * G; j += 256) s_wh[j] = snap[A.Pg + j];
+    return A.ts + (size_t)k * R2 + r0 + (e < nr ? e : 0);
+  });
+  glds(s_fl, nfl + nlin, [&](int j) { return snap + j; });
+  glds(s_wh, d * G, [&](int j) { return snap + A.Pg + j; });
   (void)tsf_stage_daff(A, nr, [&](int rl) { const int row = r0 + rl; return row < B ? row : row - B; }, s_dg, s_da,
-                       s_dr, s_w, s_r, s_ab);
+                       s_gc, s_dr, s_w, s_r, s_ab);
   PROBE_AT(1);
   const FDiv fG = fdiv(G);
   // dg = daff W_h (the same for a batch index's s row and s1 row); rows past nr are zero
@@ -289,6 +342,7 @@ __device__ void tsf_bwd_flows(const TsfArgs& A, float* sm, float* s_dr, float* s
     wk = __fmul_rn(lm, fp[lc]);
   };
   PROBE_AT(3);
+  const bool zok = valid && li < n_s, bok = valid && li == 0;
   float nt = 0.f, nz = 0.f, nu = 0.f, nw = 0.f;
   if (K > 0) ld(K - 1, nt, nz, nu, nw);
   for (int k = K - 1; k >= 0; --k) {
@@ -296,14 +350,10 @@ __device__ void tsf_bwd_flows(const TsfArgs& A, float* sm, float* s_dr, float* s
     if (k > 0) ld(k - 1, nt, nz, nu, nw);
     const float su = tsf_row_sum<LPR>(__fmul_rn(dz, uk));
     const float da = __fmul_rn(su, __fsub_rn(1.f, __fmul_rn(t, t)));
-    if (valid) {
-      float* pk = pr + (size_t)k * R2 * fs;
-      if (li < n_s) {
-        pk[li] = __fmul_rn(da, zk);
-        pk[n_s + 1 + li] = __fmul_rn(dz, t);
-      }
-      if (li == 0) pk[n_s] = da;
-    }
+    float* pk = pr + (size_t)k * R2 * fs;
+    *(zok ? pk + li : A.trash) = __fmul_rn(da, zk);
+    *(zok ? pk + n_s + 1 + li : A.trash) = __fmul_rn(dz, t);
+    *(bok ? pk + n_s : A.trash) = da;
     dz = __fadd_rn(dz, __fmul_rn(da, wk));
   }
   PROBE_REC(11, t0_);
@@ -327,9 +377,10 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A) {
   const float* snap = A.snap;
   const int step = *A.step;
   const FDiv fG = fdiv(G);
-  // LDS: daff [0, 4096) | role operands [4096, 12288) | φ̃ rows [12288, 16384)
+  // LDS: daff [0, 4096) | role operands [4096, 12288) | φ̃ rows [12288, 16384) | ψ gradient rows [16384, 20480)
   float* s_da = sm;
   float* s_tp = sm + 3 * (TSF_LDS / 2);
+  float* s_gc = sm + 4 * (TSF_LDS / 2);
   const bool wrole = role == A.nh + A.nlin;
   float* s_gf = sm + TSF_LDS / 2;       // h role: [2B][G]
   float* s_whs = sm + TSF_LDS / 2;      // g-Linear role: [d][TSF_QS] pre-step W_h columns
@@ -337,15 +388,15 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A) {
   float* s_dg = s_zk + 2048;            // g-Linear role: [B][TSF_QS]
   const int q0 = (role - A.nh) * TSF_QS, nq = min(TSF_QS, G - q0);
   if (!wrole && role < A.nh) {
-    for (int j = tid; j < R2 * G; j += 256) s_gf[j] = A.gfeat[j];
+    glds(s_gf, R2 * G, [&](int j) { return A.gfeat + j; });
   } else if (!wrole) {
-    for (int j = tid; j < d * TSF_QS; j += 256) {
+    glds(s_whs, d * TSF_QS, [&](int j) {
       const int c = j / TSF_QS, qq = j - c * TSF_QS;
-      s_whs[j] = qq < nq ? snap[A.Pg + c * G + q0 + qq] : 0.f;
-    }
-    for (int j = tid; j < R2 * n_s; j += 256) s_zk[j] = A.zs[(size_t)K * R2 * n_s + j];
+      return snap + A.Pg + c * G + q0 + (qq < nq ? qq : 0);  // columns past G: zeroed below
+    });
+    glds(s_zk, R2 * n_s, [&](int j) { return A.zs + (size_t)K * R2 * n_s + j; });
   }
-  const float se = tsf_stage_daff(A, B, [](int rl) { return rl; }, s_tp, s_da, s_dr, s_w, s_r, s_ab);
+  const float se = tsf_stage_daff(A, B, [](int rl) { return rl; }, s_tp, s_da, s_gc, s_dr, s_w, s_r, s_ab);
   PROBE_AT(1);
   if (wrole) {  // l2, g_w = drᵀ φ̃, Adam on w_i, the loss row
     const float sse = block_sum(se, s_red);
@@ -390,7 +441,7 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A) {
     const int b = j / TSF_QS, qq = j - b * TSF_QS;
     float acc = 0.f;
     for (int c = 0; c < d; ++c) acc = __builtin_fmaf(s_da[b * d + c], s_whs[c * TSF_QS + qq], acc);
-    s_dg[j] = acc;
+    s_dg[j] = qq < nq ? acc : 0.f;
   }
   __syncthreads();
   const AdamC cg = adam_consts(A.hpg, step);

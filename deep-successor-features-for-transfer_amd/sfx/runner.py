@@ -222,20 +222,24 @@ class EnvLoop:
 
 
 class NativeEnvLoop:
-    """The same all-task env-step loop as EnvLoop(schedule="all"), run by libsfx's native
-    runner (include/sfx.h, sfx_runner_*): C++ env + replay ring on the host, one pre-launched
-    hipGraph per env step whose gate kernel waits for the host's inputs.
+    """The env-step loop of EnvLoop run by libsfx's native runner (include/sfx.h, sfx_runner_*):
+    C++ env + replay ring on the host, one pre-launched hipGraph per env step whose gate kernel
+    waits for the host's inputs.  schedule: "all" (main_sfdqn_torch.py), "active" (sfdqn.py /
+    agents/sfdqn_sequential.py: the active head with l2 and an Adam-trained w, no LMS) or "tsf"
+    (TSFDQN.update_successor; needs SFEngine.tsf_setup).  p_end: per-step episode-end
+    probability of the built-in synthetic task (0: never terminates, like tasks/reacher.py).
 
     env: None for the built-in synthetic Reacher-shape task, or an object with
     ``reset(task) -> s0`` and ``step(task, a) -> (s1, phi, r, terminal)`` (numpy / floats),
     called through C callbacks (agents/agent.py's Task interface: tasks/task.py).
     """
 
-    FIELDS = ("s", "s1", "phi", "a", "gamma", "snext", "phi1", "r1")
+    FIELDS = ("s", "s1", "phi", "a", "gamma", "snext", "phi1", "r1", "rb")
+    SCHEDULES = {"all": 0, "active": 1, "tsf": 2}
 
     def __init__(self, engine: SFEngine, batch: int = 32, capacity: int = 1_000_000, gamma: float = 0.9,
                  epsilon: float = 0.1, alpha_w: float = 1e-3, episode_len: int = 500, use_gpi: bool = True,
-                 seed: int = 1, env=None):
+                 seed: int = 1, env=None, schedule: str = "all", upd_use_gpi: bool = True, p_end: float = 0.0):
         import ctypes as C
 
         from ._lib import ENV_RESET_FN, ENV_STEP_FN, check, lib
@@ -272,10 +276,13 @@ class NativeEnvLoop:
                                     1 if use_gpi else 0, seed, C.cast(reset_fn, C.c_void_p) if reset_fn else None,
                                     C.cast(step_fn, C.c_void_p) if step_fn else None, None), "sfx_runner_create")
         self._r = r
-        off = (C.c_int64 * 9)()
+        off = (C.c_int64 * 10)()
         check(lib.sfx_runner_layout(r, off), "sfx_runner_layout")
         self.layout = {k: int(off[i]) for i, k in enumerate(self.FIELDS)}
-        self.record_bytes = int(off[8])
+        self.record_bytes = int(off[9])
+        self.schedule = schedule
+        check(lib.sfx_runner_config(r, self.SCHEDULES[schedule], 1 if upd_use_gpi else 0, float(p_end)),
+              "sfx_runner_config")
         self.task_index = 0
 
     def close(self):
@@ -327,7 +334,7 @@ class NativeEnvLoop:
         C, e, B = self._C, self.eng, self.B
         shapes = {"s": ((B, e.n_s), np.float32), "s1": ((B, e.n_s), np.float32), "phi": ((B, e.d), np.float32),
                   "a": ((B,), np.int64), "gamma": ((B,), np.float32), "snext": ((e.n_s,), np.float32),
-                  "phi1": ((e.d,), np.float32), "r1": ((1,), np.float32)}
+                  "phi1": ((e.d,), np.float32), "r1": ((1,), np.float32), "rb": ((B,), np.float32)}
         out = []
         for i in range(self._lib.sfx_runner_recorded(self._r)):
             buf = np.zeros(self.record_bytes, dtype=np.uint8)

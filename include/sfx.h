@@ -222,8 +222,16 @@ int sfx_runner_create(sfx_runner_t* out, sfx_t h, int batch, int capacity, float
                       float alpha_w, int episode_len, int sel_use_gpi, unsigned long long seed,
                       sfx_env_reset_fn reset_fn, sfx_env_step_fn step_fn, void* env_ctx);
 int sfx_runner_destroy(sfx_runner_t r);
-/* byte offsets of one step's input record: s, s1, phi, a(int64), gamma, s_next, phi1, r1, total */
-int sfx_runner_layout(sfx_runner_t r, int64_t* offsets_host /* [9] */);
+/* byte offsets of one step's input record: s, s1, phi, a(int64), gamma, s_next, phi1, r1,
+ * r (minibatch rewards [batch]), total */
+int sfx_runner_layout(sfx_runner_t r, int64_t* offsets_host /* [10] */);
+/* training schedule of the env steps: 0 all-task (default; agents/sfdqn.py:47-60 with LMS w),
+ * 1 active task only (sfdqn.py:462-471, agents/sfdqn_sequential.py:63-76: l1 + l2, Adam w),
+ * 2 TSF-DQN active task (tsfdqn.py:566-580; needs sfx_tsf_setup).  use_gpi: next actions of the
+ * update by GPI (1) or the own head (0).  p_end: episode-end probability per step of the
+ * built-in synthetic task (γ = 0 on that transition; 0 = never, like tasks/reacher.py:112).
+ * Call between runs (before sfx_runner_set_task). */
+int sfx_runner_config(sfx_runner_t r, int schedule, int use_gpi, float p_end);
 /* Agent.set_active_training_task (agents/agent.py:121-139): reset the env, select the first action */
 int sfx_runner_set_task(sfx_runner_t r, int task);
 /* n random transitions into the replay (warm-up; not env steps) */

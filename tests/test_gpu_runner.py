@@ -135,3 +135,60 @@ def test_runner_with_python_env_callbacks():
     check_state(eng, st, T, n)
     loop.close()
     eng.close()
+
+
+@pytest.mark.parametrize("schedule,upd_use_gpi", [("active", True), ("active", False), ("tsf", True)])
+def test_runner_active_schedules_match_oracle(schedule, upd_use_gpi):
+    """Native runner with the active-task schedules: sfdqn.py / agents/sfdqn_sequential.py (one
+    head per env step, l1 + l2 with an Adam-trained w) and TSF-DQN (tsfdqn.py).  The oracle
+    replays the recorded minibatches (with their rewards) in order and must reproduce every
+    recorded greedy action and the final heads / w / g_i / h.  Episodes end at random
+    (p_end) so γ = 0 transitions enter the minibatches."""
+    from sfx.runner import NativeEnvLoop
+
+    spec = R.Spec(11, 32, 5, 6, ("relu", "relu"))
+    T, ev, n, task = 3, 5, 30, 2
+    eng, st = make(spec, T, ev)
+    if schedule == "tsf":
+        K, G = 2, 12
+        gs = R.GSpec(spec.n_s, G, K)
+        gen = torch.Generator().manual_seed(4)
+        g = torch.empty(T, gs.P).uniform_(-0.3, 0.3, generator=gen)
+        h = torch.empty(spec.d * G + spec.d).uniform_(-0.2, 0.2, generator=gen)
+        eng.tsf_setup(G, K, 1.0, 1e-3, 0.0, 1e-3, 0.0)
+        for t in range(T):
+            eng.tsf_load_g(t, g[t])
+        eng.tsf_load_h(h)
+        st = R.TSFState(spec, st.online, st.target, st.w, gspec=gs, g=g.clone(), h=h.clone())
+    loop = NativeEnvLoop(eng, batch=16, capacity=200, gamma=0.9, epsilon=0.3, episode_len=11, seed=9,
+                         schedule=schedule, upd_use_gpi=upd_use_gpi, p_end=0.1)
+    loop.prefill(10)
+    loop.set_task(task)
+    first = loop.action()
+    loop.record(n)
+    loop.run(n)
+    recs = loop.records()
+    assert len(recs) == n and (recs[0]["c"], recs[0]["a_greedy"]) == first
+    assert any(r["terminal"] for r in recs)
+    for k, rec in enumerate(recs):
+        assert rec["task"] == task
+        if rec["have"]:
+            batch = (torch.from_numpy(rec["s"]), torch.from_numpy(rec["a"]), torch.from_numpy(rec["rb"]).view(-1, 1),
+                     torch.from_numpy(rec["phi"]), torch.from_numpy(rec["s1"]), torch.from_numpy(rec["gamma"]))
+            if schedule == "tsf":
+                R.tsf_update(st, batch, task, use_gpi=upd_use_gpi, target_update_ev=ev)
+            else:
+                R.sf_update(st, batch, task, use_gpi=upd_use_gpi, target_update_ev=ev)
+        q, tk = R.gpi_w(R.psi_all(st.online, spec, torch.from_numpy(rec["snext"]).view(1, -1)), st.w[task])
+        want = (int(tk[0]), R.select_action(q, tk[0], task, True))
+        got = (recs[k + 1]["c"], recs[k + 1]["a_greedy"]) if k + 1 < len(recs) else loop.action()
+        assert got == want, f"step {k}: runner selected {got}, oracle {want}"
+    params_close(torch.stack([eng.get_head(t, 0) for t in range(T)]), st.online, 1e-3 * n)
+    params_close(torch.stack([eng.get_head(t, 1) for t in range(T)]), st.target, 1e-3 * n)
+    rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-3, atol=1e-6)
+    if schedule == "tsf":
+        params_close(torch.stack([eng.tsf_get_g(t)[0] for t in range(T)]), st.g, 1e-3 * n)
+        params_close(eng.tsf_get_h(), st.h, 1e-3 * n)
+    assert loop.stats()["prelaunched"] > n // 2
+    loop.close()
+    eng.close()
