@@ -200,6 +200,55 @@ def bench_sharded(args, world, rank, device, barrier, dist):
             "rounds": loop.sharded.stats}
 
 
+def bench_sharded_tsf(args, world, rank, device, barrier, dist):
+    """BASELINE config C5 (tsfdqn_nf.py, 32 source tasks over 4 GPUs): T_loc = --heads per rank,
+    T_glob = T_loc * world, one lock-step env stream on every rank, GPI maxima and the action key
+    all-reduced (MAX) over RCCL, h and w_i broadcast from the active task's owner."""
+    from sfx.engine import SFEngine
+    from sfx.runner import ShardedTSFEnvLoop
+    from sfx.shard import all_reduce_max_fn, broadcast_fn
+
+    sh, T_loc, B = TSF_SHAPE, args.heads, args.batch
+    Tg = T_loc * world
+    eng = SFEngine(T_loc, sh["n_s"], sh["H"], sh["A"], sh["d"], sh["acts"], max_batch=B, device=device)
+    eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
+    eng.set_target_update_ev(1000)
+    eng.tsf_setup(sh["G"], args.tsf_K, 1.0, 1e-3, 0.0, 1e-3, 0.0)
+    online, w, g, h = tsf_problem(Tg, args.tsf_K, seed=0)
+    if world > 1:
+        ar, bc = all_reduce_max_fn(via_host=args.via_host), broadcast_fn(via_host=args.via_host)
+    else:
+        ar, bc = (lambda t: None), (lambda t, src: None)
+    loop = ShardedTSFEnvLoop(eng, Tg, rank, ar, bc, batch=B, seed=1)
+    for t in range(T_loc):
+        eng.load_head(t, online[rank * T_loc + t], 0)
+        eng.load_head(t, online[rank * T_loc + t], 1)
+        eng.tsf_load_g(t, g[rank * T_loc + t])
+    for t in range(Tg):
+        eng.load_w(t, w[t])
+    eng.tsf_load_h(h)
+    loop.prefill(1000)
+    loop.set_task(0)
+    loop.run(max(20, args.shard_steps // 10))
+    barrier()
+    t0 = time.perf_counter()
+    loop.run(args.shard_steps)
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device="cpu" if args.via_host else device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    eng.close()
+    v = args.shard_steps / dt
+    return {"value": round(v, 2), "unit": "env steps/s", "ms_per_step": round(1000.0 * dt / args.shard_steps, 4),
+            "steps": args.shard_steps, "heads_total": Tg, "heads_per_gpu": T_loc,
+            "parallelism": f"TSF heads sharded over {world} GPU(s)",
+            "collective": (("gloo via host (rehearsal)" if args.via_host else "RCCL") +
+                           " all-reduce(MAX) of GPI maxima [B,A] + int64 action key, broadcast of h and w_i "
+                           "from the active task's owner") if world > 1 else "none (1 rank)"}
+
+
 def traffic_from_profiles(kind: str, workload: str):
     """HBM bytes per launch of `kind` from a committed rocprofv3 --pmc pass (profiles/), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -299,6 +348,8 @@ def main():
     sharded = None
     if args.shard_steps > 0 and args.schedule == "all":
         sharded = bench_sharded(args, world, rank, device, barrier, dist)
+    elif args.shard_steps > 0 and args.schedule == "tsf":
+        sharded = bench_sharded_tsf(args, world, rank, device, barrier, dist)
 
     workload = (f"reacher17-{args.schedule}-T{T}-B{B}" if args.tsf_K is None else
                 f"hopper11-tsf{'-nf' + str(args.tsf_K) if args.tsf_K else ''}-T{T}-B{B}")

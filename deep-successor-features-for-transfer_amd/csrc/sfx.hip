@@ -711,7 +711,8 @@ int update_body(sfx_handle* h, int policy, const float* S, const int64_t* a, con
 
 // TSFDQN.update_successor (sfx_tsf.inc)
 int tsf_body(sfx_handle* h, int policy, const float* S, const int64_t* a, const float* r, const float* phi,
-             const float* S1, const float* gamma, int B, int use_gpi, float* losses, int64_t* next);
+             const float* S1, const float* gamma, int B, int use_gpi, float* losses, int64_t* next,
+             const float* xmax = nullptr);
 
 int launch_step_all(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, const float* lms_phi, const float* lms_r,
                     float lms_alpha, int rounds) {

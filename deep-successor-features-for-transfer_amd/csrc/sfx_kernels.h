@@ -1696,15 +1696,17 @@ __device__ __forceinline__ void qdots(int n, int d, const float* s_w, float* s_q
 }
 
 struct QmaxArgs {
-  int M, Tg, off, guess, rows, pad_;
-  float* X;  // [Tg][M][A]: max over this rank's heads of q[b, t, a] with w of policy i
+  int M, Tg, off, guess, rows, pol0, tsel, pad_;
+  float* X;  // [npol][M][A]: max over this rank's heads of q[b, t, a] with w of policy pol0 + blockIdx.x
+             // (tsel >= 0: only local head tsel, the own-ψ branch of TSF's next actions)
 };
 
 // K5: grid (Tg, ceil(M / rows)).  Head t (global off + t) enters policy i's GPI through role
 // `guess` if off + t < i (already updated in the reference's order) else R_S1.
 __global__ __launch_bounds__(256) void k_qmax(Geo G, QmaxArgs Q) {
-  const int i = blockIdx.x, tid = threadIdx.x;
-  const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, TA = T * Aa;
+  const int i = Q.pol0 + blockIdx.x, tid = threadIdx.x;
+  const int T = Q.tsel >= 0 ? 1 : G.T, t0 = Q.tsel >= 0 ? Q.tsel : 0;
+  const int Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, TA = T * Aa;
   const FDiv fTA = fdiv(TA), fA = fdiv(Aa);
   const int b0 = blockIdx.y * Q.rows;
   const int nb = Q.M - b0 < Q.rows ? Q.M - b0 : Q.rows;
@@ -1716,7 +1718,7 @@ __global__ __launch_bounds__(256) void k_qmax(Geo G, QmaxArgs Q) {
   __syncthreads();
   const int off = Q.off, guess = Q.guess;
   qdots(nb * TA, d, s_w, s_q, [&](int idx) {
-    const int bl = idx / fTA, rem = idx - bl * TA, t = rem / fA, a = rem - t * Aa;
+    const int bl = idx / fTA, rem = idx - bl * TA, t = t0 + rem / fA, a = rem - (t - t0) * Aa;
     return G.actp(off + t < i ? guess : R_S1, t, NLm) + (size_t)(b0 + bl) * O + a * d;
   });
   __syncthreads();
@@ -1725,7 +1727,7 @@ __global__ __launch_bounds__(256) void k_qmax(Geo G, QmaxArgs Q) {
     const float* qb = s_q + bl * TA + a;
     float mx = qb[0];
     for (int t = 1; t < T; ++t) mx = fmaxf(mx, qb[t * Aa]);
-    Q.X[((size_t)i * Q.M + b0 + bl) * Aa + a] = mx;
+    Q.X[((size_t)blockIdx.x * Q.M + b0 + bl) * Aa + a] = mx;
   }
 }
 

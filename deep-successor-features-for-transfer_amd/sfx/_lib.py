@@ -73,6 +73,10 @@ SIGNATURES = {
     "sfx_shard_verify": (_I, [_VP, _VP, _VP, _VP]),
     "sfx_shard_select": (_I, [_VP, _I, _I, _I, _VP]),
     "sfx_shard_finish": (_I, [_VP, _I]),
+    "sfx_shard_tsf_maxima": (_I, [_VP, _I, _VP, _I, _I, _VP]),
+    "sfx_shard_tsf_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _VP, _VP]),
+    "sfx_shard_tsf_shared": (_I, [_VP, _I, _VP, _I]),
+    "sfx_shard_tsf_select": (_I, [_VP, _VP, _I, _I, _VP]),
     "sfx_tsf_setup": (_I, [_VP, _I, _I, _F, _D, _D, _D, _D]),
     "sfx_tsf_load_g": (_I, [_VP, _I, _FP]),
     "sfx_tsf_get_g": (_I, [_VP, _I, _FP, _FP, _FP]),

@@ -110,7 +110,7 @@ class Replay:
         np.take(self.s1, idx, axis=0, out=st.h["s1"])
         np.take(self.phi, idx, axis=0, out=st.h["phi"])
         if "r" in st.h:
-            np.take(self.r, idx, out=st.h["r"])
+            np.take(self.r, idx, out=st.h["r"].reshape(-1))
         np.take(self.a, idx, out=st.h["a"])
         np.take(self.gamma, idx, out=st.h["gamma"])
         return True
@@ -411,6 +411,73 @@ class ShardedEnvLoop:
         batch = (d["s"], d["a"], d["phi"], d["s1"], d["gamma"]) if have else None
         self.sel = self.sharded.step(batch, self.task_index, d["phi1"], d["r1"], self.alpha_w, d["snext"],
                                      self.task_index, self.use_gpi)
+        self.s = s_next
+
+    def run(self, n: int):
+        for _ in range(n):
+            self.step()
+
+
+class ShardedTSFEnvLoop:
+    """TSF-DQN's env-step loop (tsfdqn.py next_sample + train_agent, active task) with the heads
+    sharded across ranks (sfx.shard.ShardedTSF; BASELINE config C5): every rank runs the same
+    env / replay stream (same seed), the GPI maxima and the action key are all-reduced, the
+    active task's owner updates and broadcasts h and w_i."""
+
+    def __init__(self, engine: SFEngine, T_glob: int, rank: int, all_reduce_max, broadcast, batch: int = 32,
+                 capacity: int = 1_000_000, gamma: float = 0.9, epsilon: float = 0.1, episode_len: int = 500,
+                 use_gpi: bool = True, seed: int = 1, p_end: float = 0.01):
+        from .shard import LibsfxTSFShardBackend, ShardedTSF
+
+        e = engine
+        self.eng, self.B, self.Tg = engine, batch, T_glob
+        self.gamma, self.epsilon, self.T_ep, self.use_gpi = gamma, epsilon, episode_len, use_gpi
+        self.backend = LibsfxTSFShardBackend(engine, T_glob, rank * engine.T, batch)
+        self.sharded = ShardedTSF(self.backend, T_glob, rank, e.A, all_reduce_max, broadcast)
+        self.rng = np.random.default_rng(seed)
+        self.tasks = [SynthHopper(e.n_s, e.A, e.d, t, self.rng, p_end) for t in range(T_glob)]
+        self.replay = Replay(capacity, e.n_s, e.d, self.rng)
+        self.st = Staging([("s", (batch, e.n_s), torch.float32), ("s1", (batch, e.n_s), torch.float32),
+                           ("phi", (batch, e.d), torch.float32), ("r", (batch, 1), torch.float32),
+                           ("a", (batch,), torch.int64), ("gamma", (batch,), torch.float32),
+                           ("snext", (1, e.n_s), torch.float32)], e.device)
+        self.gpi_counters = np.zeros((T_glob, T_glob), dtype=np.int64)
+
+    def set_task(self, index: int):
+        self.task_index, self.task = index, self.tasks[index]
+        self.steps_in_episode = 0
+        self.s = self.task.initialize()
+        self.st.h["snext"][0] = self.s
+        self.st.upload()
+        self.sel = self.sharded.select(self.st.d["snext"], index, self.use_gpi)
+
+    def prefill(self, n: int):
+        task = getattr(self, "task", self.tasks[0])
+        for _ in range(n):
+            s = task.initialize()
+            a = int(self.rng.integers(self.eng.A))
+            s1, phi, r, _ = task.transition(a)
+            self.replay.append(s, a, r, phi, s1, self.gamma)
+
+    def step(self):
+        c, a_greedy = self.sel
+        self.gpi_counters[self.task_index, c] += 1
+        a = int(self.rng.integers(self.eng.A)) if self.rng.random() <= self.epsilon else a_greedy
+        s1, phi, r, terminal = self.task.transition(a)
+        self.replay.append(self.s, a, r, phi, s1, 0.0 if terminal else self.gamma)
+        st = self.st
+        have = self.replay.sample_into(st, self.B)
+        self.steps_in_episode += 1
+        s_next = s1
+        if terminal or self.steps_in_episode >= self.T_ep:
+            s_next = self.task.initialize()
+            self.steps_in_episode = 0
+        st.h["snext"][0] = s_next
+        st.upload()
+        d = st.d
+        if have:
+            self.sharded.update(self.task_index, (d["s"], d["a"], d["r"], d["phi"], d["s1"], d["gamma"]), self.use_gpi)
+        self.sel = self.sharded.select(d["snext"], self.task_index, self.use_gpi)
         self.s = s_next
 
     def run(self, n: int):

@@ -162,3 +162,109 @@ class LibsfxShardBackend:
 
     def finish(self, rounds_run):
         self.check(self.lib.sfx_shard_finish(self.eng.handle, int(rounds_run)), "sfx_shard_finish")
+
+
+def broadcast_fn(group=None, via_host: bool = False) -> Callable[[torch.Tensor, int], None]:
+    """broadcast(t, src) in place over the default (or given) process group (via_host: stage
+    through CPU memory, for gloo groups driving device tensors)."""
+    import torch.distributed as dist
+
+    def bc(t: torch.Tensor, src: int):
+        if via_host:
+            h = t.cpu()
+            dist.broadcast(h, src=src, group=group)
+            t.copy_(h)
+        else:
+            dist.broadcast(t, src=src, group=group)
+
+    return bc
+
+
+class ShardedTSF:
+    """TSF-DQN's active-task step with the heads sharded across ranks (BASELINE config C5:
+    tsfdqn_nf.py, 32 source tasks over 4 GPUs).
+
+    Policy i's head, g_i and its optimizer state (Adam moments of ψ_i, w_i, g_i and of the
+    shared h, which are per task in the reference: tsfdqn.py:255-270) live with its owner
+    i // T_loc.  w (all T_glob rows) and h are replicated.  One TSFDQN.update_successor
+    (tsfdqn.py:588-709): the GPI maxima of the next actions are all-reduced (MAX) over the
+    ranks, the owner runs the update, then broadcasts h and w_i (Ph + d floats).  The env
+    action (get_Q_values: SF.GPI with w of the active task) is one all-reduced int64 key.
+    Drives a backend with the sfx_shard_tsf_* protocol (include/sfx.h)."""
+
+    def __init__(self, backend, T_glob: int, rank: int, A: int, all_reduce_max: Callable[[torch.Tensor], None],
+                 broadcast: Callable[[torch.Tensor, int], None]):
+        self.be, self.Tg, self.rank, self.A, self.ar, self.bc = backend, T_glob, rank, A, all_reduce_max, broadcast
+        self.T_loc = backend.T
+
+    def owner(self, i: int) -> int:
+        return i // self.T_loc
+
+    def update(self, i: int, batch, use_gpi: bool = True):
+        """batch = (s, a, r, phi, s1, gamma) (tsfdqn.py's transition tuple).  Returns the owner's
+        losses tensor (l1 + β l2, l1, l2) on the owner, None elsewhere."""
+        be, mine = self.be, self.owner(i) == self.rank
+        X = be.X(batch[0].shape[0])
+        if use_gpi:
+            be.maxima(i, batch[4], X, False)
+            self.ar(X)
+        elif mine:
+            be.maxima(i, batch[4], X, True)
+        losses = None
+        buf = be.shared_buf
+        if mine:
+            losses = be.update(i, batch, X)
+            be.pack(i, buf)
+        self.bc(buf, self.owner(i))
+        if not mine:
+            be.unpack(i, buf)
+        return losses
+
+    def select(self, s, task: int, use_gpi: bool = True):
+        """(GPI task c, greedy action a) for state s [1, n_s] with w of `task`."""
+        key = self.be.select(s, task, use_gpi)
+        self.ar(key)
+        return decode_key(int(key.item()), self.A)
+
+
+class LibsfxTSFShardBackend:
+    """sfx_shard_tsf_* on one SFEngine holding this rank's T_loc heads (tsf_setup done)."""
+
+    def __init__(self, engine, T_glob: int, head_offset: int, max_batch: int):
+        from ._lib import check, lib
+
+        self.eng, self.lib, self.check = engine, lib, check
+        self.Tg, self.off, self.T = T_glob, head_offset, engine.T
+        check(lib.sfx_shard_setup(engine.handle, T_glob, head_offset), "sfx_shard_setup")
+        engine._refresh_w_ptrs(T_glob)
+        dev = engine.device
+        self._X = torch.empty(max_batch * engine.A, device=dev)
+        self.shared_buf = torch.empty(engine.tsf_Ph + engine.d, device=dev)
+        self.key = torch.empty(1, dtype=torch.long, device=dev)
+        self.losses = torch.empty(3, device=dev)
+
+    def X(self, B: int):
+        return self._X[: B * self.eng.A]
+
+    def maxima(self, i, S1, X, own_only):
+        self.check(self.lib.sfx_shard_tsf_maxima(self.eng.handle, int(i), S1.data_ptr(), S1.shape[0], int(own_only),
+                                                 X.data_ptr()), "sfx_shard_tsf_maxima")
+
+    def update(self, i, batch, X):
+        s, a, r, phi, s1, g = batch
+        self._keep = batch
+        self.check(self.lib.sfx_shard_tsf_update(self.eng.handle, int(i), s.data_ptr(), a.data_ptr(), r.data_ptr(),
+                                                 phi.data_ptr(), s1.data_ptr(), g.data_ptr(), s.shape[0], X.data_ptr(),
+                                                 self.losses.data_ptr()), "sfx_shard_tsf_update")
+        return self.losses
+
+    def pack(self, i, buf):
+        self.check(self.lib.sfx_shard_tsf_shared(self.eng.handle, int(i), buf.data_ptr(), 0), "sfx_shard_tsf_shared")
+
+    def unpack(self, i, buf):
+        self.check(self.lib.sfx_shard_tsf_shared(self.eng.handle, int(i), buf.data_ptr(), 1), "sfx_shard_tsf_shared")
+
+    def select(self, s, task, use_gpi) -> torch.Tensor:
+        self.check(self.lib.sfx_shard_tsf_select(self.eng.handle, s.data_ptr(), int(task), int(bool(use_gpi)),
+                                                 self.key.data_ptr()), "sfx_shard_tsf_select")
+        return self.key

@@ -294,6 +294,29 @@ int sfx_tsf_update(sfx_t h, int policy, const float* S_dev, const int64_t* a_dev
                    const float* phi_dev, const float* S1_dev, const float* gamma_dev, int B, int use_gpi,
                    float* losses_dev, int64_t* next_dev);
 
+/* ---------------------------------------------------------------------------------------
+ * TSF-DQN with the source-task heads sharded across ranks (BASELINE config C5: tsfdqn_nf.py,
+ * 32 tasks over 4 GPUs).  After sfx_shard_setup and sfx_tsf_setup; `policy` and
+ * `task` are global indices; w (T_glob rows) and h are replicated, g_i and h's Adam moments
+ * live with the policy's owner.  One TSFDQN.update_successor(transitions, i, use_gpi)
+ * (tsfdqn.py:588-709) is
+ *   use_gpi: every rank sfx_shard_tsf_maxima(i, S1, own_only 0, X), all-reduce(X, MAX)
+ *   else:    the owner  sfx_shard_tsf_maxima(i, S1, own_only 1, X)
+ *   the owner: sfx_shard_tsf_update(i, ..., X, losses); sfx_shard_tsf_shared(i, buf, 0)
+ *   broadcast(buf [Ph + d], from the owner); the others sfx_shard_tsf_shared(i, buf, 1)
+ * and the env action (tsfdqn.py get_Q_values: SF.GPI with w of the active task):
+ *   sfx_shard_tsf_select(s, task, use_gpi, key); all-reduce(key, MAX); key decodes as for
+ *   sfx_shard_select.
+ * ------------------------------------------------------------------------------------- */
+/* X_dev [B][A]: max over this rank's heads (own_only: the policy's own head) of ψ_t(S1)·w_policy */
+int sfx_shard_tsf_maxima(sfx_t h, int policy, const float* S1_dev, int B, int own_only, float* X_dev);
+int sfx_shard_tsf_update(sfx_t h, int policy, const float* S_dev, const int64_t* a_dev, const float* r_dev,
+                         const float* phi_dev, const float* S1_dev, const float* gamma_dev, int B,
+                         const float* X_dev, float* losses_dev);
+/* unpack 0: buf_dev [Ph + d] <- (h, w_policy); 1: (h, w_policy) <- buf_dev */
+int sfx_shard_tsf_shared(sfx_t h, int policy, float* buf_dev, int unpack);
+int sfx_shard_tsf_select(sfx_t h, const float* s_dev, int task, int use_gpi, long long* key_dev);
+
 #ifdef __cplusplus
 }
 #endif

@@ -403,7 +403,7 @@ class TSFState(SFState):
 
 
 def tsf_update(st: TSFState, batch, i: int, *, use_gpi: bool = True, beta: float = 1.0,
-               lr_sf=1e-3, lr_w=1e-3, lr_g=1e-3, lr_h=1e-3, target_update_ev: int = 1000):
+               lr_sf=1e-3, lr_w=1e-3, lr_g=1e-3, lr_h=1e-3, target_update_ev: int = 1000, next_actions=None):
     """TSFDQN.update_successor (tsfdqn.py:588-709; tsfdqn_nf.py identical with planar g).
 
     φ̃ = (h(g_i(s)) + h(g_i(s1))) ⊙ φ ; targets = φ̃ + γ ψ⁻_i(s1)[a'] carry gradient into g_i, h;
@@ -416,7 +416,9 @@ def tsf_update(st: TSFState, batch, i: int, *, use_gpi: bool = True, beta: float
     idx = torch.arange(B)
     w_i = st.w[i]
     with torch.no_grad():
-        if use_gpi:
+        if next_actions is not None:  # given (sharded heads: from the all-reduced GPI maxima)
+            pass
+        elif use_gpi:
             q1, _ = gpi_w(psi_all(st.online, spec, s1), w_i)
             next_actions = gpi_next_actions(q1)
         else:

@@ -110,3 +110,54 @@ class OracleShardBackend:
             if self.st.since_target[t] >= self.ev:
                 self.st.target[t].copy_(self.st.online[t])
                 self.st.since_target[t] = 0
+
+
+class OracleTSFShardBackend:
+    """CPU backend of the sfx_shard_tsf_* protocol (sfx.shard.ShardedTSF): this rank's heads
+    [off, off + T_loc) with their g_i and optimizer state in an oracle TSFState (local indices),
+    the replicated w (T_glob rows) and h."""
+
+    def __init__(self, spec, gspec, online, target, g, h, w_all, off, target_update_ev=1000):
+        self.spec, self.off, self.ev = spec, off, target_update_ev
+        self.T, self.Tg = online.shape[0], w_all.shape[0]
+        self.w = w_all.clone()
+        self.st = R.TSFState(spec, online.clone(), target.clone(), self.w[off:off + self.T].clone(), gspec=gspec,
+                             g=g.clone(), h=h.clone())
+        self.shared_buf = torch.empty(h.numel() + spec.d)
+        self.losses = None
+
+    def X(self, B):
+        return torch.empty(B * self.spec.A)
+
+    def maxima(self, i, S1, X, own_only):
+        ts = [i - self.off] if own_only else range(self.T)
+        qs = [torch.matmul(R.forward(self.st.online[t], self.spec, S1)[0], self.w[i].view(-1, 1))[..., 0] for t in ts]
+        X.copy_(torch.stack(qs).max(dim=0).values.reshape(-1))
+
+    def update(self, i, batch, X):
+        loc = i - self.off
+        nxt = torch.argmax(X.view(batch[0].shape[0], self.spec.A), dim=1)
+        loss, l1, l2, _ = R.tsf_update(self.st, batch, loc, target_update_ev=self.ev, next_actions=nxt)
+        self.w[i] = self.st.w[loc]
+        self.losses = torch.tensor([float(loss), float(l1), float(l2)])
+        return self.losses
+
+    def pack(self, i, buf):
+        buf.copy_(torch.cat([self.st.h, self.w[i]]))
+
+    def unpack(self, i, buf):
+        n = self.st.h.numel()
+        self.st.h.copy_(buf[:n])
+        self.w[i] = buf[n:]
+
+    def select(self, s, task, use_gpi):
+        A = self.spec.A
+        best = -(1 << 63)
+        for t in range(self.T):
+            tg = self.off + t
+            if not use_gpi and tg != task:
+                continue
+            q = torch.matmul(R.forward(self.st.online[t], self.spec, s.reshape(1, -1))[0], self.w[task].view(-1, 1))[0, :, 0]
+            for a in range(A):
+                best = max(best, encode_key(float(q[a]), tg, a, A))
+        return torch.tensor([best], dtype=torch.long)
