@@ -24,6 +24,7 @@
 #include <map>
 #include <random>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "sfx_kernels.h"
@@ -372,6 +373,10 @@ int tdg_variant(const sfx_handle* h) {
 bool can_fuse_tdg(const sfx_handle* h) { return tdg_variant(h) != 0; }
 
 struct BwdExtra {
+  // called right after backward launch `hook_after` (0 = the first, fused-TD launch); TSF forks
+  // its own backward onto a side stream there (the ψ loss tail and output gradient are final)
+  std::function<int()> hook;
+  int hook_after = -1;
   int inc_step = 1;
   bool fuse_v0 = false;  // post-update forward of layer 0 into vRole (rows S1 ++ s_next)
   int vRole = R_V;
@@ -466,6 +471,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
       launch(h, K_BWD, by, k_bwd_tdg<4, 4>, grid, dim3(256), h->G, A);
     else
       launch(h, K_BWD, by, k_bwd, grid, dim3(256), h->G, A);
+    if (ex.hook && li == ex.hook_after && !h->rec) RC(ex.hook());
   }
   A.na = 0;
   A.tdg = 0;
@@ -490,6 +496,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), k_bwd,
          A.xcd ? dim3(8 * cdiv(nhead, 8) * ntile) : dim3(ntile, nhead), dim3(256), h->G, A);
   LAUNCHCHK();
+  if (ex.hook && ex.hook_after >= h->NL - 1) RC(ex.hook());  // fewer launches than hook_after + 1
   return SFX_OK;
 }
 
