@@ -377,15 +377,16 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A) {
   const float* snap = A.snap;
   const int step = *A.step;
   const FDiv fG = fdiv(G);
-  // LDS: daff [0, 4096) | role operands [4096, 12288) | φ̃ rows [12288, 16384) | ψ gradient rows [16384, 20480)
+  // LDS: daff [0, 4096) | role operands [4096, 12288) | φ̃ rows [12288, 16384) | ψ gradient rows
+  // [16384, 20480) | g-Linear dg [20480, 21504)
   float* s_da = sm;
   float* s_tp = sm + 3 * (TSF_LDS / 2);
   float* s_gc = sm + 4 * (TSF_LDS / 2);
   const bool wrole = role == A.nh + A.nlin;
   float* s_gf = sm + TSF_LDS / 2;       // h role: [2B][G]
   float* s_whs = sm + TSF_LDS / 2;      // g-Linear role: [d][TSF_QS] pre-step W_h columns
-  float* s_zk = s_whs + TSF_LDS / 2;    // g-Linear role: [2B][n_s] z_K
-  float* s_dg = s_zk + 2048;            // g-Linear role: [B][TSF_QS]
+  float* s_zk = s_whs + TSF_LDS / 2;    // g-Linear role: [2B][n_s] z_K (<= 4096)
+  float* s_dg = sm + 5 * (TSF_LDS / 2); // g-Linear role: [B][TSF_QS] (after the φ̃ / gradient rows)
   const int q0 = (role - A.nh) * TSF_QS, nq = min(TSF_QS, G - q0);
   if (!wrole && role < A.nh) {
     glds(s_gf, R2 * G, [&](int j) { return A.gfeat + j; });

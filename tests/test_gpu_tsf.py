@@ -100,3 +100,49 @@ def test_tsf_full_c3_vs_oracle(K):
         rel_close(eng.get_w(t)[0], st.w[t], rtol=1e-3, atol=1e-6)
     params_close(eng.tsf_get_h(), st.h, 4e-3)
     eng.close()
+
+
+@pytest.mark.parametrize("n_s,B,K,G,d,fork", [(20, 13, 5, 24, 7, "1"), (9, 7, 9, 33, 5, "0"), (30, 64, 2, 16, 12, "1")])
+def test_tsf_ragged_shapes_vs_oracle(n_s, B, K, G, d, fork, monkeypatch):
+    """Shapes that exercise the kernels' edges: n_s > 16 (32 lanes per flow row), batches that
+    leave partial row groups, d not a multiple of 4, G not a multiple of the g-Linear column
+    block, the largest batch (64), with and without the side-stream fork (SFX_TSF_FORK)."""
+    from sfx.engine import SFEngine
+    from sfx.init import reference_heads
+
+    monkeypatch.setenv("SFX_TSF_FORK", fork)
+    T = 3
+    spec = R.Spec(n_s, 24, 5, d, ("relu", "relu"))
+    gs = R.GSpec(n_s, G, K)
+    online, w = reference_heads(T, spec.n_s, spec.H, spec.A, spec.d, spec.acts, seed=2)
+    gen = torch.Generator().manual_seed(8)
+    g = torch.empty(T, gs.P).uniform_(-0.3, 0.3, generator=gen)
+    h = torch.empty(d * G + d).uniform_(-0.2, 0.2, generator=gen)
+    st = R.TSFState(spec, online.clone(), online.clone(), w.clone(), gspec=gs, g=g.clone(), h=h.clone())
+    eng = SFEngine(T, spec.n_s, spec.H, spec.A, spec.d, spec.acts, max_batch=64)
+    eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
+    eng.set_target_update_ev(3)
+    eng.tsf_setup(G, K, 0.5, 1e-3, 0.0, 1e-3, 0.0)
+    for t in range(T):
+        eng.load_head(t, online[t], 0)
+        eng.load_head(t, online[t], 1)
+        eng.load_w(t, w[t])
+        eng.tsf_load_g(t, g[t])
+    eng.tsf_load_h(h)
+    nxt = torch.empty(B, dtype=torch.int64, device="cuda")
+    for j, i in enumerate((1, 0, 2, 1, 1)):
+        s, s1 = torch.randn(B, n_s, generator=gen), torch.randn(B, n_s, generator=gen)
+        a = torch.randint(0, spec.A, (B,), generator=gen)
+        phi, r = torch.rand(B, d, generator=gen), torch.rand(B, 1, generator=gen)
+        gamma = torch.where(torch.rand(B, generator=gen) < 0.2, 0.0, 0.9)
+        loss, l1, l2, na = R.tsf_update(st, (s, a, r, phi, s1, gamma), i, use_gpi=j != 2, beta=0.5,
+                                        target_update_ev=3)
+        lo = eng.tsf_update(i, s, a, r, phi, s1, gamma, use_gpi=j != 2, next_actions=nxt)
+        assert torch.equal(nxt.cpu(), na), f"update {j}: next actions differ"
+        rel_close(lo, [float(loss), float(l1), float(l2)], rtol=2e-4, atol=1e-7)
+    params_close(torch.stack([eng.get_head(t, 0) for t in range(T)]), st.online, 5e-3)
+    params_close(torch.stack([eng.get_head(t, 1) for t in range(T)]), st.target, 5e-3)
+    params_close(torch.stack([eng.tsf_get_g(t)[0] for t in range(T)]), st.g, 5e-3)
+    params_close(eng.tsf_get_h(), st.h, 5e-3)
+    rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-3, atol=1e-6)
+    eng.close()
