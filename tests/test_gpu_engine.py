@@ -227,3 +227,55 @@ def test_lms_vs_oracle():
         eng.lms(1, phi, r.reshape(1), 0.05)
     rel_close(eng.get_w(1)[0], wr.reshape(-1), rtol=1e-5, atol=1e-7)
     eng.close()
+
+
+RAGGED = [
+    # n_s, H, A, d, acts, B
+    (17, 64, 7, 8, ("relu", "relu"), 1),
+    (17, 64, 7, 8, ("relu", "relu"), 64),
+    (11, 48, 27, 50, ("relu", "relu"), 45),
+    (6, 40, 5, 3, ("tanh",), 200),
+    (33, 96, 4, 12, ("relu", "relu", "relu"), 33),
+    (70, 32, 3, 17, ("relu", "relu"), 16),
+]
+
+
+@pytest.mark.parametrize("n_s,H,A,d,acts,B", RAGGED)
+def test_ragged_shapes_update_vs_oracle(n_s, H, A, d, acts, B):
+    """Edge geometries of the SF kernels: a single row, batches past one 32-row tile (up to
+    200), wide ψ outputs (A·d = 1350), one and three hidden layers, tanh, odd d, fan-ins past the
+    fused layer-0 limit (n_s = 70).  Active-task updates (± GPI, with l2) and all-task steps vs
+    the oracle, parameters after every step."""
+    from sfx.init import reference_heads
+
+    T = 3
+    spec = R.Spec(n_s, H, A, d, acts)
+    online, w = reference_heads(T, n_s, H, A, d, acts, seed=4)
+    eng = engine_for(spec, T, max_batch=max(B, 1))
+    for t in range(T):
+        eng.load_head(t, online[t], 0)
+        eng.load_head(t, online[t], 1)
+        eng.load_w(t, w[t])
+    st = R.SFState(spec, online.clone(), online.clone(), w.clone())
+    gen = torch.Generator().manual_seed(9)
+
+    def batch():
+        return (torch.randn(B, n_s, generator=gen), torch.randint(0, A, (B,), generator=gen),
+                torch.rand(B, 1, generator=gen), torch.rand(B, d, generator=gen), torch.randn(B, n_s, generator=gen),
+                torch.where(torch.rand(B, generator=gen) < 0.2, 0.0, 0.9))
+
+    nxt = torch.empty(B, dtype=torch.long, device="cuda")
+    for k, (i, use_gpi) in enumerate(((1, True), (2, False), (0, True))):
+        s, a, r, phi, s1, gamma = batch()
+        loss, l1, l2, na = R.sf_update(st, (s, a, r, phi, s1, gamma), i, use_gpi=use_gpi)
+        lo = eng.update(i, s, a, r, phi, s1, gamma, use_gpi=use_gpi, next_actions=nxt)
+        assert torch.equal(nxt.cpu(), na), f"update {k}: next actions differ"
+        rel_close(lo, [float(loss), float(l1), float(l2)], rtol=2e-4, atol=1e-7)
+    params_close(torch.stack([eng.get_head(t) for t in range(T)]), st.online, 3e-3)
+    rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-3, atol=1e-6)
+    for _ in range(2):
+        s, a, r, phi, s1, gamma = batch()
+        R.deep_all_task_step(st, (s, a, phi, s1, gamma))
+        eng.update_all(s, a, phi, s1, gamma)
+    params_close(torch.stack([eng.get_head(t) for t in range(T)]), st.online, 5e-3)
+    eng.close()
