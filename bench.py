@@ -11,6 +11,11 @@ features/deep.py): every one of the 8 heads is updated per env step.
 Multi-GPU: one process per GPU (torchrun).  Weak scaling: each rank owns 8 heads; ranks
 run independent replicas of the env/replay stream.
 
+`other_workloads` (N=1 only; --no-other skips it) times the other one-GPU BASELINE configs through
+the same native runner: the active-task schedule of sfdqn.py (C2 shape), Hopper TSF-DQN (C3) and
+TSF-DQN with 100 planar layers (C5's per-GPU work); `--workload hopper-tsf[-nf]` makes one of
+them the measured line instead.
+
 Prints ONE JSON line on rank 0.  `roofline` is for the dominant kernel kind, measured live
 in this process with HIP events (libsfx instrumentation, eager launches) right after the
 timed region; `cpu_baseline` times the CPU oracle (oracle/ref_cpu.py) on a bounded sample
@@ -59,6 +64,8 @@ def parse():
     p.add_argument("--prof-steps", type=int, default=50)
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-other", dest="other", action="store_false",
+                   help="skip the other one-GPU configs (active-task C2, TSF C3, TSF-NF) reported beside the headline")
     p.add_argument("--shard-steps", type=int, default=400,
                    help="also time the north-star sharded mode (heads split over ranks, RCCL all-reduce-max "
                         "GPI) for this many env steps; 0 skips it")
@@ -249,6 +256,51 @@ def bench_sharded_tsf(args, world, rank, device, barrier, dist):
                            "from the active task's owner") if world > 1 else "none (1 rank)"}
 
 
+def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) -> dict:
+    """The other BASELINE configs that fit one GPU, each through the native runner on its own
+    engine (reported beside the headline, never as `value`): the active-task schedule of
+    sfdqn.py on the C2 shape, Hopper TSF-DQN (C3) and TSF-DQN with 100 planar layers (C5's
+    per-GPU work).  env-steps/s of the same timed loop as the headline."""
+    from sfx.engine import SFEngine
+    from sfx.init import reference_heads
+    from sfx.runner import NativeEnvLoop
+
+    out = {}
+    for name, sched, K in (("reacher17-active-T8-B32", "active", None), ("hopper11-tsf-T16-B32", "tsf", 0),
+                           ("hopper11-tsf-nf100-T16-B32", "tsf", 100)):
+        sh = SHAPE if K is None else TSF_SHAPE
+        T = 8 if K is None else 16
+        eng = SFEngine(T, sh["n_s"], sh["H"], sh["A"], sh["d"], sh["acts"], max_batch=args.batch, device=device)
+        if K is None:
+            online, w = reference_heads(T, sh["n_s"], sh["H"], sh["A"], sh["d"], sh["acts"], seed=0)
+        else:
+            online, w, g, h = tsf_problem(T, K, seed=0)
+            eng.tsf_setup(sh["G"], K, 1.0, 1e-3, 0.0, 1e-3, 0.0)
+            for t in range(T):
+                eng.tsf_load_g(t, g[t])
+            eng.tsf_load_h(h)
+        for t in range(T):
+            eng.load_head(t, online[t], 0)
+            eng.load_head(t, online[t], 1)
+            eng.load_w(t, w[t])
+        eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
+        eng.set_target_update_ev(1000)
+        loop = NativeEnvLoop(eng, batch=args.batch, seed=1, schedule=sched, p_end=0.0 if K is None else 0.01)
+        loop.prefill(1000)
+        loop.set_task(0)
+        loop.run(warmup)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        loop.run(steps)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        out[name] = {"value": round(steps / dt, 2), "unit": "env steps/s", "ms_per_step": round(1000.0 * dt / steps, 4),
+                     "steps": steps}
+        loop.close()
+        eng.close()
+    return out
+
+
 def traffic_from_profiles(kind: str, workload: str):
     """HBM bytes per launch of `kind` from a committed rocprofv3 --pmc pass (profiles/), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -375,6 +427,9 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, args.cpu_seconds)
+        other = None
+        if world == 1 and args.other and args.tsf_K is None and args.schedule == "all":
+            other = bench_other_workloads(args, device)
         out = {
             "metric": METRIC if args.tsf_K is None else
                       f"env steps/sec, Hopper 16-task TSF-DQN{' + planar-flow g' if args.tsf_K else ''} (BASELINE config "
@@ -393,6 +448,7 @@ def main():
             "roofline": roofline,
             "speculation": spec_stats,
             "sharded": sharded,
+            "other_workloads": other,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
