@@ -531,6 +531,7 @@ struct TdgArgs {
 };
 
 __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
+  PROBE_T(pt0);
   const int b = blockIdx.x, pol = A.pol0 + blockIdx.y, tid = threadIdx.x;
   const int T = G.T, Aa = G.A, d = G.d, O = G.O, M = A.M, NLm = G.lastOff;
   __shared__ float s_w[DMAX];
@@ -612,6 +613,7 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
     for (int k = 0; k < d; ++k) s = __fadd_rn(s, s_sq[k]);
     G.rowloss[(long long)pol * MMAX + b] = s;
   }
+  PROBE_REC(17, pt0);
 }
 
 // -------------------------------------------------------------------------------------
@@ -1415,7 +1417,11 @@ __device__ void gpi_row(const Geo& G, const GpiArgs& A, int b) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_gpi(Geo G, GpiArgs A) { gpi_row(G, A, blockIdx.x); }
+__global__ __launch_bounds__(256) void k_gpi(Geo G, GpiArgs A) {
+  PROBE_T(pt0);
+  gpi_row(G, A, blockIdx.x);
+  PROBE_REC(16, pt0);
+}
 
 // -------------------------------------------------------------------------------------
 // K5  Verification of a speculative round of the all-task update + action selection.
@@ -1633,7 +1639,9 @@ __global__ __launch_bounds__(256) void k_gate(GateArgs g) {
 
 
 __global__ void k_publish(const int64_t* sel, const int* flag, HostResult* out, const long long* dctr) {
+  PROBE_T(pt0);
   if (threadIdx.x == 0) publish_result(sel, flag, out, dctr);
+  PROBE_REC(18, pt0);
 }
 
 }  // namespace sfx

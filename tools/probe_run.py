@@ -18,12 +18,16 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "deep-successor-features-for-transfer_a
 import numpy as np
 import torch
 
-KIDS = {1: "fwd", 2: "fwdL0", 3: "bwd_tdg", 4: "dx", 5: "dw", 6: "dw_v0", 7: "round", 8: "ver", 9: "gate"}
+KIDS = {1: "fwd", 2: "fwdL0", 3: "bwd_tdg", 4: "dx", 5: "dw", 6: "dw_v0", 7: "round", 8: "ver", 9: "gate",
+        10: "tsf_fwd", 11: "tsf_flows", 12: "tsf_h", 13: "tsf_glin", 14: "tsf_w", 15: "tsf_flow", 16: "gpi", 17: "tdg",
+        18: "publish"}
 
 
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
-    from bench import SHAPE
+    # workload: all (default, the headline), active, tsf, tsf-nf
+    work = sys.argv[2] if len(sys.argv) > 2 else "all"
+    from bench import SHAPE, TSF_SHAPE, tsf_problem
     from sfx import _lib
     from sfx.engine import SFEngine
     from sfx.init import reference_heads
@@ -31,16 +35,27 @@ def main():
 
     lib = _lib.lib
     lib.sfx_probe_dump.argtypes = [C.c_void_p, C.c_int]
-    T, B = 8, 32
-    eng = SFEngine(T, SHAPE["n_s"], SHAPE["H"], SHAPE["A"], SHAPE["d"], SHAPE["acts"], max_batch=B)
-    online, w = reference_heads(T, SHAPE["n_s"], SHAPE["H"], SHAPE["A"], SHAPE["d"], SHAPE["acts"], seed=0)
+    B = 32
+    K = {"tsf": 0, "tsf-nf": 100}.get(work)
+    sh = SHAPE if K is None else TSF_SHAPE
+    T = 8 if K is None else 16
+    eng = SFEngine(T, sh["n_s"], sh["H"], sh["A"], sh["d"], sh["acts"], max_batch=B)
+    if K is None:
+        online, w = reference_heads(T, sh["n_s"], sh["H"], sh["A"], sh["d"], sh["acts"], seed=0)
+    else:
+        online, w, g, h = tsf_problem(T, K, seed=0)
+        eng.tsf_setup(sh["G"], K, 1.0, 1e-3, 0.0, 1e-3, 0.0)
+        for t in range(T):
+            eng.tsf_load_g(t, g[t])
+        eng.tsf_load_h(h)
     for t in range(T):
         eng.load_head(t, online[t], 0)
         eng.load_head(t, online[t], 1)
         eng.load_w(t, w[t])
     eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
     eng.set_target_update_ev(1000)
-    loop = NativeEnvLoop(eng, batch=B, seed=1)
+    loop = NativeEnvLoop(eng, batch=B, seed=1, schedule="all" if work == "all" else ("active" if work == "active" else "tsf"),
+                         p_end=0.0 if K is None else 0.01)
     loop.prefill(1000)
     loop.set_task(0)
     dt = np.dtype([("kid", "<u4"), ("blk", "<u4"), ("t", "<u8", (10,))])
