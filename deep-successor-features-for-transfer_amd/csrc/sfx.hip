@@ -153,6 +153,11 @@ struct sfx_handle {
   // k_round (one launch per speculative round, see sfx_kernels.h); SFX_ROUND=1 turns it on
   bool use_round = false;
   unsigned* round_ctr = nullptr;  // [T] per-head arrival counters
+  // split-N dX of wide layers (run_bwd): partial tiles and per-(head, tile) arrival counters
+  int dxs_max = 1, dx_ntile = 1;
+  float* dxpart = nullptr;
+  unsigned* dxctr = nullptr;
+  bool split_dx = true;  // SFX_SPLIT_DX=0: one workgroup reduces all of N
   struct RoundRec {               // launch arguments recorded instead of launched
     std::vector<BwdArgs> b;
     std::vector<FwdArgs> f;
@@ -451,6 +456,16 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     const double by = nhead * (dx_bytes(l) + (l + 1 <= h->NL - 1 ? dw_bytes(l + 1) : 0.0)) + (A.tdg ? tdg_bytes : 0.0);
     A.ra = geo(l);
     A.na = cdiv(M, 32) * cdiv(h->L[l].K, 16);
+    // wide layers: the dX tiles split N in <= 256-wide chunks over workgroups (not in a fused
+    // TD launch, not in k_round's recorded launches)
+    A.dxs = 1;
+    if (!A.tdg && !h->rec && h->split_dx && h->dxpart && h->L[l].N > DX_SPLIT_N && M <= 32 * cdiv(h->Mmax, 32) &&
+        nhead <= h->T) {
+      A.dxs = cdiv(h->L[l].N, DX_SPLIT_N);
+      A.dxpart = h->dxpart;
+      A.dxctr = h->dxctr;
+      A.na *= A.dxs;
+    }
     if (l + 1 <= h->NL - 1) {
       A.rb = geo(l + 1);
       A.nb = dw_tiles(l + 1);
@@ -474,6 +489,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     if (ex.hook && li == ex.hook_after && !h->rec) RC(ex.hook());
   }
   A.na = 0;
+  A.dxs = 1;
   A.tdg = 0;
   A.rb = geo(1);
   A.nb = dw_tiles(1);
@@ -598,7 +614,7 @@ void free_all(sfx_handle* h) {
   for (hipEvent_t e : h->prof_pool) (void)hipEventDestroy(e);
   for (void* p : {(void*)h->online, (void*)h->target, (void*)h->am, (void*)h->av, (void*)h->w, (void*)h->wm,
                   (void*)h->wv, (void*)h->step, (void*)h->adamc, (void*)h->round_ctr, (void*)h->act, (void*)h->dz, (void*)h->rowloss, (void*)h->spec_next,
-                  (void*)h->dout})
+                  (void*)h->dout, (void*)h->dxpart, (void*)h->dxctr})
     if (p) (void)hipFree(p);
   if (h->hout) (void)hipHostFree(h->hout);
   if (h->cap) (void)hipStreamDestroy(h->cap);
@@ -805,6 +821,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->fwd_waves = efw && std::atoi(efw) == 4 ? 4 : 8;
   const char* el0 = std::getenv("SFX_FUSE_L0");
   h->fuse_l0 = !(el0 && el0[0] == '0');
+  const char* esd = std::getenv("SFX_SPLIT_DX");
+  h->split_dx = !(esd && esd[0] == '0');
   int off = 0, ptorch = 0;
   for (int l = 0; l < h->NL; ++l) {
     LayerGeo Lr{};
@@ -855,6 +873,19 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   alloc((void**)&h->step, sizeof(int) * T);
   alloc((void**)&h->adamc, sizeof(AdamC) * T);
   alloc((void**)&h->round_ctr, sizeof(unsigned) * T);
+  {  // split-N dX: every layer's N split into <= 256-wide chunks, tiles of 32 rows x 16 columns
+    int nmax = 0, kmax = 0;
+    for (const LayerGeo& L : h->L) {
+      nmax = std::max(nmax, L.N);
+      kmax = std::max(kmax, L.K);
+    }
+    h->dxs_max = std::max(1, cdiv(nmax, DX_SPLIT_N));
+    h->dx_ntile = cdiv(max_batch, 32) * cdiv(kmax, 16);
+    if (h->dxs_max > 1) {
+      alloc((void**)&h->dxpart, sizeof(float) * 512 * (size_t)T * h->dx_ntile * h->dxs_max);
+      alloc((void**)&h->dxctr, sizeof(unsigned) * (size_t)T * h->dx_ntile);
+    }
+  }
   alloc((void**)&h->act, sizeof(float) * (size_t)NROLE * T * h->actSize);
   alloc((void**)&h->dz, sizeof(float) * (size_t)T * h->actSize);
   alloc((void**)&h->rowloss, sizeof(float) * (size_t)T * MMAX);

@@ -32,6 +32,7 @@ constexpr int OMAX = 4096;    // A*d (row of a ψ output) held in LDS
 constexpr int DMAX = 256;     // feature dimension d
 constexpr int MMAX = 1024;    // rows of one update
 constexpr int KFUSE = 64;     // layer-0 fan-in up to which the post-update forward is fused
+constexpr int DX_SPLIT_N = 256;  // dX of a layer wider than this splits N over workgroups
 constexpr int VFUSE = 4096;   // (rows x fan-in) of that forward's input, staged in LDS
 constexpr int TQF = 4096;     // 32 rows x (T*A) q values / 32 rows x A*d gradients of the fused TD target
 
@@ -648,8 +649,13 @@ struct BwdArgs {
   int tdg_poloff, pad3_;
   int* flag;
   int fuse_v0, vM, vOff, act0;  // fused forward: rows (S1 ++ s_next), layer-0 offset, layer-0 act
-  int vRole, pad_;              // role block the fused forward writes
+  int vRole, dxs;               // role block the fused forward writes; dX split over N (1: none)
   unsigned long long mask;
+  // dxs > 1 (wide layers): the dX tiles of one (head, tile) split N over dxs workgroups; each
+  // writes its partial tile to dxpart (coherent stores), arrives on dxctr[head][tile], and the
+  // last to arrive sums the partials in split order (deterministic) and stores dZ_{l-1}
+  float* dxpart;
+  unsigned* dxctr;
   RoleGeo ra, rb, rc;  // dX role (layer la), dW roles (lb, lc)
   AdamHP hp, hpw;
   const float* x0;     // layer-0 input (the minibatch states S)
@@ -827,6 +833,11 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
   const RoleGeo L = A.ra;
   const int N = L.N, K = L.K, M = A.M;
   const int ntk = (K + 15) >> 4;
+  // split of N (TDG launches never split: their N <= 128)
+  const int split = TDG ? 0 : tile % A.dxs;
+  tile = TDG ? tile : tile / A.dxs;
+  const int nchunk = ((N + A.dxs - 1) / A.dxs + 63) & ~63;
+  const int nbeg = split * nchunk, nend = min(N, nbeg + nchunk);
   const int k0 = (tile % ntk) * 16, m0 = (tile / ntk) * 32;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
   const float* W = G.online + G.slot_off(rslot(A.mask, head), head) + L.wOff;
@@ -889,13 +900,13 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
   } else {
     const float* dZ = G.dzp(head, L.dzOff);
     const bool vec = (N & 63) == 0;
-    for (int nc = wave * 64; nc < N; nc += 256) {
+    for (int nc = nbeg + wave * 64; nc < nend; nc += 256) {
       const int nb = nc + g * 16;
       float a0[16], a1[16], bw[16];
-      load16u<C>(a0, dZ + (size_t)ma * N, nb, N, oka, vec);
-      load16u<C>(a1, dZ + (size_t)mb * N, nb, N, okb, vec);
+      load16u<C>(a0, dZ + (size_t)ma * N, nb, nend, oka, vec);
+      load16u<C>(a1, dZ + (size_t)mb * N, nb, nend, okb, vec);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) bw[j] = (okk && nb + j < N) ? W[(size_t)(nb + j) * K + kk] : 0.f;
+      for (int j = 0; j < 16; ++j) bw[j] = (okk && nb + j < nend) ? W[(size_t)(nb + j) * K + kk] : 0.f;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         acc0 = mfma4(a0[j], bw[j], acc0);
@@ -907,6 +918,44 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
   red[wave][0][lane] = acc0;
   red[wave][1][lane] = acc1;
   __syncthreads();
+  if (!TDG && A.dxs > 1) {  // partial tile -> dxpart; the last of the dxs splits finishes it
+    const int ntile = ((M + 31) >> 5) * ntk;
+    const size_t pt = ((size_t)(head - A.head0) * ntile + tile) * A.dxs;
+    __shared__ int s_last;
+    if (threadIdx.x < 128) {
+      floatx4 v = red[0][s][Lx];
+      v += red[1][s][Lx];
+      v += red[2][s][Lx];
+      v += red[3][s][Lx];
+      float* o = A.dxpart + ((pt + split) * 128 + threadIdx.x) * 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) stc<true>(o + i, v[i]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned* ctr = A.dxctr + (size_t)(head - A.head0) * ntile + tile;
+      const unsigned prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = prev == (unsigned)A.dxs - 1;
+      if (s_last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_last || threadIdx.x >= 128) return;
+    floatx4 v = {0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < A.dxs; ++q) {
+      const float* o = A.dxpart + ((pt + q) * 128 + threadIdx.x) * 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = __fadd_rn(v[i], ldc<true>(o + i));
+    }
+    if (col < K) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + 16 * s + (Lx >> 4) * 4 + i;
+        if (row < M) stc<C>(out + (size_t)row * K + col, act_bwd(v[i], xin[i], L.actIn));
+      }
+    }
+    return;
+  }
   if (threadIdx.x < 128) {
     floatx4 v = red[0][s][Lx];
     v += red[1][s][Lx];
