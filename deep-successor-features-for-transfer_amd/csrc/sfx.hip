@@ -158,6 +158,7 @@ struct sfx_handle {
   float* dxpart = nullptr;
   unsigned* dxctr = nullptr;
   bool split_dx = true;  // SFX_SPLIT_DX=0: one workgroup reduces all of N
+  bool gemv_fwd = true;  // SFX_GEMV_FWD=0: wide layers of a <= 4-row forward through the MFMA tiles
   struct RoundRec {               // launch arguments recorded instead of launched
     std::vector<BwdArgs> b;
     std::vector<FwdArgs> f;
@@ -311,7 +312,11 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     if (l0) by += 4.0 * ninst * ((double)h->L[0].N * h->L[0].K + h->L[0].N + (double)M * h->L[0].K);
     // the vector path needs K % (256/NW) == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
     const bool aligned = l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0);
-    if (h->rec) {  // k_round's post-update forward runs 4-wave tiles
+    const bool gemv = !l0 && !h->rec && h->gemv_fwd && M <= GEMV_M && L.N >= GEMV_N && L.K % 16 == 0 &&
+                      (l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0));
+    if (gemv) {
+      launch(h, K_FWD, by, k_fwd_gemv, dim3(cdiv(L.N, 64), ninst), dim3(256), h->G, F);
+    } else if (h->rec) {  // k_round's post-update forward runs 4-wave tiles
       h->rec->f.push_back(F);
       h->rec->bytes.push_back(by);
       h->rec->fvec = h->rec->fvec && (L.K % 64) == 0 && aligned && !l0;
@@ -823,6 +828,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->fuse_l0 = !(el0 && el0[0] == '0');
   const char* esd = std::getenv("SFX_SPLIT_DX");
   h->split_dx = !(esd && esd[0] == '0');
+  const char* egv = std::getenv("SFX_GEMV_FWD");
+  h->gemv_fwd = !(egv && egv[0] == '0');
   int off = 0, ptorch = 0;
   for (int l = 0; l < h->NL; ++l) {
     LayerGeo Lr{};

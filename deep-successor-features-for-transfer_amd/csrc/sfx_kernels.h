@@ -32,6 +32,8 @@ constexpr int OMAX = 4096;    // A*d (row of a ψ output) held in LDS
 constexpr int DMAX = 256;     // feature dimension d
 constexpr int MMAX = 1024;    // rows of one update
 constexpr int KFUSE = 64;     // layer-0 fan-in up to which the post-update forward is fused
+constexpr int GEMV_N = 512;   // layer width from which a forward of <= GEMV_M rows runs k_fwd_gemv
+constexpr int GEMV_M = 4;
 constexpr int DX_SPLIT_N = 256;  // dX of a layer wider than this splits N over workgroups
 constexpr int VFUSE = 4096;   // (rows x fan-in) of that forward's input, staged in LDS
 constexpr int TQF = 4096;     // 32 rows x (T*A) q values / 32 rows x A*d gradients of the fused TD target
@@ -502,6 +504,66 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
     if (F.lms_head >= 0) lms_block(G, F);
   }
   PROBE_REC(L0 ? 2 : 1, pt0);
+}
+
+// K1b  Forward of a wide layer (N >= GEMV_N) for a few rows (M <= GEMV_M: the B = 1 action
+// choice): GEMV-shaped, no MFMA.  Grid (ceil(N / 64), n_inst), 256 threads; a wave owns 16
+// output columns, 4 lanes per column each summing K / 4 products (lane q takes k = 16 i + 4 q
+// .. + 3, so the 4 lanes of a column read 64 contiguous bytes of its W row per step), a quad
+// DPP butterfly finishes the dot.  Every W and X load of a lane is issued before the first FMA.
+__global__ __launch_bounds__(256) void k_fwd_gemv(Geo G, FwdArgs F) {
+  PROBE_T(pt0);
+  int y = blockIdx.y;
+  FwdGroup grp = F.g0;
+  if (F.ngroups > 1 && y >= grp.n) { y -= grp.n; grp = F.g1; }
+  if (F.ngroups > 2 && y >= grp.n) { y -= grp.n; grp = F.g2; }
+  if (F.ngroups > 3 && y >= grp.n) { y -= grp.n; grp = F.g3; }
+  const int head = grp.head0 + y;
+  const int M = F.M, N = F.N, K = F.K;
+  const float* P = grp.which == P_TARGET ? G.target + (long long)head * G.P
+                                         : G.online + G.slot_off(rslot(F.mask, head) ^ (grp.which == P_NEW), head);
+  const float* X = F.xOff < 0 ? (grp.xsel == 1 ? F.xa : F.xb) : G.actp(grp.role, head, F.xOff);
+  float* Y = G.actp(grp.role, head, F.yOff);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane & 3;
+  const int n = blockIdx.x * 64 + wave * 16 + (lane >> 2);
+  const bool okn = n < N;
+  const float* wr = P + F.wOff + (size_t)(okn ? n : 0) * K;
+  float acc[GEMV_M];
+#pragma unroll
+  for (int m = 0; m < GEMV_M; ++m) acc[m] = 0.f;
+  // K in chunks of 256 (4 lanes x 16 steps x float4); K % 16 == 0 (checked by the host)
+  for (int kc = 0; kc < K; kc += 256) {
+    float4 wv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int k = kc + 16 * i + 4 * q;
+      wv[i] = k < K ? *reinterpret_cast<const float4*>(wr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int m = 0; m < GEMV_M; ++m) {
+      if (m < M) {
+        const float* xr = X + (size_t)m * K;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int k = kc + 16 * i + 4 * q;
+          const float4 xv = k < K ? *reinterpret_cast<const float4*>(xr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+          acc[m] = __builtin_fmaf(xv.x, wv[i].x, acc[m]);
+          acc[m] = __builtin_fmaf(xv.y, wv[i].y, acc[m]);
+          acc[m] = __builtin_fmaf(xv.z, wv[i].z, acc[m]);
+          acc[m] = __builtin_fmaf(xv.w, wv[i].w, acc[m]);
+        }
+      }
+    }
+  }
+  const float bias = okn ? P[F.bOff + n] : 0.f;
+#pragma unroll
+  for (int m = 0; m < GEMV_M; ++m) {
+    float v = acc[m];
+    v = __fadd_rn(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false)));
+    v = __fadd_rn(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false)));
+    if (m < M && okn && q == 0) Y[(size_t)m * N + n] = act_fwd(__fadd_rn(v, bias), F.act);
+  }
+  PROBE_REC(19, pt0);
 }
 
 // -------------------------------------------------------------------------------------

@@ -20,7 +20,7 @@ import torch
 
 KIDS = {1: "fwd", 2: "fwdL0", 3: "bwd_tdg", 4: "dx", 5: "dw", 6: "dw_v0", 7: "round", 8: "ver", 9: "gate",
         10: "tsf_fwd", 11: "tsf_flows", 12: "tsf_h", 13: "tsf_glin", 14: "tsf_w", 15: "tsf_flow", 16: "gpi", 17: "tdg",
-        18: "publish"}
+        18: "publish", 19: "fwd_gemv"}
 
 
 def main():
