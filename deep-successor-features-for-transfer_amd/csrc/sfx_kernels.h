@@ -332,16 +332,30 @@ constexpr int L0_KMAX = 64, L0_NMAX = 256;  // layer-0 fan-in / width handled in
 // One 32-row x 16-column output tile of instance y (flattened over the groups).  C: the layer
 // input X, the parameters and the output are handed between workgroups inside the launch
 // (k_round's post-update forward) -- coherent accesses.
+// instance y of a forward launch -> its group (y becomes the index inside the group)
+__device__ __forceinline__ FwdGroup fwd_group(const FwdArgs& F, int& y) {
+  int gs = 0;
+  if (F.ngroups > 1 && y >= F.g0.n) { y -= F.g0.n; gs = 1; }
+  if (F.ngroups > 2 && gs == 1 && y >= F.g1.n) { y -= F.g1.n; gs = 2; }
+  if (F.ngroups > 3 && gs == 2 && y >= F.g2.n) { y -= F.g2.n; gs = 3; }
+  auto pick = [gs](int a, int b, int c, int d) { return gs == 0 ? a : gs == 1 ? b : gs == 2 ? c : d; };
+  FwdGroup g;
+  g.role = pick(F.g0.role, F.g1.role, F.g2.role, F.g3.role);
+  g.which = pick(F.g0.which, F.g1.which, F.g2.which, F.g3.which);
+  g.xsel = pick(F.g0.xsel, F.g1.xsel, F.g2.xsel, F.g3.xsel);
+  g.head0 = pick(F.g0.head0, F.g1.head0, F.g2.head0, F.g3.head0);
+  g.n = pick(F.g0.n, F.g1.n, F.g2.n, F.g3.n);
+  return g;
+}
+
 template <bool VEC, int NW, bool L0, bool C>
 __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, int tN, int tM) {
   static_assert(!(L0 && C), "the in-tile layer 0 reads only inputs of earlier launches");
   constexpr int KW = 256 / NW;  // K chunk of one wave per iteration (NW waves cover 256)
   constexpr int KL = KW / 4;    // consecutive k per lane (4 lane groups per MFMA k-step)
-  // instance -> (group, head) with constant-index selects (no dynamic kernarg indexing)
-  FwdGroup grp = F.g0;
-  if (F.ngroups > 1 && y >= grp.n) { y -= grp.n; grp = F.g1; }
-  if (F.ngroups > 2 && y >= grp.n) { y -= grp.n; grp = F.g2; }
-  if (F.ngroups > 3 && y >= grp.n) { y -= grp.n; grp = F.g3; }
+  // instance -> (group, head) by scalar selects of each field (no dynamic kernarg indexing, and
+  // no FwdGroup copy: conditionally copied structs were demoted to scratch, 17 dwords per lane)
+  const FwdGroup grp = fwd_group(F, y);
   const int head = grp.head0 + y;
   const int M = F.M, N = F.N, K = F.K;
   const float* P = grp.which == P_TARGET ? G.target + (long long)head * G.P
@@ -514,10 +528,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
 __global__ __launch_bounds__(256) void k_fwd_gemv(Geo G, FwdArgs F) {
   PROBE_T(pt0);
   int y = blockIdx.y;
-  FwdGroup grp = F.g0;
-  if (F.ngroups > 1 && y >= grp.n) { y -= grp.n; grp = F.g1; }
-  if (F.ngroups > 2 && y >= grp.n) { y -= grp.n; grp = F.g2; }
-  if (F.ngroups > 3 && y >= grp.n) { y -= grp.n; grp = F.g3; }
+  const FwdGroup grp = fwd_group(F, y);
   const int head = grp.head0 + y;
   const int M = F.M, N = F.N, K = F.K;
   const float* P = grp.which == P_TARGET ? G.target + (long long)head * G.P
