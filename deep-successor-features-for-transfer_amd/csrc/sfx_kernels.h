@@ -372,6 +372,15 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
   const float bias = (threadIdx.x < 128 && col < N) ? ldc<C>(P + F.bOff + col) : 0.f;
   constexpr int AS = L0 ? L0_NMAX + 4 : 4;  // LDS row stride of a0 (padded against bank conflicts)
   __shared__ __align__(16) float sA[L0 ? 32 * AS : 4];
+  // L0: the first K chunk of this lane's W row is requested before layer 0 is computed, so its
+  // latency overlaps the in-tile layer 0 instead of following it
+  float4 wpre[VEC && L0 ? KL / 4 : 1];
+  if constexpr (VEC && L0) {
+    const int kb0 = wave * KW + g * KL;
+#pragma unroll
+    for (int q = 0; q < KL / 4; ++q)
+      wpre[q] = okn && kb0 < K ? ldc4<C>(wr + kb0 + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   if constexpr (L0) {
     __shared__ float sX[32 * L0_KMAX];
     const int K0 = F.K0;
@@ -454,7 +463,12 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
           ta = oka ? ldc4<C>(xra + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
           tb = okb ? ldc4<C>(xrb + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        const float4 tw = okn ? ldc4<C>(wr + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 tw;
+        if constexpr (L0) {
+          tw = kc == wave * KW ? wpre[q] : (okn ? ldc4<C>(wr + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f));
+        } else {
+          tw = okn ? ldc4<C>(wr + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
         a0[4 * q] = ta.x; a0[4 * q + 1] = ta.y; a0[4 * q + 2] = ta.z; a0[4 * q + 3] = ta.w;
         a1[4 * q] = tb.x; a1[4 * q + 1] = tb.y; a1[4 * q + 2] = tb.z; a1[4 * q + 3] = tb.w;
         bw[4 * q] = tw.x; bw[4 * q + 1] = tw.y; bw[4 * q + 2] = tw.z; bw[4 * q + 3] = tw.w;
