@@ -260,6 +260,17 @@ __device__ __forceinline__ AdamC adam_consts(const AdamHP& hp, int step) {
   return c;
 }
 
+// Adam moments are read again only by the next step's update of the same head: stored
+// non-temporally (measured +1 % env-steps/s on the all-task step, 3 A/B pairs: less dirty L2 for
+// the kernel-boundary writeback; -DSFX_PLAIN_MV restores plain stores)
+__device__ __forceinline__ void st_moment(float* p, float v) {
+#ifdef SFX_PLAIN_MV
+  *p = v;
+#else
+  __builtin_nontemporal_store(v, p);
+#endif
+}
+
 __device__ __forceinline__ void adam_apply(float& pp, float& mm, float& vv, float g, const AdamC& c) {
   if (c.wd != 0.f) g = __fadd_rn(g, __fmul_rn(c.wd, pp));
   mm = __builtin_fmaf(c.omb1, __fsub_rn(g, mm), mm);  // vectorized lerp: fmadd(w, end-start, start)
@@ -1196,8 +1207,8 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
         const size_t off = (size_t)L.wOff + (size_t)n * K + k;
         adam_apply(pp[e], pm[e], pv[e], h ? acc1[i] : acc0[i], c);
         stc<C>(Pw + off, pp[e]);
-        Mw[off] = pm[e];
-        Vw[off] = pv[e];
+        st_moment(Mw + off, pm[e]);
+        st_moment(Vw + off, pv[e]);
         if (fuse) sW[(n - nbase) * KFUSE + k] = pp[e];
       }
     }
@@ -1205,8 +1216,8 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
   if (dob) {
     adam_apply(bp, bm, bv, bsum, c);
     stc<C>(Pw + L.bOff + nbias, bp);
-    Mw[L.bOff + nbias] = bm;
-    Vw[L.bOff + nbias] = bv;
+    st_moment(Mw + L.bOff + nbias, bm);
+    st_moment(Vw + L.bOff + nbias, bv);
     if (fuse) sB[nbias - nbase] = bp;
   }
   if (fuse) fused_v0<C>(G, A, L, head, nbase, sW, sB, sX);
