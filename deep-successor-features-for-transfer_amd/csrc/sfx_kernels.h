@@ -595,8 +595,8 @@ __global__ __launch_bounds__(256) void k_fwd_gemv(Geo G, FwdArgs F) {
 #pragma unroll
   for (int m = 0; m < GEMV_M; ++m) {
     float v = acc[m];
-    v = __fadd_rn(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false)));
-    v = __fadd_rn(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false)));
+    v = __fadd_rn(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));
+    v = __fadd_rn(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));
     if (m < M && okn && q == 0) Y[(size_t)m * N + n] = act_fwd(__fadd_rn(v, bias), F.act);
   }
   PROBE_REC(19, pt0);

@@ -94,7 +94,7 @@ __device__ __forceinline__ float tsf_tanh(float x) {
 template <int LPR>
 __device__ __forceinline__ float tsf_row_sum(float v) {
 #define SFX_DPP_ADD(ctrl) \
-  v = __fadd_rn(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xF, 0xF, false)))
+  v = __fadd_rn(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false)))
   SFX_DPP_ADD(0xB1);   // quad_perm [1,0,3,2]
   SFX_DPP_ADD(0x4E);   // quad_perm [2,3,0,1]
   SFX_DPP_ADD(0x141);  // row_half_mirror
