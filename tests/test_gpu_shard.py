@@ -24,57 +24,65 @@ def _need_gpu():
         pytest.skip("no HIP device")
 
 
-def _stream(seed):
+# BASELINE config C4's per-rank shape (Reacher, 256-wide heads), two ranks of 8 heads each
+FULL = dict(spec=dict(n_s=17, H=256, A=7, d=8, acts=("relu", "relu")), tg=16, b=32, steps=5)
+SMALL = dict(spec=SPEC, tg=TG, b=B, steps=STEPS)
+
+
+def _stream(seed, cfg=SMALL):
+    spec, tg, b = cfg["spec"], cfg["tg"], cfg["b"]
     g = torch.Generator().manual_seed(seed)
     out = []
-    for j in range(STEPS):
+    for j in range(cfg["steps"]):
         batch = None
         if j > 0:
-            batch = (torch.randn(B, SPEC["n_s"], generator=g), torch.randint(0, SPEC["A"], (B,), generator=g),
-                     torch.rand(B, SPEC["d"], generator=g), torch.randn(B, SPEC["n_s"], generator=g),
-                     torch.where(torch.rand(B, generator=g) < 0.2, 0.0, 0.9))
-        out.append((batch, j % TG, torch.rand(SPEC["d"], generator=g), torch.rand(1, generator=g),
-                    torch.randn(SPEC["n_s"], generator=g)))
+            batch = (torch.randn(b, spec["n_s"], generator=g), torch.randint(0, spec["A"], (b,), generator=g),
+                     torch.rand(b, spec["d"], generator=g), torch.randn(b, spec["n_s"], generator=g),
+                     torch.where(torch.rand(b, generator=g) < 0.2, 0.0, 0.9))
+        out.append((batch, j % tg, torch.rand(spec["d"], generator=g), torch.rand(1, generator=g),
+                    torch.randn(spec["n_s"], generator=g)))
     return out
 
 
-def _run_rank(rank, world, rounds, ar):
+def _run_rank(rank, world, rounds, ar, cfg=SMALL):
     from sfx.engine import SFEngine
     from sfx.init import reference_heads
     from sfx.shard import LibsfxShardBackend, ShardedAllTask
 
-    online, w = reference_heads(TG, SPEC["n_s"], SPEC["H"], SPEC["A"], SPEC["d"], SPEC["acts"], seed=3)
-    T_loc = TG // world
-    eng = SFEngine(T_loc, SPEC["n_s"], SPEC["H"], SPEC["A"], SPEC["d"], SPEC["acts"], max_batch=B)
+    sp, tg, b = cfg["spec"], cfg["tg"], cfg["b"]
+    online, w = reference_heads(tg, sp["n_s"], sp["H"], sp["A"], sp["d"], sp["acts"], seed=3)
+    T_loc = tg // world
+    eng = SFEngine(T_loc, sp["n_s"], sp["H"], sp["A"], sp["d"], sp["acts"], max_batch=b)
     eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
     eng.set_target_update_ev(EV)
-    be = LibsfxShardBackend(eng, TG, rank * T_loc, B)
+    be = LibsfxShardBackend(eng, tg, rank * T_loc, b)
     for t in range(T_loc):
         eng.load_head(t, online[rank * T_loc + t], 0)
         eng.load_head(t, online[rank * T_loc + t], 1)
-    for t in range(TG):
+    for t in range(tg):
         eng.load_w(t, w[t])
-    step = ShardedAllTask(be, TG, SPEC["A"], ar, rounds=rounds)
+    step = ShardedAllTask(be, tg, sp["A"], ar, rounds=rounds)
     actions = []
     dev = eng.device
-    for batch, task, phi1, r1, s_next in _stream(11):
+    for batch, task, phi1, r1, s_next in _stream(11, cfg):
         db = None if batch is None else tuple(x.to(dev).contiguous() for x in batch)
         actions.append(step.step(db, task, phi1.to(dev), r1.to(dev), 0.05, s_next.to(dev), task))
     heads = torch.stack([eng.get_head(t) for t in range(T_loc)])
     targets = torch.stack([eng.get_head(t, 1) for t in range(T_loc)])
-    ws = torch.stack([eng.get_w(t)[0] for t in range(TG)])
+    ws = torch.stack([eng.get_w(t)[0] for t in range(tg)])
     eng.close()
     return actions, heads, targets, ws, step.stats
 
 
-def _oracle():
-    spec = R.Spec(**SPEC)
+def _oracle(cfg=SMALL):
+    sp, tg = cfg["spec"], cfg["tg"]
+    spec = R.Spec(**sp)
     from sfx.init import reference_heads
 
-    online, w0 = reference_heads(TG, SPEC["n_s"], SPEC["H"], SPEC["A"], SPEC["d"], SPEC["acts"], seed=3)
+    online, w0 = reference_heads(tg, sp["n_s"], sp["H"], sp["A"], sp["d"], sp["acts"], seed=3)
     st = R.SFState(spec, online.clone(), online.clone(), w0.clone())
     want = []
-    for batch, task, phi1, r1, s_next in _stream(11):
+    for batch, task, phi1, r1, s_next in _stream(11, cfg):
         st.w[task] = R.lms_update(st.w[task].view(-1, 1), phi1, r1[0], 0.05).view(-1)
         if batch is not None:
             R.deep_all_task_step(st, batch, lr=1e-3, target_update_ev=EV)
@@ -83,12 +91,12 @@ def _oracle():
     return want, st
 
 
-def _check(actions, heads, targets, ws, want, st):
+def _check(actions, heads, targets, ws, want, st, steps=STEPS):
     from tests.test_gpu_engine import params_close, rel_close
 
     assert actions == want
-    params_close(heads, st.online, 1e-3 * STEPS)
-    params_close(targets, st.target, 1e-3 * STEPS)
+    params_close(heads, st.online, 1e-3 * steps)
+    params_close(targets, st.target, 1e-3 * steps)
     rel_close(ws, st.w, rtol=1e-5, atol=1e-7)
 
 
@@ -100,7 +108,7 @@ def test_single_rank_shard_protocol(rounds):
     assert stats["steps"] == STEPS - 1
 
 
-def _worker(rank, port, q):
+def _worker(rank, port, q, cfg=SMALL):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -108,7 +116,7 @@ def _worker(rank, port, q):
     from sfx.shard import all_reduce_max_fn
 
     try:
-        actions, heads, targets, ws, stats = _run_rank(rank, 2, 2, all_reduce_max_fn(via_host=True))
+        actions, heads, targets, ws, stats = _run_rank(rank, 2, 2, all_reduce_max_fn(via_host=True), cfg)
         parts = [None, None]
         dist.all_gather_object(parts, (heads, targets))
         if rank == 0:
@@ -117,7 +125,7 @@ def _worker(rank, port, q):
         dist.destroy_process_group()
 
 
-def test_two_ranks_on_one_gpu():
+def _two_ranks(worker, cfg):
     import torch.multiprocessing as mp
 
     s = socket.socket()
@@ -126,97 +134,110 @@ def test_two_ranks_on_one_gpu():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=worker, args=(r, port, q, cfg)) for r in range(2)]
     for p in procs:
         p.start()
-    actions, heads, targets, ws, stats = q.get(timeout=300)
+    out = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    want, st = _oracle()
-    _check(actions, heads, targets, ws, want, st)
-
-
-# ---- sharded TSF-DQN (sfx_shard_tsf_*, BASELINE config C5) ---------------------------------
-TSF_SPEC = dict(n_s=11, H=32, A=9, d=6, acts=("relu", "relu"))
-TSF_G, TSF_K, TSF_STEPS = 10, 3, 8
-
-
-def _tsf_problem():
-    from sfx.init import reference_heads
-
-    online, w = reference_heads(TG, TSF_SPEC["n_s"], TSF_SPEC["H"], TSF_SPEC["A"], TSF_SPEC["d"], TSF_SPEC["acts"],
-                                seed=5)
-    gs = R.GSpec(TSF_SPEC["n_s"], TSF_G, TSF_K)
-    gen = torch.Generator().manual_seed(6)
-    g = torch.empty(TG, gs.P).uniform_(-0.3, 0.3, generator=gen)
-    h = torch.empty(TSF_SPEC["d"] * TSF_G + TSF_SPEC["d"]).uniform_(-0.3, 0.3, generator=gen)
-    return online, w, gs, g, h
-
-
-def _tsf_stream(seed):
-    g = torch.Generator().manual_seed(seed)
-    out = []
-    for j in range(TSF_STEPS):
-        batch = (torch.randn(B, TSF_SPEC["n_s"], generator=g), torch.randint(0, TSF_SPEC["A"], (B,), generator=g),
-                 torch.rand(B, 1, generator=g), torch.rand(B, TSF_SPEC["d"], generator=g),
-                 torch.randn(B, TSF_SPEC["n_s"], generator=g), torch.where(torch.rand(B, generator=g) < 0.2, 0.0, 0.9))
-        out.append((batch, (3 * j + 1) % TG, torch.randn(TSF_SPEC["n_s"], generator=g)))
     return out
 
 
-def _tsf_run_rank(rank, world, use_gpi, ar, bc):
+@pytest.mark.parametrize("cfg", [SMALL, FULL], ids=["small", "c4-shape"])
+def test_two_ranks_on_one_gpu(cfg):
+    actions, heads, targets, ws, stats = _two_ranks(_worker, cfg)
+    want, st = _oracle(cfg)
+    _check(actions, heads, targets, ws, want, st, cfg["steps"])
+
+
+# ---- sharded TSF-DQN (sfx_shard_tsf_*, BASELINE config C5) ---------------------------------
+TSF_SMALL = dict(spec=dict(n_s=11, H=32, A=9, d=6, acts=("relu", "relu")), tg=TG, b=B, G=10, K=3, steps=8,
+                 init=0.3)
+# C5's shape (Hopper, tsfdqn_nf.py): 256-wide heads, 27 actions, d=50, g_i width 100 with 100 planar
+# layers; two ranks of 8 heads, flows at a small init (PlanarFlow's U(-0.01, 0.01) scale, widened)
+TSF_FULL = dict(spec=dict(n_s=11, H=256, A=27, d=50, acts=("relu", "relu")), tg=16, b=32, G=100, K=100, steps=4,
+                init=0.05)
+
+
+def _tsf_problem(cfg):
+    from sfx.init import reference_heads
+
+    sp, tg = cfg["spec"], cfg["tg"]
+    online, w = reference_heads(tg, sp["n_s"], sp["H"], sp["A"], sp["d"], sp["acts"], seed=5)
+    gs = R.GSpec(sp["n_s"], cfg["G"], cfg["K"])
+    gen = torch.Generator().manual_seed(6)
+    g = torch.empty(tg, gs.P).uniform_(-cfg["init"], cfg["init"], generator=gen)
+    h = torch.empty(sp["d"] * cfg["G"] + sp["d"]).uniform_(-cfg["init"], cfg["init"], generator=gen)
+    return online, w, gs, g, h
+
+
+def _tsf_stream(seed, cfg):
+    sp, tg, b = cfg["spec"], cfg["tg"], cfg["b"]
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for j in range(cfg["steps"]):
+        batch = (torch.randn(b, sp["n_s"], generator=g), torch.randint(0, sp["A"], (b,), generator=g),
+                 torch.rand(b, 1, generator=g), torch.rand(b, sp["d"], generator=g),
+                 torch.randn(b, sp["n_s"], generator=g), torch.where(torch.rand(b, generator=g) < 0.2, 0.0, 0.9))
+        out.append((batch, (3 * j + 1) % tg, torch.randn(sp["n_s"], generator=g)))
+    return out
+
+
+def _tsf_run_rank(rank, world, use_gpi, ar, bc, cfg=TSF_SMALL):
     from sfx.engine import SFEngine
     from sfx.shard import LibsfxTSFShardBackend, ShardedTSF
 
-    online, w, gs, g, h = _tsf_problem()
-    T_loc = TG // world
-    eng = SFEngine(T_loc, TSF_SPEC["n_s"], TSF_SPEC["H"], TSF_SPEC["A"], TSF_SPEC["d"], TSF_SPEC["acts"], max_batch=B)
+    sp, TGc, Bc = cfg["spec"], cfg["tg"], cfg["b"]
+    online, w, gs, g, h = _tsf_problem(cfg)
+    T_loc = TGc // world
+    eng = SFEngine(T_loc, sp["n_s"], sp["H"], sp["A"], sp["d"], sp["acts"], max_batch=Bc)
     eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
     eng.set_target_update_ev(EV)
-    eng.tsf_setup(TSF_G, TSF_K, 1.0, 1e-3, 0.0, 1e-3, 0.0)
-    be = LibsfxTSFShardBackend(eng, TG, rank * T_loc, B)
+    eng.tsf_setup(cfg["G"], cfg["K"], 1.0, 1e-3, 0.0, 1e-3, 0.0)
+    be = LibsfxTSFShardBackend(eng, TGc, rank * T_loc, Bc)
     for t in range(T_loc):
         eng.load_head(t, online[rank * T_loc + t], 0)
         eng.load_head(t, online[rank * T_loc + t], 1)
         eng.tsf_load_g(t, g[rank * T_loc + t])
-    for t in range(TG):
+    for t in range(TGc):
         eng.load_w(t, w[t])
     eng.tsf_load_h(h)
-    step = ShardedTSF(be, TG, rank, TSF_SPEC["A"], ar, bc)
+    step = ShardedTSF(be, TGc, rank, sp["A"], ar, bc)
     dev = eng.device
     actions = []
-    for batch, i, s in _tsf_stream(13):
+    for batch, i, s in _tsf_stream(13, cfg):
         step.update(i, tuple(x.to(dev).contiguous() for x in batch), use_gpi=use_gpi)
         actions.append(step.select(s.to(dev).view(1, -1), i))
     out = (actions, torch.stack([eng.get_head(t) for t in range(T_loc)]),
            torch.stack([eng.tsf_get_g(t)[0] for t in range(T_loc)]), eng.tsf_get_h(),
-           torch.stack([eng.get_w(t)[0] for t in range(TG)]))
+           torch.stack([eng.get_w(t)[0] for t in range(TGc)]))
     eng.close()
     return out
 
 
-def _tsf_oracle(use_gpi):
-    spec = R.Spec(**TSF_SPEC)
-    online, w0, gs, g0, h0 = _tsf_problem()
+def _tsf_oracle(use_gpi, cfg):
+    spec = R.Spec(**cfg["spec"])
+    online, w0, gs, g0, h0 = _tsf_problem(cfg)
     st = R.TSFState(spec, online.clone(), online.clone(), w0.clone(), gspec=gs, g=g0.clone(), h=h0.clone())
     want = []
-    for batch, i, s in _tsf_stream(13):
+    for batch, i, s in _tsf_stream(13, cfg):
         R.tsf_update(st, batch, i, use_gpi=use_gpi, target_update_ev=EV)
         qv, tk = R.gpi_w(R.psi_all(st.online, spec, s.view(1, -1)), st.w[i])
         want.append((int(tk[0]), R.select_action(qv, tk[0], i, True)))
     return want, st
 
 
-def _tsf_check(res, use_gpi):
+def _tsf_check(res, use_gpi, cfg=TSF_SMALL):
     from tests.test_gpu_engine import params_close, rel_close
 
     actions, heads, gg, h, w = res
-    want, st = _tsf_oracle(use_gpi)
+    want, st = _tsf_oracle(use_gpi, cfg)
     assert actions == want
-    params_close(heads, st.online, 1e-3 * TSF_STEPS)
-    params_close(gg, st.g, 1e-3 * TSF_STEPS)
-    params_close(h, st.h, 1e-3 * TSF_STEPS)
+    n = cfg["steps"]
+    params_close(heads, st.online, 1e-3 * n)
+    params_close(gg, st.g, 1e-3 * n)
+    params_close(h, st.h, 1e-3 * n)
     rel_close(w, st.w, rtol=1e-3, atol=1e-6)
 
 
@@ -225,7 +246,7 @@ def test_tsf_single_rank_shard_protocol(use_gpi):
     _tsf_check(_tsf_run_rank(0, 1, use_gpi, lambda t: None, lambda t, src: None), use_gpi)
 
 
-def _tsf_worker(rank, port, q):
+def _tsf_worker(rank, port, q, cfg=TSF_SMALL):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -234,7 +255,7 @@ def _tsf_worker(rank, port, q):
 
     try:
         actions, heads, gg, h, w = _tsf_run_rank(rank, 2, True, all_reduce_max_fn(via_host=True),
-                                                 broadcast_fn(via_host=True))
+                                                 broadcast_fn(via_host=True), cfg)
         parts = [None, None]
         dist.all_gather_object(parts, (heads, gg))
         if rank == 0:
@@ -243,20 +264,6 @@ def _tsf_worker(rank, port, q):
         dist.destroy_process_group()
 
 
-def test_tsf_two_ranks_on_one_gpu():
-    import torch.multiprocessing as mp
-
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_tsf_worker, args=(r, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = q.get(timeout=300)
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
-    _tsf_check(res, True)
+@pytest.mark.parametrize("cfg", [TSF_SMALL, TSF_FULL], ids=["small", "c5-shape"])
+def test_tsf_two_ranks_on_one_gpu(cfg):
+    _tsf_check(_two_ranks(_tsf_worker, cfg), True, cfg)
