@@ -59,6 +59,9 @@ def parse():
                         "configs C3 / C5 on one GPU (TSF-DQN, active-task schedule, python host loop)")
     p.add_argument("--heads", type=int, default=None, help="source tasks (ψ heads) per GPU (8; 16 for hopper-tsf*)")
     p.add_argument("--batch", type=int, default=32)
+    p.add_argument("--replay", choices=["host", "device"], default="host",
+                   help="replay ring on the host (north_star; the headline) or in HBM with on-device sampling "
+                        "(SURVEY §8f rank 2; native loop only)")
     p.add_argument("--spec-rounds", type=int, default=2,
                    help="speculative rounds of the all-task step launched on the device (more run from the host)")
     p.add_argument("--prof-steps", type=int, default=50)
@@ -266,8 +269,10 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
     from sfx.runner import NativeEnvLoop
 
     out = {}
-    for name, sched, K in (("reacher17-active-T8-B32", "active", None), ("hopper11-tsf-T16-B32", "tsf", 0),
-                           ("hopper11-tsf-nf100-T16-B32", "tsf", 100)):
+    for name, sched, K, dev in (("reacher17-active-T8-B32", "active", None, False),
+                                ("reacher17-all-T8-B32-device-replay", "all", None, True),
+                                ("hopper11-tsf-T16-B32", "tsf", 0, False),
+                                ("hopper11-tsf-nf100-T16-B32", "tsf", 100, False)):
         sh = SHAPE if K is None else TSF_SHAPE
         T = 8 if K is None else 16
         eng = SFEngine(T, sh["n_s"], sh["H"], sh["A"], sh["d"], sh["acts"], max_batch=args.batch, device=device)
@@ -285,7 +290,9 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
             eng.load_w(t, w[t])
         eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
         eng.set_target_update_ev(1000)
-        loop = NativeEnvLoop(eng, batch=args.batch, seed=1, schedule=sched, p_end=0.0 if K is None else 0.01)
+        eng.set_spec_rounds(args.spec_rounds)
+        loop = NativeEnvLoop(eng, batch=args.batch, seed=1, schedule=sched, p_end=0.0 if K is None else 0.01,
+                             device_replay=dev)
         loop.prefill(1000)
         loop.set_task(0)
         loop.run(warmup)
@@ -363,7 +370,7 @@ def main():
     native = args.loop == "native"
     if native:
         loop = NativeEnvLoop(eng, batch=B, seed=1 + rank, schedule=args.schedule,
-                             p_end=0.0 if args.tsf_K is None else 0.01)
+                             p_end=0.0 if args.tsf_K is None else 0.01, device_replay=args.replay == "device")
         loop.prefill(1000)
         loop.set_task(0)
     else:
@@ -442,7 +449,7 @@ def main():
                                                f" (Hopper-shape |s|=11 |a|=27 d=50, psi MLP 256x2, g/h width 100, "
                                                f"{args.tsf_K} planar layers, active head only: "
                                                f"{'tsfdqn_nf.py' if args.tsf_K else 'tsfdqn.py'} path)"),
-                       "heads_per_gpu": T, "global_batch": B * world, "parallelism": f"replica{world}" if world > 1 else "single",
+                       "heads_per_gpu": T, "global_batch": B * world, "replay": args.replay if native else "host", "parallelism": f"replica{world}" if world > 1 else "single",
                        "loop": (f"native C++ runner (sfx_runner_run, {args.schedule} schedule): host env + replay, one "
                                 "pre-launched gated hipGraph per env step" if native else "python host loop over libsfx graphs")},
             "roofline": roofline,

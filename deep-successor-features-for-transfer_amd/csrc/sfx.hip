@@ -159,6 +159,7 @@ struct sfx_handle {
   unsigned* dxctr = nullptr;
   bool split_dx = true;  // SFX_SPLIT_DX=0: one workgroup reduces all of N
   bool gemv_fwd = true;  // SFX_GEMV_FWD=0: wide layers of a <= 4-row forward through the MFMA tiles
+  bool dw_wide = false;  // SFX_DW_WIDE=1: 64 x 64 dW tiles for wide hidden layers (measured: no gain)
   struct RoundRec {               // launch arguments recorded instead of launched
     std::vector<BwdArgs> b;
     std::vector<FwdArgs> f;
@@ -431,7 +432,12 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.train_w = r != nullptr;
   A.losses = losses;
   A.inc_step = ex.inc_step;
-  auto dw_tiles = [&](int l) { return cdiv(h->L[l].N, 32) * cdiv(h->L[l].K, 64); };
+  // opt-in 64 x 64 dW tiles (role_dw_wide) for wide hidden layers when several heads share a
+  // launch, which then stays within about one workgroup per CU (measured: no gain)
+  auto dw_nw = [&](int l) {
+    return l >= 1 && h->dw_wide && !h->rec && nhead >= 4 && h->L[l].N >= 128 && h->L[l].K >= 64 ? 2 : 1;
+  };
+  auto dw_tiles = [&](int l) { return cdiv(h->L[l].N, 32 * dw_nw(l)) * cdiv(h->L[l].K, 64); };
   auto geo = [&](int l) {
     const LayerGeo& L = h->L[l];
     RoleGeo r{};
@@ -443,6 +449,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     r.xOff = l == 0 ? -1 : h->actOff[l - 1];
     r.dzOff = h->actOff[l];
     r.dzIn = l == 0 ? 0 : h->actOff[l - 1];
+    r.nw = dw_nw(l);
     return r;
   };
   // algorithmic bytes: dX reads W, dZ, X and writes dZ_{l-1}; dW reads dZ, X and does Adam's
@@ -830,6 +837,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->split_dx = !(esd && esd[0] == '0');
   const char* egv = std::getenv("SFX_GEMV_FWD");
   h->gemv_fwd = !(egv && egv[0] == '0');
+  const char* edw = std::getenv("SFX_DW_WIDE");
+  h->dw_wide = edw && edw[0] == '1';  // opt-in
   int off = 0, ptorch = 0;
   for (int l = 0; l < h->NL; ++l) {
     LayerGeo Lr{};

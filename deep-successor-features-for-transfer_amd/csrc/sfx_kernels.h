@@ -733,6 +733,7 @@ struct RoleGeo {
   int xOff;   // input activation offset (R_S block); < 0: the minibatch states x0
   int dzOff;  // this layer's output-gradient offset (dz block)
   int dzIn;   // dX role: offset of the gradient it writes (layer l-1)
+  int nw;     // dW role: 16-column groups per wave (1: 32 x 64 tiles, role_dw; 2: 64 x 64, role_dw_wide)
 };
 
 struct BwdArgs {
@@ -1223,6 +1224,131 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
   if (fuse) fused_v0<C>(G, A, L, head, nbase, sW, sB, sX);
 }
 
+// dW + Adam of a 64 (output columns) x 64 (inputs) tile of a wide hidden layer (RoleGeo::nw == 2,
+// several heads per launch): role_dw with two 16-column groups per wave, so the launch needs
+// half the workgroups and stays within about one per CU (the 32-column tiles put 384 / 320
+// workgroups on 256 CUs at the C2 shape, and the co-resident pairs finish last).  Per column
+// the accumulation order is role_dw's, so the results are the same bits.  Layer 0 (with the
+// fused post-update forward) keeps role_dw.
+__device__ void role_dw_wide(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile) {
+  constexpr int NW = 2;
+  const int N = L.N, K = L.K, M = A.M;
+  const int ntk = (K + 63) >> 6;
+  const int kt = tile % ntk, nt = tile / ntk;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  const int n0 = nt * 32 * NW + (wave & 1) * 16 * NW, k0 = kt * 64 + (wave >> 1) * 32;
+  const float* dZ = G.dzp(head, L.dzOff);
+  const float* X = layer_input(G, A, head, L.xOff);
+  const int rs = rslot(A.mask, head);
+  const long long ro = G.slot_off(rs, head), wo = G.slot_off(rs ^ 1, head);
+  const float* Pr = G.online + ro;
+  const float* Mr = G.am + ro;
+  const float* Vr = G.av + ro;
+  float* Pw = G.online + wo;
+  float* Mw = G.am + wo;
+  float* Vw = G.av + wo;
+  const AdamC c = load_adamc<false>(G.adamc + head);
+  const int kb0 = k0 + r, kb1 = k0 + 16 + r;
+  // optimizer state of the 8·NW weights this lane updates, requested first
+  float pp[8 * NW], pm[8 * NW], pv[8 * NW];
+  bool ok[8 * NW];
+#pragma unroll
+  for (int s = 0; s < NW; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + 16 * s + g * 4 + i;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = h ? kb1 : kb0;
+        const int e = (s * 4 + i) * 2 + h;
+        ok[e] = n < N && k < K;
+        const size_t off = (size_t)L.wOff + (size_t)n * K + k;
+        pp[e] = ok[e] ? Pr[off] : 0.f;
+        pm[e] = ok[e] ? Mr[off] : 0.f;
+        pv[e] = ok[e] ? Vr[off] : 0.f;
+      }
+    }
+  // biases of columns n0 + 16 s + r (lanes r of the k-half-0 waves of the kt == 0 tiles),
+  // gradients from the dZ operands in registers
+  bool dob[NW];
+  float bp[NW], bm[NW], bv[NW];
+#pragma unroll
+  for (int s = 0; s < NW; ++s) {
+    const int nb = n0 + 16 * s + r;
+    dob[s] = kt == 0 && wave < 2 && g == 0 && nb < N;
+    bp[s] = dob[s] ? Pr[L.bOff + nb] : 0.f;
+    bm[s] = dob[s] ? Mr[L.bOff + nb] : 0.f;
+    bv[s] = dob[s] ? Vr[L.bOff + nb] : 0.f;
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep those loads ahead of the MFMA operands
+  floatx4 acc[NW][2];
+  float bsum[NW];
+#pragma unroll
+  for (int s = 0; s < NW; ++s) {
+    acc[s][0] = floatx4{0.f, 0.f, 0.f, 0.f};
+    acc[s][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+    bsum[s] = 0.f;
+  }
+  for (int mc = 0; mc < M; mc += MT) {
+    float av[NW][MT / 4], bv0[MT / 4], bv1[MT / 4];
+#pragma unroll
+    for (int j = 0; j < MT / 4; ++j) {
+      const int m = mc + 4 * j + g;
+      const bool okm = m < M;
+#pragma unroll
+      for (int s = 0; s < NW; ++s) {
+        const int nn = n0 + 16 * s + r;
+        av[s][j] = (okm && nn < N) ? ldc<false>(dZ + (size_t)m * N + nn) : 0.f;
+      }
+      bv0[j] = (okm && kb0 < K) ? X[(size_t)m * K + kb0] : 0.f;
+      bv1[j] = (okm && kb1 < K) ? X[(size_t)m * K + kb1] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < MT / 4; ++j)
+#pragma unroll
+      for (int s = 0; s < NW; ++s) {
+        acc[s][0] = mfma4(av[s][j], bv0[j], acc[s][0]);
+        acc[s][1] = mfma4(av[s][j], bv1[j], acc[s][1]);
+      }
+#pragma unroll
+    for (int j = 0; j < MT / 4; ++j)
+#pragma unroll
+      for (int s = 0; s < NW; ++s) bsum[s] = __fadd_rn(bsum[s], av[s][j]);  // rows mc + 4j + g
+  }
+#pragma unroll
+  for (int s = 0; s < NW; ++s) {  // + the other three row classes, fixed order
+    bsum[s] = __fadd_rn(bsum[s], __shfl_xor(bsum[s], 16));
+    bsum[s] = __fadd_rn(bsum[s], __shfl_xor(bsum[s], 32));
+  }
+  PROBE_MARK();
+#pragma unroll
+  for (int s = 0; s < NW; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + 16 * s + g * 4 + i;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int e = (s * 4 + i) * 2 + h;
+        if (ok[e]) {
+          const size_t off = (size_t)L.wOff + (size_t)n * K + (h ? kb1 : kb0);
+          adam_apply(pp[e], pm[e], pv[e], acc[s][h][i], c);
+          stc<false>(Pw + off, pp[e]);
+          st_moment(Mw + off, pm[e]);
+          st_moment(Vw + off, pv[e]);
+        }
+      }
+    }
+#pragma unroll
+  for (int s = 0; s < NW; ++s)
+    if (dob[s]) {
+      const int nb = n0 + 16 * s + r;
+      adam_apply(bp[s], bm[s], bv[s], bsum[s], c);
+      stc<false>(Pw + L.bOff + nb, bp[s]);
+      st_moment(Mw + L.bOff + nb, bm[s]);
+      st_moment(Vw + L.bOff + nb, bv[s]);
+    }
+}
+
 // loss finalisation, optional w step, Adam step counter (one workgroup per head)
 // Deterministic block sum (fixed pairwise tree over 256 partials) -- result in every thread.
 __device__ __forceinline__ float block_sum(float v, float* red) {
@@ -1309,7 +1435,10 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
   }
   bx -= A.na;
   if (bx < A.nb) {
-    role_dw(G, A, head, A.rb, bx, false);
+    if (A.rb.nw == 2)
+      role_dw_wide(G, A, head, A.rb, bx);
+    else
+      role_dw(G, A, head, A.rb, bx, false);
     PROBE_REC(5, pt0);
     return;
   }
@@ -1784,6 +1913,122 @@ __global__ __launch_bounds__(256) void k_gate(GateArgs g) {
   PROBE_REC(9, pt0);
 }
 
+
+// -------------------------------------------------------------------------------------
+// Device-resident replay (opt-in, sfx_runner_device_replay): the ring
+// lives in HBM and the gate of each step appends the step's transition and draws the
+// uniform minibatch itself, so the host hands over one transition (≈ 2n_s + d + 8 words)
+// instead of the collated batch.  Index b of a step with key k over a ring of `size` rows:
+//   x = splitmix64(k + (b + 1)·0x9E3779B97F4A7C15),  idx = ((x >> 32) · size) >> 32
+// (replay_index below; the host mirror uses the same function, so the recorded minibatch
+// of a step is the one the device gathered).
+// -------------------------------------------------------------------------------------
+struct ReplayMeta {  // tail of the host staging, written by the host per step
+  long long a, slot, size;
+  unsigned long long key;
+  float r, gamma;
+  int have, pad_;
+};
+
+__host__ __device__ inline unsigned replay_index(unsigned long long key, int b, long long size) {
+  unsigned long long x = key + (unsigned long long)(b + 1) * 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (unsigned)(((x >> 32) * (unsigned long long)size) >> 32);
+}
+
+struct ReplayGateArgs {
+  GateArgs g;         // src/dst/n16 cover [tail0, bytes) of the staging: s_next, φ1, r1, transition
+  int tail0;          // 16-byte word where the host-written tail starts
+  int n_s, d, B;
+  int off_s, off_s1, off_phi, off_a, off_g, off_rb;  // device minibatch fields (bytes)
+  int tr_s, tr_s1, tr_phi, tr_meta;                  // transition fields (bytes, from tail0)
+  float *rs, *rs1, *rphi, *rr, *rg;                  // ring [cap][...]
+  long long* ra;
+};
+
+constexpr int REPLAY_TAIL_MAX = 4096;  // bytes of the staged tail held in LDS
+
+__global__ __launch_bounds__(256) void k_gate_replay(ReplayGateArgs A) {
+  __shared__ int ok;
+  __shared__ __attribute__((aligned(16))) unsigned char tail[REPLAY_TAIL_MAX];
+  const GateArgs& g = A.g;
+  PROBE_T(pt0);
+  if (threadIdx.x == 0) {
+    ok = 1;
+    const long long want = *g.dctr + 1;
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(g.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+      if (wall_clock64() - t0 > g.timeout) {
+        ok = 0;
+        __hip_atomic_store(g.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+    *g.dctr = want;
+  }
+  __syncthreads();
+  if (!ok) return;
+  PROBE_MARK();
+  uint4* lt = reinterpret_cast<uint4*>(tail);
+  for (int i = threadIdx.x; i < g.n16; i += 256) {
+    const uint4 v = g.src[A.tail0 + i];
+    lt[i] = v;
+    g.dst[A.tail0 + i] = v;
+  }
+  __syncthreads();
+  const ReplayMeta& m = *reinterpret_cast<const ReplayMeta*>(tail + A.tr_meta);
+  const float* ts = reinterpret_cast<const float*>(tail + A.tr_s);
+  const float* ts1 = reinterpret_cast<const float*>(tail + A.tr_s1);
+  const float* tphi = reinterpret_cast<const float*>(tail + A.tr_phi);
+  const int n_s = A.n_s, d = A.d;
+  const long long slot = m.slot;  // < 0: no transition this step (first action of an episode)
+  // append (agents/buffer.py:34-50); the gathers below take row `slot` from LDS, so they do
+  // not depend on these stores being visible within this launch
+  if (slot >= 0) {
+    for (int k = threadIdx.x; k < n_s; k += 256) {
+      A.rs[slot * n_s + k] = ts[k];
+      A.rs1[slot * n_s + k] = ts1[k];
+    }
+    for (int k = threadIdx.x; k < d; k += 256) A.rphi[slot * d + k] = tphi[k];
+    if (threadIdx.x == 0) {
+      A.rr[slot] = m.r;
+      A.rg[slot] = m.gamma;
+      A.ra[slot] = m.a;
+    }
+  }
+  if (!m.have) {
+    PROBE_REC(9, pt0);
+    return;
+  }
+  // uniform minibatch (agents/buffer.py:52-64): row b of every field from ring row idx_b
+  unsigned char* dst = reinterpret_cast<unsigned char*>(g.dst);
+  float* S = reinterpret_cast<float*>(dst + A.off_s);
+  float* S1 = reinterpret_cast<float*>(dst + A.off_s1);
+  float* PHI = reinterpret_cast<float*>(dst + A.off_phi);
+  const int w = 2 * n_s + d;
+  for (int e = threadIdx.x; e < A.B * w; e += 256) {
+    const int b = e / w, k = e - b * w;
+    const long long i = replay_index(m.key, b, m.size);
+    const bool own = i == slot;
+    if (k < n_s)
+      S[b * n_s + k] = own ? ts[k] : A.rs[i * n_s + k];
+    else if (k < 2 * n_s)
+      S1[b * n_s + k - n_s] = own ? ts1[k - n_s] : A.rs1[i * n_s + k - n_s];
+    else
+      PHI[b * d + k - 2 * n_s] = own ? tphi[k - 2 * n_s] : A.rphi[i * d + k - 2 * n_s];
+  }
+  for (int b = threadIdx.x; b < A.B; b += 256) {
+    const long long i = replay_index(m.key, b, m.size);
+    const bool own = i == slot;
+    reinterpret_cast<long long*>(dst + A.off_a)[b] = own ? m.a : A.ra[i];
+    reinterpret_cast<float*>(dst + A.off_g)[b] = own ? m.gamma : A.rg[i];
+    reinterpret_cast<float*>(dst + A.off_rb)[b] = own ? m.r : A.rr[i];
+  }
+  PROBE_REC(9, pt0);
+}
 
 __global__ void k_publish(const int64_t* sel, const int* flag, HostResult* out, const long long* dctr) {
   PROBE_T(pt0);

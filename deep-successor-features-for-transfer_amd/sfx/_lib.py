@@ -56,6 +56,7 @@ SIGNATURES = {
     "sfx_runner_destroy": (_I, [_VP]),
     "sfx_runner_layout": (_I, [_VP, C.POINTER(C.c_int64)]),
     "sfx_runner_config": (_I, [_VP, _I, _I, _F]),
+    "sfx_runner_device_replay": (_I, [_VP, _I]),
     "sfx_runner_set_task": (_I, [_VP, _I]),
     "sfx_runner_prefill": (_I, [_VP, _I]),
     "sfx_runner_run": (_I, [_VP, _I]),

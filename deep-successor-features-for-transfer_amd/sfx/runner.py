@@ -239,7 +239,8 @@ class NativeEnvLoop:
 
     def __init__(self, engine: SFEngine, batch: int = 32, capacity: int = 1_000_000, gamma: float = 0.9,
                  epsilon: float = 0.1, alpha_w: float = 1e-3, episode_len: int = 500, use_gpi: bool = True,
-                 seed: int = 1, env=None, schedule: str = "all", upd_use_gpi: bool = True, p_end: float = 0.0):
+                 seed: int = 1, env=None, schedule: str = "all", upd_use_gpi: bool = True, p_end: float = 0.0,
+                 device_replay: bool = False):
         import ctypes as C
 
         from ._lib import ENV_RESET_FN, ENV_STEP_FN, check, lib
@@ -284,6 +285,13 @@ class NativeEnvLoop:
         check(lib.sfx_runner_config(r, self.SCHEDULES[schedule], 1 if upd_use_gpi else 0, float(p_end)),
               "sfx_runner_config")
         self.task_index = 0
+        if device_replay:
+            self.set_device_replay(True)
+
+    def set_device_replay(self, on: bool):
+        """SURVEY §8f rank 2 (opt-in; the north_star keeps the replay on the host): the ring in
+        HBM, appended and sampled by each step's gate kernel; the host ring stays as a mirror."""
+        self._check(self._lib.sfx_runner_device_replay(self._r, 1 if on else 0), "sfx_runner_device_replay")
 
     def close(self):
         if getattr(self, "_r", None):

@@ -232,6 +232,12 @@ int sfx_runner_layout(sfx_runner_t r, int64_t* offsets_host /* [10] */);
  * built-in synthetic task (γ = 0 on that transition; 0 = never, like tasks/reacher.py:112).
  * Call between runs (before sfx_runner_set_task). */
 int sfx_runner_config(sfx_runner_t r, int schedule, int use_gpi, float p_end);
+/* Device-resident replay (opt-in -- the north_star keeps the replay on the
+ * host, and so does the headline bench): the ring moves to HBM, each step hands the device only
+ * its transition, and the step's gate kernel appends it and draws the uniform minibatch (index
+ * function replay_index in csrc/sfx_kernels.h).  The host ring stays as a mirror (prefill,
+ * records); switching uploads it before the next run.  Replaces agents/buffer.py:34-64. */
+int sfx_runner_device_replay(sfx_runner_t r, int enable);
 /* Agent.set_active_training_task (agents/agent.py:121-139): reset the env, select the first action */
 int sfx_runner_set_task(sfx_runner_t r, int task);
 /* n random transitions into the replay (warm-up; not env steps) */

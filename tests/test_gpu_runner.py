@@ -96,6 +96,27 @@ def test_runner_matches_oracle(pipeline, round_kernel, monkeypatch):
     eng.close()
 
 
+def test_runner_wide_dw_tiles(monkeypatch):
+    """Opt-in 64 x 64 dW tiles (SFX_DW_WIDE=1, role_dw_wide): used for the 128-wide hidden
+    layers here (4 heads share each backward launch) -- same results as the oracle."""
+    from sfx.runner import NativeEnvLoop
+
+    monkeypatch.setenv("SFX_DW_WIDE", "1")
+    spec = R.Spec(17, 128, 7, 8, ("relu", "relu"))
+    T, ev, alpha, n = 4, 5, 0.05, 16
+    eng, st = make(spec, T, ev)
+    loop = NativeEnvLoop(eng, batch=16, capacity=100, gamma=0.9, epsilon=0.3, alpha_w=alpha, episode_len=7, seed=8)
+    loop.prefill(16)
+    loop.set_task(2)
+    loop.record(n)
+    loop.run(n)
+    recs = loop.records()
+    replay_with_oracle(st, spec, recs, alpha, ev, loop.action())
+    check_state(eng, st, T, n)
+    loop.close()
+    eng.close()
+
+
 def test_runner_with_python_env_callbacks():
     """A host env passed as callbacks (tasks/task.py interface) drives the same loop."""
     from sfx.runner import NativeEnvLoop

@@ -6,6 +6,7 @@ Adam tolerance of test_gpu_engine.py."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 
@@ -120,7 +121,8 @@ def _worker(rank, port, q, cfg=SMALL):
         parts = [None, None]
         dist.all_gather_object(parts, (heads, targets))
         if rank == 0:
-            q.put((actions, torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts]), ws, stats))
+            q.put((actions, torch.cat([p[0] for p in parts]).numpy(), torch.cat([p[1] for p in parts]).numpy(),
+                   ws.numpy(), stats))
     finally:
         dist.destroy_process_group()
 
@@ -137,7 +139,9 @@ def _two_ranks(worker, cfg):
     procs = [ctx.Process(target=worker, args=(r, port, q, cfg)) for r in range(2)]
     for p in procs:
         p.start()
-    out = q.get(timeout=300)
+    # tensors travel as numpy arrays (pickled by value): torch's fd-shared storages need the
+    # sending rank alive until the parent has unpickled them, and rank 0 exits right after
+    out = tuple(torch.from_numpy(x) if isinstance(x, np.ndarray) else x for x in q.get(timeout=300))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -259,7 +263,8 @@ def _tsf_worker(rank, port, q, cfg=TSF_SMALL):
         parts = [None, None]
         dist.all_gather_object(parts, (heads, gg))
         if rank == 0:
-            q.put((actions, torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts]), h, w))
+            q.put((actions, torch.cat([p[0] for p in parts]).numpy(), torch.cat([p[1] for p in parts]).numpy(),
+                   h.numpy(), w.numpy()))
     finally:
         dist.destroy_process_group()
 
