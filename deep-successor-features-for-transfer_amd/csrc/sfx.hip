@@ -140,6 +140,7 @@ struct sfx_handle {
   float *online = nullptr, *target = nullptr, *am = nullptr, *av = nullptr;
   float *w = nullptr, *wm = nullptr, *wv = nullptr;
   int* step = nullptr;
+  int* dcancel = nullptr;  // Geo::cancel: written by runner gates, 0 otherwise
   AdamC* adamc = nullptr;
   float *act = nullptr, *dz = nullptr, *rowloss = nullptr;
   int64_t* spec_next = nullptr;
@@ -211,10 +212,11 @@ void launch(sfx_handle* h, int kind, double bytes, void (*kern)(KArgs...), dim3 
   h->prof_recs.push_back({kind, bytes, a, b});
 }
 
-// Capture `body` (which launches on h->stream) into a graph keyed by `key`, then replay.
+// Capture `body` (which launches on h->stream) into a graph keyed by `key`, then replay
+// (launch = false: instantiate only -- sfx_runner_warm).
 template <class F>
-int run_graph(sfx_handle* h, const GraphKey& key, F body) {
-  if (!h->use_graphs || h->prof) return body();
+int run_graph(sfx_handle* h, const GraphKey& key, F body, bool launch_it = true) {
+  if (!h->use_graphs || h->prof) return launch_it ? body() : SFX_OK;
   auto it = h->graphs.find(key);
   if (it == h->graphs.end()) {
     hipStream_t saved = h->stream;
@@ -236,7 +238,7 @@ int run_graph(sfx_handle* h, const GraphKey& key, F body) {
     if (h->graphs.size() > 256) clear_graphs(h);
     it = h->graphs.emplace(key, ex).first;
   }
-  HIPCHK(hipGraphLaunch(it->second, h->stream));
+  if (launch_it) HIPCHK(hipGraphLaunch(it->second, h->stream));
   return SFX_OK;
 }
 
@@ -625,7 +627,7 @@ void free_all(sfx_handle* h) {
   }
   for (hipEvent_t e : h->prof_pool) (void)hipEventDestroy(e);
   for (void* p : {(void*)h->online, (void*)h->target, (void*)h->am, (void*)h->av, (void*)h->w, (void*)h->wm,
-                  (void*)h->wv, (void*)h->step, (void*)h->adamc, (void*)h->round_ctr, (void*)h->act, (void*)h->dz, (void*)h->rowloss, (void*)h->spec_next,
+                  (void*)h->wv, (void*)h->step, (void*)h->dcancel, (void*)h->adamc, (void*)h->round_ctr, (void*)h->act, (void*)h->dz, (void*)h->rowloss, (void*)h->spec_next,
                   (void*)h->dout, (void*)h->dxpart, (void*)h->dxctr})
     if (p) (void)hipFree(p);
   if (h->hout) (void)hipHostFree(h->hout);
@@ -887,6 +889,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   alloc((void**)&h->wm, wBytes);
   alloc((void**)&h->wv, wBytes);
   alloc((void**)&h->step, sizeof(int) * T);
+  alloc((void**)&h->dcancel, 64);
   alloc((void**)&h->adamc, sizeof(AdamC) * T);
   alloc((void**)&h->round_ctr, sizeof(unsigned) * T);
   {  // split-N dX: every layer's N split into <= 256-wide chunks, tiles of 32 rows x 16 columns
@@ -941,6 +944,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   G.act = h->act;
   G.dz = h->dz;
   G.rowloss = h->rowloss;
+  G.cancel = h->dcancel;
   G.lastOff = h->actOff[h->NL - 1];
   *out = h;
   return SFX_OK;

@@ -171,6 +171,7 @@ struct Geo {
   float* act;         // [NROLE][T][actSize]
   float* dz;          // [T][actSize]
   float* rowloss;     // [T][MMAX] per-row Σ (c - t)^2 of the last TD target
+  const int* cancel;  // runner steps: 1 when the step's gate cancelled it (see step_cancelled)
   int lastOff;        // offset of the last layer's output inside an activation block
 
   // off: per-layer offset inside a block (passed per launch as a scalar, never indexed)
@@ -186,6 +187,13 @@ struct Geo {
 };
 
 __device__ __forceinline__ int rslot(unsigned long long mask, int head) { return (int)((mask >> head) & 1ull); }
+
+// A runner step whose gate cancelled it (the host aborted, or the gate timed out waiting for the
+// host) runs its launches anyway -- they are already queued -- but must not commit: every store
+// to persistent state (parameters and moments of the write slot, Adam step counters, w, g, h) is
+// predicated on this word, written by the step's gate (0 outside runner steps).  Read once at
+// entry, used only at the stores, so its latency overlaps the operand loads.
+__device__ __forceinline__ int step_cancelled(const int* c) { return __builtin_nontemporal_load(c); }
 
 // Division by a runtime divisor 1 <= d, for 0 <= x < 2^22: one multiply by a float reciprocal
 // and one correction step (a hardware integer divide is a ~40-instruction sequence, and the
@@ -322,6 +330,7 @@ __device__ void lms_block(const Geo& G, const FwdArgs& F) {
   __shared__ float s_e;
   const int tid = threadIdx.x, d = G.d;
   float* w = G.w + (long long)F.lms_head * G.dpad;
+  const int cx = step_cancelled(G.cancel);
   const float wk = tid < d ? w[tid] : 0.f, pk = tid < d ? F.lms_phi[tid] : 0.f;
   if (tid < d) s_p[tid] = __fmul_rn(pk, wk);
   __syncthreads();
@@ -331,7 +340,7 @@ __device__ void lms_block(const Geo& G, const FwdArgs& F) {
     s_e = __fmul_rn(F.lms_alpha, __fsub_rn(F.lms_r[0], rf));
   }
   __syncthreads();
-  if (tid < d) w[tid] = __fadd_rn(wk, __fmul_rn(s_e, pk));
+  if (tid < d && !cx) w[tid] = __fadd_rn(wk, __fmul_rn(s_e, pk));
 }
 
 // L0 = true (layer-1 launches of a forward from the states): the workgroup first computes the
@@ -958,7 +967,7 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
   if constexpr (TDG) {
     // N = A*d <= 128: at most one 64-wide chunk per wave; its W slice is fetched before K2
     __shared__ TdgSmem sm;
-    if (tile == 0 && A.inc_step && threadIdx.x == 0) {  // no dW reads them in this launch
+    if (tile == 0 && A.inc_step && threadIdx.x == 0 && !step_cancelled(G.cancel)) {  // no dW reads them in this launch
       const int st = G.step[head] + 1;
       const AdamC ac = adam_consts(A.hp, st);
       if constexpr (C) {  // read by this launch's dW tiles
@@ -1121,6 +1130,7 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
   float* Mw = G.am + wo;
   float* Vw = G.av + wo;
   const AdamC c = load_adamc<C>(G.adamc + head);  // bias corrections of this step (double pow once per head)
+  const int cx = step_cancelled(G.cancel);
   const int nn = n0 + r, kb0 = k0 + r, kb1 = k0 + 16 + r;
   // prefetch the optimizer state of the 8 weights this lane will update
   float pp[8], pm[8], pv[8];
@@ -1207,18 +1217,22 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
         const int k = h ? kb1 : kb0;
         const size_t off = (size_t)L.wOff + (size_t)n * K + k;
         adam_apply(pp[e], pm[e], pv[e], h ? acc1[i] : acc0[i], c);
-        stc<C>(Pw + off, pp[e]);
-        st_moment(Mw + off, pm[e]);
-        st_moment(Vw + off, pv[e]);
+        if (!cx) {
+          stc<C>(Pw + off, pp[e]);
+          st_moment(Mw + off, pm[e]);
+          st_moment(Vw + off, pv[e]);
+        }
         if (fuse) sW[(n - nbase) * KFUSE + k] = pp[e];
       }
     }
   }
   if (dob) {
     adam_apply(bp, bm, bv, bsum, c);
-    stc<C>(Pw + L.bOff + nbias, bp);
-    st_moment(Mw + L.bOff + nbias, bm);
-    st_moment(Vw + L.bOff + nbias, bv);
+    if (!cx) {
+      stc<C>(Pw + L.bOff + nbias, bp);
+      st_moment(Mw + L.bOff + nbias, bm);
+      st_moment(Vw + L.bOff + nbias, bv);
+    }
     if (fuse) sB[nbias - nbase] = bp;
   }
   if (fuse) fused_v0<C>(G, A, L, head, nbase, sW, sB, sX);
@@ -1248,6 +1262,7 @@ __device__ void role_dw_wide(const Geo& G, const BwdArgs& A, int head, const Rol
   float* Mw = G.am + wo;
   float* Vw = G.av + wo;
   const AdamC c = load_adamc<false>(G.adamc + head);
+  const int cx = step_cancelled(G.cancel);
   const int kb0 = k0 + r, kb1 = k0 + 16 + r;
   // optimizer state of the 8·NW weights this lane updates, requested first
   float pp[8 * NW], pm[8 * NW], pv[8 * NW];
@@ -1329,7 +1344,7 @@ __device__ void role_dw_wide(const Geo& G, const BwdArgs& A, int head, const Rol
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int e = (s * 4 + i) * 2 + h;
-        if (ok[e]) {
+        if (ok[e] && !cx) {
           const size_t off = (size_t)L.wOff + (size_t)n * K + (h ? kb1 : kb0);
           adam_apply(pp[e], pm[e], pv[e], acc[s][h][i], c);
           stc<false>(Pw + off, pp[e]);
@@ -1340,7 +1355,7 @@ __device__ void role_dw_wide(const Geo& G, const BwdArgs& A, int head, const Rol
     }
 #pragma unroll
   for (int s = 0; s < NW; ++s)
-    if (dob[s]) {
+    if (dob[s] && !cx) {
       const int nb = n0 + 16 * s + r;
       adam_apply(bp[s], bm[s], bv[s], bsum[s], c);
       stc<false>(Pw + L.bOff + nb, bp[s]);
@@ -1373,6 +1388,7 @@ __device__ void role_tail(const Geo& G, const BwdArgs& A, int head) {
   __shared__ float s_red[256];
   __shared__ float s_phi[2048];
   const int step = A.step_in_tail && A.inc_step ? G.step[head] + 1 : G.step[head];
+  const int cx = step_cancelled(G.cancel);
   const float* rl = G.rowloss + (long long)head * MMAX;
   float* w = G.w + (long long)head * G.dpad;
   float part = 0.f;  // this thread's rows of Σ_b rowloss (b = tid, tid + 256, ...)
@@ -1400,7 +1416,7 @@ __device__ void role_tail(const Geo& G, const BwdArgs& A, int head) {
       for (int b = 0; b < M; ++b) gw = __builtin_fmaf(__fmul_rn(nrm, s_e[b]), ph[(size_t)b * d + tid], gw);
     }
     __syncthreads();
-    if (tid < d) adam_el(w + tid, G.wm + (long long)head * G.dpad + tid, G.wv + (long long)head * G.dpad + tid, gw, c);
+    if (tid < d && !cx) adam_el(w + tid, G.wm + (long long)head * G.dpad + tid, G.wv + (long long)head * G.dpad + tid, gw, c);
     l2 = (float)((double)se / (double)M);
   }
   const float s = A.losses ? block_sum(part, s_red) : 0.f;
@@ -1412,7 +1428,7 @@ __device__ void role_tail(const Geo& G, const BwdArgs& A, int head) {
       lo[1] = l1;
       lo[2] = l2;
     }
-    if (A.step_in_tail) {
+    if (A.step_in_tail && !cx) {
       G.step[head] = step;
       G.adamc[head] = adam_consts(A.hp, step);
     }
@@ -1711,20 +1727,23 @@ __global__ __launch_bounds__(256) void k_gpi(Geo G, GpiArgs A) {
 // -------------------------------------------------------------------------------------
 struct HostResult {  // host-coherent; seq written last
   long long sel0, sel1;
-  int flag, err;
+  int flag, err;       // err: a gate timed out (set by the gate itself, system scope)
+  int cancelled, pad_; // the published step was cancelled at its gate: nothing of it committed
   long long seq;
 };
 
 // Post the step's result (selected action, speculation verdict) to host-coherent memory;
 // seq is written last (system release).  The inputs are read with coherent (sc1) loads.
 __device__ __forceinline__ void publish_result(const int64_t* sel, const int* flag, HostResult* out,
-                                               const long long* dctr) {
+                                               const long long* dctr, const int* cancel) {
   const long long s0 = __hip_atomic_load(sel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const long long s1 = __hip_atomic_load(sel + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int cx = __hip_atomic_load(cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   out->sel0 = s0;
   out->sel1 = s1;
   out->flag = f;
+  out->cancelled = cx;
   __threadfence_system();
   __hip_atomic_store(&out->seq, *dctr, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1840,7 +1859,7 @@ __global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
       const unsigned prev = __hip_atomic_fetch_add(V.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("" ::: "memory");
       if (prev == (unsigned)V.nblocks - 1) {
-        publish_result(V.g.sel_out, V.flag, V.pub, V.pub_dctr);
+        publish_result(V.g.sel_out, V.flag, V.pub, V.pub_dctr, G.cancel);
         __hip_atomic_store(V.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -1887,25 +1906,38 @@ struct GateArgs {
   long long* dctr;      // device: last step a gate opened (this gate opens dctr + 1)
   long long timeout;
   int* err;             // host-coherent
+  const int* hcancel;   // written by the host (sfx_runner abort): cancel every step still waiting
+  int* cancel;          // device: this step's verdict for its kernels (Geo::cancel)
 };
+
+// Wait for the host's go of this step (bounded); 1 if the step may run, 0 if it is cancelled.
+// One thread.  dctr advances either way, so the gates of later steps keep their numbering.
+__device__ __forceinline__ int gate_wait(const GateArgs& g) {
+  int ok = 1;
+  const long long want = *g.dctr + 1;
+  const long long t0 = wall_clock64();
+  unsigned it = 0;
+  while (__hip_atomic_load(g.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+    if ((++it & 15) == 0 && __hip_atomic_load(g.hcancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+      ok = 0;
+      break;
+    }
+    if (wall_clock64() - t0 > g.timeout) {
+      ok = 0;
+      __hip_atomic_store(g.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+  *g.dctr = want;
+  *g.cancel = ok ? 0 : 1;
+  return ok;
+}
 
 __global__ __launch_bounds__(256) void k_gate(GateArgs g) {
   __shared__ int ok;
   PROBE_T(pt0);
-  if (threadIdx.x == 0) {
-    ok = 1;
-    const long long want = *g.dctr + 1;
-    const long long t0 = wall_clock64();
-    while (__hip_atomic_load(g.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
-      if (wall_clock64() - t0 > g.timeout) {
-        ok = 0;
-        __hip_atomic_store(g.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(8);
-    }
-    *g.dctr = want;
-  }
+  if (threadIdx.x == 0) ok = gate_wait(g);
   __syncthreads();
   if (!ok) return;
   PROBE_MARK();
@@ -1955,20 +1987,7 @@ __global__ __launch_bounds__(256) void k_gate_replay(ReplayGateArgs A) {
   __shared__ __attribute__((aligned(16))) unsigned char tail[REPLAY_TAIL_MAX];
   const GateArgs& g = A.g;
   PROBE_T(pt0);
-  if (threadIdx.x == 0) {
-    ok = 1;
-    const long long want = *g.dctr + 1;
-    const long long t0 = wall_clock64();
-    while (__hip_atomic_load(g.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
-      if (wall_clock64() - t0 > g.timeout) {
-        ok = 0;
-        __hip_atomic_store(g.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(8);
-    }
-    *g.dctr = want;
-  }
+  if (threadIdx.x == 0) ok = gate_wait(g);
   __syncthreads();
   if (!ok) return;
   PROBE_MARK();
@@ -2030,9 +2049,10 @@ __global__ __launch_bounds__(256) void k_gate_replay(ReplayGateArgs A) {
   PROBE_REC(9, pt0);
 }
 
-__global__ void k_publish(const int64_t* sel, const int* flag, HostResult* out, const long long* dctr) {
+__global__ void k_publish(const int64_t* sel, const int* flag, HostResult* out, const long long* dctr,
+                          const int* cancel) {
   PROBE_T(pt0);
-  if (threadIdx.x == 0) publish_result(sel, flag, out, dctr);
+  if (threadIdx.x == 0) publish_result(sel, flag, out, dctr, cancel);
   PROBE_REC(18, pt0);
 }
 

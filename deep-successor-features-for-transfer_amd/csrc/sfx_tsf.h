@@ -65,6 +65,7 @@ struct TsfArgs {
   float* losses; // [3]: [1] = l1 (written by the ψ tail); [0], [2] written here
   const float* dzlast;  // output gradient of the policy's ψ head [B][O] (written by K2)
   const int* step;      // Adam step of the policy (already bumped by the ψ path)
+  const int* cancel;    // runner steps: the gate's cancel word (Geo::cancel); no commit when set
   float* w;             // [d] reward weights of the policy (+ moments; its global row when sharded)
   float* wm;
   float* wv;
@@ -376,6 +377,7 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A) {
   PROBE_T(t0_);
   const float* snap = A.snap;
   const int step = *A.step;
+  const int cx = step_cancelled(A.cancel);
   const FDiv fG = fdiv(G);
   // LDS: daff [0, 4096) | role operands [4096, 12288) | φ̃ rows [12288, 16384) | ψ gradient rows
   // [16384, 20480) | g-Linear dg [20480, 21504)
@@ -404,7 +406,7 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A) {
     if (tid < d) {
       float gw = 0.f;
       for (int b = 0; b < B; ++b) gw = __builtin_fmaf(s_dr[b], s_tp[b * d + tid], gw);
-      adam_el(A.w + tid, A.wm + tid, A.wv + tid, gw, adam_consts(A.hpw, step));
+      if (!step_cancelled(A.cancel)) adam_el(A.w + tid, A.wm + tid, A.wv + tid, gw, adam_consts(A.hpw, step));
     }
     if (tid == 0 && A.losses) {
       const float l2 = (float)((double)sse / (double)B);
@@ -433,7 +435,7 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A) {
       g = __fmul_rn(2.f, sb);
     }
     const long long ho = (long long)A.pol * A.Ph;
-    if (j < A.Ph) adam_el(A.hp + j, A.hm + ho + j, A.hv + ho + j, g, adam_consts(A.hph, step));
+    if (j < A.Ph && !cx) adam_el(A.hp + j, A.hm + ho + j, A.hv + ho + j, g, adam_consts(A.hph, step));
     PROBE_REC(12, t0_);
     return;
   }
@@ -449,7 +451,7 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A) {
   float* gp = A.g + (long long)A.pol * A.Pg;
   float* gm = A.gm + (long long)A.pol * A.Pg;
   float* gv = A.gv + (long long)A.pol * A.Pg;
-  for (int j = tid; j < nq * (n_s + 1); j += 256) {
+  for (int j = tid; j < (cx ? 0 : nq * (n_s + 1)); j += 256) {
     const int qq = j / (n_s + 1), i = j - qq * (n_s + 1);
     int o;
     float g;
@@ -494,7 +496,7 @@ __global__ __launch_bounds__(256) void k_tsf_flow(TsfArgs A) {
   }
   const float g = __fadd_rn(g0, g1);
   const long long go = (long long)A.pol * A.Pg;
-  if (j0 < nfl) adam_el(A.g + go + j, A.gm + go + j, A.gv + go + j, g, adam_consts(A.hpg, *A.step));
+  if (j0 < nfl && !step_cancelled(A.cancel)) adam_el(A.g + go + j, A.gm + go + j, A.gv + go + j, g, adam_consts(A.hpg, *A.step));
   PROBE_REC(15, t0_);
 }
 

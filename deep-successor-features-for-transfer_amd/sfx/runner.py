@@ -319,13 +319,22 @@ class NativeEnvLoop:
         self._check(self._lib.sfx_runner_action(self._r, out), "sfx_runner_action")
         return int(out[0]), int(out[1])
 
+    def warm(self):
+        """Instantiate this schedule's step graphs (all span lengths, both slot parities) now."""
+        self._check(self._lib.sfx_runner_warm(self._r), "sfx_runner_warm")
+
+    def set_gate_timeout(self, seconds: float):
+        """Bound of each step's gate wait; a step released later is cancelled and re-issued."""
+        self._check(self._lib.sfx_runner_gate_timeout(self._r, float(seconds)), "sfx_runner_gate_timeout")
+
     def stats(self) -> dict:
         C = self._C
-        a, b, c, w = C.c_longlong(), C.c_longlong(), C.c_longlong(), C.c_double()
+        a, b, c, w, rt = C.c_longlong(), C.c_longlong(), C.c_longlong(), C.c_double(), C.c_longlong()
         self._check(self._lib.sfx_runner_stats(self._r, C.byref(a), C.byref(b), C.byref(c), C.byref(w)),
                     "sfx_runner_stats")
+        self._check(self._lib.sfx_runner_retried(self._r, C.byref(rt)), "sfx_runner_retried")
         return {"env_steps": a.value, "prelaunched": b.value, "host_round_steps": c.value,
-                "host_wait_us": round(w.value, 1)}
+                "host_wait_us": round(w.value, 1), "retried": rt.value}
 
     def gpi_counters(self) -> np.ndarray:
         T = self.eng.T

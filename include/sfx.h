@@ -248,7 +248,20 @@ int sfx_runner_run(sfx_runner_t r, int n);
 int sfx_runner_action(sfx_runner_t r, int64_t* out_host /* [3] */);
 int sfx_runner_stats(sfx_runner_t r, long long* env_steps, long long* prelaunched, long long* host_round_steps,
                      double* wait_us);
-/* SF.gpi_counters (features/successor.py:270-272): [T][T] counts of the GPI task per active task */
+/* Bound of a step's gate wait (default 5 s).  A step whose inputs the host releases later is
+ * cancelled at its gate -- none of its launches commits parameters, moments, step counters or w --
+ * and the runner issues it again from the same staged inputs (counted by sfx_runner_retried).
+ * On any error of sfx_runner_run (an env callback, a launch, the device) the steps queued behind
+ * the host are cancelled the same way before the error returns: the heads hold the last
+ * completed step and the runner stays usable. */
+int sfx_runner_gate_timeout(sfx_runner_t r, double seconds);
+/* Instantiate the step graphs of the current schedule and task ahead of the first steps (every
+ * span length, both slot parities) without running them: a short run then measures replays, not
+ * graph captures. */
+int sfx_runner_warm(sfx_runner_t r);
+int sfx_runner_retried(sfx_runner_t r, long long* retried);
+/* SF.gpi_counters (features/successor.py:270-272): [T][T] counts of the GPI task per active task
+ * (counted only with GPI action selection, as SF.GPI(update_counters=use_gpi), agents/sfdqn.py:41) */
 int sfx_runner_gpi_counters(sfx_runner_t r, long long* out_host /* [T*T] */);
 /* test hooks: keep the input record and (task, have_batch, c, greedy a, taken a, terminal) of
  * the next `capacity` steps */

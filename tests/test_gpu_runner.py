@@ -213,3 +213,136 @@ def test_runner_active_schedules_match_oracle(schedule, upd_use_gpi):
     assert loop.stats()["prelaunched"] > n // 2
     loop.close()
     eng.close()
+
+
+@pytest.mark.parametrize("schedule", ["all", "active"])
+def test_runner_gate_timeouts_cancel_and_retry(schedule):
+    """A gate bound of 10 ns: every pre-launched step's gate gives up before the host releases
+    it, so the step is cancelled (none of its launches commits -- parameters, moments, step
+    counters, w) and re-issued from the same staged inputs.  The results must still be the
+    oracle's, step for step."""
+    from sfx.runner import NativeEnvLoop
+
+    spec = R.Spec(17, 32, 7, 8, ("relu", "relu"))
+    T, ev, alpha, n = 3, 1000, 0.05, 20
+    eng, st = make(spec, T, ev)
+    loop = NativeEnvLoop(eng, batch=16, capacity=200, gamma=0.9, epsilon=0.3, alpha_w=alpha, episode_len=7, seed=5,
+                         schedule=schedule)
+    loop.prefill(16)
+    loop.set_task(1)
+    loop.set_gate_timeout(1e-8)
+    loop.record(n)
+    loop.run(n)
+    stats = loop.stats()
+    assert stats["retried"] > 0 and stats["prelaunched"] > 0, stats
+    recs = loop.records()
+    if schedule == "all":
+        replay_with_oracle(st, spec, recs, alpha, ev, loop.action())
+        check_state(eng, st, T, n)
+    else:
+        for rec in recs:
+            batch = (torch.from_numpy(rec["s"]), torch.from_numpy(rec["a"]), torch.from_numpy(rec["rb"]).view(-1, 1),
+                     torch.from_numpy(rec["phi"]), torch.from_numpy(rec["s1"]), torch.from_numpy(rec["gamma"]))
+            R.sf_update(st, batch, 1, use_gpi=True, target_update_ev=ev)
+        params_close(torch.stack([eng.get_head(t, 0) for t in range(T)]), st.online, 1e-3 * n)
+        rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-3, atol=1e-6)
+    # the default bound again: pre-launched steps run without being re-issued
+    loop.set_gate_timeout(5.0)
+    before = loop.stats()["retried"]
+    loop.run(8)
+    assert loop.stats()["retried"] == before
+    loop.close()
+    eng.close()
+
+
+def test_runner_env_error_cancels_queue():
+    """The env callback raises in the middle of a run while later steps are already queued on
+    the device (8-step graphs): the run fails, the queued steps are cancelled at their gates, the
+    heads hold the last completed step, and the runner continues afterwards -- the whole recorded
+    sequence still replays through the oracle step for step."""
+    from sfx._lib import SFXError
+    from sfx.runner import NativeEnvLoop
+
+    class FlakyEnv:
+        def __init__(self, n_s, d, fail_at):
+            self.n_s, self.d, self.t, self.fail_at = n_s, d, 0, fail_at
+
+        def reset(self, task):
+            return np.full(self.n_s, 0.2 + 0.1 * task, np.float32)
+
+        def step(self, task, a):
+            self.t += 1
+            if self.t == self.fail_at:
+                raise RuntimeError("env failure")
+            s1 = np.cos(np.arange(self.n_s, dtype=np.float32) * 0.3 * (self.t % 11)).astype(np.float32)
+            phi = ((np.arange(self.d) + self.t) % 5).astype(np.float32) * 0.1
+            return s1, phi, float(phi[task % self.d]), False
+
+    spec = R.Spec(17, 32, 7, 8, ("relu", "relu"))
+    T, ev, alpha = 3, 1000, 0.05
+    eng, st = make(spec, T, ev)
+    env = FlakyEnv(spec.n_s, spec.d, fail_at=14 + 12)  # 14 prefill calls, then the 12th env step fails
+    loop = NativeEnvLoop(eng, batch=8, capacity=100, gamma=0.9, epsilon=0.2, alpha_w=alpha, episode_len=50, seed=2,
+                         env=env)
+    loop.prefill(14)
+    loop.set_task(2)
+    loop.record(40)
+    with pytest.raises(SFXError):
+        loop.run(20)
+    recs = loop.records()
+    assert len(recs) == 11
+    st_mid = R.SFState(spec, st.online.clone(), st.target.clone(), st.w.clone())
+    for k, rec in enumerate(recs):  # the heads after the failure: exactly the 11 completed steps
+        st_mid.w[2] = R.lms_update(st_mid.w[2].view(-1, 1), torch.from_numpy(rec["phi1"]), float(rec["r1"][0]),
+                                   alpha).view(-1)
+        batch = (torch.from_numpy(rec["s"]), torch.from_numpy(rec["a"]), torch.from_numpy(rec["phi"]),
+                 torch.from_numpy(rec["s1"]), torch.from_numpy(rec["gamma"]))
+        R.deep_all_task_step(st_mid, batch, lr=1e-3, target_update_ev=ev)
+    check_state(eng, st_mid, T, len(recs))
+    loop.run(10)
+    recs = loop.records()
+    assert len(recs) == 21
+    replay_with_oracle(st, spec, recs, alpha, ev, loop.action())
+    check_state(eng, st, T, len(recs))
+    loop.close()
+    eng.close()
+
+
+def test_runner_forced_host_rounds_with_spans():
+    """sfx_debug_force_rerun on the native runner: every step's device rounds are treated as
+    failed from policy 1 on, so each step finishes with host rounds on the side stream while the
+    next 8-step graph waits at its gate -- with target syncs every 3 updates.  Same results."""
+    from sfx.runner import NativeEnvLoop
+
+    spec = R.Spec(17, 32, 7, 8, ("relu", "relu"))
+    T, ev, alpha, n = 4, 3, 0.05, 24
+    eng, st = make(spec, T, ev)
+    eng.debug_force_rerun(1)
+    loop = NativeEnvLoop(eng, batch=8, capacity=100, gamma=0.9, epsilon=0.3, alpha_w=alpha, episode_len=9, seed=7)
+    loop.prefill(8)
+    loop.set_task(0)
+    loop.record(n)
+    loop.run(n)
+    stats = loop.stats()
+    assert stats["host_round_steps"] == n and stats["prelaunched"] > 0, stats
+    replay_with_oracle(st, spec, recs := loop.records(), alpha, ev, loop.action())
+    assert len(recs) == n
+    check_state(eng, st, T, n)
+    loop.close()
+    eng.close()
+
+
+def test_runner_gpi_counters_follow_use_gpi():
+    """SF.GPI(update_counters=use_gpi) (agents/sfdqn.py:41): without GPI action selection the
+    counters stay at zero."""
+    from sfx.runner import NativeEnvLoop
+
+    spec = R.Spec(17, 32, 7, 8, ("relu", "relu"))
+    eng, _ = make(spec, 2, 1000)
+    loop = NativeEnvLoop(eng, batch=8, capacity=100, use_gpi=False, seed=3)
+    loop.prefill(8)
+    loop.set_task(1)
+    loop.run(6)
+    assert loop.gpi_counters().sum() == 0
+    loop.close()
+    eng.close()
