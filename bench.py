@@ -65,10 +65,15 @@ def parse():
     p.add_argument("--spec-rounds", type=int, default=2,
                    help="speculative rounds of the all-task step launched on the device (more run from the host)")
     p.add_argument("--prof-steps", type=int, default=50)
+    p.add_argument("--repeats", type=int, default=3,
+                   help="time the same K-step window this many more times after the measured one (spread only)")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-other", dest="other", action="store_false",
                    help="skip the other one-GPU configs (active-task C2, TSF C3, TSF-NF) reported beside the headline")
+    p.add_argument("--layout", choices=["sharded", "replicas"], default="sharded",
+                   help="N > 1 headline: the north-star sharded layout (C4: 8 heads per GPU, one env stream, "
+                        "libsfx RCCL all-reduces; default) or N independent single-GPU replicas (side key otherwise)")
     p.add_argument("--shard-steps", type=int, default=400,
                    help="also time the north-star sharded mode (heads split over ranks, RCCL all-reduce-max "
                         "GPI) for this many env steps; 0 skips it")
@@ -102,6 +107,46 @@ def tsf_problem(T: int, K: int, seed: int):
         gs.append(torch.cat(parts))
     hl = torch.nn.Linear(sh["G"], sh["d"])
     return online, w, torch.stack(gs), torch.cat([hl.weight.detach().reshape(-1), hl.bias.detach()])
+
+
+def head_params(sh) -> int:
+    """P of SURVEY §8: parameters of one ψ head, (n_s·H + H) + n_hidden·(H² + H) + (H·A·d + A·d)."""
+    n_s, H, A, d, nh = sh["n_s"], sh["H"], sh["A"], sh["d"], len(sh["acts"])
+    return (n_s * H + H) + nh * (H * H + H) + (H * A * d + A * d)
+
+
+def algorithmic_step_bytes(T: int, U: int, P: int, weight_bytes: int) -> float:
+    """bytes one env step must move at minimum -- the action-select GPI reads all T
+    heads, the update-path GPI over s' reads them once more, and each of the U updated heads is
+    read by the target and online forwards and the backward, plus Adam's fp32 read of p, g, m, v
+    (16 B) and write of p, m, v (12 B).  weight_bytes = 2 is §8(d)'s bf16-weights figure
+    (U·P·34); 4 is the same count for fp32 weights, the arithmetic this build runs (U·P·40)."""
+    wb = weight_bytes
+    return 2.0 * wb * T * P + U * P * (3 * wb + 28)
+
+
+def cpu_info() -> dict:
+    """Host CPU model and physical core count (unique (package, core) pairs of /proc/cpuinfo)."""
+    model, cores = None, set()
+    try:
+        phys = core = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name" and model is None:
+                model = v
+            elif k == "physical id":
+                phys = v
+            elif k == "core id":
+                core = v
+            elif not k and phys is not None:
+                cores.add((phys, core))
+                phys = core = None
+        if phys is not None:
+            cores.add((phys, core))
+    except OSError:
+        pass
+    return {"cpu_model": model, "physical_cores_on_host": len(cores) or None, "logical_cpus_on_host": os.cpu_count()}
 
 
 def cpu_baseline(args, seconds: float):
@@ -160,54 +205,71 @@ def cpu_baseline(args, seconds: float):
             el = time.perf_counter() - t0
             if el >= seconds:
                 break
-    return {"value": steps / el, "unit": "env steps/s", "cores": cores, "kind": "port",
-            "sample": f"{steps} env steps ({el:.1f} s) of the same {args.schedule}-task loop, T={T}, B={B}, "
-                      f"oracle/ref_cpu.py on torch CPU with {cores} threads"}
+    out = {"value": steps / el, "unit": "env steps/s", "cores": cores, "kind": "port",
+           "sample": f"{steps} env steps ({el:.1f} s) of the same {args.schedule}-task loop, T={T}, B={B}, "
+                     f"oracle/ref_cpu.py on torch CPU with {cores} threads (cores = torch intra-op threads used)"}
+    out.update(cpu_info())
+    return out
 
 
-def bench_sharded(args, world, rank, device, barrier, dist):
-    """North-star multi-GPU mode: T_loc = --heads heads per rank, T_glob =
-    T_loc * world source tasks, one lock-step env stream replicated on every rank, GPI maxima
-    all-reduced (MAX) over RCCL.  Returns env-steps/s of that one stream (max over ranks)."""
+def bench_sharded(args, world, rank, device, barrier, dist, steps=None, warmup=None):
+    """North-star multi-GPU layout (BASELINE config C4): T_loc = --heads heads per rank,
+    T_glob = T_loc * world source tasks, ONE env / replay stream replicated on every rank with the
+    same seed, every head updated per env step (agents/sfdqn.py:47-60), GPI maxima and the env
+    action's q table all-reduced (MAX) by libsfx itself -- RCCL calls captured in the step graphs
+    of the native runner (sfx_runner schedule "sharded").  Returns env-steps/s of that stream
+    (max-over-ranks time)."""
     from sfx.engine import SFEngine
     from sfx.init import reference_heads
-    from sfx.runner import ShardedEnvLoop
-    from sfx.shard import all_reduce_max_fn
+    from sfx.runner import NativeEnvLoop
+    from sfx.shard import init_comm, set_host_comm
 
+    steps = args.shard_steps if steps is None else steps
+    warmup = max(20, steps // 10) if warmup is None else warmup
     T_loc, B = args.heads, args.batch
     Tg = T_loc * world
     eng = SFEngine(T_loc, SHAPE["n_s"], SHAPE["H"], SHAPE["A"], SHAPE["d"], SHAPE["acts"], max_batch=B, device=device)
     online, w = reference_heads(Tg, SHAPE["n_s"], SHAPE["H"], SHAPE["A"], SHAPE["d"], SHAPE["acts"], seed=0)
     eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
     eng.set_target_update_ev(1000)
-    ar = all_reduce_max_fn(via_host=args.via_host) if world > 1 else (lambda t: None)
-    loop = ShardedEnvLoop(eng, Tg, rank, ar, batch=B, seed=1)
+    eng.set_spec_rounds(args.spec_rounds)
+    eng.shard_setup(Tg, rank * T_loc)
     for t in range(T_loc):
         eng.load_head(t, online[rank * T_loc + t], 0)
         eng.load_head(t, online[rank * T_loc + t], 1)
     for t in range(Tg):
         eng.load_w(t, w[t])
+    if args.via_host:
+        set_host_comm(eng, rank, world)
+    else:
+        init_comm(eng, rank, world)
+    loop = NativeEnvLoop(eng, batch=B, seed=1, schedule="sharded")
     loop.prefill(1000)
     loop.set_task(0)
-    loop.run(max(20, args.shard_steps // 10))
+    loop.warm()
+    loop.run(warmup)
     barrier()
     t0 = time.perf_counter()
-    loop.run(args.shard_steps)
+    loop.run(steps)
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
         t = torch.tensor([dt], device="cpu" if args.via_host else device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    st = loop.stats()
+    st.update(eng.step_stats())
+    loop.close()
     eng.close()
-    v = args.shard_steps / dt
-    return {"value": round(v, 2), "unit": "env steps/s", "ms_per_step": round(1000.0 * dt / args.shard_steps, 4),
-            "steps": args.shard_steps, "heads_total": Tg, "heads_per_gpu": T_loc,
+    v = steps / dt
+    return {"value": round(v, 2), "unit": "env steps/s", "ms_per_step": round(1000.0 * dt / steps, 4),
+            "steps": steps, "warmup": warmup, "heads_total": Tg, "heads_per_gpu": T_loc,
             "head_updates_per_s": round(v * Tg, 1), "parallelism": f"heads sharded over {world} GPU(s)",
-            "collective": (("gloo via host (rehearsal)" if args.via_host else "RCCL") +
-                           " all-reduce(MAX) of GPI maxima [T_glob,B,A] per round + int64 action key")
-                          if world > 1 else "none (1 rank)",
-            "rounds": loop.sharded.stats}
+            "loop": "native C++ runner (sfx_runner schedule sharded): one pre-launched graph per env step",
+            "collective": ("gloo via host (rehearsal)" if args.via_host else "RCCL (library-owned communicator)") +
+                          " all-reduce(MAX): GPI maxima [T_glob,B,A] per speculative round, then verification "
+                          "maxima ++ the env action's q table [T_glob,A] in one call",
+            "rounds": st}
 
 
 def bench_sharded_tsf(args, world, rank, device, barrier, dist):
@@ -373,6 +435,7 @@ def main():
                              p_end=0.0 if args.tsf_K is None else 0.01, device_replay=args.replay == "device")
         loop.prefill(1000)
         loop.set_task(0)
+        loop.warm()  # instantiate every step graph now: the timed steps replay graphs, never capture
     else:
         task_cls = SynthReacher if args.tsf_K is None else SynthHopper
         loop = EnvLoop(eng, schedule=args.schedule, batch=B, seed=1 + rank, task_cls=task_cls)
@@ -395,6 +458,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     value = world * args.steps / dt
+    # spread: the same K-step window timed again (not part of `value`)
+    repeats = []
+    if args.repeats > 0:
+        for _ in range(args.repeats):
+            barrier()
+            t1 = time.perf_counter()
+            loop.run(args.steps)
+            barrier()
+            repeats.append(round(world * args.steps / (time.perf_counter() - t1), 2))
 
     # live per-kernel durations (HIP events around each launch) for the roofline figure
     eng.prof_reset()
@@ -404,8 +476,18 @@ def main():
     eng.prof_enable(False)
     eng.prof_reset()
 
-    sharded = None
-    if args.shard_steps > 0 and args.schedule == "all":
+    sharded = replicas = None
+    layout = "single" if world == 1 else f"replica{world}"
+    if world > 1 and args.schedule == "all" and args.tsf_K is None and args.layout == "sharded":
+        # the headline at N > 1 is config C4's layout, timed with the same W / K; the replicas just
+        # measured stay beside it
+        replicas = {"value": round(value, 2), "unit": "env steps/s", "ms_per_step": round(1000.0 * dt / args.steps, 4),
+                    "parallelism": f"replica{world}", "note": f"{world} independent 8-head learners, no collective"}
+        sharded = bench_sharded(args, world, rank, device, barrier, dist, steps=args.steps, warmup=args.warmup)
+        value = sharded["value"]
+        dt = sharded["ms_per_step"] * args.steps / 1000.0
+        layout = f"shard{world}"
+    elif args.shard_steps > 0 and args.schedule == "all":
         sharded = bench_sharded(args, world, rank, device, barrier, dist)
     elif args.shard_steps > 0 and args.schedule == "tsf":
         sharded = bench_sharded_tsf(args, world, rank, device, barrier, dist)
@@ -424,10 +506,26 @@ def main():
                     "bytes_per_launch": round(bpl), "avg_launch_us": round(avg_us, 3),
                     "share_of_gpu_time": round(us / max(sum(v[1] for v in stats.values()), 1e-9), 3),
                     "per_kind_avg_us": {KIND_NAMES[k]: round(v[1] / max(v[0], 1), 3) for k, v in stats.items() if v[0]}}
-        # SURVEY §8(d)'s whole-step figure: algorithmic bytes of every launch of an env step x env-steps/s
-        step_bytes = sum(v[2] for v in stats.values()) / max(args.prof_steps, 1)
-        roofline["per_step"] = {"bytes_per_env_step": round(step_bytes), "achieved": round(step_bytes * value / 1e9, 2),
-                                "frac": round(step_bytes * value / 1e9 / HBM_PEAK_GBS, 5), "unit": "GB/s"}
+        # SURVEY §8(d)'s whole-step figure: the ALGORITHMIC bytes of one env step x env-steps/s / peak,
+        # per GPU.  Launched bytes (each launch's own minimum, summed -- speculative re-work included)
+        # are reported beside it as a ratio, never as achieved bandwidth.
+        P = head_params(sh)
+        U = T if args.schedule == "all" else 1
+        alg = algorithmic_step_bytes(T, U, P, 2)
+        alg32 = algorithmic_step_bytes(T, U, P, 4)
+        launched = sum(v[2] for v in stats.values()) / max(args.prof_steps, 1)
+        # each GPU runs every env step of the sharded stream (its T heads); replicas split the total
+        per_gpu_rate = value if layout.startswith("shard") else value / world
+        roofline["per_step"] = {
+            "formula": "SURVEY 8(d): 2*wb*T*P + U*P*(3*wb + 28), P = params per head",
+            "T": T, "U": U, "P": P,
+            "algorithmic_bytes_per_env_step": round(alg), "achieved": round(alg * per_gpu_rate / 1e9, 2),
+            "frac": round(alg * per_gpu_rate / 1e9 / HBM_PEAK_GBS, 5),
+            "fp32_algorithmic_bytes_per_env_step": round(alg32),
+            "fp32_achieved": round(alg32 * per_gpu_rate / 1e9, 2),
+            "fp32_frac": round(alg32 * per_gpu_rate / 1e9 / HBM_PEAK_GBS, 5),
+            "launched_bytes_per_env_step": round(launched),
+            "launched_over_fp32_algorithmic": round(launched / alg32, 3), "unit": "GB/s"}
         spec_stats = eng.step_stats()
         if native:
             spec_stats.update(loop.stats())
@@ -443,18 +541,23 @@ def main():
                       f"{'C5' if args.tsf_K else 'C3'}, one GPU)", "value": round(value, 2), "unit": "env steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000.0 * dt / args.steps, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-            "config": {"workload": workload + (f" (Reacher-shape |s|=17 |a|=7 d=8, psi MLP 256x2, "
+            "config": {"workload": (f"C4 layout: {T * world} Reacher tasks, {T} heads per GPU, one env stream; " if
+                                    layout.startswith("shard") else "") + workload + (f" (Reacher-shape |s|=17 |a|=7 d=8, psi MLP 256x2, "
                                                f"{'all heads updated per env step: main_sfdqn_torch.py path' if args.schedule == 'all' else 'active head only: sfdqn.py path'})"
                                                if args.tsf_K is None else
                                                f" (Hopper-shape |s|=11 |a|=27 d=50, psi MLP 256x2, g/h width 100, "
                                                f"{args.tsf_K} planar layers, active head only: "
                                                f"{'tsfdqn_nf.py' if args.tsf_K else 'tsfdqn.py'} path)"),
-                       "heads_per_gpu": T, "global_batch": B * world, "replay": args.replay if native else "host", "parallelism": f"replica{world}" if world > 1 else "single",
+                       "heads_per_gpu": T, "heads_total": T * world if layout.startswith("shard") else T,
+                       "global_batch": B if layout.startswith("shard") else B * world,
+                       "replay": args.replay if native else "host", "parallelism": layout,
                        "loop": (f"native C++ runner (sfx_runner_run, {args.schedule} schedule): host env + replay, one "
                                 "pre-launched gated hipGraph per env step" if native else "python host loop over libsfx graphs")},
             "roofline": roofline,
+            "repeats": {"values": repeats, "steps_each": args.steps} if repeats else None,
             "speculation": spec_stats,
             "sharded": sharded,
+            "replicas": replicas,
             "other_workloads": other,
             "cpu_baseline": cpu,
         }

@@ -14,6 +14,7 @@
 // arguments, including the slot mask) and replayed afterwards; SFX_GRAPHS=0 disables graphs.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cmath>
 #include <cstdio>
@@ -130,6 +131,16 @@ struct sfx_handle {
   // sharded heads (sfx_shard_*): this handle's heads are global [off, off + T) of Tg; w has Tg rows
   int Tg = 0, off = 0;
   struct sfx_tsf_state* tsf = nullptr;  // TSF-DQN state (sfx_tsf_setup)
+  // collective of the sharded step (sfx_comm_init / sfx_set_comm / sfx_set_comm_host): all-reduce
+  // (MAX) of fp32 buffers over the ranks that share the source tasks
+  int comm_rank = 0, comm_world = 0;  // world 0: no communicator
+  ncclComm_t comm = nullptr;
+  bool comm_owned = false;
+  int (*host_ar)(void*, float*, int) = nullptr;  // host transport: (ctx, host buffer, count)
+  void* host_ar_ctx = nullptr;
+  float* host_ar_buf = nullptr;  // pinned staging of the host transport
+  size_t host_ar_cap = 0;
+  float *sx = nullptr, *sy = nullptr;  // sharded step: X [Tg][Mmax][A]; Y [Tg][Mmax][A] ++ q [Tg][A]
   struct ShardPending {
     bool active = false;
     int B = 0;
@@ -631,6 +642,10 @@ void free_all(sfx_handle* h) {
                   (void*)h->dout, (void*)h->dxpart, (void*)h->dxctr})
     if (p) (void)hipFree(p);
   if (h->hout) (void)hipHostFree(h->hout);
+  if (h->host_ar_buf) (void)hipHostFree(h->host_ar_buf);
+  if (h->sx) (void)hipFree(h->sx);
+  if (h->sy) (void)hipFree(h->sy);
+  if (h->comm && h->comm_owned) (void)ncclCommDestroy(h->comm);
   if (h->cap) (void)hipStreamDestroy(h->cap);
 }
 
@@ -1288,6 +1303,7 @@ int sfx_synchronize(sfx_t h) {
 
 }  // extern "C"
 
-#include "sfx_runner.inc"
+#include "sfx_comm.inc"
 #include "sfx_shard.inc"
+#include "sfx_runner.inc"
 #include "sfx_tsf.inc"

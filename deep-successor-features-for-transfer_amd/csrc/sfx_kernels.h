@@ -2217,4 +2217,91 @@ __global__ __launch_bounds__(256) void k_skey(Geo G, KeyArgs K) {
   if (tid == 0) *K.key = (long long)(s_best ^ 0x8000000000000000ull);
 }
 
+// -------------------------------------------------------------------------------------
+// The sharded env step in the native runner (sfx_runner schedule "sharded").
+// Action selection goes through the same all-reduce(MAX) as the verification maxima: this
+// rank writes q[t][a] = ψ_t(s_next)[a]·w_task of its own heads into its slice of a [T_glob][A]
+// block and -inf into every other slice, so the all-reduced block is the full GPI q table on
+// every rank; k_sfinish then picks argmax_t max_a and argmax_a (first index on ties:
+// SF.GPI_w + agent argmax, features/successor.py:223-273).
+// -------------------------------------------------------------------------------------
+struct SselArgs {
+  int role, row, task, use_gpi, off, Tg;
+  float* q;  // [Tg][A]
+};
+
+// grid cdiv(Tg * A, 256)
+__global__ __launch_bounds__(256) void k_ssel(Geo G, SselArgs S) {
+  __shared__ float s_w[DMAX];
+  const int tid = threadIdx.x, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff;
+  const float* wrow = G.w + (long long)S.task * G.dpad;
+  for (int k = tid; k < d; k += 256) s_w[k] = wrow[k];
+  __syncthreads();
+  const int j = blockIdx.x * 256 + tid;
+  if (j >= S.Tg * Aa) return;
+  const int tg = j / Aa, a = j - tg * Aa, t = tg - S.off;
+  float q = -INFINITY;
+  if (t >= 0 && t < G.T && (S.use_gpi || tg == S.task)) {
+    const float* p = G.actp(S.role, t, NLm) + (size_t)S.row * O + a * d;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < d; ++k) acc = __builtin_fmaf(p[k], s_w[k], acc);  // the GPI kernels' k order
+    q = __fadd_rn(acc, 0.f);  // -0 -> +0
+  }
+  S.q[j] = q;
+}
+
+struct SfinArgs {
+  const float* X;  // [Tg][M][A] all-reduced TD maxima of the last round (null: no update)
+  const float* Y;  // [Tg][M][A] all-reduced verification maxima
+  const float* q;  // [Tg][A] all-reduced selection table
+  int Tg, M, A, pad_;
+  int* flag;       // first policy whose next actions changed (Tg: verified)
+  int64_t* sel;    // (GPI task c, greedy action a)
+};
+
+// One workgroup: verification of the speculated next actions (k_sverify) and the env action.
+__global__ __launch_bounds__(256) void k_sfinish(SfinArgs F) {
+  __shared__ int s_min;
+  __shared__ unsigned long long s_best;
+  const int tid = threadIdx.x, Aa = F.A;
+  if (tid == 0) {
+    s_min = F.Tg;
+    s_best = 0ull;
+  }
+  __syncthreads();
+  int mine = F.Tg;
+  if (F.X) {
+    const FDiv fM = fdiv(F.M);
+    for (int j = tid; j < F.Tg * F.M; j += 256) {
+      const float* x = F.X + (size_t)j * Aa;
+      const float* y = F.Y + (size_t)j * Aa;
+      int ax = 0, ay = 0;
+      float bx = x[0], by = y[0];
+      for (int a = 1; a < Aa; ++a) {
+        if (x[a] > bx) { bx = x[a]; ax = a; }
+        if (y[a] > by) { by = y[a]; ay = a; }
+      }
+      if (ax != ay) mine = min(mine, j / fM);
+    }
+  }
+  // packed (q, first index) keys as k_skey: the max key is argmax_t max_a, then argmax_a
+  unsigned long long best = 0ull;
+  for (int j = tid; j < F.Tg * Aa; j += 256) {
+    const float q = F.q[j];
+    if (q == -INFINITY) continue;
+    const unsigned long long key = ((unsigned long long)orderable(q) << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)j);
+    best = key > best ? key : best;
+  }
+  atomicMin(&s_min, mine);
+  atomicMax(&s_best, best);
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned idx = 0xFFFFFFFFu - (unsigned)(s_best & 0xFFFFFFFFull);
+    *F.flag = s_min;
+    F.sel[0] = idx / (unsigned)Aa;
+    F.sel[1] = idx % (unsigned)Aa;
+  }
+}
+
 }  // namespace sfx

@@ -69,6 +69,11 @@ SIGNATURES = {
     "sfx_runner_record": (_I, [_VP, _I]),
     "sfx_runner_recorded": (_I, [_VP]),
     "sfx_runner_get_record": (_I, [_VP, _I, _VP, C.POINTER(C.c_int64)]),
+    "sfx_comm_id_bytes": (_I, []),
+    "sfx_comm_unique_id": (_I, [_VP]),
+    "sfx_comm_init": (_I, [_VP, _VP, _I, _I]),
+    "sfx_set_comm": (_I, [_VP, _VP, _I, _I]),
+    "sfx_set_comm_host": (_I, [_VP, _VP, _VP, _I, _I]),
     "sfx_shard_setup": (_I, [_VP, _I, _I]),
     "sfx_shard_begin": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _F, _VP]),
     "sfx_shard_td_maxima": (_I, [_VP, _I, _VP]),
@@ -93,6 +98,10 @@ SIGNATURES = {
 ENV_RESET_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_float))
 ENV_STEP_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float),
                           C.POINTER(C.c_float), C.POINTER(C.c_int))
+
+
+# host all-reduce(MAX) callback of sfx_set_comm_host: (ctx, float* host buffer, count) -> 0 on success
+HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_float), C.c_int)
 
 
 class SFXError(RuntimeError):

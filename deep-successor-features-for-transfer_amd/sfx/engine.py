@@ -45,7 +45,15 @@ class SFEngine:
         self._h = h
         self.P = lib.sfx_head_numel(h)
         self._sel = torch.zeros(2, dtype=torch.long, device=self.device)
+        self.T_glob, self.head_offset = T, 0
         self._refresh_w_ptrs(T)
+
+    def shard_setup(self, T_glob: int, head_offset: int):
+        """This engine's T heads become the global heads [head_offset, head_offset + T) of T_glob;
+        w gets T_glob rows (the rows loaded so far move to their global index)."""
+        check(lib.sfx_shard_setup(self._h, int(T_glob), int(head_offset)), "sfx_shard_setup")
+        self.T_glob, self.head_offset = int(T_glob), int(head_offset)
+        self._refresh_w_ptrs(self.T_glob)
 
     def _refresh_w_ptrs(self, Tw: int):
         """Device pointers of the w rows (Tw = T, or T_glob after sfx_shard_setup)."""

@@ -235,7 +235,7 @@ class NativeEnvLoop:
     """
 
     FIELDS = ("s", "s1", "phi", "a", "gamma", "snext", "phi1", "r1", "rb")
-    SCHEDULES = {"all": 0, "active": 1, "tsf": 2}
+    SCHEDULES = {"all": 0, "active": 1, "tsf": 2, "sharded": 3}
 
     def __init__(self, engine: SFEngine, batch: int = 32, capacity: int = 1_000_000, gamma: float = 0.9,
                  epsilon: float = 0.1, alpha_w: float = 1e-3, episode_len: int = 500, use_gpi: bool = True,
@@ -337,7 +337,7 @@ class NativeEnvLoop:
                 "host_wait_us": round(w.value, 1), "retried": rt.value}
 
     def gpi_counters(self) -> np.ndarray:
-        T = self.eng.T
+        T = self.eng.T_glob if self.schedule == "sharded" else self.eng.T
         out = np.zeros(T * T, dtype=np.int64)
         self._check(self._lib.sfx_runner_gpi_counters(self._r, out.ctypes.data_as(self._C.POINTER(self._C.c_longlong))),
                     "sfx_runner_gpi_counters")

@@ -109,8 +109,7 @@ class LibsfxShardBackend:
 
         self.eng, self.lib, self.check = engine, lib, check
         self.Tg, self.off = T_glob, head_offset
-        check(lib.sfx_shard_setup(engine.handle, T_glob, head_offset), "sfx_shard_setup")
-        engine._refresh_w_ptrs(T_glob)
+        engine.shard_setup(T_glob, head_offset)
         dev = engine.device
         self._X = torch.empty(T_glob * max_batch * engine.A, device=dev)
         self._Y = torch.empty_like(self._X)
@@ -235,8 +234,7 @@ class LibsfxTSFShardBackend:
 
         self.eng, self.lib, self.check = engine, lib, check
         self.Tg, self.off, self.T = T_glob, head_offset, engine.T
-        check(lib.sfx_shard_setup(engine.handle, T_glob, head_offset), "sfx_shard_setup")
-        engine._refresh_w_ptrs(T_glob)
+        engine.shard_setup(T_glob, head_offset)
         dev = engine.device
         self._X = torch.empty(max_batch * engine.A, device=dev)
         self.shared_buf = torch.empty(engine.tsf_Ph + engine.d, device=dev)
@@ -268,3 +266,53 @@ class LibsfxTSFShardBackend:
         self.check(self.lib.sfx_shard_tsf_select(self.eng.handle, s.data_ptr(), int(task), int(bool(use_gpi)),
                                                  self.key.data_ptr()), "sfx_shard_tsf_select")
         return self.key
+
+
+# ---------------------------------------------------------------- the library's own collective
+def init_comm(engine, rank: int, world: int, group=None):
+    """RCCL communicator for the native sharded step (include/sfx.h sfx_comm_init): rank 0 makes
+    the unique id, torch.distributed broadcasts its bytes, every rank joins.  Afterwards the
+    library all-reduces on its own stream (inside the step graphs); torch is not on the path."""
+    import ctypes as C
+
+    import torch.distributed as dist
+
+    from ._lib import check, lib
+
+    n = lib.sfx_comm_id_bytes()
+    buf = (C.c_uint8 * n)()
+    if rank == 0:
+        check(lib.sfx_comm_unique_id(buf), "sfx_comm_unique_id")
+    t = torch.tensor(list(bytes(buf)), dtype=torch.uint8)
+    if world > 1:
+        backend = dist.get_backend(group)
+        dev = engine.device if backend == "nccl" else "cpu"
+        t = t.to(dev)
+        dist.broadcast(t, src=0, group=group)
+        t = t.cpu()
+    raw = (C.c_uint8 * n)(*t.tolist())
+    check(lib.sfx_comm_init(engine.handle, raw, rank, world), "sfx_comm_init")
+
+
+def set_host_comm(engine, rank: int, world: int, group=None):
+    """Host transport (sfx_set_comm_host): the library stages each all-reduce through pinned host
+    memory and this callback runs all-reduce(MAX) over a gloo group -- for ranks sharing one GPU
+    (tests), where RCCL cannot run.  Keeps the callback alive on the engine."""
+    import numpy as np
+    import torch.distributed as dist
+
+    from ._lib import HOST_ALLREDUCE_FN, check, lib
+
+    def _ar(_ctx, buf, count):
+        try:
+            a = np.ctypeslib.as_array(buf, shape=(count,))
+            t = torch.from_numpy(a)
+            if world > 1:
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            return 0
+        except Exception:
+            return 1
+
+    cb = HOST_ALLREDUCE_FN(_ar)
+    engine._host_ar_cb = cb
+    check(lib.sfx_set_comm_host(engine.handle, cb, None, rank, world), "sfx_set_comm_host")

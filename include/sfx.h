@@ -270,6 +270,26 @@ int sfx_runner_recorded(sfx_runner_t r);
 int sfx_runner_get_record(sfx_runner_t r, int i, void* stage_host, int64_t* meta_host /* [6] */);
 
 /* ---------------------------------------------------------------------------------------
+ * Collective of the sharded step (SURVEY.md §8b sfx_set_comm, §8e): all-reduce(MAX) of fp32
+ * GPI maxima over the ranks that share the source tasks.  Replaces the reference's in-process
+ * loop over all heads (agents/sfdqn.py:57-60 / SF.GPI, features/successor.py:223-273) when the
+ * heads live on several GPUs.  One of:
+ *  - sfx_comm_init: the library creates (and owns) an RCCL communicator from a unique id that
+ *    rank 0 made with sfx_comm_unique_id and the caller distributed (e.g. over torch.distributed);
+ *    all ranks call it together;
+ *  - sfx_set_comm: the caller's ncclComm_t (borrowed; it must outlive the handle's use of it);
+ *  - sfx_set_comm_host: a host callback all-reducing (MAX, in place) a pinned host buffer -- for
+ *    ranks that cannot run RCCL (several ranks on one GPU in tests); its steps are not graphed.
+ * RCCL all-reduces are enqueued on the handle's stream and captured into the step graphs.
+ * ------------------------------------------------------------------------------------- */
+typedef int (*sfx_host_allreduce_fn)(void* ctx, float* buf_host, int count);
+int sfx_comm_id_bytes(void);
+int sfx_comm_unique_id(void* id_out /* sfx_comm_id_bytes() bytes */);
+int sfx_comm_init(sfx_t h, const void* unique_id, int rank, int world);
+int sfx_set_comm(sfx_t h, void* rccl_comm, int rank, int world);
+int sfx_set_comm_host(sfx_t h, sfx_host_allreduce_fn fn, void* ctx, int rank, int world);
+
+/* ---------------------------------------------------------------------------------------
  * Heads sharded across ranks (BASELINE config C4: 64 tasks, 8 per GPU).
  * This handle's T heads are the global heads [head_offset, head_offset + T) of T_glob; w has
  * T_glob rows (replicated: load every task's w on every rank).  One all-task env step

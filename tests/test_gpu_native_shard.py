@@ -1,0 +1,148 @@
+"""GPU parity of the NATIVE sharded all-task runner (sfx_runner schedule "sharded"; SURVEY §8e,
+BASELINE config C4): each rank owns T_loc heads, every rank runs the same env / replay stream
+(same seed), and the GPI maxima -- plus the selection table of the env action -- are all-reduced
+(MAX) by the library itself, inside the step.
+
+* one rank with an RCCL communicator the library creates (sfx_comm_init): the all-reduces are
+  ncclAllReduce calls captured into the pre-launched step graphs;
+* several ranks sharing this box's one GPU through the host transport (sfx_set_comm_host over
+  gloo; RCCL refuses two ranks on one device), including C4 at its stated size: 8 ranks x 8
+  Reacher heads = 64 source tasks, 256-wide heads, minibatch 32.
+
+The oracle replays rank 0's recorded inputs with ALL heads in the reference's order
+(agents/sfdqn.py:47-60 over features/deep.py) and must reproduce every recorded env action
+(bit-exact GPI argmax); the gathered heads, target heads and w must match it within the Adam
+tolerance of test_gpu_engine.py; every rank must have recorded the same stream."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_cpu as R
+from tests.conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+SMALL = dict(spec=dict(n_s=17, H=32, A=7, d=8, acts=("relu", "relu")), world=2, t_loc=2, b=16, steps=16, ev=5,
+             eps=0.3, ep=7, prefill=8)
+C4 = dict(spec=dict(n_s=17, H=256, A=7, d=8, acts=("relu", "relu")), world=8, t_loc=8, b=32, steps=6, ev=1000,
+          eps=0.1, ep=500, prefill=30)
+ALPHA = 0.05
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if not gpu_available():
+        pytest.skip("no HIP device")
+
+
+def _run_rank(rank, cfg, comm):
+    from sfx.engine import SFEngine
+    from sfx.init import reference_heads
+    from sfx.runner import NativeEnvLoop
+    from sfx.shard import init_comm, set_host_comm
+
+    sp, world, T_loc, b = cfg["spec"], cfg["world"], cfg["t_loc"], cfg["b"]
+    Tg = world * T_loc
+    online, w = reference_heads(Tg, sp["n_s"], sp["H"], sp["A"], sp["d"], sp["acts"], seed=3)
+    eng = SFEngine(T_loc, sp["n_s"], sp["H"], sp["A"], sp["d"], sp["acts"], max_batch=b)
+    eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
+    eng.set_target_update_ev(cfg["ev"])
+    eng.shard_setup(Tg, rank * T_loc)
+    for t in range(T_loc):
+        eng.load_head(t, online[rank * T_loc + t], 0)
+        eng.load_head(t, online[rank * T_loc + t], 1)
+    for t in range(Tg):
+        eng.load_w(t, w[t])
+    if comm == "rccl":
+        init_comm(eng, rank, world)
+    else:
+        set_host_comm(eng, rank, world)
+    loop = NativeEnvLoop(eng, batch=b, capacity=500, gamma=0.9, epsilon=cfg["eps"], alpha_w=ALPHA,
+                         episode_len=cfg["ep"], seed=17, schedule="sharded")
+    loop.prefill(cfg["prefill"])  # the first steps run without a minibatch
+    loop.set_task(Tg - 1)
+    loop.record(cfg["steps"])
+    loop.run(cfg["steps"])
+    recs = loop.records()
+    final = loop.action()
+    stats = loop.stats()
+    heads = torch.stack([eng.get_head(t) for t in range(T_loc)])
+    targets = torch.stack([eng.get_head(t, 1) for t in range(T_loc)])
+    ws = torch.stack([eng.get_w(t)[0] for t in range(Tg)])
+    counters = loop.gpi_counters()
+    loop.close()
+    eng.close()
+    return recs, final, heads, targets, ws, stats, counters
+
+
+def _oracle_check(cfg, recs, final, heads, targets, ws):
+    from tests.test_gpu_engine import params_close, rel_close
+    from tests.test_gpu_runner import replay_with_oracle
+
+    sp, Tg = cfg["spec"], cfg["world"] * cfg["t_loc"]
+    spec = R.Spec(**sp)
+    from sfx.init import reference_heads
+
+    online, w = reference_heads(Tg, sp["n_s"], sp["H"], sp["A"], sp["d"], sp["acts"], seed=3)
+    st = R.SFState(spec, online.clone(), online.clone(), w.clone())
+    replay_with_oracle(st, spec, recs, ALPHA, cfg["ev"], final)
+    n = len(recs)
+    params_close(heads, st.online, 1e-3 * n)
+    params_close(targets, st.target, 1e-3 * n)
+    rel_close(ws, st.w, rtol=1e-5, atol=1e-7)
+
+
+def test_native_sharded_single_rank_rccl():
+    """World 1 with the library's own RCCL communicator: ncclAllReduce inside the step graphs."""
+    cfg = dict(SMALL, world=1, t_loc=4)
+    recs, final, heads, targets, ws, stats, counters = _run_rank(0, cfg, "rccl")
+    assert stats["prelaunched"] >= cfg["steps"] - 1, stats
+    assert counters.sum() == cfg["steps"]
+    _oracle_check(cfg, recs, final, heads, targets, ws)
+
+
+def _worker(rank, port, q, cfg):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=cfg["world"])
+    try:
+        recs, final, heads, targets, ws, stats, _ = _run_rank(rank, cfg, "host")
+        parts = [None] * cfg["world"]
+        dist.all_gather_object(parts, (heads.numpy(), targets.numpy(), [(r["c"], r["a_greedy"], r["a_taken"])
+                                                                        for r in recs]))
+        if rank == 0:
+            q.put((recs, final, np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]),
+                   ws.numpy(), stats, [p[2] for p in parts]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _ranks(cfg):
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, port, q, cfg)) for r in range(cfg["world"])]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return out
+
+
+@pytest.mark.parametrize("cfg", [SMALL, C4], ids=["2x2-small", "c4-8x8-h256"])
+def test_native_sharded_ranks_on_one_gpu(cfg):
+    recs, final, heads, targets, ws, stats, streams = _ranks(cfg)
+    assert all(s == streams[0] for s in streams), "ranks diverged"
+    assert len(recs) == cfg["steps"]
+    _oracle_check(cfg, recs, final, torch.from_numpy(heads), torch.from_numpy(targets), torch.from_numpy(ws))
