@@ -136,11 +136,15 @@ struct sfx_handle {
   int comm_rank = 0, comm_world = 0;  // world 0: no communicator
   ncclComm_t comm = nullptr;
   bool comm_owned = false;
-  int (*host_ar)(void*, float*, int) = nullptr;  // host transport: (ctx, host buffer, count)
+  bool comm_force = false;  // SFX_RCCL_WORLD1=1: call RCCL even with one rank (tests)
+  int (*host_ar)(void*, int32_t*, int) = nullptr;  // host transport: (ctx, host buffer, count)
   void* host_ar_ctx = nullptr;
-  float* host_ar_buf = nullptr;  // pinned staging of the host transport
+  int32_t* host_ar_buf = nullptr;  // pinned staging of the host transport
   size_t host_ar_cap = 0;
-  float *sx = nullptr, *sy = nullptr;  // sharded step: X [Tg][Mmax][A]; Y [Tg][Mmax][A] ++ q [Tg][A]
+  // sharded step, sortable int32: maxima buffers xb[2] ([Tg][Mmax][A] ++ q table [Tg][A]) and the
+  // pre-step part xge ([Tg][Mmax][A]) of the fused path (shard_fused)
+  int *xb[2] = {nullptr, nullptr}, *xge = nullptr;
+  bool shard_qa = true;  // SFX_SHARD_QA=0: maxima by separate k_qmax launches
   struct ShardPending {
     bool active = false;
     int B = 0;
@@ -275,6 +279,9 @@ struct FwdExtra {
   float lms_alpha = 0.f;
   int* flag = nullptr;   // reset to flag_value in block 0 of the first layer
   int flag_value = 0;
+  // sharded step: GPI maxima accumulated by the last layer's tiles of group role qa_role
+  int qa_role = -1, qa_M = 0, qa_row = -1, qa_task = 0, qa_use_gpi = 1;
+  int *qa_all = nullptr, *qa_ge = nullptr, *qa_lt = nullptr, *qa_sel = nullptr;
 };
 
 int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const float* xa, const float* xb,
@@ -285,6 +292,7 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
   F.xb = xb;
   F.mask = h->mask;
   F.lms_head = -1;
+  F.qa_role = -1;
   int ninst = 0;
   bool uniform = true;  // every group covers heads 0..T-1: XCD-aware grid possible
   FwdGroup* slots[4] = {&F.g0, &F.g1, &F.g2, &F.g3};
@@ -321,12 +329,26 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     F.flag_value = ex.flag_value;
     F.ntN = cdiv(L.N, 16);
     F.ntM = cdiv(M, 32);
+    const bool qa = ex.qa_role >= 0 && l == h->NL - 1;  // the maxima come from the ψ output layer
+    if (qa) {
+      F.qa_role = ex.qa_role;
+      F.qa_Tg = h->Tg;
+      F.qa_off = h->off;
+      F.qa_M = ex.qa_M;
+      F.qa_all = ex.qa_all;
+      F.qa_ge = ex.qa_ge;
+      F.qa_lt = ex.qa_lt;
+      F.qa_sel = ex.qa_sel;
+      F.qa_row = ex.qa_row;
+      F.qa_task = ex.qa_task;
+      F.qa_use_gpi = ex.qa_use_gpi;
+    }
     const dim3 grid = F.xcd ? dim3(8 * cdiv(h->T, 8) * F.ntN * F.ntM * F.ngroups) : dim3(F.ntN, ninst, F.ntM);
     double by = 4.0 * ninst * ((double)L.N * L.K + L.N + (double)M * L.K + (double)M * L.N);
     if (l0) by += 4.0 * ninst * ((double)h->L[0].N * h->L[0].K + h->L[0].N + (double)M * h->L[0].K);
     // the vector path needs K % (256/NW) == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
     const bool aligned = l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0);
-    const bool gemv = !l0 && !h->rec && h->gemv_fwd && M <= GEMV_M && L.N >= GEMV_N && L.K % 16 == 0 &&
+    const bool gemv = !l0 && !qa && !h->rec && h->gemv_fwd && M <= GEMV_M && L.N >= GEMV_N && L.K % 16 == 0 &&
                       (l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0));
     if (gemv) {
       launch(h, K_FWD, by, k_fwd_gemv, dim3(cdiv(L.N, 64), ninst), dim3(256), h->G, F);
@@ -349,7 +371,7 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
 }
 
 int run_tdg(sfx_handle* h, int pol0, int npol, int guess, int M, int use_gpi, const int64_t* a, const float* phi,
-            const float* gamma, int64_t* next, int next_stride, int* flag = nullptr, const float* xmax = nullptr,
+            const float* gamma, int64_t* next, int next_stride, int* flag = nullptr, const int* xmax = nullptr,
             int poloff = 0) {
   TdgArgs A{};
   A.xmax = xmax;
@@ -381,8 +403,12 @@ struct TdgSpec {
   const float* gamma = nullptr;
   int64_t* next = nullptr;
   int* flag = nullptr;
-  const float* xmax = nullptr;  // sharded heads: all-reduced GPI maxima [T_glob][M][A]
+  const int* xmax = nullptr;    // sharded heads: all-reduced GPI maxima [T_glob][M][A] (sortable)
   int poloff = 0;               // global index of local head 0
+  // sharded step: the fused-TD launch re-initialises the next round's maxima (BwdArgs::xi_*)
+  const int* xi_src = nullptr;
+  int* xi_dst = nullptr;
+  int xi_copy = 0, xi_n = 0;
 };
 
 // 0: K2 as its own launch; 1: fused, d <= 8; 2: fused, d <= 16 (see tdg_rows)
@@ -414,6 +440,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
             float* losses, const TdgSpec& td, const BwdExtra& ex = BwdExtra()) {
   const bool fuse = can_fuse_tdg(h) && ((uintptr_t)phi & 15) == 0 &&  // fused K2 reads φ rows as float4
                     (!td.xmax || 32 * h->A <= 1024);                     // and up to 4 maxima per thread
+  if (!fuse && td.xi_dst) SFX_FAIL(SFX_E_STATE, "run_bwd: maxima re-initialisation needs the fused TD launch");
   if (!fuse)
     RC(run_tdg(h, head0, nhead, td.guess, M, td.use_gpi, td.a, phi, td.gamma, td.next, td.next_stride, td.flag,
                td.xmax, td.poloff));
@@ -478,6 +505,10 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   for (int l = h->NL - 1; l >= 1; --l) {
     const int li = h->NL - 1 - l;
     A.tdg = fuse && li == 0 ? 1 : 0;
+    A.xi_src = A.tdg ? td.xi_src : nullptr;
+    A.xi_dst = A.tdg ? td.xi_dst : nullptr;
+    A.xi_copy = td.xi_copy;
+    A.xi_n = td.xi_n;
     const double by = nhead * (dx_bytes(l) + (l + 1 <= h->NL - 1 ? dw_bytes(l + 1) : 0.0)) + (A.tdg ? tdg_bytes : 0.0);
     A.ra = geo(l);
     A.na = cdiv(M, 32) * cdiv(h->L[l].K, 16);
@@ -516,6 +547,8 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.na = 0;
   A.dxs = 1;
   A.tdg = 0;
+  A.xi_dst = nullptr;
+  A.xi_src = nullptr;
   A.rb = geo(1);
   A.nb = dw_tiles(1);
   A.rc = geo(0);
@@ -643,8 +676,8 @@ void free_all(sfx_handle* h) {
     if (p) (void)hipFree(p);
   if (h->hout) (void)hipHostFree(h->hout);
   if (h->host_ar_buf) (void)hipHostFree(h->host_ar_buf);
-  if (h->sx) (void)hipFree(h->sx);
-  if (h->sy) (void)hipFree(h->sy);
+  for (int* p : {h->xb[0], h->xb[1]})  // xge lives in xb[0]'s block
+    if (p) (void)hipFree(p);
   if (h->comm && h->comm_owned) (void)ncclCommDestroy(h->comm);
   if (h->cap) (void)hipStreamDestroy(h->cap);
 }
@@ -764,7 +797,7 @@ int update_body(sfx_handle* h, int policy, const float* S, const int64_t* a, con
 // TSFDQN.update_successor (sfx_tsf.inc)
 int tsf_body(sfx_handle* h, int policy, const float* S, const int64_t* a, const float* r, const float* phi,
              const float* S1, const float* gamma, int B, int use_gpi, float* losses, int64_t* next,
-             const float* xmax = nullptr);
+             const int* xmax = nullptr);
 
 int launch_step_all(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, const float* lms_phi, const float* lms_r,
                     float lms_alpha, int rounds) {
@@ -854,6 +887,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->split_dx = !(esd && esd[0] == '0');
   const char* egv = std::getenv("SFX_GEMV_FWD");
   h->gemv_fwd = !(egv && egv[0] == '0');
+  const char* eqa = std::getenv("SFX_SHARD_QA");
+  h->shard_qa = !(eqa && eqa[0] == '0');
   const char* edw = std::getenv("SFX_DW_WIDE");
   h->dw_wide = edw && edw[0] == '1';  // opt-in
   int off = 0, ptorch = 0;

@@ -188,6 +188,26 @@ struct Geo {
 
 __device__ __forceinline__ int rslot(unsigned long long mask, int head) { return (int)((mask >> head) & 1ull); }
 
+// GPI maxima handed between ranks travel as "sortable" int32: an order-preserving map of the
+// fp32 value (-0 folded into +0), so all-reduce(MAX) and atomicMax run on plain int32 and the
+// decoded max is exactly the fp32 max.  SORT_EMPTY (INT_MIN) marks an entry no head filled.
+constexpr int SORT_EMPTY = (int)0x80000000;
+__host__ __device__ __forceinline__ int sortable(float f) {
+  union { float f; int i; } u;
+  u.f = f + 0.f;
+  return u.i >= 0 ? u.i : u.i ^ 0x7FFFFFFF;
+}
+__host__ __device__ __forceinline__ float unsortable(int i) {
+  union { float f; int i; } u;
+  u.i = i >= 0 ? i : i ^ 0x7FFFFFFF;
+  return u.f;
+}
+
+// dst[j] = src[j] for j < n_copy, SORT_EMPTY for n_copy <= j < n; grid-strided over a launch
+__device__ __forceinline__ void fill_sortable(int* dst, const int* src, int n_copy, int n, int gtid, int gthreads) {
+  for (int j = gtid; j < n; j += gthreads) dst[j] = j < n_copy ? src[j] : SORT_EMPTY;
+}
+
 // A runner step whose gate cancelled it (the host aborted, or the gate timed out waiting for the
 // host) runs its launches anyway -- they are already queued -- but must not commit: every store
 // to persistent state (parameters and moments of the write slot, Adam step counters, w, g, h) is
@@ -323,7 +343,62 @@ struct FwdArgs {
   const float* lms_r;
   float lms_alpha;
   int* flag;             // set to flag_value when non-null
+  // sharded step (d | 16): GPI maxima accumulated by the last layer's tiles of group role qa_role
+  // (see q_accumulate); qa_role < 0: off
+  int qa_role, qa_Tg, qa_off, qa_M;
+  int* qa_all;   // max over every local head (X of round 0)
+  int* qa_ge;    // max over local heads with global index >= policy (the pre-step part)
+  int* qa_lt;    // max over local heads with global index < policy (post-update rounds)
+  int* qa_sel;   // [Tg][A] selection table of row qa_row with w of qa_task (null: none)
+  int qa_row, qa_task, qa_use_gpi, pad3_;
 };
+
+// The sharded step's GPI maxima, fused into the forward of the ψ output layer: a 32 x 16 tile
+// of head t holds whole actions (16 / d of them), so it forms q[i][b][a] = ψ_t(s1_b)[a]·w_i for
+// every global policy i straight from the tile (the GPI kernels' k-ordered fmaf chain) and
+// atomically maxes it (sortable int32) into X[i][b][a] -- for all i (round 0: every head enters
+// through its pre-step values), for i <= t (the pre-step part of later rounds) or for i > t (heads
+// already updated in the reference's order: agents/sfdqn.py:57-60).  Row qa_row (s_next) fills the
+// selection table with w of the active task.  Replaces a k_qmax launch per round.
+constexpr int QA_WMAX = 2048;  // Tg * d of the policies' w rows staged in LDS
+__device__ void q_accumulate(const Geo& G, const FwdArgs& F, int head, int tN, int tM, const float* sT) {
+  __shared__ float sw[QA_WMAX];
+  const int d = G.d, Aa = G.A, Tg = F.qa_Tg, tid = threadIdx.x, nt = blockDim.x;
+  const int n0 = tN * 16, m0 = tM * 32, na = 16 / d, a0 = n0 / d, tg = F.qa_off + head;
+  for (int j = tid; j < Tg * d; j += nt) {
+    const int i = j / d;
+    sw[j] = G.w[(long long)i * G.dpad + (j - i * d)];
+  }
+  __syncthreads();
+  const int mrows = F.qa_M - m0 < 32 ? F.qa_M - m0 : 32;
+  const int per_i = (mrows > 0 ? mrows : 0) * na;
+  for (int it = tid; it < Tg * per_i; it += nt) {
+    const int i = it / per_i, rem = it - i * per_i, bl = rem / na, al = rem - bl * na, a = a0 + al;
+    if (a >= Aa) continue;
+    const bool all = F.qa_all != nullptr, ge = F.qa_ge && tg >= i, lt = F.qa_lt && tg < i;
+    if (!all && !ge && !lt) continue;
+    const float* p = sT + bl * 16 + al * d;
+    const float* w = sw + i * d;
+    float q = 0.f;
+    for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], w[k], q);
+    const int v = sortable(q);
+    const size_t o = ((size_t)i * F.qa_M + m0 + bl) * Aa + a;
+    if (all) atomicMax(F.qa_all + o, v);
+    if (ge) atomicMax(F.qa_ge + o, v);
+    if (lt) atomicMax(F.qa_lt + o, v);
+  }
+  const int rl = F.qa_row - m0;
+  if (F.qa_sel && rl >= 0 && rl < 32 && (F.qa_use_gpi || tg == F.qa_task))
+    for (int al = tid; al < na; al += nt) {
+      const int a = a0 + al;
+      if (a >= Aa) continue;
+      const float* p = sT + rl * 16 + al * d;
+      const float* w = sw + F.qa_task * d;
+      float q = 0.f;
+      for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], w[k], q);
+      F.qa_sel[(size_t)tg * Aa + a] = sortable(q);
+    }
+}
 
 __device__ void lms_block(const Geo& G, const FwdArgs& F) {
   __shared__ float s_p[DMAX];
@@ -369,7 +444,7 @@ __device__ __forceinline__ FwdGroup fwd_group(const FwdArgs& F, int& y) {
 }
 
 template <bool VEC, int NW, bool L0, bool C>
-__device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, int tN, int tM) {
+__device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, int tN, int tM, float* sT = nullptr) {
   static_assert(!(L0 && C), "the in-tile layer 0 reads only inputs of earlier launches");
   constexpr int KW = 256 / NW;  // K chunk of one wave per iteration (NW waves cover 256)
   constexpr int KL = KW / 4;    // consecutive k per lane (4 lane groups per MFMA k-step)
@@ -527,11 +602,15 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = m0 + 16 * s + (Lx >> 4) * 4 + i;
-        if (row < M) stc<C>(Y + (size_t)row * N + col, act_fwd(__fadd_rn(v[i], bias), F.act));
+        const float o = act_fwd(__fadd_rn(v[i], bias), F.act);
+        if (row < M) stc<C>(Y + (size_t)row * N + col, o);
+        if (sT) sT[(row - m0) * 16 + (col - n0)] = row < M ? o : 0.f;
       }
     }
   }
 }
+
+constexpr int qa_tile_floats(bool L0) { return L0 ? 1 : 32 * 16; }  // L0 launches never accumulate
 
 template <bool VEC, int NW, bool L0>
 __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
@@ -546,7 +625,17 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
     if (hd >= F.nh || gi >= F.ngroups) return;
     y = gi * F.nh + hd;
   }
-  fwd_tile<VEC, NW, L0, false>(G, F, y, tN, tM);
+  bool qa = false;
+  int head = 0;
+  if (F.qa_role >= 0) {  // the sharded step's maxima from this tile (last layer, group role qa_role)
+    int yy = y;
+    const FwdGroup grp = fwd_group(F, yy);
+    qa = grp.role == F.qa_role;
+    head = grp.head0 + yy;
+  }
+  __shared__ float sT[qa_tile_floats(L0)];
+  fwd_tile<VEC, NW, L0, false>(G, F, y, tN, tM, qa ? sT : nullptr);
+  if (qa) q_accumulate(G, F, head, tN, tM, sT);
   if (tN == 0 && tM == 0 && blockIdx.y == 0 && (F.xcd ? blockIdx.x == 0 : true)) {
     if (F.flag && threadIdx.x == 0) *F.flag = F.flag_value;
     if (F.lms_head >= 0) lms_block(G, F);
@@ -632,9 +721,9 @@ struct TdgArgs {
   const float* gamma;
   int64_t* next;  // next[(policy - pol0) * next_stride + b] or null
   int* flag;      // reset to flag_value by block (0, 0) when non-null
-  // sharded heads: max over ALL heads of q[b, t, a] (all-reduced across ranks), indexed by the
-  // global policy poloff + pol; replaces the local GPI reduction when non-null
-  const float* xmax;
+  // sharded heads: max over ALL heads of q[b, t, a] (all-reduced across ranks, sortable int32),
+  // indexed by the global policy poloff + pol; replaces the local GPI reduction when non-null
+  const int* xmax;
   int poloff, pad2_;
 };
 
@@ -663,8 +752,8 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   }
   __syncthreads();
   if (A.xmax) {
-    const float* xr = A.xmax + ((size_t)(A.poloff + pol) * M + b) * Aa;
-    for (int a = tid; a < Aa; a += 256) s_m[a] = xr[a];
+    const int* xr = A.xmax + ((size_t)(A.poloff + pol) * M + b) * Aa;
+    for (int a = tid; a < Aa; a += 256) s_m[a] = unsortable(xr[a]);
   } else {
     const int t0 = A.use_gpi ? 0 : pol, nt = A.use_gpi ? T : 1;
     const FDiv fA = fdiv(Aa);
@@ -753,7 +842,7 @@ struct BwdArgs {
   const int64_t* tdg_a;
   const float* tdg_gamma;
   int64_t* tdg_next;
-  const float* tdg_xmax;  // sharded heads: all-reduced GPI maxima (see TdgArgs::xmax)
+  const int* tdg_xmax;  // sharded heads: all-reduced GPI maxima (see TdgArgs::xmax)
   int tdg_poloff, pad3_;
   int* flag;
   int fuse_v0, vM, vOff, act0;  // fused forward: rows (S1 ++ s_next), layer-0 offset, layer-0 act
@@ -772,6 +861,11 @@ struct BwdArgs {
   float* losses;       // tail: [n_head][3] (l1+l2, l1, l2) or null
   const float* v_x;    // fused forward input rows 0..M-1 (S1)
   const float* v_xn;   // fused forward input row M (s_next) or null
+  // sharded step: the fused-TD launch re-initialises the next round's maxima buffer (xi_dst[j] =
+  // xi_src[j] for j < xi_copy, SORT_EMPTY up to xi_n) -- its last reader was an earlier launch
+  const int* xi_src;
+  int* xi_dst;
+  int xi_copy, xi_n;
 };
 
 __device__ __forceinline__ const float* layer_input(const Geo& G, const BwdArgs& A, int head, int xOff) {
@@ -830,9 +924,9 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
   const float gam_l = tid < nb ? A.tdg_gamma[m0 + tid] : 0.f;
   float xv[4];
   if (xm) {  // the all-reduced maxima rows of this policy: stage C's output
-    const float* xr = A.tdg_xmax + ((size_t)(A.tdg_poloff + pol) * M + m0) * Aa;
+    const int* xr = A.tdg_xmax + ((size_t)(A.tdg_poloff + pol) * M + m0) * Aa;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) xv[u] = tid + u * 256 < nb * Aa ? xr[tid + u * 256] : 0.f;
+    for (int u = 0; u < 4; ++u) xv[u] = tid + u * 256 < nb * Aa ? unsortable(xr[tid + u * 256]) : 0.f;
   }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -1472,6 +1566,9 @@ template <int VMAX, int U>
 __global__ __launch_bounds__(256) void k_bwd_tdg(Geo G, BwdArgs A) {
   __shared__ floatx4 red[4][2][64];
   PROBE_T(pt0);
+  if (A.xi_dst)
+    fill_sortable(A.xi_dst, A.xi_src, A.xi_copy, A.xi_n, (blockIdx.y * gridDim.x + blockIdx.x) * 256 + threadIdx.x,
+                  gridDim.x * gridDim.y * 256);
   int head = A.head0 + blockIdx.y, bx = blockIdx.x;
   if (A.xcd) {
     if (!xcd_decode(blockIdx.x, A.nhead, A.na, head, bx)) return;
@@ -1908,6 +2005,8 @@ struct GateArgs {
   int* err;             // host-coherent
   const int* hcancel;   // written by the host (sfx_runner abort): cancel every step still waiting
   int* cancel;          // device: this step's verdict for its kernels (Geo::cancel)
+  int* clr;             // sharded steps: SORT_EMPTY-fill clr[0, nclr) (round 0's maxima buffers)
+  int nclr, pad2_;
 };
 
 // Wait for the host's go of this step (bounded); 1 if the step may run, 0 if it is cancelled.
@@ -1938,6 +2037,7 @@ __global__ __launch_bounds__(256) void k_gate(GateArgs g) {
   __shared__ int ok;
   PROBE_T(pt0);
   if (threadIdx.x == 0) ok = gate_wait(g);
+  if (g.clr) fill_sortable(g.clr, nullptr, 0, g.nclr, threadIdx.x, 256);
   __syncthreads();
   if (!ok) return;
   PROBE_MARK();
@@ -1988,6 +2088,7 @@ __global__ __launch_bounds__(256) void k_gate_replay(ReplayGateArgs A) {
   const GateArgs& g = A.g;
   PROBE_T(pt0);
   if (threadIdx.x == 0) ok = gate_wait(g);
+  if (g.clr) fill_sortable(g.clr, nullptr, 0, g.nclr, threadIdx.x, 256);
   __syncthreads();
   if (!ok) return;
   PROBE_MARK();
@@ -2117,8 +2218,8 @@ __device__ __forceinline__ void qdots(int n, int d, const float* s_w, float* s_q
 
 struct QmaxArgs {
   int M, Tg, off, guess, rows, pol0, tsel, pad_;
-  float* X;  // [npol][M][A]: max over this rank's heads of q[b, t, a] with w of policy pol0 + blockIdx.x
-             // (tsel >= 0: only local head tsel, the own-ψ branch of TSF's next actions)
+  int* X;  // [npol][M][A]: max over this rank's heads of q[b, t, a] with w of policy pol0 + blockIdx.x,
+           // sortable int32 (tsel >= 0: only local head tsel, the own-ψ branch of TSF's next actions)
 };
 
 // K5: grid (Tg, ceil(M / rows)).  Head t (global off + t) enters policy i's GPI through role
@@ -2147,28 +2248,34 @@ __global__ __launch_bounds__(256) void k_qmax(Geo G, QmaxArgs Q) {
     const float* qb = s_q + bl * TA + a;
     float mx = qb[0];
     for (int t = 1; t < T; ++t) mx = fmaxf(mx, qb[t * Aa]);
-    Q.X[((size_t)blockIdx.x * Q.M + b0 + bl) * Aa + a] = mx;
+    Q.X[((size_t)blockIdx.x * Q.M + b0 + bl) * Aa + a] = sortable(mx);
   }
+}
+
+// first argmax (torch.argmax tie-breaking) of A sortable maxima
+__device__ __forceinline__ int first_argmax(const int* x, int Aa) {
+  int am = 0;
+  float b = unsortable(x[0]);
+  for (int a = 1; a < Aa; ++a) {
+    const float v = unsortable(x[a]);
+    if (v > b) {
+      b = v;
+      am = a;
+    }
+  }
+  return am;
 }
 
 // K6: first policy whose next actions differ between the TD maxima X (from the guesses) and
 // the verification maxima Y (from the post-update heads); Tg if none.  One workgroup.
-__global__ __launch_bounds__(256) void k_sverify(const float* X, const float* Y, int Tg, int M, int Aa, int* flag) {
+__global__ __launch_bounds__(256) void k_sverify(const int* X, const int* Y, int Tg, int M, int Aa, int* flag) {
   __shared__ int s_min;
   if (threadIdx.x == 0) s_min = Tg;
   __syncthreads();
   int mine = Tg;
   const FDiv fM = fdiv(M);
   for (int j = threadIdx.x; j < Tg * M; j += 256) {
-    const float* x = X + (size_t)j * Aa;
-    const float* y = Y + (size_t)j * Aa;
-    int ax = 0, ay = 0;
-    float bx = x[0], by = y[0];
-    for (int a = 1; a < Aa; ++a) {
-      if (x[a] > bx) { bx = x[a]; ax = a; }
-      if (y[a] > by) { by = y[a]; ay = a; }
-    }
-    if (ax != ay) mine = min(mine, j / fM);
+    if (first_argmax(X + (size_t)j * Aa, Aa) != first_argmax(Y + (size_t)j * Aa, Aa)) mine = min(mine, j / fM);
   }
   atomicMin(&s_min, mine);
   __syncthreads();
@@ -2221,13 +2328,13 @@ __global__ __launch_bounds__(256) void k_skey(Geo G, KeyArgs K) {
 // The sharded env step in the native runner (sfx_runner schedule "sharded").
 // Action selection goes through the same all-reduce(MAX) as the verification maxima: this
 // rank writes q[t][a] = ψ_t(s_next)[a]·w_task of its own heads into its slice of a [T_glob][A]
-// block and -inf into every other slice, so the all-reduced block is the full GPI q table on
-// every rank; k_sfinish then picks argmax_t max_a and argmax_a (first index on ties:
+// table and SORT_EMPTY into every other slice, so the all-reduced table is the full GPI q table
+// on every rank; k_sfinish then picks argmax_t max_a and argmax_a (first index on ties:
 // SF.GPI_w + agent argmax, features/successor.py:223-273).
 // -------------------------------------------------------------------------------------
 struct SselArgs {
   int role, row, task, use_gpi, off, Tg;
-  float* q;  // [Tg][A]
+  int* q;  // [Tg][A] sortable
 };
 
 // grid cdiv(Tg * A, 256)
@@ -2240,27 +2347,31 @@ __global__ __launch_bounds__(256) void k_ssel(Geo G, SselArgs S) {
   const int j = blockIdx.x * 256 + tid;
   if (j >= S.Tg * Aa) return;
   const int tg = j / Aa, a = j - tg * Aa, t = tg - S.off;
-  float q = -INFINITY;
+  int q = SORT_EMPTY;
   if (t >= 0 && t < G.T && (S.use_gpi || tg == S.task)) {
     const float* p = G.actp(S.role, t, NLm) + (size_t)S.row * O + a * d;
     float acc = 0.f;
 #pragma unroll 8
     for (int k = 0; k < d; ++k) acc = __builtin_fmaf(p[k], s_w[k], acc);  // the GPI kernels' k order
-    q = __fadd_rn(acc, 0.f);  // -0 -> +0
+    q = sortable(acc);
   }
   S.q[j] = q;
 }
 
 struct SfinArgs {
-  const float* X;  // [Tg][M][A] all-reduced TD maxima of the last round (null: no update)
-  const float* Y;  // [Tg][M][A] all-reduced verification maxima
-  const float* q;  // [Tg][A] all-reduced selection table
+  const int* X;  // [Tg][M][A] all-reduced TD maxima of the last round (null: no update this step)
+  const int* Y;  // [Tg][M][A] all-reduced verification maxima
+  const int* q;  // [Tg][A] all-reduced selection table
   int Tg, M, A, pad_;
-  int* flag;       // first policy whose next actions changed (Tg: verified)
-  int64_t* sel;    // (GPI task c, greedy action a)
+  int* flag;     // first policy whose next actions changed (Tg: verified)
+  int64_t* sel;  // (GPI task c, greedy action a)
+  HostResult* pub;        // runner steps: publish (flag, sel) to the host (k_publish folded in)
+  const long long* dctr;
+  const int* cancel;
 };
 
-// One workgroup: verification of the speculated next actions (k_sverify) and the env action.
+// One workgroup: verification of the speculated next actions (k_sverify), the env action, and
+// in runner steps the publication of both.
 __global__ __launch_bounds__(256) void k_sfinish(SfinArgs F) {
   __shared__ int s_min;
   __shared__ unsigned long long s_best;
@@ -2273,24 +2384,16 @@ __global__ __launch_bounds__(256) void k_sfinish(SfinArgs F) {
   int mine = F.Tg;
   if (F.X) {
     const FDiv fM = fdiv(F.M);
-    for (int j = tid; j < F.Tg * F.M; j += 256) {
-      const float* x = F.X + (size_t)j * Aa;
-      const float* y = F.Y + (size_t)j * Aa;
-      int ax = 0, ay = 0;
-      float bx = x[0], by = y[0];
-      for (int a = 1; a < Aa; ++a) {
-        if (x[a] > bx) { bx = x[a]; ax = a; }
-        if (y[a] > by) { by = y[a]; ay = a; }
-      }
-      if (ax != ay) mine = min(mine, j / fM);
-    }
+    for (int j = tid; j < F.Tg * F.M; j += 256)
+      if (first_argmax(F.X + (size_t)j * Aa, Aa) != first_argmax(F.Y + (size_t)j * Aa, Aa)) mine = min(mine, j / fM);
   }
   // packed (q, first index) keys as k_skey: the max key is argmax_t max_a, then argmax_a
   unsigned long long best = 0ull;
   for (int j = tid; j < F.Tg * Aa; j += 256) {
-    const float q = F.q[j];
-    if (q == -INFINITY) continue;
-    const unsigned long long key = ((unsigned long long)orderable(q) << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)j);
+    const int qi = F.q[j];
+    if (qi == SORT_EMPTY) continue;
+    const unsigned long long key =
+        ((unsigned long long)orderable(unsortable(qi)) << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)j);
     best = key > best ? key : best;
   }
   atomicMin(&s_min, mine);
@@ -2298,9 +2401,18 @@ __global__ __launch_bounds__(256) void k_sfinish(SfinArgs F) {
   __syncthreads();
   if (tid == 0) {
     const unsigned idx = 0xFFFFFFFFu - (unsigned)(s_best & 0xFFFFFFFFull);
+    const long long c = idx / (unsigned)Aa, a = idx % (unsigned)Aa;
     *F.flag = s_min;
-    F.sel[0] = idx / (unsigned)Aa;
-    F.sel[1] = idx % (unsigned)Aa;
+    F.sel[0] = c;
+    F.sel[1] = a;
+    if (F.pub) {
+      F.pub->sel0 = c;
+      F.pub->sel1 = a;
+      F.pub->flag = s_min;
+      F.pub->cancelled = *F.cancel;
+      __threadfence_system();
+      __hip_atomic_store(&F.pub->seq, *F.dctr, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 

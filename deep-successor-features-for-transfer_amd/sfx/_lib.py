@@ -101,7 +101,7 @@ ENV_STEP_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_f
 
 
 # host all-reduce(MAX) callback of sfx_set_comm_host: (ctx, float* host buffer, count) -> 0 on success
-HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_float), C.c_int)
+HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_int32), C.c_int)
 
 
 class SFXError(RuntimeError):

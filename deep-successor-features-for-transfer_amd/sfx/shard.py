@@ -111,7 +111,8 @@ class LibsfxShardBackend:
         self.Tg, self.off = T_glob, head_offset
         engine.shard_setup(T_glob, head_offset)
         dev = engine.device
-        self._X = torch.empty(T_glob * max_batch * engine.A, device=dev)
+        # GPI maxima as sortable int32 (include/sfx.h): all-reduce(MAX) on int32 is the fp32 max
+        self._X = torch.empty(T_glob * max_batch * engine.A, device=dev, dtype=torch.int32)
         self._Y = torch.empty_like(self._X)
         self.key = torch.empty(1, dtype=torch.long, device=dev)
         self.flag = torch.empty(1, dtype=torch.int32, device=dev)
@@ -236,7 +237,7 @@ class LibsfxTSFShardBackend:
         self.Tg, self.off, self.T = T_glob, head_offset, engine.T
         engine.shard_setup(T_glob, head_offset)
         dev = engine.device
-        self._X = torch.empty(max_batch * engine.A, device=dev)
+        self._X = torch.empty(max_batch * engine.A, device=dev, dtype=torch.int32)  # sortable int32 maxima
         self.shared_buf = torch.empty(engine.tsf_Ph + engine.d, device=dev)
         self.key = torch.empty(1, dtype=torch.long, device=dev)
         self.losses = torch.empty(3, device=dev)
@@ -295,8 +296,8 @@ def init_comm(engine, rank: int, world: int, group=None):
 
 
 def set_host_comm(engine, rank: int, world: int, group=None):
-    """Host transport (sfx_set_comm_host): the library stages each all-reduce through pinned host
-    memory and this callback runs all-reduce(MAX) over a gloo group -- for ranks sharing one GPU
+    """Host transport (sfx_set_comm_host): the library stages each all-reduce (sortable int32
+    maxima) through pinned host memory and this callback runs all-reduce(MAX) over a gloo group -- for ranks sharing one GPU
     (tests), where RCCL cannot run.  Keeps the callback alive on the engine."""
     import numpy as np
     import torch.distributed as dist

@@ -282,7 +282,10 @@ int sfx_runner_get_record(sfx_runner_t r, int i, void* stage_host, int64_t* meta
  *    ranks that cannot run RCCL (several ranks on one GPU in tests); its steps are not graphed.
  * RCCL all-reduces are enqueued on the handle's stream and captured into the step graphs.
  * ------------------------------------------------------------------------------------- */
-typedef int (*sfx_host_allreduce_fn)(void* ctx, float* buf_host, int count);
+/* GPI maxima cross ranks as "sortable" int32: the order-preserving map of the fp32 value
+ * (i = bits(f + 0); i >= 0 ? i : i ^ 0x7FFFFFFF), so all-reduce(MAX) runs on int32 and the
+ * decoded maximum is exactly the fp32 one; INT32_MIN marks an empty entry. */
+typedef int (*sfx_host_allreduce_fn)(void* ctx, int32_t* buf_host, int count);
 int sfx_comm_id_bytes(void);
 int sfx_comm_unique_id(void* id_out /* sfx_comm_id_bytes() bytes */);
 int sfx_comm_init(sfx_t h, const void* unique_id, int rank, int world);
@@ -294,7 +297,7 @@ int sfx_set_comm_host(sfx_t h, sfx_host_allreduce_fn fn, void* ctx, int rank, in
  * This handle's T heads are the global heads [head_offset, head_offset + T) of T_glob; w has
  * T_glob rows (replicated: load every task's w on every rank).  One all-task env step
  * (agents/sfdqn.py:47-60, exact in-order semantics) is the sequence below, with the caller
- * running all-reduce(MAX) over ranks on X, Y (fp32 [T_glob][B][A]) and key (int64) in between:
+ * running all-reduce(MAX) over ranks on X, Y (sortable int32 [T_glob][B][A]) and key (int64) in between:
  *   begin; for r < R: td_maxima(r, X), AR(X), td_update(r, X); ver_maxima(R-1, Y), AR(Y);
  *   verify(X, Y, flag) -> while flag < T_glob: one more round r = R, R+1, ... (td_maxima,
  *   AR, td_update, ver_maxima, AR, verify);  select(r_last, task, use_gpi, key), AR(key);
@@ -308,10 +311,10 @@ int sfx_shard_begin(sfx_t h, const float* S_dev, const int64_t* a_dev, const flo
                     const float* S1_dev, const float* gamma_dev, int B, int lms_task,
                     const float* lms_phi_dev, const float* lms_r_dev, float lms_alpha,
                     const float* s_next_dev);
-int sfx_shard_td_maxima(sfx_t h, int round, float* X_dev);
-int sfx_shard_td_update(sfx_t h, int round, const float* X_dev);
-int sfx_shard_ver_maxima(sfx_t h, int round, float* Y_dev);
-int sfx_shard_verify(sfx_t h, const float* X_dev, const float* Y_dev, int* flag_dev);
+int sfx_shard_td_maxima(sfx_t h, int round, int32_t* X_dev);
+int sfx_shard_td_update(sfx_t h, int round, const int32_t* X_dev);
+int sfx_shard_ver_maxima(sfx_t h, int round, int32_t* Y_dev);
+int sfx_shard_verify(sfx_t h, const int32_t* X_dev, const int32_t* Y_dev, int* flag_dev);
 int sfx_shard_select(sfx_t h, int round, int task, int use_gpi, long long* key_dev);
 int sfx_shard_finish(sfx_t h, int rounds_run);
 
@@ -348,10 +351,10 @@ int sfx_tsf_update(sfx_t h, int policy, const float* S_dev, const int64_t* a_dev
  *   sfx_shard_select.
  * ------------------------------------------------------------------------------------- */
 /* X_dev [B][A]: max over this rank's heads (own_only: the policy's own head) of ψ_t(S1)·w_policy */
-int sfx_shard_tsf_maxima(sfx_t h, int policy, const float* S1_dev, int B, int own_only, float* X_dev);
+int sfx_shard_tsf_maxima(sfx_t h, int policy, const float* S1_dev, int B, int own_only, int32_t* X_dev);
 int sfx_shard_tsf_update(sfx_t h, int policy, const float* S_dev, const int64_t* a_dev, const float* r_dev,
                          const float* phi_dev, const float* S1_dev, const float* gamma_dev, int B,
-                         const float* X_dev, float* losses_dev);
+                         const int32_t* X_dev, float* losses_dev);
 /* unpack 0: buf_dev [Ph + d] <- (h, w_policy); 1: (h, w_policy) <- buf_dev */
 int sfx_shard_tsf_shared(sfx_t h, int policy, float* buf_dev, int unpack);
 int sfx_shard_tsf_select(sfx_t h, const float* s_dev, int task, int use_gpi, long long* key_dev);

@@ -95,8 +95,14 @@ def _oracle_check(cfg, recs, final, heads, targets, ws):
     rel_close(ws, st.w, rtol=1e-5, atol=1e-7)
 
 
-def test_native_sharded_single_rank_rccl():
-    """World 1 with the library's own RCCL communicator: ncclAllReduce inside the step graphs."""
+@pytest.mark.parametrize("fused", [True, False], ids=["fused-maxima", "qmax-launches"])
+def test_native_sharded_single_rank_rccl(fused, monkeypatch):
+    """World 1 with the library's own RCCL communicator; SFX_RCCL_WORLD1=1 makes the one-rank
+    all-reduces real ncclAllReduce calls inside the step graphs.  fused: the maxima come out of the
+    ψ output layer's forward tiles (d | 16); else from separate k_qmax launches."""
+    monkeypatch.setenv("SFX_RCCL_WORLD1", "1")
+    if not fused:
+        monkeypatch.setenv("SFX_SHARD_QA", "0")
     cfg = dict(SMALL, world=1, t_loc=4)
     recs, final, heads, targets, ws, stats, counters = _run_rank(0, cfg, "rccl")
     assert stats["prelaunched"] >= cfg["steps"] - 1, stats
@@ -107,7 +113,7 @@ def test_native_sharded_single_rank_rccl():
 def _worker(rank, port, q, cfg):
     import torch.distributed as dist
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **cfg.get("env", {}))
     dist.init_process_group("gloo", rank=rank, world_size=cfg["world"])
     try:
         recs, final, heads, targets, ws, stats, _ = _run_rank(rank, cfg, "host")
@@ -140,7 +146,12 @@ def _ranks(cfg):
     return out
 
 
-@pytest.mark.parametrize("cfg", [SMALL, C4], ids=["2x2-small", "c4-8x8-h256"])
+# d = 6 does not divide 16: the maxima of every round come from k_qmax launches
+ODD_D = dict(SMALL, spec=dict(n_s=9, H=32, A=5, d=6, acts=("relu", "relu")), world=3, t_loc=2)
+
+
+@pytest.mark.parametrize("cfg", [SMALL, dict(SMALL, env={"SFX_SHARD_QA": "0"}), ODD_D, C4],
+                         ids=["2x2-small", "2x2-qmax-launches", "3x2-d6", "c4-8x8-h256"])
 def test_native_sharded_ranks_on_one_gpu(cfg):
     recs, final, heads, targets, ws, stats, streams = _ranks(cfg)
     assert all(s == streams[0] for s in streams), "ranks diverged"

@@ -346,3 +346,41 @@ def test_runner_gpi_counters_follow_use_gpi():
     assert loop.gpi_counters().sum() == 0
     loop.close()
     eng.close()
+
+
+@pytest.mark.parametrize("schedule", ["all", "active"])
+def test_runner_c1_cartpole_shape(schedule):
+    """BASELINE config C1 at its stated shape: CartPole-v2 SF-DQN, n_s=4, A=2, d=20
+    (configs/cartpole_phi.cfg:52), 2 source tasks, 256-wide heads, minibatch 32 -- the all-task
+    schedule (main_sfdqn_torch.py) and the active-task one (sfdqn.py), against the oracle."""
+    from sfx.runner import NativeEnvLoop
+
+    spec = R.Spec(4, 256, 2, 20, ("relu", "relu"))
+    T, ev, alpha, n = 2, 7, 0.05, 24
+    eng, st = make(spec, T, ev, max_batch=32)
+    loop = NativeEnvLoop(eng, batch=32, capacity=300, gamma=0.9, epsilon=0.2, alpha_w=alpha, episode_len=9, seed=4,
+                         schedule=schedule, p_end=0.05)
+    loop.prefill(30)
+    loop.set_task(1)
+    loop.record(n)
+    loop.run(n)
+    recs = loop.records()
+    if schedule == "all":
+        replay_with_oracle(st, spec, recs, alpha, ev, loop.action())
+        check_state(eng, st, T, n)
+    else:
+        for k, rec in enumerate(recs):
+            if rec["have"]:
+                batch = (torch.from_numpy(rec["s"]), torch.from_numpy(rec["a"]),
+                         torch.from_numpy(rec["rb"]).view(-1, 1), torch.from_numpy(rec["phi"]),
+                         torch.from_numpy(rec["s1"]), torch.from_numpy(rec["gamma"]))
+                R.sf_update(st, batch, 1, use_gpi=True, target_update_ev=ev)
+            q, tk = R.gpi_w(R.psi_all(st.online, spec, torch.from_numpy(rec["snext"]).view(1, -1)), st.w[1])
+            want = (int(tk[0]), R.select_action(q, tk[0], 1, True))
+            got = (recs[k + 1]["c"], recs[k + 1]["a_greedy"]) if k + 1 < len(recs) else loop.action()
+            assert got == want, f"step {k}: runner selected {got}, oracle {want}"
+        params_close(torch.stack([eng.get_head(t, 0) for t in range(T)]), st.online, 1e-3 * n)
+        params_close(torch.stack([eng.get_head(t, 1) for t in range(T)]), st.target, 1e-3 * n)
+        rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-3, atol=1e-6)
+    loop.close()
+    eng.close()

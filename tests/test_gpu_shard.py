@@ -136,7 +136,7 @@ def _two_ranks(worker, cfg):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=worker, args=(r, port, q, cfg)) for r in range(2)]
+    procs = [ctx.Process(target=worker, args=(r, port, q, cfg)) for r in range(cfg.get("world", 2))]
     for p in procs:
         p.start()
     # tensors travel as numpy arrays (pickled by value): torch's fd-shared storages need the
@@ -162,6 +162,8 @@ TSF_SMALL = dict(spec=dict(n_s=11, H=32, A=9, d=6, acts=("relu", "relu")), tg=TG
 # layers; two ranks of 8 heads, flows at a small init (PlanarFlow's U(-0.01, 0.01) scale, widened)
 TSF_FULL = dict(spec=dict(n_s=11, H=256, A=27, d=50, acts=("relu", "relu")), tg=16, b=32, G=100, K=100, steps=4,
                 init=0.05)
+# BASELINE config C5 at its stated size: 32 TSF-NF tasks over 4 ranks (8 heads each), K = 100
+TSF_C5 = dict(TSF_FULL, tg=32, world=4)
 
 
 def _tsf_problem(cfg):
@@ -253,14 +255,15 @@ def test_tsf_single_rank_shard_protocol(use_gpi):
 def _tsf_worker(rank, port, q, cfg=TSF_SMALL):
     import torch.distributed as dist
 
+    world = cfg.get("world", 2)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     from sfx.shard import all_reduce_max_fn, broadcast_fn
 
     try:
-        actions, heads, gg, h, w = _tsf_run_rank(rank, 2, True, all_reduce_max_fn(via_host=True),
+        actions, heads, gg, h, w = _tsf_run_rank(rank, world, True, all_reduce_max_fn(via_host=True),
                                                  broadcast_fn(via_host=True), cfg)
-        parts = [None, None]
+        parts = [None] * world
         dist.all_gather_object(parts, (heads, gg))
         if rank == 0:
             q.put((actions, torch.cat([p[0] for p in parts]).numpy(), torch.cat([p[1] for p in parts]).numpy(),
@@ -269,6 +272,6 @@ def _tsf_worker(rank, port, q, cfg=TSF_SMALL):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg", [TSF_SMALL, TSF_FULL], ids=["small", "c5-shape"])
+@pytest.mark.parametrize("cfg", [TSF_SMALL, TSF_FULL, TSF_C5], ids=["small", "c5-shape", "c5-4x8-k100"])
 def test_tsf_two_ranks_on_one_gpu(cfg):
     _tsf_check(_two_ranks(_tsf_worker, cfg), True, cfg)
