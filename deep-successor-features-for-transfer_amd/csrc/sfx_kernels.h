@@ -2037,9 +2037,10 @@ __global__ __launch_bounds__(256) void k_gate(GateArgs g) {
   __shared__ int ok;
   PROBE_T(pt0);
   if (threadIdx.x == 0) ok = gate_wait(g);
-  if (g.clr) fill_sortable(g.clr, nullptr, 0, g.nclr, threadIdx.x, 256);
   __syncthreads();
   if (!ok) return;
+  // after the wait: until then a step before this one may still be running its host rounds
+  if (g.clr) fill_sortable(g.clr, nullptr, 0, g.nclr, threadIdx.x, 256);
   PROBE_MARK();
   for (int i = threadIdx.x; i < g.n16; i += 256) g.dst[i] = g.src[i];
   PROBE_REC(9, pt0);
@@ -2088,9 +2089,10 @@ __global__ __launch_bounds__(256) void k_gate_replay(ReplayGateArgs A) {
   const GateArgs& g = A.g;
   PROBE_T(pt0);
   if (threadIdx.x == 0) ok = gate_wait(g);
-  if (g.clr) fill_sortable(g.clr, nullptr, 0, g.nclr, threadIdx.x, 256);
   __syncthreads();
   if (!ok) return;
+  // after the wait: until then a step before this one may still be running its host rounds
+  if (g.clr) fill_sortable(g.clr, nullptr, 0, g.nclr, threadIdx.x, 256);
   PROBE_MARK();
   uint4* lt = reinterpret_cast<uint4*>(tail);
   for (int i = threadIdx.x; i < g.n16; i += 256) {

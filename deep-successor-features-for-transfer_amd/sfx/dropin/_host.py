@@ -1,0 +1,28 @@
+"""What the drop-in library takes from the host program: the torch device the training script
+chose (the reference's ``utils.torch`` global, set by ``set_torch_device`` before the library is
+built) and the target-network copy of utils/torch.py:31-33.  The user's utils package is read
+when it is importable; replays without it (tests/test_gpu_dropin.py) get ``None`` -- outputs then
+stay on the engine's device."""
+from __future__ import annotations
+
+import sys
+
+import torch
+
+
+def torch_device():
+    mod = sys.modules.get("utils.torch")
+    if mod is None:
+        try:
+            import utils.torch as mod  # the user's checkout
+        except ImportError:
+            return None
+    get = getattr(mod, "get_torch_device", None)
+    return get() if get is not None else getattr(mod, "device", None)
+
+
+def copy_weights(model: torch.nn.Module, target_model: torch.nn.Module) -> None:
+    """target <- model, parameter by parameter (update_models_weights, utils/torch.py:31-33)."""
+    with torch.no_grad():
+        for dst, src in zip(target_model.parameters(), model.parameters()):
+            dst.copy_(src)

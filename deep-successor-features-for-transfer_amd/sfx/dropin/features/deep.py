@@ -22,8 +22,9 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from features.successor import SF
-from utils.torch import get_torch_device, update_models_weights
+from sfx.dropin._host import copy_weights as update_models_weights
+from sfx.dropin._host import torch_device as get_torch_device
+from .successor import SF
 
 
 def _geometry(model: torch.nn.Module):

@@ -12,8 +12,8 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from features import deep as _deep
-from utils.torch import update_models_weights
+from sfx.dropin._host import copy_weights as update_models_weights
+from . import deep as _deep
 
 
 class _FitWLinear(list):

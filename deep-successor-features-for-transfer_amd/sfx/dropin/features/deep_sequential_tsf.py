@@ -16,20 +16,34 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from features import deep_sequential as _seq
-from utils.torch import update_models_weights
+from sfx.dropin._host import copy_weights as update_models_weights
+from . import deep_sequential as _seq
+
+
+def _g_tensors(g):
+    """g_i's tensors in the engine's packing (include/sfx.h sfx_tsf_load_g): per planar flow
+    weight [1, n_s], bias [1], scale [1, n_s], then the Linear's weight and bias.  Flows are read by
+    attribute: tsfdqn_nf.py's PlanarFlow moves its Parameters with .to(device) on a GPU, which
+    leaves them unregistered; they train here either way."""
+    mods = list(g) if isinstance(g, torch.nn.Sequential) else [g]
+    *flows, lin = mods
+    out = []
+    for f in flows:
+        out += [getattr(f, "weight", None), getattr(f, "bias", None), getattr(f, "scale", None)]
+    return out + [getattr(lin, "weight", None), getattr(lin, "bias", None)]
 
 
 def _g_geometry(g, n_s):
     """(K, G) of a g_i: nn.Linear(n_s, G) (tsfdqn.py, agents/tsfdqn_sequential.py) or K planar flows
-    (modules with weight [1, n_s], bias [1], scale [1, n_s]) followed by nn.Linear(n_s, G)
-    (tsfdqn_nf.py:331-358); raises for anything else."""
+    (weight [1, n_s], bias [1], scale [1, n_s]) followed by nn.Linear(n_s, G) (tsfdqn_nf.py:331-358);
+    raises for anything else."""
     mods = list(g) if isinstance(g, torch.nn.Sequential) else [g]
     *flows, lin = mods
     ok = isinstance(lin, torch.nn.Linear) and lin.bias is not None and lin.in_features == n_s
     for f in flows:
-        names = [n for n, _ in f.named_parameters()]
-        ok = ok and names == ["weight", "bias", "scale"] and f.weight.shape == (1, n_s) and f.scale.shape == (1, n_s)
+        w, b, sc = (getattr(f, k, None) for k in ("weight", "bias", "scale"))
+        ok = ok and all(isinstance(x, torch.Tensor) for x in (w, b, sc))
+        ok = ok and tuple(w.shape) == (1, n_s) and tuple(sc.shape) == (1, n_s) and b.numel() == 1
     if not ok:
         raise NotImplementedError("sfx DeepTSF: g_i must be nn.Linear(n_s, G) with bias, optionally after planar "
                                   f"flows (weight, bias, scale); got {g}")
@@ -37,16 +51,24 @@ def _g_geometry(g, n_s):
 
 
 def _params_flat(m: torch.nn.Module):
-    """Parameters in registration order (the engine's packing, include/sfx.h sfx_tsf_load_g)."""
+    """Parameters in registration order (h; g_i through _g_tensors)."""
     return torch.cat([p.detach().reshape(-1).float().cpu() for p in m.parameters()])
 
 
-def _params_load(m: torch.nn.Module, flat):
+def _tensors_flat(ts):
+    return torch.cat([t.detach().reshape(-1).float().cpu() for t in ts])
+
+
+def _tensors_load(ts, flat):
     off = 0
     with torch.no_grad():
-        for p in m.parameters():
+        for p in ts:
             p.copy_(flat[off:off + p.numel()].view_as(p).to(p.device, p.dtype))
             off += p.numel()
+
+
+def _params_load(m: torch.nn.Module, flat):
+    _tensors_load(list(m.parameters()), flat)
 
 
 class DeepTSF(_seq.DeepSF):
@@ -126,7 +148,7 @@ class DeepTSF(_seq.DeepSF):
             eng.tsf_setup(G, K, float(hp.get("beta_loss_coefficient", 1.0)), hp["learning_rate_g"],
                           hp["weight_decay_g"], hp["learning_rate_h"], hp["weight_decay_h"])
             for t, g in enumerate(self._g):
-                eng.tsf_load_g(t, _params_flat(g))
+                eng.tsf_load_g(t, _tensors_flat(_g_tensors(g)))
             eng.tsf_load_h(_params_flat(h))
         return eng
 
@@ -135,7 +157,7 @@ class DeepTSF(_seq.DeepSF):
         if self._eng is None or not self._tsf_stale:
             return
         for t, g in enumerate(self._g):
-            _params_load(g, self._eng.tsf_get_g(t)[0])
+            _tensors_load(_g_tensors(g), self._eng.tsf_get_g(t)[0])
         _params_load(self._h, self._eng.tsf_get_h())
         self._tsf_stale = False
 

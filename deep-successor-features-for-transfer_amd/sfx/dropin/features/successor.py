@@ -9,7 +9,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from utils.torch import get_torch_device
+from sfx.dropin._host import torch_device as get_torch_device
 
 
 class SF:

@@ -1,30 +1,150 @@
-"""CPU checks of the drop-in module tree (no GPU compute): the reference's import names
-resolve to sfx's modules, the ψ architecture is recognised or rejected, the library keeps
-the reference's bookkeeping, and compute fails loudly without a HIP device."""
+"""CPU checks of the drop-in binding (no GPU compute): the import hook binds a reference checkout
+to sfx's libraries and leaves the user's agents, utils and tasks alone; the ψ architecture is
+recognised or rejected; the library keeps the reference's bookkeeping; compute fails loudly
+without a HIP device."""
+import os
+import sys
+import textwrap
+
 import pytest
 import torch
 
 from tests.golden.recipe import AgentTask, agent_psi_lambda
 
+REF = "/root/reference/source"
 
-@pytest.fixture(scope="module")
-def mods():
+
+def _uninstall():
     from sfx import dropin
 
+    sys.meta_path[:] = [f for f in sys.meta_path if not isinstance(f, dropin._Finder)]
+    for name in list(sys.modules):
+        top = name.split(".")[0]
+        if top in ("features", "agents", "utils", "tasks", "sfdqn", "tsfdqn", "tsfdqn_nf"):
+            del sys.modules[name]
+
+
+@pytest.fixture
+def checkout(tmp_path):
+    """A minimal checkout with the reference's module names (our stand-ins: only the names and the
+    methods the binding touches)."""
+    files = {
+        "features/__init__.py": "",
+        "features/tabular.py": "WHO = 'user'\n",
+        "features/deep.py": "WHO = 'user'\n",
+        "agents/__init__.py": "",
+        "agents/sfdqn.py": "WHO = 'user'\nclass SFDQN:\n    pass\n",
+        "agents/tsfdqn_sequential.py": textwrap.dedent("""
+            WHO = 'user'
+            class TSFDQN:
+                def update_successor(self, transitions, policy_index, use_gpi=True):
+                    return 'user update'
+                def test_agent(self, task, test_index):
+                    return ('user test', task, test_index)
+            """),
+        "utils/__init__.py": "",
+        "utils/torch.py": "device = None\ndef get_torch_device():\n    return device\n",
+        "sfdqn.py": "WHO = 'user'\nclass DeepSF:\n    pass\nclass SFDQN:\n    pass\nclass ReplayBuffer:\n    pass\n",
+        "tsfdqn_nf.py": textwrap.dedent("""
+            WHO = 'user'
+            class DeepTSF:
+                pass
+            class PlanarFlow:
+                pass
+            class TSFDQN:
+                def update_successor(self, transitions, policy_index, use_gpi=True):
+                    return 'user update'
+                def test_agent(self, task, test_index):
+                    return 'user test'
+            """),
+    }
+    for rel, text in files.items():
+        p = tmp_path / rel
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_text(text)
+    _uninstall()
+    sys.path.insert(0, str(tmp_path))
+    yield tmp_path
+    sys.path.remove(str(tmp_path))
+    _uninstall()
+
+
+def test_install_binds_the_sf_library_only(checkout):
+    from sfx import dropin
+    from sfx.dropin import bind
+
     root = dropin.install()
-    import agents.buffer
     import agents.sfdqn
+    import agents.tsfdqn_sequential as ats
     import features.deep
-    import utils.torch as ut
+    import features.deep_sequential_tsf
+    import features.tabular
+    import sfdqn
+    import tsfdqn_nf
+    import utils.torch
 
-    ut.set_torch_device(False)
-    for m in (features.deep, agents.sfdqn, agents.buffer):
-        assert m.__file__.startswith(root)
-    return features.deep, agents.sfdqn, agents.buffer
+    assert features.deep.__file__.startswith(root) and features.deep_sequential_tsf.__file__.startswith(root)
+    assert features.tabular.WHO == "user" and agents.sfdqn.WHO == "user" and utils.torch.__file__.startswith(
+        str(checkout))
+    # single-file modules: the user's file, with sfx's library classes and the TSF update bound
+    assert sfdqn.WHO == "user" and sfdqn.__file__.startswith(str(checkout))
+    assert sfdqn.DeepSF is bind.SingleFileDeepSF and sfdqn.SFDQN.__module__ == "sfdqn"
+    assert tsfdqn_nf.DeepTSF is bind.SingleFileDeepTSF and tsfdqn_nf.PlanarFlow.__module__ == "tsfdqn_nf"
+    for cls in (tsfdqn_nf.TSFDQN, ats.TSFDQN):
+        assert cls.update_successor is bind.tsf_update_successor
+        synced = []
+
+        class _SF:
+            def sync_tsf_modules(self):
+                synced.append(True)
+
+        agent = cls()
+        agent.sf = _SF()
+        agent.test_agent("task", 0)  # the user's own method, after a g / h sync
+        assert synced == [True]
+        assert agent.update_successor(None, 0) is None
 
 
-def test_geometry_recognised_and_rejected(mods):
-    deep, _, _ = mods
+def test_install_on_the_reference_checkout():
+    """The hook on the real reference tree (this container only): its scripts' imports resolve
+    to sfx's libraries and to the reference's own agents."""
+    if not os.path.isdir(REF):
+        pytest.skip("reference checkout not present")
+    import types
+
+    from sfx import dropin
+    from sfx.dropin import bind
+
+    _uninstall()
+    tb = types.ModuleType("torch.utils.tensorboard")  # utils/logger.py imports it; not installed here
+    tb.SummaryWriter = object
+    saved_tb = sys.modules.get("torch.utils.tensorboard")
+    sys.modules["torch.utils.tensorboard"] = tb
+    sys.path.insert(0, REF)
+    try:
+        dropin.install()
+        import agents.sfdqn
+        import agents.tsfdqn_sequential
+        import features.deep
+        import features.tabular
+        import tsfdqn
+
+        assert features.deep.__file__.startswith(dropin.ROOT)
+        assert features.tabular.__file__.startswith(REF) and agents.sfdqn.__file__.startswith(REF)
+        assert tsfdqn.__file__.startswith(REF) and tsfdqn.DeepTSF is bind.SingleFileDeepTSF
+        assert agents.tsfdqn_sequential.TSFDQN.update_successor is bind.tsf_update_successor
+    finally:
+        sys.path.remove(REF)
+        if saved_tb is None:
+            del sys.modules["torch.utils.tensorboard"]
+        else:
+            sys.modules["torch.utils.tensorboard"] = saved_tb
+        _uninstall()
+
+
+def test_geometry_recognised_and_rejected():
+    from sfx.dropin.features import deep
+
     model, _, _ = agent_psi_lambda(32, ("relu", "tanh"), 1e-3, "cpu")(17, 56, (7, 8))
     assert deep._geometry(model) == (17, 32, ("relu", "tanh"), 56)
     bad = torch.nn.Sequential(torch.nn.Linear(4, 8), torch.nn.ReLU(), torch.nn.Linear(8, 6))
@@ -32,8 +152,29 @@ def test_geometry_recognised_and_rejected(mods):
         deep._geometry(bad)
 
 
-def test_library_bookkeeping_and_loud_failure(mods):
-    deep, _, _ = mods
+def test_planar_flow_g_recognised_by_attribute():
+    """tsfdqn_nf.py's PlanarFlow on a GPU leaves its tensors unregistered (.to(device) on the
+    Parameters); the library reads them by attribute either way."""
+    from sfx.dropin.features import deep_sequential_tsf as dts
+
+    class Flow(torch.nn.Module):
+        def __init__(self, n, registered):
+            super().__init__()
+            mk = torch.nn.Parameter if registered else (lambda t: t)
+            self.weight, self.bias, self.scale = mk(torch.zeros(1, n)), mk(torch.zeros(1)), mk(torch.zeros(1, n))
+
+    for registered in (True, False):
+        g = torch.nn.Sequential(Flow(5, registered), Flow(5, registered), torch.nn.Linear(5, 7))
+        assert dts._g_geometry(g, 5) == (2, 7)
+        assert sum(t.numel() for t in dts._g_tensors(g)) == 2 * 11 + 5 * 7 + 7
+    assert dts._g_geometry(torch.nn.Linear(5, 7), 5) == (0, 7)
+    with pytest.raises(NotImplementedError):
+        dts._g_geometry(torch.nn.Linear(4, 7), 5)
+
+
+def test_library_bookkeeping_and_loud_failure():
+    from sfx.dropin.features import deep
+
     sf = deep.DeepSF(pytorch_model_handle=agent_psi_lambda(16, ("relu",), 1e-3, "cpu"), target_update_ev=5,
                      hyperparameters={"learning_rate_w": 0.1})
     sf.reset()
@@ -49,54 +190,3 @@ def test_library_bookkeeping_and_loud_failure(mods):
     if not torch.cuda.is_available():
         with pytest.raises(RuntimeError, match="HIP device"):
             sf.get_successors(torch.zeros(2, 6))
-
-
-def test_replay_buffer_semantics(mods):
-    _, _, buf = mods
-    b = buf.ReplayBuffer(n_samples=4, n_batch=2)
-    b.reset()
-    assert b.replay() is None
-    for i in range(6):
-        b.append(torch.full((1, 3), float(i)), torch.tensor(i % 2), torch.ones(1, 2), torch.zeros(1, 3), 0.9)
-    assert b.size == 4 and b.index == 2
-    s, a, phi, s1, g = b.replay()
-    assert s.shape == (2, 3) and a.shape == (2,) and phi.shape == (2, 2) and g.dtype == torch.float32
-
-
-def test_sequential_modules_and_buffer(mods):
-    """main_sfdqn_sequential_torch.py's imports resolve to the drop-in tree; the per-task buffer
-    keeps agents/buffer_sequential.py's 6-tuples, ring order and np.random sampling."""
-    import numpy as np
-
-    from sfx import dropin
-
-    root = dropin.install()
-    import agents.buffer_sequential as bs
-    import agents.buffer_tsf_sequential as bts
-    import agents.sfdqn_sequential as ss
-    import agents.tsfdqn_sequential as ts
-    import features.deep_sequential as ds
-    import features.deep_sequential_tsf as dts
-
-    import sfdqn
-    import tsfdqn
-    import tsfdqn_nf
-
-    for m in (bs, ss, ds, bts, ts, dts, sfdqn, tsfdqn, tsfdqn_nf):
-        assert m.__file__.startswith(root)
-    b = bs.ReplayBuffer(n_samples=4, n_batch=3)
-    assert b.replay() is None
-    for i in range(6):
-        b.append(torch.full((1, 3), float(i)), i % 2, torch.tensor(0.5 * i), torch.ones(1, 2) * i,
-                 torch.zeros(1, 3), 0.9)
-    assert b.size == 4 and b.index == 2
-    np.random.seed(3)
-    idx = np.random.randint(low=0, high=4, size=(3,))
-    np.random.seed(3)
-    s, a, r, phi, s1, g = b.replay()
-    # ring slots: 0 <- sample 4, 1 <- sample 5, 2 <- sample 2, 3 <- sample 3
-    src = np.array([4, 5, 2, 3])[idx]
-    assert torch.equal(s[:, 0], torch.tensor(src, dtype=torch.float32))
-    assert torch.equal(r[:, 0], torch.tensor(0.5 * src, dtype=torch.float32))
-    assert r.shape == (3, 1) and phi.shape == (3, 2) and a.tolist() == [int(x) % 2 for x in src]
-    assert g.dtype == torch.float32

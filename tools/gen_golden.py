@@ -354,38 +354,161 @@ def gen_tsf(name, module, shape, T, k, K):
     np.savez_compressed(os.path.join(OUT, f"upd_{name}.npz"), **rec)
 
 
-def gen_agent_run():
-    """The main_sfdqn_torch.py stack end to end: reference agents/sfdqn.py SFDQN +
-    agents/buffer.py ReplayBuffer + features/deep.py DeepSF on synthetic tasks."""
+# ---------------------------------------------------------------------------------------
+# SF-boundary call logs: the reference's own agents (agents/sfdqn.py, agents/sfdqn_sequential.py,
+# agents/tsfdqn_sequential.py and the single-file sfdqn.py / tsfdqn.py / tsfdqn_nf.py) run the
+# seeded recipes of tests/golden/recipe.py on the CPU, and every call they make across the SF
+# boundary -- GPI, get_successor(s), get_next_successors, update_reward, update_successor, and for
+# TSF the agent's own update_successor (tsfdqn.py:588-709), which the drop-in binds to the library
+# -- is logged in order with its inputs and outputs, together with the library state before the
+# first call and after the run.  tests/test_gpu_dropin.py replays the log through sfx's drop-in
+# library on the GPU.  The agents themselves never leave this container.
+# ---------------------------------------------------------------------------------------
+class CallLog:
+    def __init__(self):
+        self.calls, self.depth, self.init, self.agent = [], 0, None, None
+
+    def call(self, sf, name, thunk, fields):
+        if self.depth == 0 and self.init is None:
+            self.init = lib_state(sf, self.agent)
+        self.depth += 1
+        try:
+            out = thunk()
+        finally:
+            self.depth -= 1
+        if self.depth == 0:  # only the agent's own calls, not the library's calls into itself
+            self.calls.append((name, fields(out)))
+        return out
+
+    def save(self, path, final):
+        rec = {"names": np.array([n for n, _ in self.calls])}
+        for k, (_, f) in enumerate(self.calls):
+            for key, v in f.items():
+                rec[f"c{k}.{key}"] = _val(v)
+        for key, v in self.init.items():
+            rec["init." + key] = v
+        for key, v in final.items():
+            rec["final." + key] = v
+        np.savez_compressed(path, **rec)
+
+
+def _val(v):
+    if isinstance(v, torch.Tensor):
+        return v.detach().cpu().numpy()
+    return np.asarray(v)
+
+
+def _w_flat(w):
+    w = w.weight if hasattr(w, "weight") else w
+    return w.detach().reshape(-1).cpu().clone()
+
+
+def lib_state(sf, agent=None):
+    T = sf.n_tasks
+    st = dict(online=np_(torch.stack([flat(sf.psi[t][0][0]) for t in range(T)])),
+              target=np_(torch.stack([flat(sf.psi[t][1][0]) for t in range(T)])),
+              w=np_(torch.stack([_w_flat(sf.fit_w[t]) for t in range(T)])))
+    if agent is not None and getattr(agent, "g_functions", None):
+        st["g"] = np_(torch.stack([flat(agent.g_functions[t]) for t in range(T)]))
+        st["h"] = np_(flat(agent.h_function))
+    return st
+
+
+def _transitions(tr):
+    return {} if tr is None else {f"t{i}": x for i, x in enumerate(tr)}
+
+
+def recording_sf(cls, log):
+    class Recording(cls):
+        def GPI(self, state, task_index, update_counters=False):
+            return log.call(self, "GPI", lambda: cls.GPI(self, state, task_index, update_counters),
+                            lambda o: dict(state=state, task_index=task_index, update_counters=update_counters,
+                                           q=o[0], task=o[1]))
+
+        def get_successors(self, state):
+            return log.call(self, "get_successors", lambda: cls.get_successors(self, state),
+                            lambda o: dict(state=state, psi=o))
+
+        def get_successor(self, state, policy_index):
+            return log.call(self, "get_successor", lambda: cls.get_successor(self, state, policy_index),
+                            lambda o: dict(state=state, policy_index=policy_index, psi=o))
+
+        def update_reward(self, phi, r, task_index, exact=False):
+            return log.call(self, "update_reward", lambda: cls.update_reward(self, phi, r, task_index, exact),
+                            lambda o: dict(phi=phi, r=torch.as_tensor(r).float(), task_index=task_index,
+                                           w=_w_flat(self.fit_w[task_index])))
+
+        def update_successor(self, transitions, policy_index, *args, **kwargs):
+            use_gpi = kwargs.get("use_gpi", args[0] if args else True)
+            out = {}
+
+            def fields(o):
+                f = dict(_transitions(transitions), policy_index=policy_index, use_gpi=bool(use_gpi),
+                         has_batch=transitions is not None)
+                if isinstance(o, tuple):
+                    f["losses"] = torch.stack([torch.as_tensor(x).detach().float() for x in o])
+                return f
+
+            return log.call(self, "update_successor",
+                            lambda: cls.update_successor(self, transitions, policy_index, *args, **kwargs), fields)
+
+    if hasattr(cls, "get_next_successors"):
+        def get_next_successors(self, state):
+            return log.call(self, "get_next_successors", lambda: cls.get_next_successors(self, state),
+                            lambda o: dict(state=state, psi=o))
+
+        Recording.get_next_successors = get_next_successors
+    Recording.__name__ = cls.__name__
+    return Recording
+
+
+def recording_tsf_agent(cls, log):
+    class Recording(cls):
+        def __init__(self, *a, **k):
+            super().__init__(*a, **k)
+            log.agent = self
+
+        def update_successor(self, transitions, policy_index, use_gpi=True):
+            def fields(o):
+                f = dict(_transitions(transitions), policy_index=policy_index, use_gpi=bool(use_gpi),
+                         has_batch=transitions is not None)
+                if isinstance(o, tuple):
+                    f["losses"] = torch.stack([torch.as_tensor(x).detach().float() for x in o])
+                return f
+
+            return log.call(self.sf, "tsf_update",
+                            lambda: cls.update_successor(self, transitions, policy_index, use_gpi), fields)
+
+    Recording.__name__ = cls.__name__
+    return Recording
+
+
+def _final(agent, log):
+    sf = agent.sf
+    st = lib_state(sf, log.agent)
+    st["gpi_counters"] = np.stack([np.asarray(c) for c in sf.gpi_counters])
+    st["since_target"] = np.array(sf.updates_since_target_updated)
+    return st
+
+
+def gen_call_log_alltask():
+    """main_sfdqn_torch.py's stack: agents/sfdqn.py SFDQN + agents/buffer.py + features/deep.py."""
     import contextlib
     import io
 
     from agents.buffer import ReplayBuffer
     from agents.sfdqn import SFDQN
-    from tests.golden.recipe import AGENT_RUN, agent_run
+    from tests.golden.recipe import agent_run
 
+    log = CallLog()
     with contextlib.redirect_stdout(io.StringIO()):
-        agent, tasks, test_tasks, returns = agent_run(ref_deep.DeepSF, SFDQN, ReplayBuffer, torch.device("cpu"))
-    sf = agent.sf
-    T = sf.n_tasks
-    rec = dict(online=np_(torch.stack([flat(sf.psi[t][0][0]) for t in range(T)])),
-               target=np_(torch.stack([flat(sf.psi[t][1][0]) for t in range(T)])),
-               w=np_(torch.stack([sf.fit_w[t].reshape(-1).clone() for t in range(T)])),
-               gpi_counters=np.stack([np.asarray(c) for c in sf.gpi_counters]),
-               since_target=np.array(sf.updates_since_target_updated),
-               actions=np.array([a for t in tasks for a in t.actions]),
-               test_actions=np.array(test_tasks[0].actions),
-               test_w=np_(agent.test_tasks_weights[0].weight.detach().reshape(-1)),
-               returns=np.array([float(r) for r in returns]),
-               reward_hist=np.array([float(x) for x in agent.reward_hist]),
-               cum_reward=float(agent.cum_reward), total_steps=agent.total_training_steps)
-    np.savez_compressed(os.path.join(OUT, "run_sfdqn_agent.npz"), **rec)
+        agent, *_ = agent_run(recording_sf(ref_deep.DeepSF, log), SFDQN, ReplayBuffer, torch.device("cpu"))
+    log.save(os.path.join(OUT, "calls_sfdqn_alltask.npz"), _final(agent, log))
 
 
-def gen_agent_run_sequential(single_file=False):
-    """The main_sfdqn_sequential_torch.py stack end to end: reference agents/sfdqn_sequential.py
-    SFDQN + agents/buffer_sequential.py + features/deep_sequential.py DeepSF; single_file: the
-    same agent from sfdqn.py (its SFDQN, ReplayBuffer and DeepSF)."""
+def gen_call_log_sequential(single_file=False):
+    """main_sfdqn_sequential_torch.py's stack (agents/sfdqn_sequential.py + features/deep_sequential.py)
+    or the single-file sfdqn.py."""
     import contextlib
     import io
 
@@ -397,35 +520,16 @@ def gen_agent_run_sequential(single_file=False):
         from agents.buffer_sequential import ReplayBuffer
         from agents.sfdqn_sequential import SFDQN
         from features.deep_sequential import DeepSF
-
+    log = CallLog()
     with contextlib.redirect_stdout(io.StringIO()):
-        agent, tasks, test_tasks, returns = agent_run_sequential(DeepSF, SFDQN, ReplayBuffer, torch.device("cpu"))
-    sf = agent.sf
-    T = sf.n_tasks
-    tw, _ = agent.test_tasks_weights[0]
-    rec = dict(online=np_(torch.stack([flat(sf.psi[t][0][0]) for t in range(T)])),
-               target=np_(torch.stack([flat(sf.psi[t][1][0]) for t in range(T)])),
-               w=np_(torch.stack([sf.fit_w[t].weight.detach().reshape(-1).clone() for t in range(T)])),
-               gpi_counters=np.stack([np.asarray(c) for c in sf.gpi_counters]),
-               since_target=np.array(sf.updates_since_target_updated),
-               actions=np.array([a for t in tasks for a in t.actions]),
-               test_actions=np.array(test_tasks[0].actions),
-               test_w=np_(tw.weight.detach().reshape(-1)),
-               returns=np.array([float(r) for r in returns]),
-               reward_hist=np.array([float(x) for x in agent.reward_hist]),
-               cum_reward=float(agent.cum_reward), total_steps=agent.total_training_steps)
-    np.savez_compressed(os.path.join(OUT, "run_sfdqn_singlefile_agent.npz" if single_file
-                                     else "run_sfdqn_sequential_agent.npz"), **rec)
+        agent, *_ = agent_run_sequential(recording_sf(DeepSF, log), SFDQN, ReplayBuffer, torch.device("cpu"))
+    name = "calls_sfdqn_singlefile" if single_file else "calls_sfdqn_sequential"
+    log.save(os.path.join(OUT, name + ".npz"), _final(agent, log))
 
 
-def gen_agent_run_singlefile():
-    gen_agent_run_sequential(single_file=True)
-
-
-def gen_agent_run_tsf(nf=False, single_file=False):
-    """The main_tsfdqn_sequential_torch.py stack end to end: reference agents/tsfdqn_sequential.py
-    TSFDQN + agents/buffer_tsf_sequential.py + features/deep_sequential_tsf.py DeepTSF; nf: the
-    single-file tsfdqn_nf.py of main_tsfdqn_sequential_torch_nf.py (planar-flow g_i)."""
+def gen_call_log_tsf(nf=False, single_file=False):
+    """main_tsfdqn_sequential_torch.py's stack (agents/tsfdqn_sequential.py +
+    features/deep_sequential_tsf.py), the single-file tsfdqn.py, or tsfdqn_nf.py (planar flows)."""
     import contextlib
     import io
 
@@ -439,34 +543,21 @@ def gen_agent_run_tsf(nf=False, single_file=False):
         from agents.buffer_tsf_sequential import ReplayBuffer
         from agents.tsfdqn_sequential import TSFDQN
         from features.deep_sequential_tsf import DeepTSF
+    log = CallLog()
     with contextlib.redirect_stdout(io.StringIO()):
-        agent, tasks, test_tasks, returns = agent_run_tsf(DeepTSF, TSFDQN, ReplayBuffer, torch.device("cpu"), nf=nf)
-    sf = agent.sf
-    T = sf.n_tasks
-    tw, _, _ = agent.test_tasks_weights[0]
-    rec = dict(online=np_(torch.stack([flat(sf.psi[t][0][0]) for t in range(T)])),
-               target=np_(torch.stack([flat(sf.psi[t][1][0]) for t in range(T)])),
-               w=np_(torch.stack([sf.fit_w[t].weight.detach().reshape(-1).clone() for t in range(T)])),
-               g=np_(torch.stack([flat(agent.g_functions[t]) for t in range(T)])),
-               h=np_(flat(agent.h_function)),
-               gpi_counters=np.stack([np.asarray(c) for c in sf.gpi_counters]),
-               since_target=np.array(sf.updates_since_target_updated),
-               actions=np.array([a for t in tasks for a in t.actions]),
-               test_actions=np.array(test_tasks[0].actions),
-               test_w=np_(tw.weight.detach().reshape(-1)),
-               omegas=np_(agent.omegas[0].detach().reshape(-1)),
-               returns=np.array([float(r) for r in returns]),
-               cum_reward=float(agent.cum_reward), total_steps=agent.total_training_steps)
-    name = "run_tsfdqn_nf_agent" if nf else "run_tsfdqn_singlefile_agent" if single_file else "run_tsfdqn_sequential_agent"
-    np.savez_compressed(os.path.join(OUT, name + ".npz"), **rec)
+        agent, *_ = agent_run_tsf(recording_sf(DeepTSF, log), recording_tsf_agent(TSFDQN, log), ReplayBuffer,
+                                  torch.device("cpu"), nf=nf)
+    name = "calls_tsfdqn_nf" if nf else "calls_tsfdqn_singlefile" if single_file else "calls_tsfdqn_sequential"
+    log.save(os.path.join(OUT, name + ".npz"), _final(agent, log))
 
 
-def gen_agent_run_tsf_singlefile():
-    gen_agent_run_tsf(single_file=True)
-
-
-def gen_agent_run_tsf_nf():
-    gen_agent_run_tsf(nf=True)
+def gen_call_logs():
+    gen_call_log_alltask()
+    gen_call_log_sequential()
+    gen_call_log_sequential(single_file=True)
+    gen_call_log_tsf()
+    gen_call_log_tsf(single_file=True)
+    gen_call_log_tsf(nf=True)
 
 
 def main():
@@ -485,12 +576,7 @@ def main():
     gen_deep_alltask(SHAPES["reacher17"], 4, 6, 3)
     gen_tsf("tsf", ref_tsfdqn, SHAPES["hopper11"], 3, 8, 0)
     gen_tsf("tsf_nf", ref_tsfdqn_nf, SHAPES["hopper11"], 3, 6, 3)
-    gen_agent_run()
-    gen_agent_run_sequential()
-    gen_agent_run_singlefile()
-    gen_agent_run_tsf()
-    gen_agent_run_tsf_nf()
-    gen_agent_run_tsf_singlefile()
+    gen_call_logs()
     print("golden vectors written to", os.path.abspath(OUT))
 
 
