@@ -2033,6 +2033,22 @@ __device__ __forceinline__ int gate_wait(const GateArgs& g) {
   return ok;
 }
 
+// Queue-sharing probe (runner setup): k_qwait spins, bounded, on a device word that k_qset --
+// launched afterwards on another stream -- sets.  If both streams feed the same hardware queue
+// the set only runs after the wait gave up, and `seen` stays 0.
+__global__ void k_qwait(const int* word, int* seen, long long timeout) {
+  if (threadIdx.x != 0) return;
+  const long long t0 = wall_clock64();
+  int s = 0;
+  while (!(s = __hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) && wall_clock64() - t0 < timeout)
+    __builtin_amdgcn_s_sleep(8);
+  __hip_atomic_store(seen, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void k_qset(int* word) {
+  if (threadIdx.x == 0) __hip_atomic_store(word, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ __launch_bounds__(256) void k_gate(GateArgs g) {
   __shared__ int ok;
   PROBE_T(pt0);

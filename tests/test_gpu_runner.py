@@ -384,3 +384,47 @@ def test_runner_c1_cartpole_shape(schedule):
         rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-3, atol=1e-6)
     loop.close()
     eng.close()
+
+
+def test_runner_host_rounds_with_every_queue_shared():
+    """Host rounds run on the runner's side stream while the next pre-launched step spins at its
+    gate on the handle's stream.  With more streams alive than hardware queues
+    (GPU_MAX_HW_QUEUES) the runtime hands new streams existing queues; the runner must not pick
+    a side stream on the gate's queue (the rounds would wait behind the gate until it times out,
+    which cancelled bench.py's sharded run after the all-task run).  12 extra streams first, then
+    the forced-host-round runner of the test above."""
+    import ctypes
+
+    from sfx.runner import NativeEnvLoop
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    extra = []
+    for _ in range(12):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreateWithFlags(ctypes.byref(s), 1) == 0
+        extra.append(s)
+    try:
+        spec = R.Spec(17, 32, 7, 8, ("relu", "relu"))
+        T, ev, alpha, n = 4, 5, 0.05, 20
+        for rep in range(3):  # a fresh runner (and side stream) each time
+            eng, st = make(spec, T, ev, seed=rep)
+            eng.debug_force_rerun(2)
+            loop = NativeEnvLoop(eng, batch=8, capacity=100, gamma=0.9, epsilon=0.3, alpha_w=alpha, episode_len=9,
+                                 seed=11 + rep)
+            loop.prefill(8)
+            loop.set_task(rep % T)
+            loop.record(n)
+            loop.run(n)
+            stats = loop.stats()
+            assert stats["host_round_steps"] == n and stats["retried"] == 0, stats
+            replay_with_oracle(st, spec, recs := loop.records(), alpha, ev, loop.action())
+            check_state(eng, st, T, len(recs))
+            loop.close()
+            eng.close()
+            s = ctypes.c_void_p()  # and one more stream in between
+            assert hip.hipStreamCreateWithFlags(ctypes.byref(s), 1) == 0
+            extra.append(s)
+    finally:
+        torch.cuda.synchronize()
+        for s in extra:
+            hip.hipStreamDestroy(s)
