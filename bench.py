@@ -125,6 +125,17 @@ def algorithmic_step_bytes(T: int, U: int, P: int, weight_bytes: int) -> float:
     return 2.0 * wb * T * P + U * P * (3 * wb + 28)
 
 
+def skippable_head_bytes(sh, M: int) -> float:
+    """Algorithmic bytes (fp32, the formulas of sfx.hip run_bwd) of one head's backward in one
+    speculative round that a skipped policy does not move: dX of layers NL-1 .. 1 and dW + Adam of
+    every layer."""
+    n_s, H, A, d, nh = sh["n_s"], sh["H"], sh["A"], sh["d"], len(sh["acts"])
+    layers = [(H, n_s)] + [(H, H)] * nh + [(A * d, H)]  # (N, K) per Linear
+    dx = sum(4.0 * (N * K + M * N + 2.0 * M * K) for N, K in layers[1:])
+    dw = sum(24.0 * (N * K + N) + 4.0 * (M * N + M * K) for N, K in layers)
+    return dx + dw
+
+
 def cpu_info() -> dict:
     """Host CPU model and physical core count (unique (package, core) pairs of /proc/cpuinfo)."""
     model, cores = None, set()
@@ -470,11 +481,13 @@ def main():
 
     # live per-kernel durations (HIP events around each launch) for the roofline figure
     eng.prof_reset()
+    skip0 = eng.skip_stats()
     eng.prof_enable(True)
     loop.run(args.prof_steps)
     stats = eng.prof_collect()
     eng.prof_enable(False)
     eng.prof_reset()
+    prof_skip = {k: v - skip0[k] for k, v in eng.skip_stats().items()}
 
     sharded = replicas = None
     layout = "single" if world == 1 else f"replica{world}"
@@ -514,6 +527,11 @@ def main():
         alg = algorithmic_step_bytes(T, U, P, 2)
         alg32 = algorithmic_step_bytes(T, U, P, 4)
         launched = sum(v[2] for v in stats.values()) / max(args.prof_steps, 1)
+        # the launched-bytes sum counts every round's backward + Adam of every head; a policy that
+        # repeats the previous round's next actions skips them on the device (BwdArgs::skip), so
+        # those bytes are never moved: subtract them (device counters over the same steps)
+        skipped = prof_skip["policies_skipped"] * skippable_head_bytes(sh, B) / max(args.prof_steps, 1)
+        launched_moved = launched - skipped
         # each GPU runs every env step of the sharded stream (its T heads); replicas split the total
         per_gpu_rate = value if layout.startswith("shard") else value / world
         roofline["per_step"] = {
@@ -525,8 +543,11 @@ def main():
             "fp32_achieved": round(alg32 * per_gpu_rate / 1e9, 2),
             "fp32_frac": round(alg32 * per_gpu_rate / 1e9 / HBM_PEAK_GBS, 5),
             "launched_bytes_per_env_step": round(launched),
-            "launched_over_fp32_algorithmic": round(launched / alg32, 3), "unit": "GB/s"}
+            "skipped_policy_rounds_per_env_step": round(prof_skip["policies_skipped"] / max(args.prof_steps, 1), 3),
+            "moved_bytes_per_env_step": round(launched_moved),
+            "moved_over_fp32_algorithmic": round(launched_moved / alg32, 3), "unit": "GB/s"}
         spec_stats = eng.step_stats()
+        spec_stats.update(eng.skip_stats())
         if native:
             spec_stats.update(loop.stats())
         cpu = None

@@ -158,7 +158,10 @@ struct sfx_handle {
   int* dcancel = nullptr;  // Geo::cancel: written by runner gates, 0 otherwise
   AdamC* adamc = nullptr;
   float *act = nullptr, *dz = nullptr, *rowloss = nullptr;
-  int64_t* spec_next = nullptr;
+  int64_t* spec_next = nullptr;  // [2][T][MMAX]: next actions of even / odd speculative rounds
+  int* skip = nullptr;            // [T]: the policy repeats the previous round (BwdArgs::skip)
+  unsigned long long* skipc = nullptr;  // [0] policies checked, [1] skipped (rounds >= 1)
+  bool skip_rounds = true;        // SFX_SKIP=0: every round recomputes every policy
   StepOut* dout = nullptr;  // device
   // set by the runner while it captures a step: the final k_ver (with action selection)
   // publishes to pub_res instead of a separate k_publish; pub_folded reports that it did
@@ -409,6 +412,9 @@ struct TdgSpec {
   const int* xi_src = nullptr;
   int* xi_dst = nullptr;
   int xi_copy = 0, xi_n = 0;
+  // rounds r >= 1: round r-1's next actions; policies that repeat them skip (BwdArgs::tdg_prev)
+  const int64_t* prev = nullptr;
+  bool skip = false;
 };
 
 // 0: K2 as its own launch; 1: fused, d <= 8; 2: fused, d <= 16 (see tdg_rows)
@@ -458,6 +464,11 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.tdg_poloff = td.poloff;
   A.flag = td.flag;
   A.flag_value = h->T;
+  if (fuse && td.skip && !h->rec && M <= 32) {  // k_round's recorded launches never skip
+    A.tdg_prev = td.prev;
+    A.skip = h->skip;
+    A.skipc = h->skipc;
+  }
   const int tail_at = fuse ? 1 : 0;  // launch index of the loss tail (needs every row's loss)
   const bool need_tail = losses || r || !fuse;  // losses, a w step or the Adam step bump
   const double tdg_bytes = 4.0 * nhead * M * ((td.use_gpi ? h->T : 1) * h->O + 2.0 * h->O + 2.0 * h->d + 4);
@@ -599,14 +610,14 @@ int run_gpi(sfx_handle* h, const GpiArgs& A) {
   return SFX_OK;
 }
 
-int run_ver(sfx_handle* h, int M, int npol, bool sel, int post, const GpiArgs& g) {
+int run_ver(sfx_handle* h, int M, int npol, bool sel, int post, const GpiArgs& g, const int64_t* spec) {
   VerArgs V{};
   V.M = M;
   V.post = post;
   V.npol = npol;
   V.sel = sel ? 1 : 0;
   V.spec_stride = MMAX;
-  V.spec_next = h->spec_next;
+  V.spec_next = spec;
   V.flag = &h->dout->flag;
   V.g = g;
   const int TA = h->T * h->A;
@@ -671,7 +682,7 @@ void free_all(sfx_handle* h) {
   }
   for (hipEvent_t e : h->prof_pool) (void)hipEventDestroy(e);
   for (void* p : {(void*)h->online, (void*)h->target, (void*)h->am, (void*)h->av, (void*)h->w, (void*)h->wm,
-                  (void*)h->wv, (void*)h->step, (void*)h->dcancel, (void*)h->adamc, (void*)h->round_ctr, (void*)h->act, (void*)h->dz, (void*)h->rowloss, (void*)h->spec_next,
+                  (void*)h->wv, (void*)h->step, (void*)h->dcancel, (void*)h->adamc, (void*)h->round_ctr, (void*)h->act, (void*)h->dz, (void*)h->rowloss, (void*)h->spec_next, (void*)h->skip, (void*)h->skipc,
                   (void*)h->dout, (void*)h->dxpart, (void*)h->dxctr})
     if (p) (void)hipFree(p);
   if (h->hout) (void)hipHostFree(h->hout);
@@ -683,6 +694,8 @@ void free_all(sfx_handle* h) {
 }
 
 inline int round_role(int r) { return (r & 1) ? R_V2 : R_V; }
+// next actions of speculative round r (two buffers: round r reads round r-1's while it writes)
+inline int64_t* spec_buf(sfx_handle* h, int r) { return h->spec_next + (size_t)(r & 1) * h->T * MMAX; }
 
 // One speculative round r of the all-task update: every policy takes its GPI next actions
 // with heads t < i seen through role `guess` (round 0: the pre-step heads), every head
@@ -698,9 +711,11 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
   td.guess = guess;
   td.a = p.a;
   td.gamma = p.gamma;
-  td.next = h->spec_next;
+  td.next = spec_buf(h, r);
   td.next_stride = MMAX;
   td.flag = &h->dout->flag;
+  td.prev = r > 0 ? spec_buf(h, r - 1) : nullptr;
+  td.skip = h->skip_rounds;
   BwdExtra bx;
   bx.inc_step = r == 0 ? 1 : 0;  // later rounds redo the same optimizer step
   const bool want_sel = p.sel && final;
@@ -756,7 +771,8 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
   const bool verify = p.use_gpi != 0;
   if (verify || sel)
     RC(run_ver(h, B, verify ? T : 1, sel, out,
-               gpi_args(out, B, 0, wsel, nullptr, nullptr, nullptr, nullptr, h->dout->sel, p.task, p.sel_use_gpi, 1)));
+               gpi_args(out, B, 0, wsel, nullptr, nullptr, nullptr, nullptr, h->dout->sel, p.task, p.sel_use_gpi, 1),
+               spec_buf(h, r)));
   if (p.sel && !bx.fuse_v0) {  // selection through the plain forward path
     RC(run_fwd(h, {{R_A, P_NEW, 1, 0, T}}, 1, p.s_next, nullptr));
     RC(run_gpi(h, gpi_args(R_A, 0, 0, wsel, nullptr, nullptr, nullptr, nullptr, h->dout->sel, p.task, p.sel_use_gpi,
@@ -891,6 +907,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->shard_qa = !(eqa && eqa[0] == '0');
   const char* edw = std::getenv("SFX_DW_WIDE");
   h->dw_wide = edw && edw[0] == '1';  // opt-in
+  const char* esk = std::getenv("SFX_SKIP");
+  h->skip_rounds = !(esk && esk[0] == '0');
   int off = 0, ptorch = 0;
   for (int l = 0; l < h->NL; ++l) {
     LayerGeo Lr{};
@@ -958,7 +976,9 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   alloc((void**)&h->act, sizeof(float) * (size_t)NROLE * T * h->actSize);
   alloc((void**)&h->dz, sizeof(float) * (size_t)T * h->actSize);
   alloc((void**)&h->rowloss, sizeof(float) * (size_t)T * MMAX);
-  alloc((void**)&h->spec_next, sizeof(int64_t) * (size_t)T * MMAX);
+  alloc((void**)&h->spec_next, sizeof(int64_t) * 2 * (size_t)T * MMAX);
+  alloc((void**)&h->skip, sizeof(int) * (size_t)T);
+  alloc((void**)&h->skipc, 64);
   alloc((void**)&h->dout, sizeof(StepOut));
   if (rc == SFX_OK && hipHostMalloc((void**)&h->hout, sizeof(StepOut), hipHostMallocDefault) != hipSuccess) {
     g_err = "hipHostMalloc failed";
@@ -1245,6 +1265,17 @@ int sfx_step_stats(sfx_t h, long long* steps, long long* fallbacks, long long* r
   if (steps) *steps = h->steps_spec;
   if (fallbacks) *fallbacks = h->steps_fallback;
   if (rerun_policies) *rerun_policies = h->policies_rerun;
+  return SFX_OK;
+}
+
+int sfx_skip_stats(sfx_t h, long long* checked, long long* skipped, int reset) {
+  if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
+  unsigned long long c[2] = {0, 0};
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(c, h->skipc, sizeof(c), hipMemcpyDeviceToHost));
+  if (checked) *checked = (long long)c[0];
+  if (skipped) *skipped = (long long)c[1];
+  if (reset) HIPCHK(hipMemset(h->skipc, 0, sizeof(c)));
   return SFX_OK;
 }
 

@@ -866,6 +866,16 @@ struct BwdArgs {
   const int* xi_src;
   int* xi_dst;
   int xi_copy, xi_n;
+  // speculative rounds r >= 1 (fused TD launch only): tdg_prev = round r-1's next actions
+  // [head][MMAX].  A policy whose next actions all equal them repeats round r-1's update bit
+  // for bit -- same targets, same gradients, same Adam step from the same read slot into the same
+  // write slot -- so its tiles skip: the TD launch sets skip[head] (0 or 1, every round: round 0
+  // has no tdg_prev and clears it) and the later launches of the round test it.  The post-update
+  // forward still runs for every head (reading the write slot, which already holds the result).
+  // skipc: [0] policies checked, [1] policies skipped (statistics).
+  const int64_t* tdg_prev;
+  int* skip;
+  unsigned long long* skipc;
 };
 
 __device__ __forceinline__ const float* layer_input(const Geo& G, const BwdArgs& A, int head, int xOff) {
@@ -887,8 +897,10 @@ struct TdgSmem {
   float dz[32 * TDG_ROWS_O];
 };
 
+// Returns 1 when the policy repeats the previous round's update (BwdArgs::tdg_prev): then the
+// output gradient and the row losses are left as that round wrote them.
 template <int VMAX, int U, bool C>
-__device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pub, TdgSmem& sm) {
+__device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pub, TdgSmem& sm) {
   const int tid = threadIdx.x, T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, M = A.M;
   const int nb = M - m0 < 32 ? M - m0 : 32;
   const bool xm = A.tdg_xmax != nullptr;
@@ -977,6 +989,8 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
   }
   __syncthreads();
   // ---- stage D: first argmax over actions
+  const int64_t* prev = A.tdg_prev ? A.tdg_prev + (size_t)(pol - A.head0) * A.tdg_next_stride + m0 : nullptr;
+  int differs = prev == nullptr || m0 != 0 || nb != M;  // skipping needs every row of the policy
   for (int bl = tid; bl < nb; bl += 256) {
     const float* mb = sm.m + bl * Aa;
     int am = 0;
@@ -987,9 +1001,18 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
         am = a;
       }
     sm.n[bl] = am;
+    if (prev && prev[bl] != am) differs = 1;
     if (pub && A.tdg_next) A.tdg_next[(size_t)(pol - A.head0) * A.tdg_next_stride + m0 + bl] = am;
   }
-  __syncthreads();
+  const int same = !__syncthreads_or(differs);
+  if (pub && A.skip && tid == 0) {
+    A.skip[pol] = same;
+    if (A.skipc && prev) {
+      atomicAdd(A.skipc, 1ull);
+      if (same) atomicAdd(A.skipc + 1, 1ull);
+    }
+  }
+  if (same) return 1;
   PROBE_AT(4);
   // ---- stage E: output gradient rows -- nonzero only at the taken action: one thread per
   // (row, feature) of it -- and the rows' squared errors (into sm.q, free after stage C)
@@ -1028,6 +1051,7 @@ __device__ void tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool p
       G.rowloss[(long long)pol * MMAX + m0 + bl] = sacc;
     }
   }
+  return 0;
 }
 
 template <bool TDG, int VMAX = 2, int U = 8, bool C = false>
@@ -1088,7 +1112,7 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       bw[j] = (j >= j0 && j < j0 + jw && okk && nb + j < N) ? W[(size_t)(nb + j) * K + kk] : 0.f;
-    tdg_rows<VMAX, U, C>(G, A, head, m0, tile % ntk == 0, sm);
+    if (tdg_rows<VMAX, U, C>(G, A, head, m0, tile % ntk == 0, sm)) return;  // repeats round r-1 (block-uniform)
     const float* da = sm.dz + (size_t)r * N + nb;
     const float* db = sm.dz + (size_t)(16 + r) * N + nb;
 #pragma unroll
@@ -1204,6 +1228,27 @@ __device__ void fused_v0(const Geo& G, const BwdArgs& A, const RoleGeo& L, int h
       }
     }
   }
+}
+
+// A layer-0 dW tile of a policy that repeats the previous round (BwdArgs::skip): no gradient,
+// no Adam -- the write slot already holds this round's weights -- only the fused post-update
+// forward of its 32 columns, from those weights (the bits role_dw would have staged).
+// Fused layers have K <= KFUSE <= 64: one k-tile, so tile = column tile.
+__device__ void role_v0_only(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile) {
+  const int N = L.N, K = L.K, M = A.M, tid = threadIdx.x, nbase = tile * 32;
+  const float* Pw = G.online + G.slot_off(rslot(A.mask, head) ^ 1, head);
+  __shared__ float sW[32 * KFUSE];
+  __shared__ float sB[32];
+  __shared__ float sX[VFUSE];
+  const FDiv fK = fdiv(K);
+  for (int j = tid; j < 32 * K; j += 256) {
+    const int nl = j / fK, k = j - nl * K;
+    sW[nl * KFUSE + k] = nbase + nl < N ? Pw[L.wOff + (size_t)(nbase + nl) * K + k] : 0.f;
+  }
+  if (tid < 32) sB[tid] = nbase + tid < N ? Pw[L.bOff + nbase + tid] : 0.f;
+  const int nxs = A.vM * K;
+  for (int j = tid; j < nxs; j += 256) sX[j] = j < M * K ? A.v_x[j] : A.v_xn[j - M * K];
+  fused_v0<false>(G, A, L, head, nbase, sW, sB, sX);
 }
 
 template <bool C = false>
@@ -1538,13 +1583,16 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
     head += A.head0;
   }
   PROBE_MARKA();
+  const bool skip = A.skip && __builtin_nontemporal_load(A.skip + head) != 0;  // repeats round r-1
   if (bx < A.na) {
+    if (skip) return;
     role_dx<false>(G, A, head, bx, red);
     PROBE_REC(4, pt0);
     return;
   }
   bx -= A.na;
   if (bx < A.nb) {
+    if (skip) return;
     if (A.rb.nw == 2)
       role_dw_wide(G, A, head, A.rb, bx);
     else
@@ -1554,6 +1602,10 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
   }
   bx -= A.nb;
   if (bx < A.nc) {
+    if (skip) {
+      if (A.fuse_v0) role_v0_only(G, A, head, A.rc, bx);
+      return;
+    }
     role_dw(G, A, head, A.rc, bx, A.fuse_v0 != 0);
     PROBE_REC(6, pt0);
     return;

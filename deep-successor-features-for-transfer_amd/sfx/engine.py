@@ -260,6 +260,13 @@ class SFEngine:
         check(lib.sfx_step_stats(self._h, C.byref(s), C.byref(f), C.byref(r), C.byref(n)), "sfx_step_stats")
         return {"steps": s.value, "host_round_steps": f.value, "unverified_policies": r.value, "rounds": n.value}
 
+    def skip_stats(self, reset: bool = False):
+        """Policies checked / skipped in speculative rounds r >= 1 (their next actions repeated
+        round r-1's, so their update would have too)."""
+        c, s = C.c_longlong(), C.c_longlong()
+        check(lib.sfx_skip_stats(self._h, C.byref(c), C.byref(s), int(reset)), "sfx_skip_stats")
+        return {"policies_checked": c.value, "policies_skipped": s.value}
+
     def lms(self, t: int, phi, r, alpha: float):
         phi = self._f(phi, (-1,))
         r = self._f(r, (1,))

@@ -166,6 +166,10 @@ int sfx_set_spec_rounds(sfx_t h, int rounds);
 /* Counters of fused steps: total, those that needed host-issued rounds, the policies
  * still unverified after the device rounds, and all rounds run. */
 int sfx_step_stats(sfx_t h, long long* steps, long long* fallbacks, long long* rerun_policies, long long* rounds);
+/* Speculative rounds r >= 1 skip a policy whose next actions repeat round r-1's (its update
+ * would repeat bit for bit): policies checked and skipped so far, counted on the device
+ * (synchronises the handle's stream); reset != 0 zeroes the counters afterwards. */
+int sfx_skip_stats(sfx_t h, long long* checked, long long* skipped, int reset);
 
 /* LMS reward fit SF.update_reward (features/successor.py:164-167) on w_t:
  * w <- w + alpha (r - φ·w) φ ;  phi_dev [d], r_dev [1]. */

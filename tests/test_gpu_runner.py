@@ -428,3 +428,42 @@ def test_runner_host_rounds_with_every_queue_shared():
         torch.cuda.synchronize()
         for s in extra:
             hip.hipStreamDestroy(s)
+
+
+@pytest.mark.parametrize("spec_rounds,force", [(2, -1), (2, 1), (3, -1)])
+def test_round_skip_is_bit_exact(spec_rounds, force, monkeypatch):
+    """Speculative rounds r >= 1 skip the backward and Adam of a policy whose next actions repeat
+    round r-1's (BwdArgs::skip).  The skipped update would have repeated round r-1's bit for bit,
+    so the heads, the moments and every action must be IDENTICAL with skipping off (SFX_SKIP=0)
+    -- including steps finished by host rounds (force) -- and the device counters must show
+    skipped policies."""
+    from sfx.runner import NativeEnvLoop
+
+    spec = R.Spec(17, 64, 7, 8, ("relu", "relu"))
+    T, ev, n = 6, 9, 30
+    out = {}
+    for skip in ("1", "0"):
+        monkeypatch.setenv("SFX_SKIP", skip)
+        eng, _ = make(spec, T, ev, max_batch=32)
+        eng.set_spec_rounds(spec_rounds)
+        if force >= 0:
+            eng.debug_force_rerun(force)
+        loop = NativeEnvLoop(eng, batch=32, capacity=300, gamma=0.9, epsilon=0.2, alpha_w=0.05, episode_len=11, seed=9)
+        loop.prefill(40)
+        loop.set_task(2)
+        loop.record(n)
+        loop.run(n)
+        recs = loop.records()
+        heads = torch.stack([eng.get_head(t, 0) for t in range(T)])
+        moms = [eng.get_adam(t) for t in range(T)]
+        out[skip] = (heads, moms, [(r["c"], r["a_greedy"]) for r in recs], loop.action(), eng.skip_stats())
+        loop.close()
+        eng.close()
+    h1, m1, a1, f1, s1 = out["1"]
+    h0, m0, a0, f0, s0 = out["0"]
+    assert a1 == a0 and f1 == f0
+    assert torch.equal(h1, h0)
+    for (ma, va, sa), (mb, vb, sb) in zip(m1, m0):
+        assert torch.equal(ma, mb) and torch.equal(va, vb) and sa == sb
+    assert s0["policies_checked"] == 0
+    assert s1["policies_checked"] >= n * (spec_rounds - 1) * T // 2 and s1["policies_skipped"] > 0, s1
