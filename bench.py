@@ -126,14 +126,16 @@ def algorithmic_step_bytes(T: int, U: int, P: int, weight_bytes: int) -> float:
 
 
 def skippable_head_bytes(sh, M: int) -> float:
-    """Algorithmic bytes (fp32, the formulas of sfx.hip run_bwd) of one head's backward in one
-    speculative round that a skipped policy does not move: dX of layers NL-1 .. 1 and dW + Adam of
-    every layer."""
+    """Algorithmic bytes (fp32, the formulas of sfx.hip run_bwd / run_fwd) of one head's work in one
+    speculative round that a skipped policy does not move: dX of layers NL-1 .. 1, dW + Adam of
+    every layer, the post-update forward of every layer."""
     n_s, H, A, d, nh = sh["n_s"], sh["H"], sh["A"], sh["d"], len(sh["acts"])
     layers = [(H, n_s)] + [(H, H)] * nh + [(A * d, H)]  # (N, K) per Linear
     dx = sum(4.0 * (N * K + M * N + 2.0 * M * K) for N, K in layers[1:])
     dw = sum(24.0 * (N * K + N) + 4.0 * (M * N + M * K) for N, K in layers)
-    return dx + dw
+    # and its post-update forward over the S1 rows ++ s_next (the head keeps last round's values)
+    fw = sum(4.0 * (N * K + N + (M + 1) * K + (M + 1) * N) for N, K in layers)
+    return dx + dw + fw
 
 
 def cpu_info() -> dict:

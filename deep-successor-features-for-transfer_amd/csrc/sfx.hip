@@ -285,6 +285,7 @@ struct FwdExtra {
   // sharded step: GPI maxima accumulated by the last layer's tiles of group role qa_role
   int qa_role = -1, qa_M = 0, qa_row = -1, qa_task = 0, qa_use_gpi = 1;
   int *qa_all = nullptr, *qa_ge = nullptr, *qa_lt = nullptr, *qa_sel = nullptr;
+  const int* skip = nullptr;  // post-update forward of rounds r >= 1 (FwdArgs::skip; one group)
 };
 
 int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const float* xa, const float* xb,
@@ -296,6 +297,9 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
   F.mask = h->mask;
   F.lms_head = -1;
   F.qa_role = -1;
+  F.skip = ex.skip;
+  if (ex.skip && (groups.size() != 1 || ex.flag || ex.lms_head >= 0 || ex.qa_role >= 0 || h->rec))
+    SFX_FAIL(SFX_E_STATE, "run_fwd: head skipping needs one group and no LMS / flag / maxima");
   int ninst = 0;
   bool uniform = true;  // every group covers heads 0..T-1: XCD-aware grid possible
   FwdGroup* slots[4] = {&F.g0, &F.g1, &F.g2, &F.g3};
@@ -438,6 +442,8 @@ struct BwdExtra {
   int vRole = R_V;
   const float* v_x = nullptr;
   const float* v_xn = nullptr;
+  bool skip_fwd = false;      // in: the caller skips the post-update forward of skipped heads
+  bool* skip_armed = nullptr; // out: this round's launches decide and honour BwdArgs::skip
 };
 
 bool can_fuse_v0(const sfx_handle* h, int vM) { return h->fuse_v0 && h->L[0].K <= KFUSE && vM * h->L[0].K <= VFUSE; }
@@ -464,11 +470,14 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.tdg_poloff = td.poloff;
   A.flag = td.flag;
   A.flag_value = h->T;
-  if (fuse && td.skip && !h->rec && M <= 32) {  // k_round's recorded launches never skip
+  const bool armed = fuse && td.skip && !h->rec && M <= 32;  // k_round's recorded launches never skip
+  if (armed) {
     A.tdg_prev = td.prev;
     A.skip = h->skip;
     A.skipc = h->skipc;
+    A.skip_v0 = ex.skip_fwd ? 1 : 0;
   }
+  if (ex.skip_armed) *ex.skip_armed = armed;
   const int tail_at = fuse ? 1 : 0;  // launch index of the loss tail (needs every row's loss)
   const bool need_tail = losses || r || !fuse;  // losses, a w step or the Adam step bump
   const double tdg_bytes = 4.0 * nhead * M * ((td.use_gpi ? h->T : 1) * h->O + 2.0 * h->O + 2.0 * h->d + 4);
@@ -693,7 +702,11 @@ void free_all(sfx_handle* h) {
   if (h->cap) (void)hipStreamDestroy(h->cap);
 }
 
-inline int round_role(int r) { return (r & 1) ? R_V2 : R_V; }
+// Role of round r's post-update forward.  The launches of a round run in stream order, so every
+// round can write the same role (round r's TD launch has read round r-1's values before its
+// forward overwrites them) -- which lets a head whose policy repeats round r-1 skip its forward.
+// k_round's heads progress independently inside one launch: there rounds alternate two roles.
+inline int round_role(const sfx_handle* h, int r) { return h->use_round && (r & 1) ? R_V2 : R_V; }
 // next actions of speculative round r (two buffers: round r reads round r-1's while it writes)
 inline int64_t* spec_buf(sfx_handle* h, int r) { return h->spec_next + (size_t)(r & 1) * h->T * MMAX; }
 
@@ -704,7 +717,7 @@ inline int64_t* spec_buf(sfx_handle* h, int r) { return h->spec_next + (size_t)(
 // were wrong; action selection): an earlier round's verdict would be overwritten unread.
 int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final) {
   const int T = h->T, B = p.B;
-  const int guess = r == 0 ? R_S1 : round_role(r - 1), out = round_role(r);
+  const int guess = r == 0 ? R_S1 : round_role(h, r - 1), out = round_role(h, r);
   const float* wsel = h->w + (size_t)p.task * h->dpad;
   TdgSpec td;
   td.use_gpi = p.use_gpi;
@@ -718,7 +731,12 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
   td.skip = h->skip_rounds;
   BwdExtra bx;
   bx.inc_step = r == 0 ? 1 : 0;  // later rounds redo the same optimizer step
-  const bool want_sel = p.sel && final;
+  bool armed = false;
+  bx.skip_fwd = !h->use_round;  // one role for every round (round_role)
+  bx.skip_armed = &armed;
+  // the s_next row rides along in every round that a later round may skip heads after: a skipped
+  // head's row must already be in the role when the final round's selection reads it
+  const bool want_sel = p.sel && (final || bx.skip_fwd);
   bx.fuse_v0 = can_fuse_v0(h, B + 1);
   bx.vRole = out;
   bx.v_x = p.S1;
@@ -762,6 +780,7 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
   } else if (bx.fuse_v0) {
     FwdExtra vx;
     vx.l0 = 1;
+    vx.skip = armed && r > 0 && bx.skip_fwd ? h->skip : nullptr;
     RC(run_fwd(h, {{out, P_NEW, 0, 0, T}}, vM, nullptr, nullptr, vx));
   } else {
     RC(run_fwd(h, {{out, P_NEW, 2, 0, T}}, B, p.S1, p.S1));

@@ -351,6 +351,9 @@ struct FwdArgs {
   int* qa_lt;    // max over local heads with global index < policy (post-update rounds)
   int* qa_sel;   // [Tg][A] selection table of row qa_row with w of qa_task (null: none)
   int qa_row, qa_task, qa_use_gpi, pad3_;
+  // post-update forward of speculative rounds r >= 1: heads whose policy repeats round r-1
+  // (BwdArgs::skip) keep the values that round left in the role -- their tiles exit at once
+  const int* skip;
 };
 
 // The sharded step's GPI maxima, fused into the forward of the ψ output layer: a 32 x 16 tile
@@ -627,6 +630,11 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
   }
   bool qa = false;
   int head = 0;
+  if (F.skip) {  // single group: instance y is the head
+    int yy = y;
+    const FwdGroup grp = fwd_group(F, yy);
+    if (__builtin_nontemporal_load(F.skip + grp.head0 + yy)) return;
+  }
   if (F.qa_role >= 0) {  // the sharded step's maxima from this tile (last layer, group role qa_role)
     int yy = y;
     const FwdGroup grp = fwd_group(F, yy);
@@ -653,6 +661,7 @@ __global__ __launch_bounds__(256) void k_fwd_gemv(Geo G, FwdArgs F) {
   int y = blockIdx.y;
   const FwdGroup grp = fwd_group(F, y);
   const int head = grp.head0 + y;
+  if (F.skip && __builtin_nontemporal_load(F.skip + head)) return;
   const int M = F.M, N = F.N, K = F.K;
   const float* P = grp.which == P_TARGET ? G.target + (long long)head * G.P
                                          : G.online + G.slot_off(rslot(F.mask, head) ^ (grp.which == P_NEW), head);
@@ -876,6 +885,7 @@ struct BwdArgs {
   const int64_t* tdg_prev;
   int* skip;
   unsigned long long* skipc;
+  int skip_v0, pad4_;  // skipped heads' layer-0 tiles: 1 = the post-update forward skips them too
 };
 
 __device__ __forceinline__ const float* layer_input(const Geo& G, const BwdArgs& A, int head, int xOff) {
@@ -1603,7 +1613,7 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
   bx -= A.nb;
   if (bx < A.nc) {
     if (skip) {
-      if (A.fuse_v0) role_v0_only(G, A, head, A.rc, bx);
+      if (A.fuse_v0 && !A.skip_v0) role_v0_only(G, A, head, A.rc, bx);
       return;
     }
     role_dw(G, A, head, A.rc, bx, A.fuse_v0 != 0);
