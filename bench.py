@@ -59,6 +59,8 @@ def parse():
                         "configs C3 / C5 on one GPU (TSF-DQN, active-task schedule, python host loop)")
     p.add_argument("--heads", type=int, default=None, help="source tasks (ψ heads) per GPU (8; 16 for hopper-tsf*)")
     p.add_argument("--batch", type=int, default=32)
+    p.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
+                   help="operands of the ψ forward / dX GEMMs (fp32: the reference's arithmetic, parity-tested)")
     p.add_argument("--replay", choices=["host", "device"], default="host",
                    help="replay ring on the host (north_star; the headline) or in HBM with on-device sampling "
                         "(SURVEY §8f rank 2; native loop only)")
@@ -246,6 +248,7 @@ def bench_sharded(args, world, rank, device, barrier, dist, steps=None, warmup=N
     eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
     eng.set_target_update_ev(1000)
     eng.set_spec_rounds(args.spec_rounds)
+    eng.set_precision(args.precision)
     eng.shard_setup(Tg, rank * T_loc)
     for t in range(T_loc):
         eng.load_head(t, online[rank * T_loc + t], 0)
@@ -344,10 +347,15 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
     from sfx.runner import NativeEnvLoop
 
     out = {}
-    for name, sched, K, dev in (("reacher17-active-T8-B32", "active", None, False),
-                                ("reacher17-all-T8-B32-device-replay", "all", None, True),
-                                ("hopper11-tsf-T16-B32", "tsf", 0, False),
-                                ("hopper11-tsf-nf100-T16-B32", "tsf", 100, False)):
+    # the -fp32 / -bf16 pair: the headline workload in the same 1000-step window, operands in fp32
+    # (the reference's arithmetic) and in bf16 (sfx_set_precision; not a parity mode)
+    for name, sched, K, dev, prec in (("reacher17-active-T8-B32", "active", None, False, "fp32"),
+                                      ("reacher17-all-T8-B32-device-replay", "all", None, True, "fp32"),
+                                      ("reacher17-all-T8-B32-fp32", "all", None, False, "fp32"),
+                                      ("reacher17-all-T8-B32-bf16", "all", None, False, "bf16"),
+                                      ("hopper11-tsf-T16-B32", "tsf", 0, False, "fp32"),
+                                      ("hopper11-tsf-T16-B32-bf16", "tsf", 0, False, "bf16"),
+                                      ("hopper11-tsf-nf100-T16-B32", "tsf", 100, False, "fp32")):
         sh = SHAPE if K is None else TSF_SHAPE
         T = 8 if K is None else 16
         eng = SFEngine(T, sh["n_s"], sh["H"], sh["A"], sh["d"], sh["acts"], max_batch=args.batch, device=device)
@@ -366,6 +374,7 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
         eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
         eng.set_target_update_ev(1000)
         eng.set_spec_rounds(args.spec_rounds)
+        eng.set_precision(prec)
         loop = NativeEnvLoop(eng, batch=args.batch, seed=1, schedule=sched, p_end=0.0 if K is None else 0.01,
                              device_replay=dev)
         loop.prefill(1000)
@@ -377,7 +386,7 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         out[name] = {"value": round(steps / dt, 2), "unit": "env steps/s", "ms_per_step": round(1000.0 * dt / steps, 4),
-                     "steps": steps}
+                     "steps": steps, "dtype": prec}
         loop.close()
         eng.close()
     return out
@@ -442,6 +451,7 @@ def main():
     eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
     eng.set_target_update_ev(1000)
     eng.set_spec_rounds(args.spec_rounds)
+    eng.set_precision(args.precision)
     native = args.loop == "native"
     if native:
         loop = NativeEnvLoop(eng, batch=B, seed=1 + rank, schedule=args.schedule,
@@ -563,7 +573,7 @@ def main():
                       f"env steps/sec, Hopper 16-task TSF-DQN{' + planar-flow g' if args.tsf_K else ''} (BASELINE config "
                       f"{'C5' if args.tsf_K else 'C3'}, one GPU)", "value": round(value, 2), "unit": "env steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000.0 * dt / args.steps, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
             "config": {"workload": (f"C4 layout: {T * world} Reacher tasks, {T} heads per GPU, one env stream; " if
                                     layout.startswith("shard") else "") + workload + (f" (Reacher-shape |s|=17 |a|=7 d=8, psi MLP 256x2, "
                                                f"{'all heads updated per env step: main_sfdqn_torch.py path' if args.schedule == 'all' else 'active head only: sfdqn.py path'})"

@@ -69,6 +69,7 @@ static thread_local std::string g_err;
 namespace {
 
 inline int align4(int x) { return (x + 3) & ~3; }
+inline int align8(int x) { return (x + 7) & ~7; }  // weight blocks: 16-B aligned rows of the bf16 copy too
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 struct GraphKey {
@@ -171,6 +172,11 @@ struct sfx_handle {
   bool fold_publish = true;  // SFX_FOLD_PUBLISH=0: always a separate k_publish
   // k_round (one launch per speculative round, see sfx_kernels.h); SFX_ROUND=1 turns it on
   bool use_round = false;
+  // bf16 operand mode (sfx_set_precision): bf16 copies of the online [2][T][P] / target [T][P]
+  // parameters feed the forward and dX MFMAs; fp32 master weights, moments and accumulators
+  bool bf16 = false;
+  __bf16* on16 = nullptr;
+  __bf16* tg16 = nullptr;
   unsigned* round_ctr = nullptr;  // [T] per-head arrival counters
   // split-N dX of wide layers (run_bwd): partial tiles and per-(head, tile) arrival counters
   int dxs_max = 1, dx_ntile = 1;
@@ -195,6 +201,8 @@ struct sfx_handle {
   float* am_cur(int head) const { return am + ((size_t)slot(head) * T + head) * P; }
   float* av_cur(int head) const { return av + ((size_t)slot(head) * T + head) * P; }
   float* target_of(int head) const { return target + (size_t)head * P; }
+  __bf16* on16_cur(int head) const { return on16 + ((size_t)slot(head) * T + head) * P; }
+  __bf16* tg16_of(int head) const { return tg16 + (size_t)head * P; }
 };
 
 namespace {
@@ -364,13 +372,16 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
       h->rec->bytes.push_back(by);
       h->rec->fvec = h->rec->fvec && (L.K % 64) == 0 && aligned && !l0;
     } else if (l0) {
-      launch(h, K_FWD, by, k_fwd<true, 8, true>, grid, dim3(512), h->G, F);
+      launch(h, K_FWD, by, h->bf16 ? k_fwd<true, 8, true, true> : k_fwd<true, 8, true>, grid, dim3(512), h->G, F);
     } else if (h->fwd_waves == 8) {
       const bool vec = (L.K % 32) == 0 && aligned;
-      launch(h, K_FWD, by, vec ? k_fwd<true, 8, false> : k_fwd<false, 8, false>, grid, dim3(512), h->G, F);
+      launch(h, K_FWD, by,
+             vec ? (h->bf16 ? k_fwd<true, 8, false, true> : k_fwd<true, 8, false>) : k_fwd<false, 8, false>, grid,
+             dim3(512), h->G, F);
     } else {
       const bool vec = (L.K % 64) == 0 && aligned;
-      launch(h, K_FWD, by, vec ? k_fwd<true, 4, false> : k_fwd<false, 4, false>, grid, dim3(256), h->G, F);
+      launch(h, K_FWD, by, vec ? (h->bf16 ? k_fwd<true, 4, false, true> : k_fwd<true, 4, false>) : k_fwd<false, 4, false>,
+             grid, dim3(256), h->G, F);
     }
   }
   LAUNCHCHK();
@@ -495,7 +506,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   // opt-in 64 x 64 dW tiles (role_dw_wide) for wide hidden layers when several heads share a
   // launch, which then stays within about one workgroup per CU (measured: no gain)
   auto dw_nw = [&](int l) {
-    return l >= 1 && h->dw_wide && !h->rec && nhead >= 4 && h->L[l].N >= 128 && h->L[l].K >= 64 ? 2 : 1;
+    return l >= 1 && h->dw_wide && !h->bf16 && !h->rec && nhead >= 4 && h->L[l].N >= 128 && h->L[l].K >= 64 ? 2 : 1;
   };
   auto dw_tiles = [&](int l) { return cdiv(h->L[l].N, 32 * dw_nw(l)) * cdiv(h->L[l].K, 64); };
   auto geo = [&](int l) {
@@ -561,7 +572,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     else if (A.tdg)
       launch(h, K_BWD, by, k_bwd_tdg<4, 4>, grid, dim3(256), h->G, A);
     else
-      launch(h, K_BWD, by, k_bwd, grid, dim3(256), h->G, A);
+      launch(h, K_BWD, by, h->bf16 ? k_bwd<true> : k_bwd<false>, grid, dim3(256), h->G, A);
     if (ex.hook && li == ex.hook_after && !h->rec) RC(ex.hook());
   }
   A.na = 0;
@@ -587,7 +598,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     h->rec->bytes.push_back(nhead * (dw_bytes(1) + dw_bytes(0)));
     return SFX_OK;
   }
-  launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), k_bwd,
+  launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), h->bf16 ? k_bwd<true> : k_bwd<false>,
          A.xcd ? dim3(8 * cdiv(nhead, 8) * ntile) : dim3(ntile, nhead), dim3(256), h->G, A);
   LAUNCHCHK();
   if (ex.hook && ex.hook_after >= h->NL - 1) RC(ex.hook());  // fewer launches than hook_after + 1
@@ -653,6 +664,9 @@ int maybe_sync_target(sfx_handle* h, int t) {
   if (h->since_target[t] >= h->target_update_ev) {
     HIPCHK(hipMemcpyAsync(h->target_of(t), h->online_cur(t), sizeof(float) * h->P, hipMemcpyDeviceToDevice,
                           h->stream));
+    if (h->bf16)
+      HIPCHK(hipMemcpyAsync(h->tg16_of(t), h->on16_cur(t), sizeof(__bf16) * h->P, hipMemcpyDeviceToDevice,
+                            h->stream));
     h->since_target[t] = 0;
   }
   return SFX_OK;
@@ -683,6 +697,19 @@ void unpack_head(const sfx_handle* h, const float* src, float* dst) {
 bool valid_head(const sfx_handle* h, int t) { return h && t >= 0 && t < h->T; }
 bool valid_w(const sfx_handle* h, int t) { return h && t >= 0 && t < h->Tg; }
 
+// the bf16 copy of n parameters (round to nearest even), on the handle's stream
+__global__ void k_to_bf16(const float* __restrict__ src, __bf16* __restrict__ dst, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    dst[i] = (__bf16)src[i];
+}
+
+int refresh_bf16(sfx_handle* h, const float* src, __bf16* dst, long long n) {
+  hipLaunchKernelGGL(k_to_bf16, dim3((unsigned)std::min<long long>(1024, (n + 255) / 256)), dim3(256), 0, h->stream, src,
+                     dst, n);
+  LAUNCHCHK();
+  return SFX_OK;
+}
+
 void free_all(sfx_handle* h) {
   clear_graphs(h);
   for (auto& r : h->prof_recs) {
@@ -695,6 +722,8 @@ void free_all(sfx_handle* h) {
                   (void*)h->dout, (void*)h->dxpart, (void*)h->dxctr})
     if (p) (void)hipFree(p);
   if (h->hout) (void)hipHostFree(h->hout);
+  if (h->on16) (void)hipFree(h->on16);
+  if (h->tg16) (void)hipFree(h->tg16);
   if (h->host_ar_buf) (void)hipHostFree(h->host_ar_buf);
   for (int* p : {h->xb[0], h->xb[1]})  // xge lives in xb[0]'s block
     if (p) (void)hipFree(p);
@@ -939,7 +968,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
       Lr.N = H; Lr.K = H; Lr.actOut = acts[l - 1];
     }
     Lr.actIn = l > 0 ? h->L[l - 1].actOut : ACT_NONE;
-    Lr.wOff = align4(off);
+    Lr.wOff = align8(off);
     off = Lr.wOff + Lr.N * Lr.K;
     Lr.bOff = align4(off);
     off = Lr.bOff + Lr.N;
@@ -1081,6 +1110,7 @@ int sfx_load_head(sfx_t h, int t, int which, const float* params_host) {
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipMemcpyAsync(which ? h->target_of(t) : h->online_cur(t), buf.data(), sizeof(float) * h->P,
                         hipMemcpyHostToDevice, h->stream));
+  if (h->bf16) RC(refresh_bf16(h, which ? h->target_of(t) : h->online_cur(t), which ? h->tg16_of(t) : h->on16_cur(t), h->P));
   HIPCHK(hipStreamSynchronize(h->stream));
   return SFX_OK;
 }
@@ -1271,6 +1301,32 @@ int sfx_step_finish(sfx_t h, int64_t* out_host) {
   }
   return SFX_OK;
 }
+
+int sfx_set_precision(sfx_t h, int precision) {
+  if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
+  if (precision != SFX_PREC_FP32 && precision != SFX_PREC_BF16) SFX_FAIL(SFX_E_ARG, "unknown precision");
+  const bool want = precision == SFX_PREC_BF16;
+  if (want == h->bf16) return SFX_OK;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  clear_graphs(h);
+  if (want) {
+    if (h->use_round) SFX_FAIL(SFX_E_STATE, "sfx_set_precision: bf16 operands do not run in k_round (SFX_ROUND=1)");
+    const size_t n = (size_t)h->T * h->P;
+    if (!h->on16 && hipMalloc((void**)&h->on16, sizeof(__bf16) * 2 * n) != hipSuccess)
+      SFX_FAIL(SFX_E_HIP, "hipMalloc(bf16 copy) failed");
+    if (!h->tg16 && hipMalloc((void**)&h->tg16, sizeof(__bf16) * n) != hipSuccess)
+      SFX_FAIL(SFX_E_HIP, "hipMalloc(bf16 copy) failed");
+    RC(refresh_bf16(h, h->online, h->on16, (long long)(2 * n)));
+    RC(refresh_bf16(h, h->target, h->tg16, (long long)n));
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
+  h->bf16 = want;
+  h->G.on16 = want ? h->on16 : nullptr;
+  h->G.tg16 = want ? h->tg16 : nullptr;
+  return SFX_OK;
+}
+
+int sfx_get_precision(sfx_t h) { return h ? (h->bf16 ? SFX_PREC_BF16 : SFX_PREC_FP32) : SFX_E_ARG; }
 
 int sfx_set_spec_rounds(sfx_t h, int rounds) {
   if (!h || rounds < 1) SFX_FAIL(SFX_E_ARG, "bad args");

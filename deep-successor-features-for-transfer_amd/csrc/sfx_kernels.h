@@ -106,6 +106,24 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// bf16 operand mode (sfx_set_precision): v_mfma_f32_16x16x32_bf16 -- lane l holds A[row l&15]
+// [k = 8(l>>4) + j] and B[k = 8(l>>4) + j][col l&15], j = 0..7; C as the f32 16x16x4 form.  The
+// 8 k of a lane are the KL-consecutive k the fp32 tiles already give each lane group, so a tile
+// swaps its 8 f32 k-steps for one bf16 step (the reduction order changes: not bit-exact).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ floatx4 mfma_bf16(bf16x8 a, bf16x8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8 to_bf16x8(const float* v) {  // round to nearest even
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)v[j];
+  return r;
+}
+__device__ __forceinline__ bf16x8 ld_bf16x8(const __bf16* p) {  // 16-B aligned
+  return *reinterpret_cast<const bf16x8*>(p);
+}
+
 // Loads / stores of data handed between workgroups INSIDE one launch (the round kernel,
 // k_round): C = true makes them coherent -- sc1 (L1-bypassing) dword loads and write-through
 // stores, the hand-off form of MI355X_MICROARCH.md's validated table (sc1 stores, every storing
@@ -173,6 +191,11 @@ struct Geo {
   float* rowloss;     // [T][MMAX] per-row Σ (c - t)^2 of the last TD target
   const int* cancel;  // runner steps: 1 when the step's gate cancelled it (see step_cancelled)
   int lastOff;        // offset of the last layer's output inside an activation block
+  // bf16 operand mode: bf16 copies of the online [2][T][P] and target [T][P] parameters (the
+  // fp32 ones stay the master copy; the Adam epilogue rewrites the copy of every weight it
+  // updates).  Null in fp32 mode.
+  __bf16* on16;
+  __bf16* tg16;
 
   // off: per-layer offset inside a block (passed per launch as a scalar, never indexed)
   __device__ __forceinline__ float* actp(int role, int head, int off) const {
@@ -446,9 +469,10 @@ __device__ __forceinline__ FwdGroup fwd_group(const FwdArgs& F, int& y) {
   return g;
 }
 
-template <bool VEC, int NW, bool L0, bool C>
+template <bool VEC, int NW, bool L0, bool C, bool BF = false>
 __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, int tN, int tM, float* sT = nullptr) {
   static_assert(!(L0 && C), "the in-tile layer 0 reads only inputs of earlier launches");
+  static_assert(!BF || (VEC && !C), "bf16 operands: vector tiles of plain launches");
   constexpr int KW = 256 / NW;  // K chunk of one wave per iteration (NW waves cover 256)
   constexpr int KL = KW / 4;    // consecutive k per lane (4 lane groups per MFMA k-step)
   // instance -> (group, head) by scalar selects of each field (no dynamic kernarg indexing, and
@@ -465,6 +489,12 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
   const int ma = m0 + r, mb = m0 + 16 + r, n = n0 + r;
   const bool oka = ma < M, okb = mb < M, okn = n < N;
   const float* wr = P + F.wOff + (size_t)n * K;
+  // bf16 mode: the W operand from the bf16 copy (same packing, 16-B aligned rows: wOff % 8 == 0)
+  const __bf16* wr16 = nullptr;
+  if constexpr (BF)
+    wr16 = (grp.which == P_TARGET ? G.tg16 + (long long)head * G.P
+                                  : G.on16 + G.slot_off(rslot(F.mask, head) ^ (grp.which == P_NEW), head)) +
+           F.wOff + (size_t)n * K;
   // the reducing threads fetch their bias early
   const int Lx = threadIdx.x & 63, col = n0 + (Lx & 15);
   const float bias = (threadIdx.x < 128 && col < N) ? ldc<C>(P + F.bOff + col) : 0.f;
@@ -472,12 +502,18 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
   __shared__ __align__(16) float sA[L0 ? 32 * AS : 4];
   // L0: the first K chunk of this lane's W row is requested before layer 0 is computed, so its
   // latency overlaps the in-tile layer 0 instead of following it
-  float4 wpre[VEC && L0 ? KL / 4 : 1];
-  if constexpr (VEC && L0) {
+  float4 wpre[VEC && L0 && !BF ? KL / 4 : 1];
+  bf16x8 wpre16[BF && L0 ? KL / 8 : 1];
+  if constexpr (VEC && L0 && !BF) {
     const int kb0 = wave * KW + g * KL;
 #pragma unroll
     for (int q = 0; q < KL / 4; ++q)
       wpre[q] = okn && kb0 < K ? ldc4<C>(wr + kb0 + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if constexpr (BF && L0) {
+    const int kb0 = wave * KW + g * KL;
+#pragma unroll
+    for (int q = 0; q < KL / 8; ++q) wpre16[q] = okn && kb0 < K ? ld_bf16x8(wr16 + kb0 + 8 * q) : bf16x8{};
   }
   if constexpr (L0) {
     __shared__ float sX[32 * L0_KMAX];
@@ -524,21 +560,24 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
           c11 = mfma4(x1, wB[q], c11);
         }
       }
-      const floatx4* cs[4] = {&c00, &c01, &c10, &c11};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      // (no array of pointers to the accumulators: it put them in scratch memory)
+      auto put = [&](const floatx4& c, int q) {
         const int cc = cb + (q & 1) * 16 + r;
         if (cc < K) {
           const float bb = (q & 1) ? bB : bA;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int rr = (q >> 1) * 16 + g * 4 + i;
-            const float v = __fadd_rn((*cs[q])[i], bb);
+            const float v = __fadd_rn(c[i], bb);
             sA[rr * AS + cc] = v;
             if (tN == 0 && m0 + rr < M) Y0[(size_t)(m0 + rr) * K + cc] = v;
           }
         }
-      }
+      };
+      put(c00, 0);
+      put(c01, 1);
+      put(c10, 2);
+      put(c11, 3);
       if (cb + 32 * NW < K) load_w0(cb + 32 * NW);
     }
     __syncthreads();
@@ -547,7 +586,39 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
   const float* xra = L0 ? sA + r * AS : X + (size_t)ma * K;
   const float* xrb = L0 ? sA + (16 + r) * AS : X + (size_t)mb * K;
   floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  for (int kc = wave * KW; kc < K; kc += 256) {
+  for (int kc = wave * KW; kc < K && BF; kc += 256) {
+    // bf16 operands: per lane KL consecutive k as KL / 8 MFMA steps of 8 (the fp32 path's k
+    // assignment, regrouped), X rounded to bf16 in registers, W from the bf16 copy
+    const int kb = kc + g * KL;
+    float a0[KL], a1[KL];
+    bf16x8 w16[KL / 8];
+#pragma unroll
+    for (int q = 0; q < KL / 4; ++q) {
+      float4 ta, tb;
+      if constexpr (L0) {
+        ta = reinterpret_cast<const float4*>(xra + kb)[q];
+        tb = reinterpret_cast<const float4*>(xrb + kb)[q];
+      } else {
+        ta = oka ? *reinterpret_cast<const float4*>(xra + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+        tb = okb ? *reinterpret_cast<const float4*>(xrb + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      a0[4 * q] = ta.x; a0[4 * q + 1] = ta.y; a0[4 * q + 2] = ta.z; a0[4 * q + 3] = ta.w;
+      a1[4 * q] = tb.x; a1[4 * q + 1] = tb.y; a1[4 * q + 2] = tb.z; a1[4 * q + 3] = tb.w;
+    }
+#pragma unroll
+    for (int q = 0; q < KL / 8; ++q) {
+      if constexpr (L0)
+        w16[q] = kc == wave * KW ? wpre16[q] : (okn ? ld_bf16x8(wr16 + kb + 8 * q) : bf16x8{});
+      else
+        w16[q] = okn ? ld_bf16x8(wr16 + kb + 8 * q) : bf16x8{};
+    }
+#pragma unroll
+    for (int q = 0; q < KL / 8; ++q) {
+      acc0 = mfma_bf16(to_bf16x8(a0 + 8 * q), w16[q], acc0);
+      acc1 = mfma_bf16(to_bf16x8(a1 + 8 * q), w16[q], acc1);
+    }
+  }
+  for (int kc = wave * KW; kc < K && !BF; kc += 256) {
     const int kb = kc + g * KL;
     float a0[KL], a1[KL], bw[KL];
     if constexpr (VEC) {  // K % KW == 0, rows 16-B aligned: KL/4 float4 per operand row
@@ -562,7 +633,7 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
           tb = okb ? ldc4<C>(xrb + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
         float4 tw;
-        if constexpr (L0) {
+        if constexpr (L0 && !BF) {
           tw = kc == wave * KW ? wpre[q] : (okn ? ldc4<C>(wr + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f));
         } else {
           tw = okn ? ldc4<C>(wr + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -615,7 +686,7 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
 
 constexpr int qa_tile_floats(bool L0) { return L0 ? 1 : 32 * 16; }  // L0 launches never accumulate
 
-template <bool VEC, int NW, bool L0>
+template <bool VEC, int NW, bool L0, bool BF = false>
 __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
   PROBE_T(pt0);
   int y = blockIdx.y, tN = blockIdx.x, tM = blockIdx.z;
@@ -642,7 +713,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
     head = grp.head0 + yy;
   }
   __shared__ float sT[qa_tile_floats(L0)];
-  fwd_tile<VEC, NW, L0, false>(G, F, y, tN, tM, qa ? sT : nullptr);
+  fwd_tile<VEC, NW, L0, false, BF>(G, F, y, tN, tM, qa ? sT : nullptr);
   if (qa) q_accumulate(G, F, head, tN, tM, sT);
   if (tN == 0 && tM == 0 && blockIdx.y == 0 && (F.xcd ? blockIdx.x == 0 : true)) {
     if (F.flag && threadIdx.x == 0) *F.flag = F.flag_value;
@@ -1064,8 +1135,9 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
   return 0;
 }
 
-template <bool TDG, int VMAX = 2, int U = 8, bool C = false>
+template <bool TDG, int VMAX = 2, int U = 8, bool C = false, bool BF = false>
 __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floatx4 (*red)[2][64]) {
+  static_assert(!(BF && (TDG || C)), "bf16 dX: the plain dX tiles only (the fused TD launch stays fp32)");
   const RoleGeo L = A.ra;
   const int N = L.N, K = L.K, M = A.M;
   const int ntk = (K + 15) >> 4;
@@ -1141,6 +1213,21 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
       float a0[16], a1[16], bw[16];
       load16u<C>(a0, dZ + (size_t)ma * N, nb, nend, oka, vec);
       load16u<C>(a1, dZ + (size_t)mb * N, nb, nend, okb, vec);
+      if constexpr (BF) {
+        // the reduction index n = nb + 8s + j as element j of bf16 step s (a permutation of the
+        // fp32 path's k-steps); W from the bf16 copy of the read slot
+        const __bf16* W16 = G.on16 + G.slot_off(rslot(A.mask, head), head) + L.wOff;
+        bf16x8 w16[2];
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          w16[j >> 3][j & 7] = (okk && nb + j < nend) ? W16[(size_t)(nb + j) * K + kk] : (__bf16)0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          acc0 = mfma_bf16(to_bf16x8(a0 + 8 * s2), w16[s2], acc0);
+          acc1 = mfma_bf16(to_bf16x8(a1 + 8 * s2), w16[s2], acc1);
+        }
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < 16; ++j) bw[j] = (okk && nb + j < nend) ? W[(size_t)(nb + j) * K + kk] : 0.f;
 #pragma unroll
@@ -1261,7 +1348,7 @@ __device__ void role_v0_only(const Geo& G, const BwdArgs& A, int head, const Rol
   fused_v0<false>(G, A, L, head, nbase, sW, sB, sX);
 }
 
-template <bool C = false>
+template <bool C = false, bool BF = false>
 __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile, bool fuse) {
   const int N = L.N, K = L.K, M = A.M;
   const int ntk = (K + 63) >> 6;
@@ -1370,6 +1457,7 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
           stc<C>(Pw + off, pp[e]);
           st_moment(Mw + off, pm[e]);
           st_moment(Vw + off, pv[e]);
+          if constexpr (BF) G.on16[wo + off] = (__bf16)pp[e];  // the bf16 copy of the write slot
         }
         if (fuse) sW[(n - nbase) * KFUSE + k] = pp[e];
       }
@@ -1381,6 +1469,7 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
       stc<C>(Pw + L.bOff + nbias, bp);
       st_moment(Mw + L.bOff + nbias, bm);
       st_moment(Vw + L.bOff + nbias, bv);
+      if constexpr (BF) G.on16[wo + L.bOff + nbias] = (__bf16)bp;
     }
     if (fuse) sB[nbias - nbase] = bp;
   }
@@ -1584,6 +1673,7 @@ __device__ void role_tail(const Geo& G, const BwdArgs& A, int head) {
   }
 }
 
+template <bool BF = false>
 __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
   __shared__ floatx4 red[4][2][64];
   PROBE_T(pt0);
@@ -1596,17 +1686,17 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
   const bool skip = A.skip && __builtin_nontemporal_load(A.skip + head) != 0;  // repeats round r-1
   if (bx < A.na) {
     if (skip) return;
-    role_dx<false>(G, A, head, bx, red);
+    role_dx<false, 2, 8, false, BF>(G, A, head, bx, red);
     PROBE_REC(4, pt0);
     return;
   }
   bx -= A.na;
   if (bx < A.nb) {
     if (skip) return;
-    if (A.rb.nw == 2)
+    if (A.rb.nw == 2 && !BF)  // bf16 mode never builds wide tiles (run_bwd)
       role_dw_wide(G, A, head, A.rb, bx);
     else
-      role_dw(G, A, head, A.rb, bx, false);
+      role_dw<false, BF>(G, A, head, A.rb, bx, false);
     PROBE_REC(5, pt0);
     return;
   }
@@ -1616,7 +1706,7 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
       if (A.fuse_v0 && !A.skip_v0) role_v0_only(G, A, head, A.rc, bx);
       return;
     }
-    role_dw(G, A, head, A.rc, bx, A.fuse_v0 != 0);
+    role_dw<false, BF>(G, A, head, A.rc, bx, A.fuse_v0 != 0);
     PROBE_REC(6, pt0);
     return;
   }

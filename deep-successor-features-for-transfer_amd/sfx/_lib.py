@@ -45,6 +45,8 @@ SIGNATURES = {
     "sfx_set_spec_rounds": (_I, [_VP, _I]),
     "sfx_step_stats": (_I, [_VP] + [C.POINTER(C.c_longlong)] * 4),
     "sfx_skip_stats": (_I, [_VP, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong), _I]),
+    "sfx_set_precision": (_I, [_VP, _I]),
+    "sfx_get_precision": (_I, [_VP]),
     "sfx_set_target_update_ev": (_I, [_VP, _I]),
     "sfx_get_since_target": (_I, [_VP, _I, _IP]),
     "sfx_set_since_target": (_I, [_VP, _I, _I]),

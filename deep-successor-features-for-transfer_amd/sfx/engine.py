@@ -260,6 +260,19 @@ class SFEngine:
         check(lib.sfx_step_stats(self._h, C.byref(s), C.byref(f), C.byref(r), C.byref(n)), "sfx_step_stats")
         return {"steps": s.value, "host_round_steps": f.value, "unverified_policies": r.value, "rounds": n.value}
 
+    PRECISIONS = {"fp32": 0, "bf16": 1}
+
+    def set_precision(self, precision: str):
+        """'fp32' (default: the reference's arithmetic, every parity test) or 'bf16' (bf16 MFMA
+        operands for the forward / dX GEMMs from bf16 copies of the parameters; fp32 master
+        weights, moments, gradients of W, TD targets and GPI)."""
+        check(lib.sfx_set_precision(self._h, self.PRECISIONS[precision]), "sfx_set_precision")
+
+    @property
+    def precision(self) -> str:
+        p = lib.sfx_get_precision(self._h)
+        return {v: k for k, v in self.PRECISIONS.items()}[p]
+
     def skip_stats(self, reset: bool = False):
         """Policies checked / skipped in speculative rounds r >= 1 (their next actions repeated
         round r-1's, so their update would have too)."""

@@ -37,6 +37,9 @@ extern "C" {
 #define SFX_ACT_RELU 1
 #define SFX_ACT_TANH 2
 
+#define SFX_PREC_FP32 0 /* the reference's arithmetic; every parity test runs in it (default) */
+#define SFX_PREC_BF16 1 /* bf16 MFMA operands for the forward and dX GEMMs, fp32 elsewhere */
+
 typedef struct sfx_handle* sfx_t;
 
 /* Version string of the build (for logs). */
@@ -163,6 +166,14 @@ int sfx_debug_force_rerun(sfx_t h, int first_policy);
  * re-derives every policy's next actions from round r-1's updated heads; a step whose
  * last device round still flags a policy gets further rounds from sfx_step_finish. */
 int sfx_set_spec_rounds(sfx_t h, int rounds);
+/* Operand precision of the ψ GEMMs (north_star: "MFMA bf16 for the small dense MLP GEMMs").
+ * SFX_PREC_BF16: the forward and dX tiles take bf16 operands (v_mfma_f32_16x16x32_bf16) from
+ * bf16 copies of the online / target parameters, accumulate in fp32; the master parameters,
+ * Adam moments, dW, TD target, GPI, losses stay fp32, and the Adam epilogue refreshes the copy
+ * of every parameter it writes.  Not bit-exact with the reference (argmax agrees
+ * wherever the top-2 gap exceeds the bf16 error).  Default SFX_PREC_FP32. */
+int sfx_set_precision(sfx_t h, int precision);
+int sfx_get_precision(sfx_t h);
 /* Counters of fused steps: total, those that needed host-issued rounds, the policies
  * still unverified after the device rounds, and all rounds run. */
 int sfx_step_stats(sfx_t h, long long* steps, long long* fallbacks, long long* rerun_policies, long long* rounds);
