@@ -2156,6 +2156,8 @@ struct GateArgs {
   long long timeout;
   int* err;             // host-coherent
   const int* hcancel;   // written by the host (sfx_runner abort): cancel every step still waiting
+  const int* hold;      // written by the host while it runs host rounds of the step before (see below)
+  long long hard;       // bound of a held wait (ticks)
   int* cancel;          // device: this step's verdict for its kernels (Geo::cancel)
   int* clr;             // sharded steps: SORT_EMPTY-fill clr[0, nclr) (round 0's maxima buffers)
   int nclr, pad2_;
@@ -2163,20 +2165,35 @@ struct GateArgs {
 
 // Wait for the host's go of this step (bounded); 1 if the step may run, 0 if it is cancelled.
 // One thread.  dctr advances either way, so the gates of later steps keep their numbering.
+// A cancelled step's launches still run (without committing) and overwrite the handle's
+// transient buffers, so no gate may give up while the host runs host rounds of the step before
+// on the side stream (they read those buffers).  The host raises `hold` before such rounds and
+// then reads err; a gate past its bound writes err and then reads `hold` -- each side flushing
+// its write before its read (the host reads the word back through the BAR, the gate reads err
+// back across PCIe), so at least one of them sees the other: either the host sees err = 1 and
+// drains the cancelled steps before its rounds (runner_abort), or the gate sees hold = 1, takes
+// its err back and keeps waiting (up to `hard`).
 __device__ __forceinline__ int gate_wait(const GateArgs& g) {
   int ok = 1;
   const long long want = *g.dctr + 1;
   const long long t0 = wall_clock64();
   unsigned it = 0;
+  bool held = false;
   while (__hip_atomic_load(g.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
     if ((++it & 15) == 0 && __hip_atomic_load(g.hcancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
       ok = 0;
       break;
     }
-    if (wall_clock64() - t0 > g.timeout) {
-      ok = 0;
-      __hip_atomic_store(g.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      break;
+    const long long el = wall_clock64() - t0;
+    if (el > g.timeout && (!held || (it & 15) == 0)) {
+      __hip_atomic_store(g.err, 1, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+      (void)__hip_atomic_load(g.err, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);  // the store has landed
+      if (el > g.hard || !g.hold || !__hip_atomic_load(g.hold, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM)) {
+        ok = 0;
+        break;
+      }
+      __hip_atomic_store(g.err, 0, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);  // held: not given up
+      held = true;
     }
     __builtin_amdgcn_s_sleep(8);
   }

@@ -168,7 +168,7 @@ def test_dropin_replays_reference_call_log(golden, stack):
                           for t in range(T)])
     params_close(online, g["final.online"], 1e-3 * steps)
     params_close(target, g["final.target"], 1e-3 * steps)
-    rel_close(torch.stack([_w(sf.fit_w[t]) for t in range(T)]), g["final.w"], rtol=1e-3, atol=1e-5)
+    rel_close(torch.stack([_w(sf.fit_w[t]) for t in range(T)]), g["final.w"], rtol=1e-4, atol=1e-7)
     assert np.array_equal(np.stack([np.asarray(x) for x in sf.gpi_counters]), g["final.gpi_counters"])
     assert list(sf.updates_since_target_updated) == [int(x) for x in g["final.since_target"]]
     if gfun:
@@ -211,7 +211,7 @@ def test_dropin_sequential_deepsf_vs_reference_updates(golden, case):
         dev = DEV
         loss, l1, l2 = sf.update_successor((s.to(dev), a.to(dev), r.to(dev), phi.to(dev), s1.to(dev), gamma.to(dev)),
                                            i, use_gpi=bool(g["use_gpi"]))
-        rel_close(torch.stack([loss, l1, l2]).cpu(), g["losses"][j], rtol=2e-4, atol=1e-7)
+        rel_close(torch.stack([loss, l1, l2]).cpu(), g["losses"][j], rtol=1e-4, atol=1e-7)
     k = int(g["k"])
     online = torch.stack([torch.cat([p.detach().reshape(-1).cpu() for p in sf.psi[t][0][0].parameters()])
                           for t in range(T)])

@@ -138,7 +138,7 @@ def test_update_vs_golden(golden, case):
         nxt = torch.empty(s.shape[0], dtype=torch.long, device="cuda")
         losses = eng.update(i, s, a, r, phi, s1, gamma, use_gpi=bool(g["use_gpi"]), next_actions=nxt)
         assert np.array_equal(nxt.cpu().numpy(), g["next_actions"][j]), f"step {j}"
-        rel_close(losses, g["losses"][j], rtol=2e-4, atol=1e-7)
+        rel_close(losses, g["losses"][j], rtol=1e-4, atol=1e-7)
         if j == 0:
             params_close(torch.stack([eng.get_head(t) for t in range(T)]), g["online1"], 1e-3)
     online = torch.stack([eng.get_head(t, 0) for t in range(T)])
@@ -150,8 +150,8 @@ def test_update_vs_golden(golden, case):
     for t in range(T):
         m, v, st = eng.get_adam(t)
         assert st == int(g["steps"][t])
-        params_close(m, g["m"][t], 1e-3 * k, rtol=1e-3, atol=1e-7)
-        params_close(v, g["v"][t], 1e-3 * k, rtol=1e-3, atol=1e-9)
+        params_close(m, g["m"][t], 1e-3 * k, rtol=1e-4, atol=1e-8)
+        params_close(v, g["v"][t], 1e-3 * k, rtol=1e-4, atol=1e-10)
         assert eng.since_target(t) == int(g["since_target"][t])
     eng.close()
 
@@ -270,9 +270,9 @@ def test_ragged_shapes_update_vs_oracle(n_s, H, A, d, acts, B):
         loss, l1, l2, na = R.sf_update(st, (s, a, r, phi, s1, gamma), i, use_gpi=use_gpi)
         lo = eng.update(i, s, a, r, phi, s1, gamma, use_gpi=use_gpi, next_actions=nxt)
         assert torch.equal(nxt.cpu(), na), f"update {k}: next actions differ"
-        rel_close(lo, [float(loss), float(l1), float(l2)], rtol=2e-4, atol=1e-7)
+        rel_close(lo, [float(loss), float(l1), float(l2)], rtol=1e-4, atol=1e-7)
     params_close(torch.stack([eng.get_head(t) for t in range(T)]), st.online, 3e-3)
-    rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-3, atol=1e-6)
+    rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-4, atol=1e-7)
     for _ in range(2):
         s, a, r, phi, s1, gamma = batch()
         R.deep_all_task_step(st, (s, a, phi, s1, gamma))

@@ -206,7 +206,7 @@ def test_runner_active_schedules_match_oracle(schedule, upd_use_gpi):
         assert got == want, f"step {k}: runner selected {got}, oracle {want}"
     params_close(torch.stack([eng.get_head(t, 0) for t in range(T)]), st.online, 1e-3 * n)
     params_close(torch.stack([eng.get_head(t, 1) for t in range(T)]), st.target, 1e-3 * n)
-    rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-3, atol=1e-6)
+    rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-4, atol=1e-7)
     if schedule == "tsf":
         params_close(torch.stack([eng.tsf_get_g(t)[0] for t in range(T)]), st.g, 1e-3 * n)
         params_close(eng.tsf_get_h(), st.h, 1e-3 * n)
@@ -215,17 +215,22 @@ def test_runner_active_schedules_match_oracle(schedule, upd_use_gpi):
     eng.close()
 
 
-@pytest.mark.parametrize("schedule", ["all", "active"])
-def test_runner_gate_timeouts_cancel_and_retry(schedule):
+@pytest.mark.parametrize("schedule,force", [("all", -1), ("all", 1), ("active", -1)])
+def test_runner_gate_timeouts_cancel_and_retry(schedule, force):
     """A gate bound of 10 ns: every pre-launched step's gate gives up before the host releases
     it, so the step is cancelled (none of its launches commits -- parameters, moments, step
     counters, w) and re-issued from the same staged inputs.  The results must still be the
-    oracle's, step for step."""
+    oracle's, step for step.  force = 1: every step also finishes with host rounds on the side
+    stream -- exactly when the next step's gate gives up and its (cancelled) launches would
+    overwrite the transient buffers those rounds read, unless the hold protocol (gate_wait)
+    drains them first."""
     from sfx.runner import NativeEnvLoop
 
     spec = R.Spec(17, 32, 7, 8, ("relu", "relu"))
     T, ev, alpha, n = 3, 1000, 0.05, 20
     eng, st = make(spec, T, ev)
+    if force >= 0:
+        eng.debug_force_rerun(force)
     loop = NativeEnvLoop(eng, batch=16, capacity=200, gamma=0.9, epsilon=0.3, alpha_w=alpha, episode_len=7, seed=5,
                          schedule=schedule)
     loop.prefill(16)
@@ -245,7 +250,7 @@ def test_runner_gate_timeouts_cancel_and_retry(schedule):
                      torch.from_numpy(rec["phi"]), torch.from_numpy(rec["s1"]), torch.from_numpy(rec["gamma"]))
             R.sf_update(st, batch, 1, use_gpi=True, target_update_ev=ev)
         params_close(torch.stack([eng.get_head(t, 0) for t in range(T)]), st.online, 1e-3 * n)
-        rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-3, atol=1e-6)
+        rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-4, atol=1e-7)
     # the default bound again: pre-launched steps run without being re-issued
     loop.set_gate_timeout(5.0)
     before = loop.stats()["retried"]
@@ -381,7 +386,7 @@ def test_runner_c1_cartpole_shape(schedule):
             assert got == want, f"step {k}: runner selected {got}, oracle {want}"
         params_close(torch.stack([eng.get_head(t, 0) for t in range(T)]), st.online, 1e-3 * n)
         params_close(torch.stack([eng.get_head(t, 1) for t in range(T)]), st.target, 1e-3 * n)
-        rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-3, atol=1e-6)
+        rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-4, atol=1e-7)
     loop.close()
     eng.close()
 

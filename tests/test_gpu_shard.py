@@ -244,7 +244,7 @@ def _tsf_check(res, use_gpi, cfg=TSF_SMALL):
     params_close(heads, st.online, 1e-3 * n)
     params_close(gg, st.g, 1e-3 * n)
     params_close(h, st.h, 1e-3 * n)
-    rel_close(w, st.w, rtol=1e-3, atol=1e-6)
+    rel_close(w, st.w, rtol=1e-4, atol=1e-7)
 
 
 @pytest.mark.parametrize("use_gpi", [True, False])

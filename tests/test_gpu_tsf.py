@@ -1,7 +1,10 @@
 """GPU parity of the TSF-DQN update (sfx_tsf_*: planar-flow g_i, shared h, φ̃ in the TD target
 and l2) against golden vectors from the real reference's TSFDQN.update_successor
 (tsfdqn.py:588-709 and tsfdqn_nf.py with K = 3 planar layers; tests/golden/upd_tsf*.npz).
-Tolerances as test_gpu_engine.py (fp32 reduction order differs from ATen's)."""
+Tolerances as test_gpu_engine.py: losses and w within 1e-4 relative (north_star), the other
+parameter groups through params_close.  test_tsf_error_budget_vs_float64 measures what the fp32
+results are worth: against the same updates in float64, the GPU's error is of the order of the
+reference's own fp32 (ATen) error, ~1e-8 relative on the losses at the full C3 / C5 shape."""
 import numpy as np
 import pytest
 import torch
@@ -39,10 +42,10 @@ def test_tsf_update_vs_golden(golden, case):
     for j, (s, a, r, phi, s1, gamma) in enumerate(batches_of(g)):
         i = int(g["policies"][j])
         losses = eng.tsf_update(i, s, a, r, phi, s1, gamma, use_gpi=True)
-        rel_close(losses, g["losses"][j], rtol=2e-4, atol=1e-7)
+        rel_close(losses, g["losses"][j], rtol=1e-4, atol=1e-7)
     params_close(torch.stack([eng.get_head(t, 0) for t in range(T)]), g["online"], 1e-3 * k)
     params_close(torch.stack([eng.get_head(t, 1) for t in range(T)]), g["target"], 1e-3 * k)
-    rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), g["w"], rtol=1e-3, atol=1e-6)
+    rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), g["w"], rtol=1e-4, atol=1e-7)
     params_close(torch.stack([eng.tsf_get_g(t)[0] for t in range(T)]), g["g"], 1e-3 * k)
     params_close(eng.tsf_get_h(), g["h"], 1e-3 * k)
     eng.close()
@@ -93,11 +96,11 @@ def test_tsf_full_c3_vs_oracle(K):
         loss, l1, l2, na = R.tsf_update(st, (s, a, r, phi, s1, gamma), i, use_gpi=True)
         lo = eng.tsf_update(i, s, a, r, phi, s1, gamma, use_gpi=True, next_actions=nxt)
         assert torch.equal(nxt.cpu(), na), f"update {j}: GPI next actions differ"
-        rel_close(lo, [float(loss), float(l1), float(l2)], rtol=2e-4, atol=1e-7)
+        rel_close(lo, [float(loss), float(l1), float(l2)], rtol=1e-4, atol=1e-7)
     for t in (0, 5, 15):
         params_close(eng.get_head(t, 0), st.online[t], 4e-3)
         params_close(eng.tsf_get_g(t)[0], st.g[t], 4e-3)
-        rel_close(eng.get_w(t)[0], st.w[t], rtol=1e-3, atol=1e-6)
+        rel_close(eng.get_w(t)[0], st.w[t], rtol=1e-4, atol=1e-7)
     params_close(eng.tsf_get_h(), st.h, 4e-3)
     eng.close()
 
@@ -139,10 +142,89 @@ def test_tsf_ragged_shapes_vs_oracle(n_s, B, K, G, d, fork, monkeypatch):
                                         target_update_ev=3)
         lo = eng.tsf_update(i, s, a, r, phi, s1, gamma, use_gpi=j != 2, next_actions=nxt)
         assert torch.equal(nxt.cpu(), na), f"update {j}: next actions differ"
-        rel_close(lo, [float(loss), float(l1), float(l2)], rtol=2e-4, atol=1e-7)
+        rel_close(lo, [float(loss), float(l1), float(l2)], rtol=1e-4, atol=1e-7)
     params_close(torch.stack([eng.get_head(t, 0) for t in range(T)]), st.online, 5e-3)
     params_close(torch.stack([eng.get_head(t, 1) for t in range(T)]), st.target, 5e-3)
     params_close(torch.stack([eng.tsf_get_g(t)[0] for t in range(T)]), st.g, 5e-3)
     params_close(eng.tsf_get_h(), st.h, 5e-3)
-    rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-3, atol=1e-6)
+    rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-4, atol=1e-7)
     eng.close()
+
+
+# error budget (tools/tsf_error_budget.py prints the full table)
+def to64(st):
+    return R.TSFState(st.spec, st.online.double(), st.target.double(), st.w.double(), gspec=st.gspec,
+                      g=st.g.double(), h=st.h.double(), hm=torch.zeros(st.T, st.h.numel(), dtype=torch.float64),
+                      hv=torch.zeros(st.T, st.h.numel(), dtype=torch.float64))
+
+
+def rel(a, b):
+    a, b = torch.as_tensor(a, dtype=torch.float64).cpu(), torch.as_tensor(b, dtype=torch.float64).cpu()
+    return float(((a - b).abs() / b.abs().clamp_min(1e-30)).max())
+
+
+def tsf_error_budget(K, T=16, B=32, verbose=True):
+    from sfx.engine import SFEngine
+
+    spec, gs, st = tsf_c3_problem(T, K)
+    s64 = to64(st)
+    eng = SFEngine(T, spec.n_s, spec.H, spec.A, spec.d, spec.acts, max_batch=B)
+    eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
+    eng.set_target_update_ev(1000)
+    eng.tsf_setup(gs.G, K, 1.0, 1e-3, 0.0, 1e-3, 0.0)
+    for t in range(T):
+        eng.load_head(t, st.online[t], 0)
+        eng.load_head(t, st.target[t], 1)
+        eng.load_w(t, st.w[t])
+        eng.tsf_load_g(t, st.g[t])
+    eng.tsf_load_h(st.h)
+    gen = torch.Generator().manual_seed(3)
+    rows = []
+    for j, i in enumerate((0, 5, 15, 5)):
+        s, s1 = torch.randn(B, spec.n_s, generator=gen), torch.randn(B, spec.n_s, generator=gen)
+        a = torch.randint(0, spec.A, (B,), generator=gen)
+        phi = torch.rand(B, spec.d, generator=gen)
+        r = torch.rand(B, 1, generator=gen)
+        gamma = torch.where(torch.rand(B, generator=gen) < 0.01, 0.0, 0.9)
+        l32 = R.tsf_update(st, (s, a, r, phi, s1, gamma), i, use_gpi=True)
+        na = l32[3]
+        l64 = R.tsf_update(s64, (s.double(), a, r.double(), phi.double(), s1.double(), gamma.double()), i,
+                           use_gpi=True, next_actions=na)
+        lg = eng.tsf_update(i, s, a, r, phi, s1, gamma, use_gpi=True)
+        for name, k in (("loss", 0), ("l1", 1), ("l2", 2)):
+            rows.append((f"update {j} {name}", rel(lg[k], l64[k]), rel(l32[k], l64[k])))
+    for t in (0, 5, 15):
+        rows.append((f"w[{t}] (max rel)", rel(eng.get_w(t)[0], s64.w[t]), rel(st.w[t], s64.w[t])))
+    for t in (0, 5, 15):
+        d_gpu = (eng.get_head(t, 0).double() - s64.online[t]).abs().max()
+        d_ref = (st.online[t].double() - s64.online[t]).abs().max()
+        rows.append((f"psi[{t}] max abs", float(d_gpu), float(d_ref)))
+        d_gpu = (eng.tsf_get_g(t)[0].double() - s64.g[t]).abs().max()
+        d_ref = (st.g[t].double() - s64.g[t]).abs().max()
+        rows.append((f"g[{t}] max abs", float(d_gpu), float(d_ref)))
+    rows.append(("h max abs", float((eng.tsf_get_h().double() - s64.h).abs().max()),
+                 float((st.h.double() - s64.h).abs().max())))
+    eng.close()
+    if not verbose:
+        return rows
+    print(f"K = {K}: quantity | GPU vs float64 | reference fp32 (ATen) vs float64")
+    for name, g, r in rows:
+        print(f"  {name:18s} {g:10.3e} {r:10.3e}   {'GPU <= ref' if g <= r else 'ratio %.2f' % (g / max(r, 1e-30))}")
+    return rows
+
+
+
+
+@pytest.mark.parametrize("K", [0, 100])
+def test_tsf_error_budget_vs_float64(K):
+    """Every loss of 4 full-C3 updates within 1e-6 relative of the float64 answer (measured
+    ≤ 1e-7), w within 1e-5 relative, ψ / g / h within 1e-5 absolute -- the same order as the
+    reference's own fp32 (ATen) error against float64, which the rows report beside it."""
+    rows = tsf_error_budget(K)
+    for name, gpu, ref in rows:
+        if "loss" in name or "l1" in name or "l2" in name:
+            assert gpu < 1e-6, (name, gpu, ref)
+        elif name.startswith("w["):
+            assert gpu < 1e-5, (name, gpu, ref)
+        else:
+            assert gpu < 1e-5, (name, gpu, ref)
