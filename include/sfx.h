@@ -270,10 +270,13 @@ int sfx_runner_stats(sfx_runner_t r, long long* env_steps, long long* prelaunche
  * the host are cancelled the same way before the error returns: the heads hold the last
  * completed step and the runner stays usable. */
 int sfx_runner_gate_timeout(sfx_runner_t r, double seconds);
+/* While the host runs host rounds of a step (speculation not verified on the device), the next
+ * step's gate does not give up (hold protocol) -- for at most max(bound, 20 s). */
 /* Instantiate the step graphs of the current schedule and task ahead of the first steps (every
  * span length, both slot parities) without running them: a short run then measures replays, not
  * graph captures. */
 int sfx_runner_warm(sfx_runner_t r);
+/* Steps issued again after their gate gave up (the step in flight, or steps queued behind it). */
 int sfx_runner_retried(sfx_runner_t r, long long* retried);
 /* SF.gpi_counters (features/successor.py:270-272): [T][T] counts of the GPI task per active task
  * (counted only with GPI action selection, as SF.GPI(update_counters=use_gpi), agents/sfdqn.py:41) */
