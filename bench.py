@@ -137,7 +137,7 @@ def skippable_head_bytes(sh, M: int) -> float:
     dw = sum(24.0 * (N * K + N) + 4.0 * (M * N + M * K) for N, K in layers)
     # and its post-update forward over the S1 rows ++ s_next (the head keeps last round's values)
     fw = sum(4.0 * (N * K + N + (M + 1) * K + (M + 1) * N) for N, K in layers)
-    return dx + dw + fw
+    return dx + dw, fw  # (k_bwd launches, k_fwd launches)
 
 
 def cpu_info() -> dict:
@@ -500,6 +500,16 @@ def main():
     eng.prof_enable(False)
     eng.prof_reset()
     prof_skip = {k: v - skip0[k] for k, v in eng.skip_stats().items()}
+    # the launches' algorithmic bytes (host-side, per launch) count every head of every round; a
+    # skipped policy's tiles return at once, so its bytes are not moved: take them off the kinds
+    # they belong to (device counters over the same steps), so achieved GB/s stays honest
+    launched = sum(v[2] for v in stats.values()) / max(args.prof_steps, 1)
+    skb, skf = skippable_head_bytes(sh, B)
+    nsk = prof_skip["policies_skipped"]
+    for kd, per in (("bwd", skb), ("fwd", skf)):
+        if kd in stats:
+            n_, us_, by_ = stats[kd]
+            stats[kd] = (n_, us_, max(0.0, by_ - nsk * per))
 
     sharded = replicas = None
     layout = "single" if world == 1 else f"replica{world}"
@@ -538,12 +548,7 @@ def main():
         U = T if args.schedule == "all" else 1
         alg = algorithmic_step_bytes(T, U, P, 2)
         alg32 = algorithmic_step_bytes(T, U, P, 4)
-        launched = sum(v[2] for v in stats.values()) / max(args.prof_steps, 1)
-        # the launched-bytes sum counts every round's backward + Adam of every head; a policy that
-        # repeats the previous round's next actions skips them on the device (BwdArgs::skip), so
-        # those bytes are never moved: subtract them (device counters over the same steps)
-        skipped = prof_skip["policies_skipped"] * skippable_head_bytes(sh, B) / max(args.prof_steps, 1)
-        launched_moved = launched - skipped
+        launched_moved = sum(v[2] for v in stats.values()) / max(args.prof_steps, 1)  # net of skipped work
         # each GPU runs every env step of the sharded stream (its T heads); replicas split the total
         per_gpu_rate = value if layout.startswith("shard") else value / world
         roofline["per_step"] = {

@@ -459,3 +459,70 @@ def tsf_update(st: TSFState, batch, i: int, *, use_gpi: bool = True, beta: float
         st.target[i].copy_(st.online[i])
         st.since_target[i] = 0
     return loss, l1, l2, next_actions
+
+
+# --------------------------------------------------------------------------------------
+# TSF test tasks: TSFDQN.get_test_action (tsfdqn.py:859-870) and
+# TSFDQN.update_test_reward_mapper (tsfdqn.py:917-997; tsfdqn_nf.py identical).  A test task
+# mixes the source tasks with weights ω (ω̂ = ω / Σω, ω shaped [1, T, 1, 1] in the reference)
+# and fits its own reward weights w and ω by Adam on
+#     l1 = MSE(Σ ω̂ ψ_t(s)[a], φ̃ + γ Σ ω̂ ψ⁻_t(s1)[a1]),  l2 = MSE(w·φ̃, r),
+#     loss = l1 + β l2 + λ ||ω||_1,   φ̃ = φ ⊙ (h(Σ ω̂ g_t(s)) + h(Σ ω̂ g_t(s1)))
+# with ψ, ψ⁻ and g_t under no_grad; then ω.clamp_(1e-7).
+# --------------------------------------------------------------------------------------
+@dataclass
+class TestMapper:
+    """One test task's reward mapper: w [d], ω [T] and their Adam state (one torch.optim.Adam
+    with two parameter groups, tsfdqn.py:812-831)."""
+    w: torch.Tensor
+    omega: torch.Tensor
+    wm: torch.Tensor = None
+    wv: torch.Tensor = None
+    om: torch.Tensor = None
+    ov: torch.Tensor = None
+    step: int = 0
+
+    def __post_init__(self):
+        if self.wm is None:
+            self.wm, self.wv = torch.zeros_like(self.w), torch.zeros_like(self.w)
+            self.om, self.ov = torch.zeros_like(self.omega), torch.zeros_like(self.omega)
+
+
+def tsf_test_action(st: "TSFState", s: torch.Tensor, w: torch.Tensor, omega: torch.Tensor) -> int:
+    """Greedy branch of get_test_action: argmax over the flattened q = w(Σ_t ω̂_t ψ_t(s)) [1, A, 1]."""
+    on = omega.reshape(-1) / omega.reshape(-1).sum()
+    psi = psi_all(st.online, st.spec, s.reshape(1, -1))[0]      # [T, A, d]
+    tsf = (psi * on.view(-1, 1, 1)).sum(0)                      # [A, d]
+    return int(torch.argmax(tsf @ w.reshape(-1)))
+
+
+def tsf_test_update(st: "TSFState", tm: TestMapper, s, a: int, r: float, phi, s1, a1: int, *, gamma: float,
+                    beta: float, lasso: float, lr_w: float, wd_w: float, lr_o: float, wd_o: float):
+    """update_test_reward_mapper -> (loss, l2, l1) (the reference returns loss, phi_loss, psi_loss);
+    tm is updated in place.  Gradients by autograd, as the reference's loss.backward()."""
+    spec, gs, d = st.spec, st.gspec, st.spec.d
+    s, s1 = s.reshape(1, -1), s1.reshape(1, -1)
+    with torch.no_grad():
+        gs_s = torch.cat([g_forward(st.g[t], gs, s)[0] for t in range(st.T)])     # [T, G]
+        gs_s1 = torch.cat([g_forward(st.g[t], gs, s1)[0] for t in range(st.T)])
+        psi = psi_all(st.online, spec, s)[0]                                     # [T, A, d]
+        psi1 = psi_all(st.target, spec, s1)[0]
+    w = tm.w.clone().requires_grad_(True)
+    om = tm.omega.clone().requires_grad_(True)
+    on = om / om.sum()
+    Wh, bh = st.h[:d * gs.G].view(d, gs.G), st.h[d * gs.G:]
+    ws = (gs_s * on.view(-1, 1)).sum(0)
+    ws1 = (gs_s1 * on.view(-1, 1)).sum(0)
+    tphi = phi.reshape(-1) * (F.linear(ws, Wh, bh) + F.linear(ws1, Wh, bh))
+    nxt = tphi + gamma * (psi1 * on.view(-1, 1, 1)).sum(0)[a1]
+    cur = (psi * on.view(-1, 1, 1)).sum(0)[a]
+    r_fit = (tphi * w).sum()
+    l1 = F.mse_loss(cur, nxt)
+    l2 = (r_fit - r) ** 2
+    loss = l1 + beta * l2 + lasso * om.abs().sum()
+    loss.backward()
+    tm.step += 1
+    adam_(tm.w, w.grad, tm.wm, tm.wv, tm.step, lr_w, weight_decay=wd_w)
+    adam_(tm.omega, om.grad, tm.om, tm.ov, tm.step, lr_o, weight_decay=wd_o)
+    tm.omega.clamp_(1e-7)
+    return float(loss.detach()), float(l2.detach()), float(l1.detach())

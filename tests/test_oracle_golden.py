@@ -134,3 +134,36 @@ def test_tsf_update_matches_reference(golden, case):
     close(st.w, g["w"], rtol=1e-4, atol=1e-6)
     close(st.g, g["g"], rtol=1e-4, atol=1e-6)
     close(st.h, g["h"], rtol=1e-4, atol=1e-6)
+
+
+def tsf_test_problem(g):
+    """The oracle state of a test_tsf* fixture (tools/gen_golden.py gen_tsf_test)."""
+    spec = spec_of(g)
+    gs = R.GSpec(spec.n_s, int(g["G"]), int(g["K"]))
+    T = int(g["T"])
+    st = R.TSFState(spec, torch.from_numpy(g["online"]).clone(), torch.from_numpy(g["target"]).clone(),
+                    torch.zeros(T, spec.d), gspec=gs, g=torch.from_numpy(g["g"]).clone(),
+                    h=torch.from_numpy(g["h"]).clone())
+    tm = R.TestMapper(torch.from_numpy(g["w0"]).clone(), torch.from_numpy(g["omega0"]).clone())
+    return st, tm
+
+
+def tsf_test_hyper(g, j):
+    return dict(gamma=float(g["gamma"]), beta=float(g["beta"]), lasso=float(g["lasso"]), lr_w=float(g["lr_w"]),
+                wd_w=float(g["wd_w"]), lr_o=float(g["lr_o"][j]), wd_o=float(g["wd_o"]))
+
+
+@pytest.mark.parametrize("case", ["tsf", "tsf_nf"])
+def test_tsf_test_path_matches_reference(golden, case):
+    """TSFDQN.get_test_action (greedy) and update_test_reward_mapper (tsfdqn.py:859-997) over 10
+    steps with the ω learning rate decaying: actions exact, losses, w and ω per step."""
+    g = golden("test_" + case)
+    st, tm = tsf_test_problem(g)
+    for j in range(int(g["k"])):
+        s, s1 = torch.from_numpy(g["s"][j]), torch.from_numpy(g["s1"][j])
+        assert R.tsf_test_action(st, s, tm.w, tm.omega) == int(g["greedy"][j])
+        loss, l2, l1 = R.tsf_test_update(st, tm, s, int(g["a"][j]), float(g["r"][j]), torch.from_numpy(g["phi"][j]),
+                                         s1, int(g["a1"][j]), **tsf_test_hyper(g, j))
+        close([loss, l2, l1], [g["loss"][j], g["l2"][j], g["l1"][j]], rtol=1e-5, atol=1e-8)
+        close(tm.w, g["w"][j], rtol=1e-5, atol=1e-8)
+        close(tm.omega, g["omega"][j], rtol=1e-5, atol=1e-8)

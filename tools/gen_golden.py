@@ -11,6 +11,7 @@ initial weights and outputs of:
   * DeepSF.update_successor all-task  (features/deep.py:93-131 + agents/sfdqn.py:47-60,
                                        with SF.update_reward LMS, features/successor.py:146-167)
   * TSFDQN.update_successor           (tsfdqn.py:588-709) and the planar-flow twin (tsfdqn_nf.py)
+  * TSFDQN.get_test_action / update_test_reward_mapper (tsfdqn.py:859-997), both variants
 
 into small ``.npz`` fixtures under tests/golden/.  The fixtures are data only;
 this script never travels to the GPU box (it needs /root/reference).
@@ -354,6 +355,78 @@ def gen_tsf(name, module, shape, T, k, K):
     np.savez_compressed(os.path.join(OUT, f"upd_{name}.npz"), **rec)
 
 
+class PhiTask(SynthTask):
+    """A test task whose features() hands out the recorded φ of the current step."""
+
+    phi = None
+
+    def features(self, state, action, next_state):
+        return self.phi
+
+
+def gen_tsf_test(name, module, shape, T, k, K):
+    """TSFDQN.get_test_action (greedy) and update_test_reward_mapper (tsfdqn.py:859-997): the test
+    task's w and ω set up as train() does (tsfdqn.py:797-832: ω from _init_omega normalised, one
+    Adam over {w, ω}, LambdaLR decaying ω's rate), then k steps of random (s, a, r, φ, s1, a1),
+    with scheduler.step() after each as test_agent does."""
+    torch.manual_seed(700 + K)
+    n_s, H, A, d, acts = shape
+    hyper = dict(HYPER, n_coupling_layers=K, omegas_l1_coefficient=0.05, learning_rate_omega=5e-3,
+                 learning_rate_omega_decay=0.01, weight_decay_omega=1e-4, weight_decay_w=1e-3)
+    sf = module.DeepTSF(pytorch_model_handle=psi_lambda(H, acts), use_true_reward=False,
+                        target_update_ev=4, hyperparameters=hyper)
+    agent = module.TSFDQN(deep_sf=sf, buffer_handle=lambda: None, gamma=0.9, T=500, encoding=None,
+                          use_gpi=True, test_epsilon=-1.0, hyperparameters=hyper)
+    agent.reset()
+    for t in range(T):
+        agent.add_training_task(SynthTask(n_s, A, d, t))
+    # the target heads differ from the online ones (as after training)
+    with torch.no_grad():
+        for t in range(T):
+            for p in sf.psi[t][1][0].parameters():
+                p.add_(torch.randn_like(p) * 0.01)
+        for g in agent.g_functions:  # trained-looking g / h
+            for p in g.parameters():
+                p.add_(torch.randn_like(p) * 0.05)
+    omegas = agent._init_omega(T)
+    with torch.no_grad():
+        omegas = omegas / torch.sum(omegas, axis=1, keepdim=True)
+    omegas = omegas.clone().detach().requires_grad_(True)
+    w_approx = torch.nn.Linear(d, 1, bias=False)
+    with torch.no_grad():
+        w_approx.weight = torch.nn.Parameter(torch.Tensor(1, d).uniform_(-0.01, 0.01))
+    optim = torch.optim.Adam([
+        {"params": w_approx.parameters(), "lr": hyper["learning_rate_w"], "weight_decay": hyper["weight_decay_w"]},
+        {"params": omegas, "lr": hyper["learning_rate_omega"], "weight_decay": hyper["weight_decay_omega"]}])
+    decay = hyper["learning_rate_omega_decay"]
+    scheduler = torch.optim.lr_scheduler.LambdaLR(optim, [lambda e: 1 ** e, lambda e: (1 - decay) ** e])
+    rec = dict(n_s=n_s, H=H, A=A, d=d, T=T, acts=np.array(acts), k=k, K=K, G=hyper["g_h_function_dims"],
+               beta=hyper["beta_loss_coefficient"], lasso=hyper["omegas_l1_coefficient"], gamma=0.9,
+               lr_w=hyper["learning_rate_w"], wd_w=hyper["weight_decay_w"], wd_o=hyper["weight_decay_omega"],
+               online=np_(torch.stack([flat(sf.psi[t][0][0]) for t in range(T)])),
+               target=np_(torch.stack([flat(sf.psi[t][1][0]) for t in range(T)])),
+               g=np_(torch.stack([flat(agent.g_functions[t]) for t in range(T)])), h=np_(flat(agent.h_function)),
+               w0=np_(w_approx.weight.detach().reshape(-1).clone()), omega0=np_(omegas.detach().reshape(-1).clone()))
+    gen = torch.Generator().manual_seed(11)
+    task = PhiTask(n_s, A, d, T)
+    cols = {key: [] for key in ("s", "s1", "a", "a1", "r", "phi", "lr_o", "loss", "l2", "l1", "greedy", "w", "omega")}
+    for j in range(k):
+        s, s1 = torch.randn(1, n_s, generator=gen), torch.randn(1, n_s, generator=gen)
+        a, a1 = int(torch.randint(0, A, (1,), generator=gen)), int(torch.randint(0, A, (1,), generator=gen))
+        r = float(torch.rand(1, generator=gen))
+        task.phi = torch.rand(1, d, generator=gen)
+        greedy = int(agent.get_test_action(s, w_approx, omegas))
+        cols["lr_o"].append(optim.param_groups[1]["lr"])
+        loss, l2, l1 = agent.update_test_reward_mapper(w_approx, omegas, optim, task, r, s, a, s1, a1)
+        scheduler.step()
+        for key, v in (("s", s), ("s1", s1), ("a", a), ("a1", a1), ("r", r), ("phi", task.phi), ("loss", float(loss)),
+                       ("l2", float(l2)), ("l1", float(l1)), ("greedy", greedy),
+                       ("w", w_approx.weight.detach().reshape(-1).clone()), ("omega", omegas.detach().reshape(-1).clone())):
+            cols[key].append(np_(v) if torch.is_tensor(v) else v)
+    rec.update({key: np.array(v) for key, v in cols.items()})
+    np.savez_compressed(os.path.join(OUT, f"test_{name}.npz"), **rec)
+
+
 # ---------------------------------------------------------------------------------------
 # SF-boundary call logs: the reference's own agents (agents/sfdqn.py, agents/sfdqn_sequential.py,
 # agents/tsfdqn_sequential.py and the single-file sfdqn.py / tsfdqn.py / tsfdqn_nf.py) run the
@@ -576,8 +649,14 @@ def main():
     gen_deep_alltask(SHAPES["reacher17"], 4, 6, 3)
     gen_tsf("tsf", ref_tsfdqn, SHAPES["hopper11"], 3, 8, 0)
     gen_tsf("tsf_nf", ref_tsfdqn_nf, SHAPES["hopper11"], 3, 6, 3)
+    gen_tsf_tests()
     gen_call_logs()
     print("golden vectors written to", os.path.abspath(OUT))
+
+
+def gen_tsf_tests():
+    gen_tsf_test("tsf", ref_tsfdqn, SHAPES["hopper11"], 3, 10, 0)
+    gen_tsf_test("tsf_nf", ref_tsfdqn_nf, SHAPES["hopper11"], 3, 10, 3)
 
 
 if __name__ == "__main__":
