@@ -500,4 +500,208 @@ __global__ __launch_bounds__(256) void k_tsf_flow(TsfArgs A) {
   PROBE_REC(15, t0_);
 }
 
+// -------------------------------------------------------------------------------------
+// TSF test tasks: TSFDQN.get_test_action (tsfdqn.py:859-870) and
+// update_test_reward_mapper (tsfdqn.py:917-997).  A test task mixes the source tasks with
+// ω̂ = ω / Σω and fits its reward weights w and ω by Adam on
+//   l1 = MSE(Σ_t ω̂_t ψ_t(s)[a], φ̃ + γ Σ_t ω̂_t ψ⁻_t(s1)[a1]),  l2 = (w·φ̃ - r)²,
+//   loss = l1 + β l2 + λ Σ|ω|,   φ̃ = φ ⊙ (h(Σ_t ω̂_t g_t(s)) + h(Σ_t ω̂_t g_t(s1))),
+// ψ, ψ⁻ and g_t held fixed (no_grad), then ω ≥ 1e-7.  B = 1: tiny, latency-bound kernels.
+// -------------------------------------------------------------------------------------
+struct TsfTestArgs {
+  int T, n_s, G, K, A, d, O, Pg, lastOff, pad_;
+  long long actSize;
+  const float* s;        // [n_s] (k_tsf_test_g)
+  const float* s1;
+  const float* g;        // [T][Pg] g_t parameters (TsfArgs::g packing)
+  const float* hp;       // [d][G] W_h then [d] b_h
+  float* gfeat;          // [T][2][G]: g_t(s), g_t(s1)
+  const float* psi;      // ψ_t(s):  row 0 of an activation role, head stride actSize, at lastOff
+  const float* psi1;     // ψ⁻_t(s1)
+  const float* phi;      // [d]
+  const int64_t* a;      // device scalars (the actions the agent took / will take)
+  const int64_t* a1;
+  float r, gamma, beta, lasso;
+  float* w;              // [d] the test task's reward weights (in place)
+  float* omega;          // [T] (in place)
+  float* mom;            // [2d + 2T]: m_w, v_w, m_ω, v_ω
+  int step;              // Adam step after this update (1-based)
+  int pad2_;
+  AdamHP hpw, hpo;
+  float* losses;         // [3]: loss, l2, l1 (the reference's return order)
+  int64_t* act_out;      // k_tsf_test_act: the greedy action
+};
+
+// g_t(s), g_t(s1) for every task: one wave per task, lanes 0..31 row s, 32..63 row s1, one state
+// component per lane through the K planar flows (w_k·z by a xor butterfly within the 32-lane
+// half), then Linear(n_s, G) from LDS.
+__global__ __launch_bounds__(64) void k_tsf_test_g(TsfTestArgs A) {
+  const int t = blockIdx.x, lane = threadIdx.x, row = lane >> 5, j = lane & 31, n_s = A.n_s, G = A.G;
+  const float* gp = A.g + (long long)t * A.Pg;
+  const bool on = j < n_s;
+  float z = on ? (row ? A.s1 : A.s)[j] : 0.f;
+  const int fs = 2 * n_s + 1;
+  for (int k = 0; k < A.K; ++k) {
+    const float* f = gp + (long long)k * fs;
+    const float wk = on ? f[j] : 0.f, uk = on ? f[n_s + 1 + j] : 0.f, bk = f[n_s];
+    float v = __fmul_rn(wk, z);
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) v = __fadd_rn(v, __shfl_xor(v, o, 32));
+    const float th = tsf_tanh(__fadd_rn(v, bk));
+    z = __fadd_rn(z, __fmul_rn(uk, th));
+  }
+  __shared__ float sz[2][TSF_NS];
+  if (on) sz[row][j] = z;
+  __syncthreads();
+  const float* W = gp + (long long)A.K * fs;
+  const float* b = W + (long long)G * n_s;
+  for (int idx = lane; idx < 2 * G; idx += 64) {
+    const int rr = idx >= G ? 1 : 0, o = idx - rr * G;
+    float acc = 0.f;
+    for (int q = 0; q < n_s; ++q) acc = __builtin_fmaf(W[(long long)o * n_s + q], sz[rr][q], acc);
+    A.gfeat[((long long)t * 2 + rr) * G + o] = __fadd_rn(acc, b[o]);
+  }
+}
+
+// The greedy test action: argmax_a Σ_k w_k Σ_t ω̂_t ψ_t(s)[a][k] (first index on ties), one WG.
+__global__ __launch_bounds__(256) void k_tsf_test_act(TsfTestArgs A) {
+  __shared__ float s_on[64];
+  __shared__ float s_q[256];
+  const int tid = threadIdx.x, T = A.T, d = A.d;
+  if (tid == 0) {
+    float S = 0.f;
+    for (int t = 0; t < T; ++t) S = __fadd_rn(S, A.omega[t]);
+    for (int t = 0; t < T; ++t) s_on[t] = __fdiv_rn(A.omega[t], S);
+  }
+  __syncthreads();
+  for (int a = tid; a < A.A; a += 256) {
+    float q = 0.f;
+    for (int k = 0; k < d; ++k) {
+      float m = 0.f;
+      for (int t = 0; t < T; ++t) m = __fadd_rn(m, __fmul_rn(A.psi[(long long)t * A.actSize + A.lastOff + a * d + k], s_on[t]));
+      q = __builtin_fmaf(m, A.w[k], q);
+    }
+    s_q[a] = q;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int best = 0;
+    for (int a = 1; a < A.A; ++a)
+      if (s_q[a] > s_q[best]) best = a;
+    *A.act_out = best;
+  }
+}
+
+// One update_test_reward_mapper step, one WG (T <= 64, d <= 256, G <= 512).
+__global__ __launch_bounds__(256) void k_tsf_test_step(TsfTestArgs A) {
+  const int tid = threadIdx.x, T = A.T, d = A.d, G = A.G;
+  __shared__ float s_om[64], s_on[64], s_dn[64];
+  __shared__ float s_ws[2][512], s_gws[512];
+  __shared__ float s_tphi[256], s_de[256], s_gaff[256], s_w[256];
+  __shared__ float s_S, s_rfit, s_l1, s_sumdn;
+  const int a = (int)*A.a, a1 = (int)*A.a1;
+  const float* Wh = A.hp;
+  const float* bh = A.hp + (long long)d * G;
+  if (tid < T) s_om[tid] = A.omega[tid];
+  if (tid < d) s_w[tid] = A.w[tid];
+  __syncthreads();
+  if (tid == 0) {
+    float S = 0.f;
+    for (int t = 0; t < T; ++t) S = __fadd_rn(S, s_om[t]);
+    s_S = S;
+    for (int t = 0; t < T; ++t) s_on[t] = __fdiv_rn(s_om[t], S);
+  }
+  __syncthreads();
+  // weighted g features of s and s1
+  for (int idx = tid; idx < 2 * G; idx += 256) {
+    const int rr = idx >= G ? 1 : 0, o = idx - rr * G;
+    float acc = 0.f;
+    for (int t = 0; t < T; ++t) acc = __fadd_rn(acc, __fmul_rn(A.gfeat[((long long)t * 2 + rr) * G + o], s_on[t]));
+    s_ws[rr][o] = acc;
+  }
+  __syncthreads();
+  // φ̃, the two ω-mixed successor rows, the TD error
+  if (tid < d) {
+    float h0 = 0.f, h1 = 0.f;
+    for (int g = 0; g < G; ++g) {
+      h0 = __builtin_fmaf(Wh[(long long)tid * G + g], s_ws[0][g], h0);
+      h1 = __builtin_fmaf(Wh[(long long)tid * G + g], s_ws[1][g], h1);
+    }
+    const float aff = __fadd_rn(__fadd_rn(h0, bh[tid]), __fadd_rn(h1, bh[tid]));
+    const float tphi = __fmul_rn(A.phi[tid], aff);
+    float cur = 0.f, nx = 0.f;
+    for (int t = 0; t < T; ++t) {
+      cur = __fadd_rn(cur, __fmul_rn(A.psi[(long long)t * A.actSize + A.lastOff + a * d + tid], s_on[t]));
+      nx = __fadd_rn(nx, __fmul_rn(A.psi1[(long long)t * A.actSize + A.lastOff + a1 * d + tid], s_on[t]));
+    }
+    const float e = __fsub_rn(cur, __fadd_rn(tphi, __fmul_rn(A.gamma, nx)));
+    s_tphi[tid] = tphi;
+    s_de[tid] = e;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float se = 0.f, rf = 0.f;
+    for (int k = 0; k < d; ++k) {
+      se = __builtin_fmaf(s_de[k], s_de[k], se);
+      rf = __builtin_fmaf(s_tphi[k], s_w[k], rf);
+    }
+    s_l1 = __fdiv_rn(se, (float)d);
+    s_rfit = rf;
+  }
+  __syncthreads();
+  const float q = __fmul_rn(A.beta, __fmul_rn(2.f, __fsub_rn(s_rfit, A.r)));  // dloss / dr_fit
+  const float nd = __fdiv_rn(2.f, (float)d);
+  if (tid < d) {
+    const float de = __fmul_rn(nd, s_de[tid]);                    // dl1 / dcur
+    s_gaff[tid] = __fmul_rn(__fadd_rn(-de, __fmul_rn(q, s_w[tid])), A.phi[tid]);
+    s_de[tid] = de;
+  }
+  __syncthreads();
+  for (int g = tid; g < G; g += 256) {  // d aff / d (mixed g features): W_hᵀ gaff (both rows alike)
+    float acc = 0.f;
+    for (int k = 0; k < d; ++k) acc = __builtin_fmaf(Wh[(long long)k * G + g], s_gaff[k], acc);
+    s_gws[g] = acc;
+  }
+  __syncthreads();
+  if (tid < T) {  // dloss / d ω̂_t
+    float v = 0.f;
+    for (int k = 0; k < d; ++k) {
+      v = __builtin_fmaf(s_de[k], A.psi[(long long)tid * A.actSize + A.lastOff + a * d + k], v);
+      v = __builtin_fmaf(-__fmul_rn(A.gamma, s_de[k]), A.psi1[(long long)tid * A.actSize + A.lastOff + a1 * d + k], v);
+    }
+    for (int g = 0; g < G; ++g)
+      v = __builtin_fmaf(s_gws[g], __fadd_rn(A.gfeat[((long long)tid * 2) * G + g], A.gfeat[((long long)tid * 2 + 1) * G + g]), v);
+    s_dn[tid] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float acc = 0.f;
+    for (int t = 0; t < T; ++t) acc = __builtin_fmaf(s_on[t], s_dn[t], acc);
+    s_sumdn = acc;
+    float l1n = 0.f;
+    for (int t = 0; t < T; ++t) l1n = __fadd_rn(l1n, fabsf(s_om[t]));
+    const float l2 = __fmul_rn(__fsub_rn(s_rfit, A.r), __fsub_rn(s_rfit, A.r));
+    const float loss = __fadd_rn(__fadd_rn(s_l1, __fmul_rn(A.beta, l2)), __fmul_rn(A.lasso, l1n));
+    A.losses[0] = loss;
+    A.losses[1] = l2;
+    A.losses[2] = s_l1;
+  }
+  __syncthreads();
+  float* mw = A.mom;
+  float* vw = A.mom + d;
+  float* mo = A.mom + 2 * d;
+  float* vo = A.mom + 2 * d + T;
+  if (tid < d) adam_el(A.w + tid, mw + tid, vw + tid, __fmul_rn(q, s_tphi[tid]), adam_consts(A.hpw, A.step));
+  if (tid < T) {
+    const float om = s_om[tid];
+    const float sg = om > 0.f ? 1.f : (om < 0.f ? -1.f : 0.f);
+    const float g = __fadd_rn(__fdiv_rn(__fsub_rn(s_dn[tid], s_sumdn), s_S), __fmul_rn(A.lasso, sg));
+    float pp = om, mm = mo[tid], vv = vo[tid];
+    adam_apply(pp, mm, vv, g, adam_consts(A.hpo, A.step));
+    mo[tid] = mm;
+    vo[tid] = vv;
+    A.omega[tid] = fmaxf(pp, 1e-7f);
+  }
+}
+
 }  // namespace sfx

@@ -95,6 +95,8 @@ SIGNATURES = {
     "sfx_tsf_load_h": (_I, [_VP, _FP]),
     "sfx_tsf_get_h": (_I, [_VP, _FP]),
     "sfx_tsf_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP]),
+    "sfx_tsf_test_action": (_I, [_VP, _VP, _VP, _VP, _VP]),
+    "sfx_tsf_test_update": (_I, [_VP, _VP, _VP, _VP, _VP, _F, _VP, _VP, _VP, _VP, _I] + [_F] * 7 + [_VP]),
 }
 
 # env callbacks of sfx_runner_create (include/sfx.h)

@@ -5,12 +5,18 @@ The single-file scripts define their library next to their agent: ``sfdqn.DeepSF
 agents carry the update itself (``TSFDQN.update_successor``, tsfdqn.py:588-709,
 tsfdqn_nf.py:620-741, agents/tsfdqn_sequential.py:123-252).  ``sfx.dropin.install()`` lets the
 user's own modules load unchanged and then applies ``patch``: the library classes become
-sfx's, and the TSF agents' update_successor becomes one libsfx call (DeepTSF.tsf_update).
-Nothing else of the user's agents is touched.
+sfx's, the TSF agents' update_successor becomes one libsfx call (DeepTSF.tsf_update), and their
+test-task methods get_test_action / update_test_reward_mapper (tsfdqn.py:859-997, SURVEY §8f
+rank 1) become libsfx calls too (DeepTSF.tsf_test_action / tsf_test_update), drawing from
+Python's random module exactly where the reference does.  Nothing else of the user's agents is
+touched.
 """
 from __future__ import annotations
 
 import functools
+import random
+
+import torch
 
 from .features import deep_sequential as _seq
 from .features import deep_sequential_tsf as _tsf
@@ -45,6 +51,38 @@ def tsf_update_successor(self, transitions, policy_index, use_gpi=True):
                               beta=self.hyperparameters["beta_loss_coefficient"])
 
 
+def tsf_get_test_action(self, s_enc, w, omegas):
+    """TSFDQN.get_test_action (tsfdqn.py:859-870): the same ε draw from Python's random module;
+    the greedy branch argmax_a w·Σ_t ω̂_t ψ_t(s)[a] is one library call (sfx_tsf_test_action)."""
+    with torch.no_grad():
+        if random.random() <= self.test_epsilon:
+            return torch.tensor(random.randrange(self.n_actions)).to(self.device)
+        return self.sf.tsf_test_action(s_enc, w, omegas)
+
+
+def tsf_update_test_reward_mapper(self, w_approx, omegas, optim, task, r, s, a, s1, a1):
+    """TSFDQN.update_test_reward_mapper (tsfdqn.py:917-997) as one library call
+    (sfx_tsf_test_update): φ from the user's task, the learning rates and weight decays read from
+    the agent's optimizer groups (its LambdaLR keeps decaying ω's), the Adam step on the device.
+    Returns (loss, l2, l1) as the reference does."""
+    if self.h_function is None:
+        raise Exception('Affine Function (h) is not initialized')
+    phi = task.features(s, a, s1)
+    gw, go = optim.param_groups[0], optim.param_groups[1]
+    for grp in (gw, go):
+        if tuple(grp.get("betas", (0.9, 0.999))) != (0.9, 0.999) or grp.get("eps", 1e-8) != 1e-8:
+            raise NotImplementedError("sfx: the test reward mapper's Adam runs with betas (0.9, 0.999), eps 1e-8")
+    hp = self.hyperparameters
+    loss, l2, l1 = self.sf.tsf_test_update(w_approx, omegas, phi, r, s, a, s1, a1, gamma=self.gamma,
+                                           beta=hp['beta_loss_coefficient'], lasso=hp['omegas_l1_coefficient'],
+                                           lr_w=gw['lr'], wd_w=gw['weight_decay'], lr_o=go['lr'],
+                                           wd_o=go['weight_decay'])
+    # the reference's occasional diagnostic print draws from the same random stream
+    if self.total_training_steps % 1000 == 0 and random.randint(1, 1000) < 10:
+        print(f'Target Task {task} omegas {omegas.detach()} weights {w_approx.weight.detach()}')
+    return loss, l2, l1
+
+
 def _synced(method):
     """Run the agent's own method after the device's g_i / h are copied into its modules (the test
     tasks' reward mapper, tsfdqn.py:874-997, reads them in torch)."""
@@ -61,7 +99,10 @@ def _synced(method):
 
 def patch_tsf_agent(cls) -> None:
     cls.update_successor = tsf_update_successor
-    for name in ("test_agent", "update_test_reward_mapper"):
+    if hasattr(cls, "get_test_action") and hasattr(cls, "update_test_reward_mapper"):
+        cls.get_test_action = tsf_get_test_action
+        cls.update_test_reward_mapper = tsf_update_test_reward_mapper
+    for name in ("test_agent",):
         m = getattr(cls, name, None)
         if m is not None and not getattr(m, "__sfx_bound__", False):
             setattr(cls, name, _synced(m))

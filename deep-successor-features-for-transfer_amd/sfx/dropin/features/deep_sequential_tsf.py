@@ -83,6 +83,7 @@ class DeepTSF(_seq.DeepSF):
         self._g = []
         self._h = None
         self._tsf_stale = False
+        self._test_state = {}
 
     def add_training_task(self, task, source=None, g_function_model={}, h_function_model={}):
         """features/deep_sequential_tsf.py:40-73 (w first, then the ψ networks and the optimizer)."""
@@ -173,6 +174,44 @@ class DeepTSF(_seq.DeepSF):
         self._tsf_stale = True
         loss, l1, l2 = (x.to(self._out_device()) for x in losses)
         return loss, l1, l2
+
+    # ------------------------------------------------------------------ test tasks
+    # TSFDQN.get_test_action / update_test_reward_mapper (tsfdqn.py:859-997) on the device: the
+    # agent's w_approx.weight [1, d] and ω [1, T, 1, 1] are updated in place when they live on the
+    # engine's device (staged through it otherwise); the Adam moments of each test task's {w, ω}
+    # live here, keyed by its ω tensor (the reference keeps them in the torch optimizer).
+    def _on_engine(self, t):
+        dev = self._eng.device
+        if t.device == dev and t.dtype == torch.float32 and t.is_contiguous():
+            return t, False
+        return t.detach().to(dev, torch.float32).contiguous(), True
+
+    def tsf_test_action(self, s_enc, w_approx, omegas):
+        eng = self._engine(1)
+        self._flush()
+        w, _ = self._on_engine(w_approx.weight.detach().reshape(-1))
+        om, _ = self._on_engine(omegas.detach().reshape(-1))
+        return eng.tsf_test_action(s_enc, w, om).to(self._out_device())
+
+    def tsf_test_update(self, w_approx, omegas, phi, r, s, a, s1, a1, *, gamma, beta, lasso, lr_w, wd_w, lr_o, wd_o):
+        eng = self._engine(1)
+        self._flush()
+        key = id(omegas)
+        if key not in self._test_state:
+            self._test_state[key] = [torch.zeros(2 * (self.n_features + self.n_tasks), device=eng.device), 0]
+        st = self._test_state[key]
+        st[1] += 1
+        w, w_staged = self._on_engine(w_approx.weight.detach().reshape(-1))
+        om, om_staged = self._on_engine(omegas.detach().reshape(-1))
+        losses = eng.tsf_test_update(s, s1, a, a1, float(r), phi, w, om, st[0], st[1], gamma, beta, lasso, lr_w, wd_w,
+                                     lr_o, wd_o)
+        with torch.no_grad():
+            if w_staged:
+                w_approx.weight.copy_(w.view_as(w_approx.weight))
+            if om_staged:
+                omegas.copy_(om.view_as(omegas))
+        loss, l2, l1 = (x.to(self._out_device()) for x in losses)
+        return loss, l2, l1
 
     # ------------------------------------------------------------------ ψ
     def get_next_successor(self, state, policy_index):

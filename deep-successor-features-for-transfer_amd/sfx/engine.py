@@ -24,6 +24,13 @@ def _act_code(a) -> int:
     return ACT_CODES[str(a).lower()]
 
 
+def _dev_f32(t: torch.Tensor, device) -> int:
+    """Pointer of a tensor the library updates in place: float32, contiguous, on the engine's device."""
+    if not (torch.is_tensor(t) and t.dtype == torch.float32 and t.is_contiguous() and t.device == torch.device(device)):
+        raise ValueError("expected a contiguous float32 tensor on the engine's device")
+    return t.data_ptr()
+
+
 class SFEngine:
     def __init__(self, T: int, n_s: int, H: int, A: int, d: int, acts: Sequence = ("relu", "relu"),
                  max_batch: int = 32, device=None, stream: Optional[int] = None):
@@ -316,6 +323,34 @@ class SFEngine:
         a = np.empty(self.tsf_Ph, dtype=np.float32)
         check(lib.sfx_tsf_get_h(self._h, fptr(a)), "sfx_tsf_get_h")
         return torch.from_numpy(a)
+
+    # ---------------------------------------------------------------- TSF test tasks
+    def tsf_test_action(self, s, w: torch.Tensor, omega: torch.Tensor, out: Optional[torch.Tensor] = None):
+        """TSFDQN.get_test_action's greedy branch (tsfdqn.py:859-870): a 0-d int64 device tensor.
+        w [d] / omega [T] are float32 device tensors, read in place."""
+        s = self._f(s, (-1,))
+        out = torch.empty((), dtype=torch.long, device=self.device) if out is None else out
+        check(lib.sfx_tsf_test_action(self._h, s.data_ptr(), _dev_f32(w, self.device), _dev_f32(omega, self.device),
+                                      out.data_ptr()), "sfx_tsf_test_action")
+        return out
+
+    def tsf_test_update(self, s, s1, a, a1, r: float, phi, w: torch.Tensor, omega: torch.Tensor,
+                        adam_state: torch.Tensor, step: int, gamma: float, beta: float, lasso: float,
+                        lr_w: float, wd_w: float, lr_omega: float, wd_omega: float,
+                        losses: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """TSFDQN.update_test_reward_mapper (tsfdqn.py:917-997): updates w, omega and adam_state
+        ([2d + 2T], zeros initially) in place; returns losses [3] = (loss, l2, l1)."""
+        s, s1 = self._f(s, (-1,)), self._f(s1, (-1,))
+        phi = self._f(phi, (-1,))
+        a, a1 = self._l(a), self._l(a1)
+        if losses is None:
+            losses = torch.empty(3, device=self.device)
+        check(lib.sfx_tsf_test_update(self._h, s.data_ptr(), s1.data_ptr(), a.data_ptr(), a1.data_ptr(), float(r),
+                                      phi.data_ptr(), _dev_f32(w, self.device), _dev_f32(omega, self.device),
+                                      _dev_f32(adam_state, self.device), int(step), float(gamma), float(beta),
+                                      float(lasso), float(lr_w), float(wd_w), float(lr_omega), float(wd_omega),
+                                      losses.data_ptr()), "sfx_tsf_test_update")
+        return losses
 
     def tsf_update(self, policy: int, s, a, r, phi, s1, gamma, use_gpi: bool = True,
                    losses: Optional[torch.Tensor] = None, next_actions: Optional[torch.Tensor] = None):

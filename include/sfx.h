@@ -354,6 +354,23 @@ int sfx_tsf_update(sfx_t h, int policy, const float* S_dev, const int64_t* a_dev
                    const float* phi_dev, const float* S1_dev, const float* gamma_dev, int B, int use_gpi,
                    float* losses_dev, int64_t* next_dev);
 
+/* TSF test tasks.  A test task mixes the source tasks with ω (omega_dev [T],
+ * the reference's [1, T, 1, 1] tensor) and fits its reward weights w_dev [d] and ω by Adam.
+ * sfx_tsf_test_action: TSFDQN.get_test_action's greedy branch (tsfdqn.py:859-870),
+ *   a_dev [1] = argmax_a w·Σ_t ω̂_t ψ_t(s)[a], ω̂ = ω / Σω (first index on ties).
+ * sfx_tsf_test_update: TSFDQN.update_test_reward_mapper (tsfdqn.py:917-997) for the transition
+ *   (s, a, r, φ, s1) and the next test action a1: l1 = MSE(Σ ω̂ ψ_t(s)[a], φ̃ + γ Σ ω̂ ψ⁻_t(s1)[a1]),
+ *   l2 = (w·φ̃ - r)², loss = l1 + β l2 + lasso·Σ|ω|, φ̃ = φ ⊙ (h(Σ ω̂ g_t(s)) + h(Σ ω̂ g_t(s1)));
+ *   one Adam step (number `step`, 1-based) on w (lr_w, wd_w) and ω (lr_omega, wd_omega) with
+ *   their moments in adam_state_dev [2d + 2T] (m_w, v_w, m_ω, v_ω; zeros initially), then
+ *   ω >= 1e-7.  losses_dev [3] = (loss, l2, l1), the reference's return order.  a_dev / a1_dev
+ *   are device int64 scalars (the agent's action tensors).  After sfx_tsf_setup. */
+int sfx_tsf_test_action(sfx_t h, const float* s_dev, const float* w_dev, const float* omega_dev, int64_t* a_dev);
+int sfx_tsf_test_update(sfx_t h, const float* s_dev, const float* s1_dev, const int64_t* a_dev, const int64_t* a1_dev,
+                        float r, const float* phi_dev, float* w_dev, float* omega_dev, float* adam_state_dev,
+                        int step, float gamma, float beta, float lasso, float lr_w, float wd_w, float lr_omega,
+                        float wd_omega, float* losses_dev);
+
 /* ---------------------------------------------------------------------------------------
  * TSF-DQN with the source-task heads sharded across ranks (BASELINE config C5: tsfdqn_nf.py,
  * 32 tasks over 4 GPUs).  After sfx_shard_setup and sfx_tsf_setup; `policy` and
