@@ -526,3 +526,124 @@ def tsf_test_update(st: "TSFState", tm: TestMapper, s, a: int, r: float, phi, s1
     adam_(tm.omega, om.grad, tm.om, tm.ov, tm.step, lr_o, weight_decay=wd_o)
     tm.omega.clamp_(1e-7)
     return float(loss.detach()), float(l2.detach()), float(l1.detach())
+
+
+# --------------------------------------------------------------------------------------
+# Learned φ: features/deep_phi.py DeepSF_PHI.update_successor (:93-224),
+# the library of main_sfdqn_phi_torch.py with agents/sfdqn_phi.py.  φ = phi_net(s ⊕ a ⊕ s1) is an
+# MLP (main_sfdqn_phi_torch.py phi_model_lambda: Linear(in, 2in) + ReLU, three more
+# Linear(2in, 2in) + ReLU, Linear(2in, d)); the reward model w_i is nn.Linear(d, 1) WITH bias
+# (features/deep_phi.py:280); the TD targets φ + γ ψ⁻_i(s1)[a'] carry φ's gradient; loss =
+# MSE(w_i(φ), r) + λ_i MSE(ψ_i(s), merged) with λ_i the agent's loss coefficient; the update
+# builds a NEW torch Adam every call (so every parameter moves by Adam's first step,
+# lr·g/(|g| + eps) up to rounding) over {ψ_i, φ, w_i} and λ_i with maximize=True, then clamps
+# λ_i to [1e-2, 1e6].
+# --------------------------------------------------------------------------------------
+@dataclass
+class PhiSpec:
+    n_s: int
+    d: int
+    width_mul: int = 2   # hidden width = width_mul * in
+    n_mid: int = 3       # Linear(hidden, hidden) layers between the first and the last
+
+    @property
+    def n_in(self) -> int:
+        return 2 * self.n_s + 1
+
+    @property
+    def dims(self) -> List[Tuple[int, int]]:
+        """(out, in) of each Linear."""
+        hdim = self.width_mul * self.n_in
+        return [(hdim, self.n_in)] + [(hdim, hdim)] * self.n_mid + [(self.d, hdim)]
+
+    @property
+    def P(self) -> int:
+        return sum(o * i + o for o, i in self.dims)
+
+
+def phi_unpack(flat: torch.Tensor, ps: PhiSpec):
+    out, off = [], 0
+    for o, i in ps.dims:
+        W = flat[off:off + o * i].view(o, i); off += o * i
+        b = flat[off:off + o]; off += o
+        out.append((W, b))
+    return out
+
+
+def phi_forward(flat, ps: PhiSpec, X):
+    layers = phi_unpack(flat, ps)
+    y = X
+    for l, (W, b) in enumerate(layers):
+        y = F.linear(y, W, b)
+        if l < len(layers) - 1:
+            y = torch.relu(y)
+    return y
+
+
+def fresh_adam_(p: torch.Tensor, g: torch.Tensor, lr: float, maximize: bool = False) -> None:
+    """One step of a freshly built torch Adam (moments zero, step 1)."""
+    adam_(p, -g if maximize else g, torch.zeros_like(p), torch.zeros_like(p), 1, lr)
+
+
+@dataclass
+class PhiState:
+    spec: Spec
+    pspec: PhiSpec
+    online: torch.Tensor   # [T, P]
+    target: torch.Tensor   # [T, P]
+    w: torch.Tensor        # [T, d]  Linear(d, 1).weight rows
+    wb: torch.Tensor       # [T]     Linear(d, 1).bias
+    phi: torch.Tensor      # [Pphi]  the shared φ net
+    lam: torch.Tensor      # [T]     the agent's loss coefficients
+    since_target: List[int] = field(default_factory=list)
+
+    def __post_init__(self):
+        if not self.since_target:
+            self.since_target = [0] * self.online.shape[0]
+
+
+def phi_update(st: PhiState, batch, i: int, *, use_gpi: bool = True, lr: float = 1e-3, target_update_ev: int = 1000):
+    """DeepSF_PHI.update_successor(transitions, phis_model, i, loss_coefficient, use_gpi) ->
+    (loss, psi_loss, phi_loss, λ_i) and the next actions; st is updated in place.  Gradients by
+    autograd, as the reference's loss.backward()."""
+    s, a, r, _, s1, gamma = batch
+    spec = st.spec
+    B = s.shape[0]
+    idx = torch.arange(B)
+    gamma = gamma.reshape(-1, 1)
+    with torch.no_grad():
+        if use_gpi:
+            q1 = torch.matmul(psi_all(st.online, spec, s1), st.w[i].reshape(-1, 1))[..., 0] + st.wb[i]
+            nxt = torch.argmax(torch.max(q1, dim=1).values, dim=-1)
+        else:
+            q1 = torch.matmul(forward(st.online[i], spec, s1)[0], st.w[i].reshape(-1, 1))[..., 0] + st.wb[i]
+            nxt = torch.argmax(q1, dim=1)
+        tpsi = forward(st.target[i], spec, s1)[0]
+    pt = st.online[i].clone().requires_grad_(True)
+    ph = st.phi.clone().requires_grad_(True)
+    w = st.w[i].clone().requires_grad_(True)
+    wb = st.wb[i].clone().reshape(1).requires_grad_(True)
+    lam = st.lam[i].clone().reshape(1).requires_grad_(True)
+    inp = torch.cat([s, a.reshape(B, 1).to(s.dtype), s1], dim=1)
+    phis = phi_forward(ph, st.pspec, inp)
+    cur = forward(pt, spec, s)[0]
+    targets = phis + gamma * tpsi[idx, nxt, :]
+    merged = cur.clone()
+    merged[idx, a, :] = targets
+    r_fit = F.linear(phis, w.reshape(1, -1), wb)
+    phi_loss = F.mse_loss(r_fit, r.reshape(B, 1))
+    psi_loss = F.mse_loss(cur, merged)
+    loss = phi_loss + lam * psi_loss
+    loss.backward()
+    with torch.no_grad():
+        fresh_adam_(st.online[i], pt.grad, lr)
+        fresh_adam_(st.phi, ph.grad, lr)
+        fresh_adam_(st.w[i], w.grad, lr)
+        fresh_adam_(st.wb[i:i + 1], wb.grad, lr)
+        fresh_adam_(st.lam[i:i + 1], lam.grad, lr, maximize=True)
+        st.lam[i:i + 1].clamp_(1e-2, 1e6)
+    st.since_target[i] += 1
+    if st.since_target[i] >= target_update_ev:
+        st.target[i].copy_(st.online[i])
+        st.since_target[i] = 0
+    return float(loss.detach()), float(psi_loss.detach()), float(phi_loss.detach()), float(st.lam[i]), nxt

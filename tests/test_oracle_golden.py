@@ -167,3 +167,38 @@ def test_tsf_test_path_matches_reference(golden, case):
         close([loss, l2, l1], [g["loss"][j], g["l2"][j], g["l1"][j]], rtol=1e-5, atol=1e-8)
         close(tm.w, g["w"][j], rtol=1e-5, atol=1e-8)
         close(tm.omega, g["omega"][j], rtol=1e-5, atol=1e-8)
+
+
+def phi_problem(g):
+    """The oracle state of an upd_phi* fixture (tools/gen_golden.py gen_phi)."""
+    spec = spec_of(g)
+    T = int(g["T"])
+    online0 = torch.from_numpy(g["online0"])
+    st = R.PhiState(spec, R.PhiSpec(spec.n_s, spec.d), online0.clone(), online0.clone(),
+                    torch.from_numpy(g["w0"]).clone(), torch.from_numpy(g["wb0"]).clone(),
+                    torch.from_numpy(g["phi0"]).clone(), torch.ones(T))
+    return st
+
+
+def phi_batches(g):
+    return [tuple(torch.from_numpy(g[f"b_{n}"][j]) for n in ("s", "a", "r", "phi", "s1", "gamma"))
+            for j in range(int(g["k"]))]
+
+
+@pytest.mark.parametrize("case", ["phi_gpi", "phi_nogpi"])
+def test_phi_update_matches_reference(golden, case):
+    """features/deep_phi.py DeepSF_PHI.update_successor (learned φ): losses, the
+    loss coefficient, ψ online / target, w (with bias) and the φ net after k updates."""
+    g = golden("upd_" + case)
+    st = phi_problem(g)
+    assert st.phi.numel() == st.pspec.P
+    for j, b in enumerate(phi_batches(g)):
+        loss, psi_loss, phi_loss, lam, _ = R.phi_update(st, b, int(g["policies"][j]), use_gpi=bool(g["use_gpi"]),
+                                                        target_update_ev=int(g["target_update_ev"]))
+        close([loss, psi_loss, phi_loss, lam], g["losses"][j], rtol=1e-5, atol=1e-8)
+    close(st.online, g["online"], rtol=1e-4, atol=1e-6)
+    close(st.target, g["target"], rtol=1e-4, atol=1e-6)
+    close(st.w, g["w"], rtol=1e-4, atol=1e-6)
+    close(st.wb, g["wb"], rtol=1e-4, atol=1e-6)
+    close(st.phi, g["phi"], rtol=1e-4, atol=1e-6)
+    close(st.lam, g["lam"], rtol=1e-6)

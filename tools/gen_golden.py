@@ -60,6 +60,7 @@ import sfdqn as ref_sfdqn          # noqa: E402
 import tsfdqn as ref_tsfdqn        # noqa: E402
 import tsfdqn_nf as ref_tsfdqn_nf  # noqa: E402
 from features import deep as ref_deep  # noqa: E402
+from features import deep_phi as ref_deep_phi  # noqa: E402
 
 HYPER = {
     "learning_rate_sf": 1e-3, "learning_rate_w": 1e-3, "learning_rate_g": 1e-3,
@@ -650,6 +651,7 @@ def main():
     gen_tsf("tsf", ref_tsfdqn, SHAPES["hopper11"], 3, 8, 0)
     gen_tsf("tsf_nf", ref_tsfdqn_nf, SHAPES["hopper11"], 3, 6, 3)
     gen_tsf_tests()
+    gen_phis()
     gen_call_logs()
     print("golden vectors written to", os.path.abspath(OUT))
 
@@ -657,6 +659,58 @@ def main():
 def gen_tsf_tests():
     gen_tsf_test("tsf", ref_tsfdqn, SHAPES["hopper11"], 3, 10, 0)
     gen_tsf_test("tsf_nf", ref_tsfdqn_nf, SHAPES["hopper11"], 3, 10, 3)
+
+
+def phi_net(n_s, d):
+    """main_sfdqn_phi_torch.py's phi_model_lambda (its model only): in = 2 n_s + 1 (s, a, s1)."""
+    n_in = 2 * n_s + 1
+    return torch.nn.Sequential(
+        torch.nn.Linear(n_in, n_in * 2), torch.nn.ReLU(),
+        torch.nn.Linear(n_in * 2, n_in * 2), torch.nn.ReLU(),
+        torch.nn.Linear(n_in * 2, n_in * 2), torch.nn.ReLU(),
+        torch.nn.Linear(n_in * 2, n_in * 2), torch.nn.ReLU(),
+        torch.nn.Linear(n_in * 2, d))
+
+
+def gen_phi(name, shape, T, k, use_gpi, target_update_ev):
+    """features/deep_phi.py DeepSF_PHI.update_successor (:93-224): k updates of rotating policies
+    with the agent's (agents/sfdqn_phi.py) φ model tuple and per-task loss coefficients."""
+    torch.manual_seed(900 + int(use_gpi))
+    n_s, H, A, d, acts = shape
+    sf = ref_deep_phi.DeepSF_PHI(pytorch_model_handle=psi_lambda(H, acts), use_true_reward=False,
+                                 target_update_ev=target_update_ev)
+    sf.reset()
+    for t in range(T):
+        sf.add_training_task(SynthTask(n_s, A, d, t))
+    pm = phi_net(n_s, d)
+    phis_model = ((pm, torch.nn.MSELoss(), None), (None, None, None))
+    lams = [torch.ones(1, requires_grad=True) for _ in range(T)]
+    rec = dict(n_s=n_s, H=H, A=A, d=d, T=T, acts=np.array(acts), k=k, use_gpi=int(use_gpi),
+               target_update_ev=target_update_ev,
+               online0=np_(torch.stack([flat(sf.psi[t][0][0]) for t in range(T)])),
+               w0=np_(torch.stack([sf.fit_w[t].weight.detach().reshape(-1).clone() for t in range(T)])),
+               wb0=np_(torch.stack([sf.fit_w[t].bias.detach().reshape(-1).clone() for t in range(T)]).reshape(-1)),
+               phi0=np_(flat(pm)))
+    batches = batch_stream(n_s, A, d, 32, k, torch.Generator().manual_seed(19))
+    rec.update(stack_batches(batches))
+    out, policies = [], []
+    for j, b in enumerate(batches):
+        i = (3 * j) % T
+        policies.append(i)
+        loss, psi_loss, phi_loss, lam = sf.update_successor(b, phis_model, i, lams[i], use_gpi)
+        out.append([float(loss), float(psi_loss), float(phi_loss), float(lam)])
+    rec.update(policies=np.array(policies), losses=np.array(out),
+               online=np_(torch.stack([flat(sf.psi[t][0][0]) for t in range(T)])),
+               target=np_(torch.stack([flat(sf.psi[t][1][0]) for t in range(T)])),
+               w=np_(torch.stack([sf.fit_w[t].weight.detach().reshape(-1).clone() for t in range(T)])),
+               wb=np_(torch.stack([sf.fit_w[t].bias.detach().reshape(-1).clone() for t in range(T)]).reshape(-1)),
+               phi=np_(flat(pm)), lam=np.array([float(x) for x in lams]))
+    np.savez_compressed(os.path.join(OUT, f"upd_{name}.npz"), **rec)
+
+
+def gen_phis():
+    gen_phi("phi_gpi", SHAPES["reacher17"], 3, 8, True, 3)
+    gen_phi("phi_nogpi", SHAPES["reacher17"], 3, 6, False, 1000)
 
 
 if __name__ == "__main__":
