@@ -30,6 +30,7 @@
 
 #include "sfx_kernels.h"
 #include "sfx_tsf.h"
+#include "sfx_phi.h"
 #include "../../include/sfx.h"
 
 using namespace sfx;
@@ -132,6 +133,7 @@ struct sfx_handle {
   // sharded heads (sfx_shard_*): this handle's heads are global [off, off + T) of Tg; w has Tg rows
   int Tg = 0, off = 0;
   struct sfx_tsf_state* tsf = nullptr;  // TSF-DQN state (sfx_tsf_setup)
+  struct sfx_phi_state* phi = nullptr;  // learned φ (sfx_phi_setup)
   // collective of the sharded step (sfx_comm_init / sfx_set_comm / sfx_set_comm_host): all-reduce
   // (MAX) of fp32 buffers over the ranks that share the source tasks
   int comm_rank = 0, comm_world = 0;  // world 0: no communicator
@@ -390,8 +392,9 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
 
 int run_tdg(sfx_handle* h, int pol0, int npol, int guess, int M, int use_gpi, const int64_t* a, const float* phi,
             const float* gamma, int64_t* next, int next_stride, int* flag = nullptr, const int* xmax = nullptr,
-            int poloff = 0) {
+            int poloff = 0, const float* dz_scale = nullptr) {
   TdgArgs A{};
+  A.dz_scale = dz_scale;
   A.xmax = xmax;
   A.poloff = poloff;
   A.M = M;
@@ -430,6 +433,9 @@ struct TdgSpec {
   // rounds r >= 1: round r-1's next actions; policies that repeat them skip (BwdArgs::tdg_prev)
   const int64_t* prev = nullptr;
   bool skip = false;
+  // learned φ (sfx_phi.inc): output gradient scaled by a device scalar, a fresh Adam per update
+  const float* dz_scale = nullptr;
+  bool fresh_adam = false;
 };
 
 // 0: K2 as its own launch; 1: fused, d <= 8; 2: fused, d <= 16 (see tdg_rows)
@@ -466,7 +472,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   if (!fuse && td.xi_dst) SFX_FAIL(SFX_E_STATE, "run_bwd: maxima re-initialisation needs the fused TD launch");
   if (!fuse)
     RC(run_tdg(h, head0, nhead, td.guess, M, td.use_gpi, td.a, phi, td.gamma, td.next, td.next_stride, td.flag,
-               td.xmax, td.poloff));
+               td.xmax, td.poloff, td.dz_scale));
   BwdArgs A{};
   A.xcd = h->xcd && nhead > 1 ? 1 : 0;
   A.nhead = nhead;
@@ -481,6 +487,8 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.tdg_poloff = td.poloff;
   A.flag = td.flag;
   A.flag_value = h->T;
+  A.dz_scale = td.dz_scale;
+  A.fresh_adam = td.fresh_adam ? 1 : 0;
   const bool armed = fuse && td.skip && !h->rec && M <= 32;  // k_round's recorded launches never skip
   if (armed) {
     A.tdg_prev = td.prev;
@@ -506,7 +514,10 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   // opt-in 64 x 64 dW tiles (role_dw_wide) for wide hidden layers when several heads share a
   // launch, which then stays within about one workgroup per CU (measured: no gain)
   auto dw_nw = [&](int l) {
-    return l >= 1 && h->dw_wide && !h->bf16 && !h->rec && nhead >= 4 && h->L[l].N >= 128 && h->L[l].K >= 64 ? 2 : 1;
+    return l >= 1 && h->dw_wide && !h->bf16 && !td.fresh_adam && !h->rec && nhead >= 4 && h->L[l].N >= 128 &&
+                   h->L[l].K >= 64
+               ? 2
+               : 1;
   };
   auto dw_tiles = [&](int l) { return cdiv(h->L[l].N, 32 * dw_nw(l)) * cdiv(h->L[l].K, 64); };
   auto geo = [&](int l) {
@@ -1069,11 +1080,13 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
 }
 
 void tsf_release(sfx_handle* h);
+void phi_release(sfx_handle* h);
 
 int sfx_destroy(sfx_t h) {
   if (!h) return SFX_OK;
   (void)hipStreamSynchronize(h->stream);
   tsf_release(h);
+  phi_release(h);
   free_all(h);
   delete h;
   return SFX_OK;
@@ -1448,3 +1461,4 @@ int sfx_synchronize(sfx_t h) {
 #include "sfx_shard.inc"
 #include "sfx_runner.inc"
 #include "sfx_tsf.inc"
+#include "sfx_phi.inc"

@@ -324,6 +324,49 @@ class SFEngine:
         check(lib.sfx_tsf_get_h(self._h, fptr(a)), "sfx_tsf_get_h")
         return torch.from_numpy(a)
 
+    # ---------------------------------------------------------------- learned φ
+    def phi_setup(self, width_mul: int = 2, n_mid: int = 3, lr: float = 1e-3):
+        """features/deep_phi.py's learned φ (main_sfdqn_phi_torch.py phi_model_lambda shape)."""
+        check(lib.sfx_phi_setup(self._h, int(width_mul), int(n_mid), float(lr)), "sfx_phi_setup")
+        self.phi_numel = lib.sfx_phi_numel(self._h)
+
+    def phi_load(self, params):
+        a = np.ascontiguousarray(torch.as_tensor(params).detach().cpu().reshape(-1).numpy(), dtype=np.float32)
+        if a.size != self.phi_numel:
+            raise ValueError(f"φ net has {self.phi_numel} parameters, got {a.size}")
+        check(lib.sfx_phi_load(self._h, fptr(a)), "sfx_phi_load")
+
+    def phi_get(self) -> torch.Tensor:
+        a = np.empty(self.phi_numel, dtype=np.float32)
+        check(lib.sfx_phi_get(self._h, fptr(a)), "sfx_phi_get")
+        return torch.from_numpy(a)
+
+    def phi_task(self, t: int, bias: Optional[float] = None, lam: Optional[float] = None):
+        """Task t's reward-model bias and loss coefficient λ: set the given ones, return both."""
+        out = np.empty(2, dtype=np.float32)
+        check(lib.sfx_phi_task(self._h, int(t), None, fptr(out)), "sfx_phi_task")
+        if bias is not None or lam is not None:
+            new = np.array([out[0] if bias is None else bias, out[1] if lam is None else lam], dtype=np.float32)
+            check(lib.sfx_phi_task(self._h, int(t), fptr(new), None), "sfx_phi_task")
+            out = new
+        return float(out[0]), float(out[1])
+
+    def phi_update(self, policy: int, s, a, r, s1, gamma, use_gpi: bool = True,
+                   losses: Optional[torch.Tensor] = None, next_actions: Optional[torch.Tensor] = None):
+        """DeepSF_PHI.update_successor (features/deep_phi.py:93-224): losses [4] = (loss, psi_loss,
+        phi_loss, λ after the step)."""
+        s, s1 = self._f(s), self._f(s1)
+        B = s.shape[0]
+        a = self._l(a)
+        gamma = self._f(gamma, (B,))
+        r = self._f(r, (B,))
+        if losses is None:
+            losses = torch.empty(4, device=self.device)
+        check(lib.sfx_phi_update(self._h, int(policy), s.data_ptr(), a.data_ptr(), r.data_ptr(), s1.data_ptr(),
+                                 gamma.data_ptr(), B, int(bool(use_gpi)), losses.data_ptr(), dptr(next_actions)),
+              "sfx_phi_update")
+        return losses
+
     # ---------------------------------------------------------------- TSF test tasks
     def tsf_test_action(self, s, w: torch.Tensor, omega: torch.Tensor, out: Optional[torch.Tensor] = None):
         """TSFDQN.get_test_action's greedy branch (tsfdqn.py:859-870): a 0-d int64 device tensor.

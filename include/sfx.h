@@ -365,6 +365,28 @@ int sfx_tsf_update(sfx_t h, int policy, const float* S_dev, const int64_t* a_dev
  *   their moments in adam_state_dev [2d + 2T] (m_w, v_w, m_ω, v_ω; zeros initially), then
  *   ω >= 1e-7.  losses_dev [3] = (loss, l2, l1), the reference's return order.  a_dev / a1_dev
  *   are device int64 scalars (the agent's action tensors).  After sfx_tsf_setup. */
+/* ---------------------------------------------------------------------------------------
+ * Learned φ: features/deep_phi.py DeepSF_PHI.update_successor (:93-224), the
+ * library of main_sfdqn_phi_torch.py (agents/sfdqn_phi.py).  φ = phi_net(s ⊕ a ⊕ s1), an MLP
+ * Linear(2 n_s + 1, hid) + ReLU, n_mid × (Linear(hid, hid) + ReLU), Linear(hid, d) with
+ * hid = width_mul (2 n_s + 1) (phi_model_lambda: width_mul 2, n_mid 3), shared by the tasks; the
+ * reward model of task t is Linear(d, 1) WITH bias: weight = the handle's w row t, bias and the
+ * agent's loss coefficient λ_t kept here.  sfx_phi_update(i): φ of the minibatch, GPI (or own-ψ)
+ * next actions, targets φ + γ ψ⁻_i(s1)[a'] (they carry φ's gradient), loss = MSE(w_i(φ), r) +
+ * λ_i MSE(ψ_i(s), merged), one step of a freshly built Adam (lr, moments zero, step 1 -- as the
+ * reference builds torch.optim.Adam inside every update) on ψ_i, the φ net, w_i and its bias,
+ * ascent on λ_i, λ_i clamped to [1e-2, 1e6]; target sync as sfx_update.  losses_dev [4] = (loss,
+ * psi_loss, phi_loss, λ_i after the step), the reference's return values.
+ * Packing of the φ net: torch parameters() order (W [out][in], b [out] per Linear). */
+int sfx_phi_setup(sfx_t h, int width_mul, int n_mid, float lr);
+int sfx_phi_numel(sfx_t h);
+int sfx_phi_load(sfx_t h, const float* params_host);
+int sfx_phi_get(sfx_t h, float* params_host);
+/* task t's (bias, λ): set from in_host[2] and/or read into out_host[2] (either may be null) */
+int sfx_phi_task(sfx_t h, int t, const float* in_host, float* out_host);
+int sfx_phi_update(sfx_t h, int policy, const float* S_dev, const int64_t* a_dev, const float* r_dev,
+                   const float* S1_dev, const float* gamma_dev, int B, int use_gpi, float* losses_dev, int64_t* next_dev);
+
 int sfx_tsf_test_action(sfx_t h, const float* s_dev, const float* w_dev, const float* omega_dev, int64_t* a_dev);
 int sfx_tsf_test_update(sfx_t h, const float* s_dev, const float* s1_dev, const int64_t* a_dev, const int64_t* a1_dev,
                         float r, const float* phi_dev, float* w_dev, float* omega_dev, float* adam_state_dev,
