@@ -100,8 +100,7 @@ SIGNATURES = {
     "sfx_phi_numel": (_I, [_VP]),
     "sfx_phi_load": (_I, [_VP, _VP]),
     "sfx_phi_get": (_I, [_VP, _VP]),
-    "sfx_phi_task": (_I, [_VP, _I, _VP, _VP]),
-    "sfx_phi_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP]),
+    "sfx_phi_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _VP]),
     "sfx_tsf_test_update": (_I, [_VP, _VP, _VP, _VP, _VP, _F, _VP, _VP, _VP, _VP, _I] + [_F] * 7 + [_VP]),
 }
 

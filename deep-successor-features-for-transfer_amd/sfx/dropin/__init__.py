@@ -4,8 +4,8 @@
 unchanged on libsfx:
 
 * ``features`` becomes sfx's package in front of the user's: ``features.deep``,
-  ``features.deep_sequential``, ``features.deep_sequential_tsf`` and ``features.successor`` are
-  sfx's SF libraries (every ψ forward, GPI, TD target, backward and Adam step in the gfx950
+  ``features.deep_sequential``, ``features.deep_sequential_tsf``, ``features.deep_phi`` (learned φ)
+  and ``features.successor`` are sfx's SF libraries (every ψ forward, GPI, TD target, backward and Adam step in the gfx950
   kernels of libsfx.so); every other ``features.*`` module stays the user's;
 * the user's single-file modules ``sfdqn``, ``tsfdqn``, ``tsfdqn_nf`` and
   ``agents.tsfdqn_sequential`` load as they are and are then bound (``sfx.dropin.bind``): their
@@ -24,8 +24,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 FEATURES = os.path.join(ROOT, "features")
-OURS = ("features.deep", "features.deep_sequential", "features.deep_sequential_tsf", "features.successor")
-BOUND = ("sfdqn", "tsfdqn", "tsfdqn_nf", "agents.tsfdqn_sequential")
+OURS = ("features.deep", "features.deep_sequential", "features.deep_sequential_tsf", "features.deep_phi",
+        "features.successor")
+BOUND = ("sfdqn", "tsfdqn", "tsfdqn_nf", "agents.tsfdqn_sequential", "agents.sfdqn_phi")
 
 
 class _BindingLoader(importlib.abc.Loader):

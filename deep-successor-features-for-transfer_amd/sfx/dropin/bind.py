@@ -108,6 +108,20 @@ def patch_tsf_agent(cls) -> None:
             setattr(cls, name, _synced(m))
 
 
+def _phi_synced(method):
+    """Run the agent's own method after the device's φ net is copied into the agent's module (its
+    test reward mapper, agents/sfdqn_phi.py update_test_reward_mapper, runs φ in torch)."""
+    @functools.wraps(method)
+    def run(self, *args, **kwargs):
+        sync = getattr(self.sf, "sync_phi_module", None)
+        if sync is not None:
+            sync()
+        return method(self, *args, **kwargs)
+
+    run.__sfx_bound__ = True
+    return run
+
+
 def patch(name: str, module) -> None:
     """Bind the user's freshly loaded module ``name`` to sfx (see the module docstring)."""
     if name == "sfdqn":
@@ -117,3 +131,7 @@ def patch(name: str, module) -> None:
         patch_tsf_agent(module.TSFDQN)
     elif name == "agents.tsfdqn_sequential":
         patch_tsf_agent(module.TSFDQN)
+    elif name == "agents.sfdqn_phi":
+        m = getattr(module.SFDQN_PHI, "test_agent", None)
+        if m is not None and not getattr(m, "__sfx_bound__", False):
+            module.SFDQN_PHI.test_agent = _phi_synced(m)

@@ -341,20 +341,11 @@ class SFEngine:
         check(lib.sfx_phi_get(self._h, fptr(a)), "sfx_phi_get")
         return torch.from_numpy(a)
 
-    def phi_task(self, t: int, bias: Optional[float] = None, lam: Optional[float] = None):
-        """Task t's reward-model bias and loss coefficient λ: set the given ones, return both."""
-        out = np.empty(2, dtype=np.float32)
-        check(lib.sfx_phi_task(self._h, int(t), None, fptr(out)), "sfx_phi_task")
-        if bias is not None or lam is not None:
-            new = np.array([out[0] if bias is None else bias, out[1] if lam is None else lam], dtype=np.float32)
-            check(lib.sfx_phi_task(self._h, int(t), fptr(new), None), "sfx_phi_task")
-            out = new
-        return float(out[0]), float(out[1])
-
-    def phi_update(self, policy: int, s, a, r, s1, gamma, use_gpi: bool = True,
+    def phi_update(self, policy: int, s, a, r, s1, gamma, bias: torch.Tensor, lam: torch.Tensor, use_gpi: bool = True,
                    losses: Optional[torch.Tensor] = None, next_actions: Optional[torch.Tensor] = None):
         """DeepSF_PHI.update_successor (features/deep_phi.py:93-224): losses [4] = (loss, psi_loss,
-        phi_loss, λ after the step)."""
+        phi_loss, λ after the step); bias / lam: one-element float32 device tensors (the policy's
+        reward-model bias and loss coefficient), updated in place."""
         s, s1 = self._f(s), self._f(s1)
         B = s.shape[0]
         a = self._l(a)
@@ -363,8 +354,8 @@ class SFEngine:
         if losses is None:
             losses = torch.empty(4, device=self.device)
         check(lib.sfx_phi_update(self._h, int(policy), s.data_ptr(), a.data_ptr(), r.data_ptr(), s1.data_ptr(),
-                                 gamma.data_ptr(), B, int(bool(use_gpi)), losses.data_ptr(), dptr(next_actions)),
-              "sfx_phi_update")
+                                 gamma.data_ptr(), B, int(bool(use_gpi)), _dev_f32(bias, self.device),
+                                 _dev_f32(lam, self.device), losses.data_ptr(), dptr(next_actions)), "sfx_phi_update")
         return losses
 
     # ---------------------------------------------------------------- TSF test tasks

@@ -371,7 +371,7 @@ int sfx_tsf_update(sfx_t h, int policy, const float* S_dev, const int64_t* a_dev
  * Linear(2 n_s + 1, hid) + ReLU, n_mid × (Linear(hid, hid) + ReLU), Linear(hid, d) with
  * hid = width_mul (2 n_s + 1) (phi_model_lambda: width_mul 2, n_mid 3), shared by the tasks; the
  * reward model of task t is Linear(d, 1) WITH bias: weight = the handle's w row t, bias and the
- * agent's loss coefficient λ_t kept here.  sfx_phi_update(i): φ of the minibatch, GPI (or own-ψ)
+ * agent's loss coefficient λ_t in caller-owned device scalars.  sfx_phi_update(i): φ of the minibatch, GPI (or own-ψ)
  * next actions, targets φ + γ ψ⁻_i(s1)[a'] (they carry φ's gradient), loss = MSE(w_i(φ), r) +
  * λ_i MSE(ψ_i(s), merged), one step of a freshly built Adam (lr, moments zero, step 1 -- as the
  * reference builds torch.optim.Adam inside every update) on ψ_i, the φ net, w_i and its bias,
@@ -382,10 +382,11 @@ int sfx_phi_setup(sfx_t h, int width_mul, int n_mid, float lr);
 int sfx_phi_numel(sfx_t h);
 int sfx_phi_load(sfx_t h, const float* params_host);
 int sfx_phi_get(sfx_t h, float* params_host);
-/* task t's (bias, λ): set from in_host[2] and/or read into out_host[2] (either may be null) */
-int sfx_phi_task(sfx_t h, int t, const float* in_host, float* out_host);
+/* bias_dev / lambda_dev: device scalars of the policy's reward-model bias and loss coefficient λ
+ * (caller-owned, e.g. the agent's tensors), updated in place. */
 int sfx_phi_update(sfx_t h, int policy, const float* S_dev, const int64_t* a_dev, const float* r_dev,
-                   const float* S1_dev, const float* gamma_dev, int B, int use_gpi, float* losses_dev, int64_t* next_dev);
+                   const float* S1_dev, const float* gamma_dev, int B, int use_gpi, float* bias_dev, float* lambda_dev,
+                   float* losses_dev, int64_t* next_dev);
 
 int sfx_tsf_test_action(sfx_t h, const float* s_dev, const float* w_dev, const float* omega_dev, int64_t* a_dev);
 int sfx_tsf_test_update(sfx_t h, const float* s_dev, const float* s1_dev, const int64_t* a_dev, const int64_t* a1_dev,

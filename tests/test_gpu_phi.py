@@ -43,9 +43,15 @@ def engine_of(st: R.PhiState, ev: int, max_batch=32):
         eng.load_w(t, st.w[t])
     eng.phi_setup(st.pspec.width_mul, st.pspec.n_mid, 1e-3)
     eng.phi_load(st.phi)
-    for t in range(T):
-        eng.phi_task(t, bias=float(st.wb[t]), lam=float(st.lam[t]))
+    # the reward-model biases and loss coefficients: caller-owned device scalars (the agent's tensors)
+    eng.test_wb = st.wb.clone().float().to(eng.device)
+    eng.test_lam = st.lam.clone().float().to(eng.device)
     return eng
+
+
+def update(eng, i, s, a, r, s1, gamma, use_gpi, next_actions=None):
+    return eng.phi_update(i, s, a, r, s1, gamma, eng.test_wb[i:i + 1], eng.test_lam[i:i + 1], use_gpi=use_gpi,
+                          next_actions=next_actions)
 
 
 def check_params(eng, st, T, k, frac=2e-3):
@@ -53,9 +59,8 @@ def check_params(eng, st, T, k, frac=2e-3):
     params_close(torch.stack([eng.get_head(t, 1) for t in range(T)]), st.target, 1e-3 * k, max_bad_frac=frac)
     params_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, 1e-3 * k, max_bad_frac=frac)
     params_close(eng.phi_get(), st.phi, 1e-3 * k, max_bad_frac=frac)
-    bl = [eng.phi_task(t) for t in range(T)]
-    params_close(torch.tensor([b for b, _ in bl]), st.wb, 1e-3 * k)
-    rel_close(torch.tensor([l for _, l in bl]), st.lam, rtol=1e-6, atol=1e-7)
+    params_close(eng.test_wb.cpu(), st.wb, 1e-3 * k)
+    rel_close(eng.test_lam.cpu(), st.lam, rtol=1e-6, atol=1e-7)
 
 
 @pytest.mark.parametrize("case", ["phi_gpi", "phi_nogpi"])
@@ -65,7 +70,7 @@ def test_phi_update_vs_golden(golden, case):
     T = int(g["T"])
     eng = engine_of(st0, int(g["target_update_ev"]))
     for j, (s, a, r, _, s1, gamma) in enumerate(phi_batches(g)):
-        lo = eng.phi_update(int(g["policies"][j]), s, a, r, s1, gamma, use_gpi=bool(g["use_gpi"]))
+        lo = update(eng, int(g["policies"][j]), s, a, r, s1, gamma, bool(g["use_gpi"]))
         rel_close(lo.cpu(), g["losses"][j], rtol=1e-4, atol=1e-7)
     ref = R.PhiState(st0.spec, st0.pspec, torch.from_numpy(g["online"]), torch.from_numpy(g["target"]),
                      torch.from_numpy(g["w"]), torch.from_numpy(g["wb"]), torch.from_numpy(g["phi"]),
@@ -96,9 +101,86 @@ def test_phi_update_full_c2_vs_oracle(use_gpi):
         gamma = torch.where(torch.rand(B, generator=gen) < 0.1, 0.0, 0.9)
         loss, psi_loss, phi_loss, lam, na = R.phi_update(st, (s, a, r, None, s1, gamma), i, use_gpi=use_gpi,
                                                          target_update_ev=3)
-        lo = eng.phi_update(i, s, a, r, s1, gamma, use_gpi=use_gpi, next_actions=nxt)
+        lo = update(eng, i, s, a, r, s1, gamma, use_gpi, next_actions=nxt)
         assert torch.equal(nxt.cpu(), na), f"update {j}: next actions"
         rel_close(lo.cpu(), [loss, psi_loss, phi_loss, lam], rtol=1e-4, atol=1e-7)
     check_params(eng, st, T, k)
     eng.close()
     np.testing.assert_equal(k, 5)
+
+
+class _Task:
+    """tasks/task.py interface, enough for add_training_task."""
+
+    def __init__(self, n_s, A, d, idx):
+        self.n_s, self.A, self.d, self.idx = n_s, A, d, idx
+
+    def action_count(self):
+        return self.A
+
+    def feature_dim(self):
+        return self.d
+
+    def encode_dim(self):
+        return self.n_s
+
+    def get_w(self):
+        w = torch.zeros(self.d, 1)
+        w[self.idx % self.d, 0] = 1.0
+        return w
+
+
+def test_dropin_deepsf_phi_vs_golden(golden, monkeypatch):
+    """sfx.dropin's features.deep_phi.DeepSF_PHI with the reference's call convention
+    (update_successor(transitions, phis_model, i, loss_coefficient, use_gpi), agents/sfdqn_phi.py):
+    the golden run's losses, the agent's loss coefficients and reward-model biases updated in place,
+    and -- after sync_phi_module -- the agent's φ net, ψ modules and fit_w as the reference left them."""
+    from sfx.dropin import _host
+    from sfx.dropin.features.deep import _flat, _unflat_into
+    from sfx.dropin.features.deep_phi import DeepSF_PHI
+    from tests.golden.recipe import agent_psi_lambda
+
+    dev = torch.device("cuda", 0)
+    monkeypatch.setattr(_host, "torch_device", lambda: dev)
+    monkeypatch.setattr("sfx.dropin.features.deep.get_torch_device", lambda: dev)
+    g = golden("upd_phi_gpi")
+    spec = R.Spec(int(g["n_s"]), int(g["H"]), int(g["A"]), int(g["d"]), tuple(str(a) for a in g["acts"]))
+    T = int(g["T"])
+    sf = DeepSF_PHI(pytorch_model_handle=agent_psi_lambda(spec.H, spec.acts, 1e-3, dev), use_true_reward=False,
+                    target_update_ev=int(g["target_update_ev"]))
+    sf.reset()
+    for t in range(T):
+        sf.add_training_task(_Task(spec.n_s, spec.A, spec.d, t))
+    with torch.no_grad():
+        for t in range(T):
+            _unflat_into(sf.psi[t][0][0], torch.from_numpy(g["online0"][t]))
+            _unflat_into(sf.psi[t][1][0], torch.from_numpy(g["online0"][t]))
+            lin = list.__getitem__(sf.fit_w, t)
+            lin.weight.copy_(torch.from_numpy(g["w0"][t]).view(1, -1))
+            lin.bias.copy_(torch.from_numpy(g["wb0"][t:t + 1]))
+    n_in = 2 * spec.n_s + 1
+    layers = [torch.nn.Linear(n_in, 2 * n_in), torch.nn.ReLU()]
+    for _ in range(3):
+        layers += [torch.nn.Linear(2 * n_in, 2 * n_in), torch.nn.ReLU()]
+    pm = torch.nn.Sequential(*layers, torch.nn.Linear(2 * n_in, spec.d)).to(dev)
+    _unflat_into(pm, torch.from_numpy(g["phi0"]))
+    phis_model = ((pm, torch.nn.MSELoss(), None), (None, None, None))
+    lams = [torch.ones(1, requires_grad=True, device=dev) for _ in range(T)]
+    lam_ptrs = [x.data_ptr() for x in lams]
+    for j, b in enumerate(phi_batches(g)):
+        b = tuple(x.to(dev) for x in b)
+        i = int(g["policies"][j])
+        loss, psi_loss, phi_loss, lam = sf.update_successor(b, phis_model, i, lams[i], True)
+        assert lam is lams[i]
+        rel_close(torch.cat([loss, psi_loss, phi_loss, lam.detach()]).cpu(), g["losses"][j], rtol=1e-4, atol=1e-7)
+    assert [x.data_ptr() for x in lams] == lam_ptrs
+    rel_close(torch.cat([x.detach() for x in lams]).cpu(), g["lam"], rtol=1e-6, atol=1e-7)
+    sf.sync_phi_module()
+    k = int(g["k"])
+    params_close(_flat(pm), g["phi"], 1e-3 * k, max_bad_frac=2e-3)
+    params_close(torch.stack([_flat(sf.psi[t][0][0]) for t in range(T)]), g["online"], 1e-3 * k, max_bad_frac=2e-3)
+    params_close(torch.stack([sf.fit_w[t].weight.detach().reshape(-1).cpu() for t in range(T)]), g["w"], 1e-3 * k)
+    params_close(torch.stack([sf.fit_w[t].bias.detach().reshape(-1).cpu() for t in range(T)]).reshape(-1), g["wb"],
+                 1e-3 * k)
+    q, task = sf.GPI(torch.from_numpy(g["b_s"][0][:4]).to(dev), 0)
+    assert q.shape == (4, T, spec.A) and task.shape == (4,)
