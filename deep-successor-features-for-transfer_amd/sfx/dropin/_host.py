@@ -10,12 +10,20 @@ import sys
 import torch
 
 
+_absent_on = None  # sys.path for which importing utils.torch last failed (a failed import is not cached by Python)
+
+
 def torch_device():
+    global _absent_on
     mod = sys.modules.get("utils.torch")
     if mod is None:
+        path = tuple(sys.path)
+        if path == _absent_on:
+            return None
         try:
             import utils.torch as mod  # the user's checkout
         except ImportError:
+            _absent_on = path
             return None
     get = getattr(mod, "get_torch_device", None)
     return get() if get is not None else getattr(mod, "device", None)

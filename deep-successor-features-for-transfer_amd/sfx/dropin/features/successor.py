@@ -15,7 +15,7 @@ from sfx.dropin._host import torch_device as get_torch_device
 class SF:
     def __init__(self, *args, use_true_reward=False, **kwargs):
         self.use_true_reward = use_true_reward
-        self.hyperparameters = kwargs.get("hyperparameters", {})
+        self.hyperparameters = kwargs.pop("hyperparameters", {})
         self.alpha_w = self.hyperparameters.get("learning_rate_w")
         if args or kwargs:
             print(f"{type(self).__name__} ignoring parameters {args} and {kwargs}")
