@@ -433,9 +433,8 @@ struct TdgSpec {
   // rounds r >= 1: round r-1's next actions; policies that repeat them skip (BwdArgs::tdg_prev)
   const int64_t* prev = nullptr;
   bool skip = false;
-  // learned φ (sfx_phi.inc): output gradient scaled by a device scalar, a fresh Adam per update
+  // learned φ (sfx_phi.inc): output gradient scaled by a device scalar
   const float* dz_scale = nullptr;
-  bool fresh_adam = false;
 };
 
 // 0: K2 as its own launch; 1: fused, d <= 8; 2: fused, d <= 16 (see tdg_rows)
@@ -488,7 +487,6 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.flag = td.flag;
   A.flag_value = h->T;
   A.dz_scale = td.dz_scale;
-  A.fresh_adam = td.fresh_adam ? 1 : 0;
   const bool armed = fuse && td.skip && !h->rec && M <= 32;  // k_round's recorded launches never skip
   if (armed) {
     A.tdg_prev = td.prev;
@@ -514,7 +512,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   // opt-in 64 x 64 dW tiles (role_dw_wide) for wide hidden layers when several heads share a
   // launch, which then stays within about one workgroup per CU (measured: no gain)
   auto dw_nw = [&](int l) {
-    return l >= 1 && h->dw_wide && !h->bf16 && !td.fresh_adam && !h->rec && nhead >= 4 && h->L[l].N >= 128 &&
+    return l >= 1 && h->dw_wide && !h->bf16 && !h->rec && nhead >= 4 && h->L[l].N >= 128 &&
                    h->L[l].K >= 64
                ? 2
                : 1;

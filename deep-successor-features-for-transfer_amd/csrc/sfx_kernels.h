@@ -959,10 +959,8 @@ struct BwdArgs {
   int* skip;
   unsigned long long* skipc;
   int skip_v0, pad4_;  // skipped heads' layer-0 tiles: 1 = the post-update forward skips them too
-  // learned φ (features/deep_phi.py): the output gradient scaled by λ (device scalar), and the
-  // parameters stepped by a freshly built Adam (zero moments, step 1) as the reference does
+  // learned φ (features/deep_phi.py): the output gradient scaled by λ (device scalar)
   const float* dz_scale;
-  int fresh_adam, pad5_;
 };
 
 __device__ __forceinline__ const float* layer_input(const Geo& G, const BwdArgs& A, int head, int xOff) {
@@ -1372,8 +1370,7 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
   float* Pw = G.online + wo;
   float* Mw = G.am + wo;
   float* Vw = G.av + wo;
-  const bool fresh = A.fresh_adam != 0;  // learned φ: a new Adam per update (moments 0, step 1)
-  const AdamC c = fresh ? adam_consts(A.hp, 1) : load_adamc<C>(G.adamc + head);  // double pow once per head
+  const AdamC c = load_adamc<C>(G.adamc + head);  // bias corrections of this step (double pow once per head)
   const int cx = step_cancelled(G.cancel);
   const int nn = n0 + r, kb0 = k0 + r, kb1 = k0 + 16 + r;
   // prefetch the optimizer state of the 8 weights this lane will update
@@ -1389,8 +1386,8 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
       ok[e] = n < N && k < K;
       const size_t off = (size_t)L.wOff + (size_t)n * K + k;
       pp[e] = ok[e] ? Pr[off] : 0.f;
-      pm[e] = ok[e] && !fresh ? Mr[off] : 0.f;
-      pv[e] = ok[e] && !fresh ? Vr[off] : 0.f;
+      pm[e] = ok[e] ? Mr[off] : 0.f;
+      pv[e] = ok[e] ? Vr[off] : 0.f;
     }
   }
   // bias of column n0 + r: lane r of waves 0/1 (k-half 0) of the kt == 0 tiles.  Its gradient
@@ -1401,8 +1398,8 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
   float bp = 0.f, bm = 0.f, bv = 0.f;
   if (dob) {
     bp = Pr[L.bOff + nbias];
-    bm = fresh ? 0.f : Mr[L.bOff + nbias];
-    bv = fresh ? 0.f : Vr[L.bOff + nbias];
+    bm = Mr[L.bOff + nbias];
+    bv = Vr[L.bOff + nbias];
   }
   // fused forward input (S1 rows ++ s_next), requested with the rest, parked in LDS below
   constexpr int XQ = VFUSE / 256;
