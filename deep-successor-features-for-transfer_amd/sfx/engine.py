@@ -288,8 +288,13 @@ class SFEngine:
         return {"policies_checked": c.value, "policies_skipped": s.value}
 
     def lms(self, t: int, phi, r, alpha: float):
-        phi = self._f(phi, (-1,))
-        r = self._f(r, (1,))
+        phi, r = torch.as_tensor(phi), torch.as_tensor(r)
+        if phi.device.type == "cpu" and r.device.type == "cpu":  # host values: one copy to the device
+            pr = self._f(torch.cat([phi.reshape(-1).float(), r.reshape(1).float()]))
+            phi, r = pr[:-1], pr[-1:]
+        else:
+            phi = self._f(phi, (-1,))
+            r = self._f(r, (1,))
         check(lib.sfx_lms(self._h, int(t), phi.data_ptr(), r.data_ptr(), float(alpha)), "sfx_lms")
 
     # ---------------------------------------------------------------- TSF-DQN (tsfdqn.py / tsfdqn_nf.py)

@@ -16,7 +16,8 @@ buffers:
   * ``reference``: agents/buffer.py's layout -- an object ring of per-transition device tensors,
     ``torch.vstack`` on the device and ``torch.tensor`` of the per-transition action tensors
     (one device read each) per replay, as the reference's program does;
-  * ``host``: a numpy ring sampled on the host, one host->device copy per field per replay.
+  * ``host``: states and φ kept as numpy arrays, a numpy ring sampled on the host, one
+    host->device copy per field per replay.
 The env, the buffer and the agent logic are the user's program, not the library; the numbers say
 what a user switching libraries gets with each.
 """
@@ -63,11 +64,14 @@ class _Task:
     def get_w(self):
         return torch.from_numpy(self.env.w_true).reshape(-1, 1)
 
-    def initialize(self):
-        return torch.from_numpy(self.env.initialize()).to(self.device)
+    def initialize(self, on_device=True):
+        s = self.env.initialize()
+        return torch.from_numpy(s).to(self.device) if on_device else s
 
-    def transition(self, a):
+    def transition(self, a, on_device=True):
         s1, phi, r, term = self.env.transition(int(a))
+        if not on_device:
+            return s1, phi, r, term
         return torch.from_numpy(s1).to(self.device), torch.from_numpy(phi).to(self.device), r, term
 
 
@@ -148,23 +152,23 @@ class DropinLoop:
         self.s_enc = None
 
     def step(self):
-        task = self.tasks[self.task]
+        task, dev = self.tasks[self.task], self.ref_buffer  # host ring: states and φ stay numpy
         if self.s_enc is None:
-            self.s_enc = task.initialize().reshape(1, -1)
+            self.s_enc = task.initialize(dev).reshape(1, -1)
         q, c = self.sf.GPI(self.s_enc, self.task, update_counters=True)
         q = q[:, c, :].flatten()
         if random.random() <= self.epsilon:
             a = torch.tensor(random.randrange(self.A)).to(self.device)
         else:
             a = torch.argmax(q)
-        s1, phi, r, term = task.transition(a)
+        s1, phi, r, term = task.transition(a, dev)
         s1_enc = s1.reshape(1, -1)
         self.sf.update_reward(phi, r, self.task)
         g = 0.0 if term else self.gamma
         if self.ref_buffer:
             self.buffer.append(self.s_enc, a, phi, s1_enc, g)
         else:
-            self.buffer.append(self.s_enc.cpu().numpy(), int(a), phi.cpu().numpy(), s1.cpu().numpy(), g)
+            self.buffer.append(self.s_enc, int(a), phi, s1, g)
         batch = self.buffer.replay()
         for i in range(self.T):
             self.sf.update_successor(batch, i)
