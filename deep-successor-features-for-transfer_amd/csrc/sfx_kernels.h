@@ -136,8 +136,12 @@ __device__ __forceinline__ float ldc(const float* p) {
 }
 template <bool C>
 __device__ __forceinline__ void stc(float* p, float v) {
+#ifdef SFX_WT_ALL  // experiment: every hand-off store to a later launch write-through too
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
   if constexpr (C) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else *p = v;
+#endif
 }
 template <bool C>
 __device__ __forceinline__ float4 ldc4(const float* p) {  // 16-B aligned
@@ -311,16 +315,17 @@ __device__ __forceinline__ AdamC adam_consts(const AdamHP& hp, int step) {
   return c;
 }
 
-// Adam moments are read again only by the next step's update of the same head: stored
-// non-temporally (measured +1 % env-steps/s on the all-task step, 3 A/B pairs: less dirty L2 for
-// the kernel-boundary writeback; -DSFX_PLAIN_MV restores plain stores)
-__device__ __forceinline__ void st_moment(float* p, float v) {
-#ifdef SFX_PLAIN_MV
-  *p = v;
-#else
-  __builtin_nontemporal_store(v, p);
-#endif
+// The Adam epilogue's stores (parameters, moments: ≈6 MB per dW launch at C2) are write-through
+// (sc1): a kernel boundary costs ≈1.45 µs plus the writeback of what the predecessor left dirty in
+// L2 (MI355X_MICROARCH.md, "boundary": + B / 6 TB/s), and the Adam tiles are the largest writers.
+// A/B on one box (tools/ab_libs.sh): plain parameters + non-temporal moments 7380 / 7396,
+// write-through 7544 / 7567 env-steps/s, non-temporal everything 7357 / 7364.
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void st_moment(float* p, float v) { st_wt(p, v); }
+template <bool C>
+__device__ __forceinline__ void st_param(float* p, float v) { st_wt(p, v); }
 
 __device__ __forceinline__ void adam_apply(float& pp, float& mm, float& vv, float g, const AdamC& c) {
   if (c.wd != 0.f) g = __fadd_rn(g, __fmul_rn(c.wd, pp));
@@ -1459,7 +1464,7 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
         const size_t off = (size_t)L.wOff + (size_t)n * K + k;
         adam_apply(pp[e], pm[e], pv[e], h ? acc1[i] : acc0[i], c);
         if (!cx) {
-          stc<C>(Pw + off, pp[e]);
+          st_param<C>(Pw + off, pp[e]);
           st_moment(Mw + off, pm[e]);
           st_moment(Vw + off, pv[e]);
           if constexpr (BF) G.on16[wo + off] = (__bf16)pp[e];  // the bf16 copy of the write slot
@@ -1471,7 +1476,7 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
   if (dob) {
     adam_apply(bp, bm, bv, bsum, c);
     if (!cx) {
-      stc<C>(Pw + L.bOff + nbias, bp);
+      st_param<C>(Pw + L.bOff + nbias, bp);
       st_moment(Mw + L.bOff + nbias, bm);
       st_moment(Vw + L.bOff + nbias, bv);
       if constexpr (BF) G.on16[wo + L.bOff + nbias] = (__bf16)bp;
@@ -1590,7 +1595,7 @@ __device__ void role_dw_wide(const Geo& G, const BwdArgs& A, int head, const Rol
         if (ok[e] && !cx) {
           const size_t off = (size_t)L.wOff + (size_t)n * K + (h ? kb1 : kb0);
           adam_apply(pp[e], pm[e], pv[e], acc[s][h][i], c);
-          stc<false>(Pw + off, pp[e]);
+          st_param<false>(Pw + off, pp[e]);
           st_moment(Mw + off, pm[e]);
           st_moment(Vw + off, pv[e]);
         }

@@ -94,12 +94,12 @@ def main():
         kinds = tuple(sorted(set(int(k) for k in L["kid"])))
         if 9 in kinds:
             pos = 0
-        key = (pos, kinds, len(L))
+        key = (pos, kinds)
         pos += 1
         t = L["t"].astype(np.int64)
         gap = (t[:, 0].min() - prev_end) * 10e-3 if prev_end is not None else np.nan
         prev_end = t[:, 9].max()
-        row = [(t[:, 0].max() - t[:, 0].min()) * 10e-3, (t[:, 9].max() - t[:, 0].min()) * 10e-3, gap] + marks(L)
+        row = [(t[:, 0].max() - t[:, 0].min()) * 10e-3, (t[:, 9].max() - t[:, 0].min()) * 10e-3, gap] + marks(L) + [len(L)]
         if key not in agg:
             agg[key], sub[key] = [], {k: [] for k in kinds}
             order.append(key)
@@ -114,11 +114,12 @@ def main():
     tot_span = tot_gap = 0.0
     f = lambda x: "    -" if np.isnan(x) else f"{x:5.2f}"
     for key in order:
-        pos, kinds, nwg = key
+        pos, kinds = key
         a = np.array(agg[key], dtype=float)
-        if len(a) < steps // 2:
+        if len(a) < steps // 3:
             continue
         m = np.nanmedian(a, axis=0)
+        nwg = int(m[-1])
         tot_span += m[1]
         tot_gap += 0 if np.isnan(m[2]) else m[2]
         name = "+".join(KIDS.get(k, str(k)) for k in kinds)
