@@ -101,6 +101,7 @@ struct sfx_handle {
   bool fuse_v0 = true;   // SFX_FUSE_V0=0: post-update layer-0 forward as its own launch
   bool xcd = true;       // SFX_XCD=0: plain (tile, head) grids instead of XCD-aware ones
   int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
+  int fwd_tpw = FWD_TPW; // column tiles per workgroup of the layer-0+1 forward; SFX_FWD_TPW=1: one
   bool fuse_l0 = true;   // SFX_FUSE_L0=0: layer 0 of a forward from the states as its own launch
   AdamHP hp_psi{1e-3, 0.0, 0.9, 0.999, 1e-8};
   AdamHP hp_w{1e-3, 0.0, 0.9, 0.999, 1e-8};
@@ -346,6 +347,7 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     F.flag_value = ex.flag_value;
     F.ntN = cdiv(L.N, 16);
     F.ntM = cdiv(M, 32);
+    F.tpw = l0 ? h->fwd_tpw : 1;  // the in-tile layer 0 computed once for tpw column tiles
     const bool qa = ex.qa_role >= 0 && l == h->NL - 1;  // the maxima come from the ψ output layer
     if (qa) {
       F.qa_role = ex.qa_role;
@@ -360,7 +362,8 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
       F.qa_task = ex.qa_task;
       F.qa_use_gpi = ex.qa_use_gpi;
     }
-    const dim3 grid = F.xcd ? dim3(8 * cdiv(h->T, 8) * F.ntN * F.ntM * F.ngroups) : dim3(F.ntN, ninst, F.ntM);
+    const int ntNb = cdiv(F.ntN, F.tpw);
+    const dim3 grid = F.xcd ? dim3(8 * cdiv(h->T, 8) * ntNb * F.ntM * F.ngroups) : dim3(ntNb, ninst, F.ntM);
     double by = 4.0 * ninst * ((double)L.N * L.K + L.N + (double)M * L.K + (double)M * L.N);
     if (l0) by += 4.0 * ninst * ((double)h->L[0].N * h->L[0].K + h->L[0].N + (double)M * h->L[0].K);
     // the vector path needs K % (256/NW) == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
@@ -954,6 +957,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->xcd = !(ex && ex[0] == '0');
   const char* efw = std::getenv("SFX_FWD_WAVES");
   h->fwd_waves = efw && std::atoi(efw) == 4 ? 4 : 8;
+  const char* etp = std::getenv("SFX_FWD_TPW");
+  h->fwd_tpw = etp && etp[0] == '1' ? 1 : FWD_TPW;
   const char* el0 = std::getenv("SFX_FUSE_L0");
   h->fuse_l0 = !(el0 && el0[0] == '0');
   const char* esd = std::getenv("SFX_SPLIT_DX");

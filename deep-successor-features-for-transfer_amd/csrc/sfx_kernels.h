@@ -361,7 +361,7 @@ struct FwdGroup {
 struct FwdArgs {
   int M, N, K, act, wOff, bOff, xOff, yOff;  // xOff < 0: layer input is xa / xb
   int ngroups, lms_head, flag_value, xcd;  // xcd: 1-D XCD-aware grid (every group has heads 0..nh-1)
-  int nh, ntN, ntM, pad2_;
+  int nh, ntN, ntM, tpw;  // tpw: column tiles per workgroup (L0 launches; else 1)
   int w0Off, b0Off, K0, y0Off;  // L0 launches: layer 0 (K0 -> K, identity) computed in-tile, stored at y0Off
   unsigned long long mask;
   FwdGroup g0, g1, g2, g3;
@@ -474,8 +474,13 @@ __device__ __forceinline__ FwdGroup fwd_group(const FwdArgs& F, int& y) {
   return g;
 }
 
+constexpr int FWD_TPW = 2;  // column tiles per workgroup of an L0 launch (FwdArgs::tpw)
+
 template <bool VEC, int NW, bool L0, bool C, bool BF = false>
 __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, int tN, int tM, float* sT = nullptr) {
+  // L0 launches: tiles tN .. tN + tpw - 1 share the workgroup's layer-0 rows (computed once)
+  constexpr int TPW = L0 ? FWD_TPW : 1;
+  const int ntile = L0 ? (F.ntN - tN < F.tpw ? F.ntN - tN : F.tpw) : 1;
   static_assert(!(L0 && C), "the in-tile layer 0 reads only inputs of earlier launches");
   static_assert(!BF || (VEC && !C), "bf16 operands: vector tiles of plain launches");
   constexpr int KW = 256 / NW;  // K chunk of one wave per iteration (NW waves cover 256)
@@ -489,36 +494,51 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
                                          : G.online + G.slot_off(rslot(F.mask, head) ^ (grp.which == P_NEW), head);
   const float* X = F.xOff < 0 ? (grp.xsel == 1 ? F.xa : F.xb) : G.actp(grp.role, head, F.xOff);
   float* Y = G.actp(grp.role, head, F.yOff);
-  const int n0 = tN * 16, m0 = tM * 32;
+  const int m0 = tM * 32;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
-  const int ma = m0 + r, mb = m0 + 16 + r, n = n0 + r;
-  const bool oka = ma < M, okb = mb < M, okn = n < N;
-  const float* wr = P + F.wOff + (size_t)n * K;
+  const int ma = m0 + r, mb = m0 + 16 + r;
+  const bool oka = ma < M, okb = mb < M;
+  const float* Pw = P + F.wOff;
   // bf16 mode: the W operand from the bf16 copy (same packing, 16-B aligned rows: wOff % 8 == 0)
-  const __bf16* wr16 = nullptr;
+  const __bf16* Pw16 = nullptr;
   if constexpr (BF)
-    wr16 = (grp.which == P_TARGET ? G.tg16 + (long long)head * G.P
+    Pw16 = (grp.which == P_TARGET ? G.tg16 + (long long)head * G.P
                                   : G.on16 + G.slot_off(rslot(F.mask, head) ^ (grp.which == P_NEW), head)) +
-           F.wOff + (size_t)n * K;
-  // the reducing threads fetch their bias early
-  const int Lx = threadIdx.x & 63, col = n0 + (Lx & 15);
-  const float bias = (threadIdx.x < 128 && col < N) ? ldc<C>(P + F.bOff + col) : 0.f;
+           F.wOff;
+  // the reducing threads fetch their biases early
+  const int Lx = threadIdx.x & 63;
+  float biasv[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int col = (tN + j) * 16 + (Lx & 15);
+    biasv[j] = (j < ntile && threadIdx.x < 128 && col < N) ? ldc<C>(P + F.bOff + col) : 0.f;
+  }
   constexpr int AS = L0 ? L0_NMAX + 4 : 4;  // LDS row stride of a0 (padded against bank conflicts)
   __shared__ __align__(16) float sA[L0 ? 32 * AS : 4];
-  // L0: the first K chunk of this lane's W row is requested before layer 0 is computed, so its
-  // latency overlaps the in-tile layer 0 instead of following it
-  float4 wpre[VEC && L0 && !BF ? KL / 4 : 1];
-  bf16x8 wpre16[BF && L0 ? KL / 8 : 1];
+  // L0: the first K chunk of this lane's W rows (every tile of the workgroup) is requested before
+  // layer 0 is computed, so its latency overlaps the in-tile layer 0 instead of following it
+  float4 wpre[TPW][VEC && L0 && !BF ? KL / 4 : 1];
+  bf16x8 wpre16[TPW][BF && L0 ? KL / 8 : 1];
   if constexpr (VEC && L0 && !BF) {
     const int kb0 = wave * KW + g * KL;
 #pragma unroll
-    for (int q = 0; q < KL / 4; ++q)
-      wpre[q] = okn && kb0 < K ? ldc4<C>(wr + kb0 + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = 0; j < TPW; ++j) {
+      const int nj = (tN + j) * 16 + r;
+      const bool ok = j < ntile && nj < N && kb0 < K;
+#pragma unroll
+      for (int q = 0; q < KL / 4; ++q)
+        wpre[j][q] = ok ? ldc4<C>(Pw + (size_t)nj * K + kb0 + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   }
   if constexpr (BF && L0) {
     const int kb0 = wave * KW + g * KL;
 #pragma unroll
-    for (int q = 0; q < KL / 8; ++q) wpre16[q] = okn && kb0 < K ? ld_bf16x8(wr16 + kb0 + 8 * q) : bf16x8{};
+    for (int j = 0; j < TPW; ++j) {
+      const int nj = (tN + j) * 16 + r;
+      const bool ok = j < ntile && nj < N && kb0 < K;
+#pragma unroll
+      for (int q = 0; q < KL / 8; ++q) wpre16[j][q] = ok ? ld_bf16x8(Pw16 + (size_t)nj * K + kb0 + 8 * q) : bf16x8{};
+    }
   }
   if constexpr (L0) {
     __shared__ float sX[32 * L0_KMAX];
@@ -590,6 +610,15 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
   }
   const float* xra = L0 ? sA + r * AS : X + (size_t)ma * K;
   const float* xrb = L0 ? sA + (16 + r) * AS : X + (size_t)mb * K;
+  __shared__ floatx4 red[NW][2][64];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+  if (j >= ntile) continue;  // block-uniform
+  const int n0 = (tN + j) * 16, n = n0 + r, col = n0 + (Lx & 15);
+  const bool okn = n < N;
+  const float* wr = Pw + (size_t)n * K;
+  const __bf16* wr16 = BF ? Pw16 + (size_t)n * K : nullptr;
+  const float bias = biasv[j];
   floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   for (int kc = wave * KW; kc < K && BF; kc += 256) {
     // bf16 operands: per lane KL consecutive k as KL / 8 MFMA steps of 8 (the fp32 path's k
@@ -613,7 +642,7 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
 #pragma unroll
     for (int q = 0; q < KL / 8; ++q) {
       if constexpr (L0)
-        w16[q] = kc == wave * KW ? wpre16[q] : (okn ? ld_bf16x8(wr16 + kb + 8 * q) : bf16x8{});
+        w16[q] = kc == wave * KW ? wpre16[j][q] : (okn ? ld_bf16x8(wr16 + kb + 8 * q) : bf16x8{});
       else
         w16[q] = okn ? ld_bf16x8(wr16 + kb + 8 * q) : bf16x8{};
     }
@@ -639,7 +668,7 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
         }
         float4 tw;
         if constexpr (L0 && !BF) {
-          tw = kc == wave * KW ? wpre[q] : (okn ? ldc4<C>(wr + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f));
+          tw = kc == wave * KW ? wpre[j][q] : (okn ? ldc4<C>(wr + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f));
         } else {
           tw = okn ? ldc4<C>(wr + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -668,7 +697,7 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
     }
   }
   PROBE_MARK();
-  __shared__ floatx4 red[NW][2][64];
+  if (j > 0) __syncthreads();  // the previous tile's reduction has read red
   red[wave][0][lane] = acc0;
   red[wave][1][lane] = acc1;
   __syncthreads();
@@ -687,6 +716,7 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
       }
     }
   }
+  }  // tiles
 }
 
 constexpr int qa_tile_floats(bool L0) { return L0 ? 1 : 32 * 16; }  // L0 launches never accumulate
@@ -695,15 +725,17 @@ template <bool VEC, int NW, bool L0, bool BF = false>
 __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
   PROBE_T(pt0);
   int y = blockIdx.y, tN = blockIdx.x, tM = blockIdx.z;
+  const int ntNb = L0 ? (F.ntN + F.tpw - 1) / F.tpw : F.ntN;  // workgroups along N
   if (F.xcd) {  // head h's tiles on the XCD of slot h % 8 (see xcd_decode)
     const int b = blockIdx.x, hp = (F.nh + 7) >> 3, k = b >> 3;
     const int r = hp == 1 ? k : k / fdiv(hp), hd = (b & 7) + 8 * (k - r * hp);
-    const int rN = r / fdiv(F.ntN), gi = rN / fdiv(F.ntM);
-    tN = r - rN * F.ntN;
+    const int rN = r / fdiv(ntNb), gi = rN / fdiv(F.ntM);
+    tN = r - rN * ntNb;
     tM = rN - gi * F.ntM;
     if (hd >= F.nh || gi >= F.ngroups) return;
     y = gi * F.nh + hd;
   }
+  if constexpr (L0) tN *= F.tpw;
   bool qa = false;
   int head = 0;
   if (F.skip) {  // single group: instance y is the head
