@@ -1438,17 +1438,32 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
     bm = Mr[L.bOff + nbias];
     bv = Vr[L.bOff + nbias];
   }
-  // fused forward input (S1 rows ++ s_next), requested with the rest, parked in LDS below
-  constexpr int XQ = VFUSE / 256;
-  float xs[XQ];
-  const int nxs = fuse ? A.vM * K : 0;
+  // fused forward input (S1 rows ++ s_next), requested with the rest, parked in LDS below: the S1
+  // rows as float4 (4 loads per lane, not 16: with the Adam state and the MFMA operands a lane
+  // stays under the 63 loads vmcnt tracks), the s_next row one float per lane
+  constexpr int XQ = VFUSE / 1024;
+  float4 xs[XQ];
+  float xn = 0.f;
+  const int nx = fuse ? M * K : 0;
+  const int nxn = fuse && A.v_xn ? K : 0;
   if (fuse) {
+    if ((nx & 3) == 0 && (reinterpret_cast<uintptr_t>(A.v_x) & 15) == 0) {
 #pragma unroll
-    for (int q = 0; q < XQ; ++q) {
-      const int j = threadIdx.x + 256 * q;
-      const float* src = j < M * K ? A.v_x + j : A.v_xn + (j - M * K);
-      xs[q] = j < nxs ? *src : 0.f;
+      for (int q = 0; q < XQ; ++q) {
+        const int j = threadIdx.x + 256 * q;
+        xs[q] = 4 * j < nx ? reinterpret_cast<const float4*>(A.v_x)[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    } else {  // rows not whole float4s: the same layout from dword loads
+#pragma unroll
+      for (int q = 0; q < XQ; ++q) {
+        const int j = 4 * (threadIdx.x + 256 * q);
+        xs[q].x = j < nx ? A.v_x[j] : 0.f;
+        xs[q].y = j + 1 < nx ? A.v_x[j + 1] : 0.f;
+        xs[q].z = j + 2 < nx ? A.v_x[j + 2] : 0.f;
+        xs[q].w = j + 3 < nx ? A.v_x[j + 3] : 0.f;
+      }
     }
+    if ((int)threadIdx.x < nxn) xn = A.v_xn[threadIdx.x];
   }
   __builtin_amdgcn_sched_barrier(0);  // keep those loads ahead of the MFMA operands
   floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -1477,13 +1492,20 @@ __device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo&
   PROBE_MARK();
   __shared__ float sW[32 * KFUSE];
   __shared__ float sB[32];
-  __shared__ float sX[VFUSE];
+  __shared__ __align__(16) float sX[VFUSE];
   if (fuse) {
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
       const int j = threadIdx.x + 256 * q;
-      if (j < nxs) sX[j] = xs[q];
+      if (4 * j + 3 < nx) {
+        reinterpret_cast<float4*>(sX)[j] = xs[q];
+      } else if (4 * j < nx) {  // the last, partial float4
+        sX[4 * j] = xs[q].x;
+        if (4 * j + 1 < nx) sX[4 * j + 1] = xs[q].y;
+        if (4 * j + 2 < nx) sX[4 * j + 2] = xs[q].z;
+      }
     }
+    if ((int)threadIdx.x < nxn) sX[nx + threadIdx.x] = xn;
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
