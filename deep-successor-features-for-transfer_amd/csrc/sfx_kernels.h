@@ -1748,6 +1748,18 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
   }
   PROBE_MARKA();
   const bool skip = A.skip && __builtin_nontemporal_load(A.skip + head) != 0;  // repeats round r-1
+  // tiles of a head in dispatch order: layer-0 dW (+ the fused post-update forward: the longest
+  // tiles, so they request their operands before the bulk of the launch does), dX, dW, tail
+  if (bx < A.nc) {
+    if (skip) {
+      if (A.fuse_v0 && !A.skip_v0) role_v0_only(G, A, head, A.rc, bx);
+      return;
+    }
+    role_dw<false, BF>(G, A, head, A.rc, bx, A.fuse_v0 != 0);
+    PROBE_REC(6, pt0);
+    return;
+  }
+  bx -= A.nc;
   if (bx < A.na) {
     if (skip) return;
     role_dx<false, 2, 8, false, BF>(G, A, head, bx, red);
@@ -1762,16 +1774,6 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
     else
       role_dw<false, BF>(G, A, head, A.rb, bx, false);
     PROBE_REC(5, pt0);
-    return;
-  }
-  bx -= A.nb;
-  if (bx < A.nc) {
-    if (skip) {
-      if (A.fuse_v0 && !A.skip_v0) role_v0_only(G, A, head, A.rc, bx);
-      return;
-    }
-    role_dw<false, BF>(G, A, head, A.rc, bx, A.fuse_v0 != 0);
-    PROBE_REC(6, pt0);
     return;
   }
   role_tail(G, A, head);

@@ -1,0 +1,4 @@
+#!/bin/bash
+# GPU tests, then A/B of this build vs libsfx_prev.so (the previous commit's build)
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+bash tools/gpu_alltests.sh && bash tools/ab_libs.sh "libsfx_prev.so libsfx.so"
