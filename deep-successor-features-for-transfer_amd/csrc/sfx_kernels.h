@@ -1748,8 +1748,8 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
   }
   PROBE_MARKA();
   const bool skip = A.skip && __builtin_nontemporal_load(A.skip + head) != 0;  // repeats round r-1
-  // tiles of a head in dispatch order: layer-0 dW (+ the fused post-update forward: the longest
-  // tiles, so they request their operands before the bulk of the launch does), dX, dW, tail
+  // tiles of a head in dispatch order, longest first so they request their operands before the
+  // bulk of the launch does: layer-0 dW (+ the fused post-update forward), dW, dX, tail
   if (bx < A.nc) {
     if (skip) {
       if (A.fuse_v0 && !A.skip_v0) role_v0_only(G, A, head, A.rc, bx);
@@ -1760,13 +1760,6 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
     return;
   }
   bx -= A.nc;
-  if (bx < A.na) {
-    if (skip) return;
-    role_dx<false, 2, 8, false, BF>(G, A, head, bx, red);
-    PROBE_REC(4, pt0);
-    return;
-  }
-  bx -= A.na;
   if (bx < A.nb) {
     if (skip) return;
     if (A.rb.nw == 2 && !BF)  // bf16 mode never builds wide tiles (run_bwd)
@@ -1774,6 +1767,13 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
     else
       role_dw<false, BF>(G, A, head, A.rb, bx, false);
     PROBE_REC(5, pt0);
+    return;
+  }
+  bx -= A.nb;
+  if (bx < A.na) {
+    if (skip) return;
+    role_dx<false, 2, 8, false, BF>(G, A, head, bx, red);
+    PROBE_REC(4, pt0);
     return;
   }
   role_tail(G, A, head);
