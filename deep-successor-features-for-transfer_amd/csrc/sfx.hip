@@ -101,7 +101,8 @@ struct sfx_handle {
   bool fuse_v0 = true;   // SFX_FUSE_V0=0: post-update layer-0 forward as its own launch
   bool xcd = true;       // SFX_XCD=0: plain (tile, head) grids instead of XCD-aware ones
   int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
-  int fwd_tpw = FWD_TPW; // column tiles per workgroup of the layer-0+1 forward; SFX_FWD_TPW=1: one
+  int fwd_tpw = FWD_TPW; // column tiles per workgroup (layer-0+1 forward, oversubscribed launches); SFX_FWD_TPW=1: one
+  int ncu = 256;         // compute units of the device
   bool fuse_l0 = true;   // SFX_FUSE_L0=0: layer 0 of a forward from the states as its own launch
   AdamHP hp_psi{1e-3, 0.0, 0.9, 0.999, 1e-8};
   AdamHP hp_w{1e-3, 0.0, 0.9, 0.999, 1e-8};
@@ -347,7 +348,7 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     F.flag_value = ex.flag_value;
     F.ntN = cdiv(L.N, 16);
     F.ntM = cdiv(M, 32);
-    F.tpw = l0 ? h->fwd_tpw : 1;  // the in-tile layer 0 computed once for tpw column tiles
+    F.tpw = 1;
     const bool qa = ex.qa_role >= 0 && l == h->NL - 1;  // the maxima come from the ψ output layer
     if (qa) {
       F.qa_role = ex.qa_role;
@@ -362,12 +363,21 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
       F.qa_task = ex.qa_task;
       F.qa_use_gpi = ex.qa_use_gpi;
     }
+    // the vector path needs K % (256/NW) == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
+    const bool aligned = l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0);
+    // two column tiles per workgroup (an L0 launch's in-tile layer 0 computed once for them, a
+    // plain launch's X operands loaded once) when the tiles would put two workgroups on at least
+    // half the CUs and fit the chip when paired: C2's first forward of three roles (384 tiles ->
+    // 192 workgroups, +1 %); Hopper TSF's 288 tiles stay unpaired (pairing measured 1 % slower)
+    const long tiles = (long)F.ntN * F.ntM * ninst;
+    if (!h->rec && !qa && h->fwd_tpw > 1 && h->fwd_waves == 8 && F.ntN > 1 && 2 * tiles >= 3L * h->ncu &&
+        tiles <= 2L * h->ncu && (l0 || ((L.K % 32) == 0 && aligned)))
+      F.tpw = h->fwd_tpw;
     const int ntNb = cdiv(F.ntN, F.tpw);
     const dim3 grid = F.xcd ? dim3(8 * cdiv(h->T, 8) * ntNb * F.ntM * F.ngroups) : dim3(ntNb, ninst, F.ntM);
     double by = 4.0 * ninst * ((double)L.N * L.K + L.N + (double)M * L.K + (double)M * L.N);
     if (l0) by += 4.0 * ninst * ((double)h->L[0].N * h->L[0].K + h->L[0].N + (double)M * h->L[0].K);
-    // the vector path needs K % (256/NW) == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
-    const bool aligned = l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0);
+    const bool tp2 = F.tpw > 1;
     const bool gemv = !l0 && !qa && !h->rec && h->gemv_fwd && M <= GEMV_M && L.N >= GEMV_N && L.K % 16 == 0 &&
                       (l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0));
     if (gemv) {
@@ -377,12 +387,17 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
       h->rec->bytes.push_back(by);
       h->rec->fvec = h->rec->fvec && (L.K % 64) == 0 && aligned && !l0;
     } else if (l0) {
-      launch(h, K_FWD, by, h->bf16 ? k_fwd<true, 8, true, true> : k_fwd<true, 8, true>, grid, dim3(512), h->G, F);
+      launch(h, K_FWD, by,
+             tp2 ? (h->bf16 ? k_fwd<true, 8, true, true, 2> : k_fwd<true, 8, true, false, 2>)
+                 : (h->bf16 ? k_fwd<true, 8, true, true> : k_fwd<true, 8, true>),
+             grid, dim3(512), h->G, F);
     } else if (h->fwd_waves == 8) {
       const bool vec = (L.K % 32) == 0 && aligned;
       launch(h, K_FWD, by,
-             vec ? (h->bf16 ? k_fwd<true, 8, false, true> : k_fwd<true, 8, false>) : k_fwd<false, 8, false>, grid,
-             dim3(512), h->G, F);
+             !vec ? k_fwd<false, 8, false>
+                  : tp2 ? (h->bf16 ? k_fwd<true, 8, false, true, 2> : k_fwd<true, 8, false, false, 2>)
+                        : (h->bf16 ? k_fwd<true, 8, false, true> : k_fwd<true, 8, false>),
+             grid, dim3(512), h->G, F);
     } else {
       const bool vec = (L.K % 64) == 0 && aligned;
       launch(h, K_FWD, by, vec ? (h->bf16 ? k_fwd<true, 4, false, true> : k_fwd<true, 4, false>) : k_fwd<false, 4, false>,
@@ -957,6 +972,12 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->xcd = !(ex && ex[0] == '0');
   const char* efw = std::getenv("SFX_FWD_WAVES");
   h->fwd_waves = efw && std::atoi(efw) == 4 ? 4 : 8;
+  {
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+      h->ncu = ncu;
+  }
   const char* etp = std::getenv("SFX_FWD_TPW");
   h->fwd_tpw = etp && etp[0] == '1' ? 1 : FWD_TPW;
   const char* el0 = std::getenv("SFX_FUSE_L0");

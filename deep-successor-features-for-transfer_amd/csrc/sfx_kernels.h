@@ -474,13 +474,16 @@ __device__ __forceinline__ FwdGroup fwd_group(const FwdArgs& F, int& y) {
   return g;
 }
 
-constexpr int FWD_TPW = 2;  // column tiles per workgroup of an L0 launch (FwdArgs::tpw)
+constexpr int FWD_TPW = 2;  // column tiles per workgroup (FwdArgs::tpw <= TP)
 
-template <bool VEC, int NW, bool L0, bool C, bool BF = false>
+// TP > 1: the workgroup computes column tiles tN .. tN + tpw - 1 of its rows -- an L0 launch's
+// layer-0 rows computed once for them, a plain launch's X operands loaded once for them (launches
+// that would otherwise put more workgroups than CUs on the chip)
+template <bool VEC, int NW, bool L0, bool C, bool BF = false, int TP = 1>
 __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, int tN, int tM, float* sT = nullptr) {
-  // L0 launches: tiles tN .. tN + tpw - 1 share the workgroup's layer-0 rows (computed once)
-  constexpr int TPW = L0 ? FWD_TPW : 1;
-  const int ntile = L0 ? (F.ntN - tN < F.tpw ? F.ntN - tN : F.tpw) : 1;
+  constexpr int TPW = TP;
+  static_assert(TP == 1 || VEC, "several tiles per workgroup: vector tiles only");
+  const int ntile = TP == 1 ? 1 : (F.ntN - tN < F.tpw ? F.ntN - tN : F.tpw);
   static_assert(!(L0 && C), "the in-tile layer 0 reads only inputs of earlier launches");
   static_assert(!BF || (VEC && !C), "bf16 operands: vector tiles of plain launches");
   constexpr int KW = 256 / NW;  // K chunk of one wave per iteration (NW waves cover 256)
@@ -611,21 +614,24 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
   const float* xra = L0 ? sA + r * AS : X + (size_t)ma * K;
   const float* xrb = L0 ? sA + (16 + r) * AS : X + (size_t)mb * K;
   __shared__ floatx4 red[NW][2][64];
+  floatx4 acc0[TPW], acc1[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) acc0[j] = acc1[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const float* wrj[TPW];
+  const __bf16* wr16j[TPW];
+  bool oknj[TPW];
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
-  if (j >= ntile) continue;  // block-uniform
-  const int n0 = (tN + j) * 16, n = n0 + r, col = n0 + (Lx & 15);
-  const bool okn = n < N;
-  const float* wr = Pw + (size_t)n * K;
-  const __bf16* wr16 = BF ? Pw16 + (size_t)n * K : nullptr;
-  const float bias = biasv[j];
-  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    const int n = (tN + j) * 16 + r;
+    oknj[j] = j < ntile && n < N;
+    wrj[j] = Pw + (size_t)(oknj[j] ? n : 0) * K;
+    wr16j[j] = BF ? Pw16 + (size_t)(oknj[j] ? n : 0) * K : nullptr;
+  }
   for (int kc = wave * KW; kc < K && BF; kc += 256) {
     // bf16 operands: per lane KL consecutive k as KL / 8 MFMA steps of 8 (the fp32 path's k
     // assignment, regrouped), X rounded to bf16 in registers, W from the bf16 copy
     const int kb = kc + g * KL;
     float a0[KL], a1[KL];
-    bf16x8 w16[KL / 8];
 #pragma unroll
     for (int q = 0; q < KL / 4; ++q) {
       float4 ta, tb;
@@ -639,22 +645,29 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
       a0[4 * q] = ta.x; a0[4 * q + 1] = ta.y; a0[4 * q + 2] = ta.z; a0[4 * q + 3] = ta.w;
       a1[4 * q] = tb.x; a1[4 * q + 1] = tb.y; a1[4 * q + 2] = tb.z; a1[4 * q + 3] = tb.w;
     }
+    bf16x8 w16[TPW][KL / 8];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j)
+#pragma unroll
+      for (int q = 0; q < KL / 8; ++q) {
+        if constexpr (L0)
+          w16[j][q] = kc == wave * KW ? wpre16[j][q] : (oknj[j] ? ld_bf16x8(wr16j[j] + kb + 8 * q) : bf16x8{});
+        else
+          w16[j][q] = oknj[j] ? ld_bf16x8(wr16j[j] + kb + 8 * q) : bf16x8{};
+      }
 #pragma unroll
     for (int q = 0; q < KL / 8; ++q) {
-      if constexpr (L0)
-        w16[q] = kc == wave * KW ? wpre16[j][q] : (okn ? ld_bf16x8(wr16 + kb + 8 * q) : bf16x8{});
-      else
-        w16[q] = okn ? ld_bf16x8(wr16 + kb + 8 * q) : bf16x8{};
-    }
+      const bf16x8 x0 = to_bf16x8(a0 + 8 * q), x1 = to_bf16x8(a1 + 8 * q);
 #pragma unroll
-    for (int q = 0; q < KL / 8; ++q) {
-      acc0 = mfma_bf16(to_bf16x8(a0 + 8 * q), w16[q], acc0);
-      acc1 = mfma_bf16(to_bf16x8(a1 + 8 * q), w16[q], acc1);
+      for (int j = 0; j < TPW; ++j) {
+        acc0[j] = mfma_bf16(x0, w16[j][q], acc0[j]);
+        acc1[j] = mfma_bf16(x1, w16[j][q], acc1[j]);
+      }
     }
   }
   for (int kc = wave * KW; kc < K && !BF; kc += 256) {
     const int kb = kc + g * KL;
-    float a0[KL], a1[KL], bw[KL];
+    float a0[KL], a1[KL], bw[TPW][KL];
     if constexpr (VEC) {  // K % KW == 0, rows 16-B aligned: KL/4 float4 per operand row
 #pragma unroll
       for (int q = 0; q < KL / 4; ++q) {
@@ -666,40 +679,52 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
           ta = oka ? ldc4<C>(xra + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
           tb = okb ? ldc4<C>(xrb + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        float4 tw;
-        if constexpr (L0 && !BF) {
-          tw = kc == wave * KW ? wpre[j][q] : (okn ? ldc4<C>(wr + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f));
-        } else {
-          tw = okn ? ldc4<C>(wr + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+          float4 tw;
+          if constexpr (L0 && !BF) {
+            tw = kc == wave * KW ? wpre[j][q]
+                                 : (oknj[j] ? ldc4<C>(wrj[j] + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f));
+          } else {
+            tw = oknj[j] ? ldc4<C>(wrj[j] + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+          bw[j][4 * q] = tw.x; bw[j][4 * q + 1] = tw.y; bw[j][4 * q + 2] = tw.z; bw[j][4 * q + 3] = tw.w;
         }
         a0[4 * q] = ta.x; a0[4 * q + 1] = ta.y; a0[4 * q + 2] = ta.z; a0[4 * q + 3] = ta.w;
         a1[4 * q] = tb.x; a1[4 * q + 1] = tb.y; a1[4 * q + 2] = tb.z; a1[4 * q + 3] = tb.w;
-        bw[4 * q] = tw.x; bw[4 * q + 1] = tw.y; bw[4 * q + 2] = tw.z; bw[4 * q + 3] = tw.w;
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < KL; ++j) {
-        const bool kin = kb + j < K;
+      for (int i = 0; i < KL; ++i) {
+        const bool kin = kb + i < K;
         if constexpr (L0) {
-          a0[j] = (oka && kin) ? xra[kb + j] : 0.f;
-          a1[j] = (okb && kin) ? xrb[kb + j] : 0.f;
+          a0[i] = (oka && kin) ? xra[kb + i] : 0.f;
+          a1[i] = (okb && kin) ? xrb[kb + i] : 0.f;
         } else {
-          a0[j] = (oka && kin) ? ldc<C>(xra + kb + j) : 0.f;
-          a1[j] = (okb && kin) ? ldc<C>(xrb + kb + j) : 0.f;
+          a0[i] = (oka && kin) ? ldc<C>(xra + kb + i) : 0.f;
+          a1[i] = (okb && kin) ? ldc<C>(xrb + kb + i) : 0.f;
         }
-        bw[j] = (okn && kin) ? ldc<C>(wr + kb + j) : 0.f;
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) bw[j][i] = (oknj[j] && kin) ? ldc<C>(wrj[j] + kb + i) : 0.f;
       }
     }
 #pragma unroll
-    for (int j = 0; j < KL; ++j) {
-      acc0 = mfma4(a0[j], bw[j], acc0);
-      acc1 = mfma4(a1[j], bw[j], acc1);
-    }
+    for (int i = 0; i < KL; ++i)
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+        acc0[j] = mfma4(a0[i], bw[j][i], acc0[j]);
+        acc1[j] = mfma4(a1[i], bw[j][i], acc1[j]);
+      }
   }
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+  if (j >= ntile) continue;  // block-uniform
+  const int n0 = (tN + j) * 16, col = n0 + (Lx & 15);
+  const float bias = biasv[j];
   PROBE_MARK();
   if (j > 0) __syncthreads();  // the previous tile's reduction has read red
-  red[wave][0][lane] = acc0;
-  red[wave][1][lane] = acc1;
+  red[wave][0][lane] = acc0[j];
+  red[wave][1][lane] = acc1[j];
   __syncthreads();
   if (threadIdx.x < 128) {
     const int s = threadIdx.x >> 6;
@@ -721,11 +746,11 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
 
 constexpr int qa_tile_floats(bool L0) { return L0 ? 1 : 32 * 16; }  // L0 launches never accumulate
 
-template <bool VEC, int NW, bool L0, bool BF = false>
+template <bool VEC, int NW, bool L0, bool BF = false, int TP = 1>
 __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
   PROBE_T(pt0);
   int y = blockIdx.y, tN = blockIdx.x, tM = blockIdx.z;
-  const int ntNb = L0 ? (F.ntN + F.tpw - 1) / F.tpw : F.ntN;  // workgroups along N
+  const int ntNb = TP > 1 ? (F.ntN + F.tpw - 1) / F.tpw : F.ntN;  // workgroups along N
   if (F.xcd) {  // head h's tiles on the XCD of slot h % 8 (see xcd_decode)
     const int b = blockIdx.x, hp = (F.nh + 7) >> 3, k = b >> 3;
     const int r = hp == 1 ? k : k / fdiv(hp), hd = (b & 7) + 8 * (k - r * hp);
@@ -735,7 +760,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
     if (hd >= F.nh || gi >= F.ngroups) return;
     y = gi * F.nh + hd;
   }
-  if constexpr (L0) tN *= F.tpw;
+  if constexpr (TP > 1) tN *= F.tpw;
   bool qa = false;
   int head = 0;
   if (F.skip) {  // single group: instance y is the head
@@ -750,7 +775,7 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
     head = grp.head0 + yy;
   }
   __shared__ float sT[qa_tile_floats(L0)];
-  fwd_tile<VEC, NW, L0, false, BF>(G, F, y, tN, tM, qa ? sT : nullptr);
+  fwd_tile<VEC, NW, L0, false, BF, TP>(G, F, y, tN, tM, qa ? sT : nullptr);
   if (qa) q_accumulate(G, F, head, tN, tM, sT);
   if (tN == 0 && tM == 0 && blockIdx.y == 0 && (F.xcd ? blockIdx.x == 0 : true)) {
     if (F.flag && threadIdx.x == 0) *F.flag = F.flag_value;
