@@ -524,10 +524,15 @@ def main():
         # measured stay beside it
         replicas = {"value": round(value, 2), "unit": "env steps/s", "ms_per_step": round(1000.0 * dt / args.steps, 4),
                     "parallelism": f"replica{world}", "note": f"{world} independent 8-head learners, no collective"}
-        sharded = bench_sharded(args, world, rank, device, barrier, dist, steps=args.steps, warmup=args.warmup)
-        value = sharded["value"]
-        dt = sharded["ms_per_step"] * args.steps / 1000.0
-        layout = f"shard{world}"
+        try:
+            sharded = bench_sharded(args, world, rank, device, barrier, dist, steps=args.steps, warmup=args.warmup)
+        except Exception as e:  # an error return (not a hang): keep the replicas' line, say why
+            print(f"rank {rank}: sharded C4 layout failed: {e!r}", file=sys.stderr, flush=True)
+            sharded = {"error": repr(e)[:400]}
+        if "error" not in sharded:
+            value = sharded["value"]
+            dt = sharded["ms_per_step"] * args.steps / 1000.0
+            layout = f"shard{world}"
     elif args.shard_steps > 0 and args.schedule == "all":
         sharded = bench_sharded(args, world, rank, device, barrier, dist)
     elif args.shard_steps > 0 and args.schedule == "tsf":
