@@ -323,9 +323,15 @@ __device__ __forceinline__ AdamC adam_consts(const AdamHP& hp, int step) {
 __device__ __forceinline__ void st_wt(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+#ifdef SFX_NO_WT  // diagnostics: the earlier stores (plain parameters, non-temporal moments)
+__device__ __forceinline__ void st_moment(float* p, float v) { __builtin_nontemporal_store(v, p); }
+template <bool C>
+__device__ __forceinline__ void st_param(float* p, float v) { stc<C>(p, v); }
+#else
 __device__ __forceinline__ void st_moment(float* p, float v) { st_wt(p, v); }
 template <bool C>
 __device__ __forceinline__ void st_param(float* p, float v) { st_wt(p, v); }
+#endif
 
 __device__ __forceinline__ void adam_apply(float& pp, float& mm, float& vv, float g, const AdamC& c) {
   if (c.wd != 0.f) g = __fadd_rn(g, __fmul_rn(c.wd, pp));
@@ -2067,25 +2073,31 @@ __global__ __launch_bounds__(256) void k_gpi(Geo G, GpiArgs A) {
 // -------------------------------------------------------------------------------------
 struct HostResult {  // host-coherent; seq written last
   long long sel0, sel1;
-  int flag, err;       // err: a gate timed out (set by the gate itself, system scope)
+  int flag, err;       // err (slot 0 only): a gate timed out (set by the gate itself, system scope)
   int cancelled, pad_; // the published step was cancelled at its gate: nothing of it committed
   long long seq;
 };
+// Results live in a ring of RES_RING slots, step seq in slot seq % RES_RING: steps queued behind
+// the host that get cancelled at their gates (runner gate bound) still publish, and must not
+// overwrite the result of the step the host is waiting for (> the runner's pre-launch span).
+constexpr int RES_RING = 64;
 
 // Post the step's result (selected action, speculation verdict) to host-coherent memory;
 // seq is written last (system release).  The inputs are read with coherent (sc1) loads.
-__device__ __forceinline__ void publish_result(const int64_t* sel, const int* flag, HostResult* out,
+__device__ __forceinline__ void publish_result(const int64_t* sel, const int* flag, HostResult* ring,
                                                const long long* dctr, const int* cancel) {
   const long long s0 = __hip_atomic_load(sel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const long long s1 = __hip_atomic_load(sel + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int cx = __hip_atomic_load(cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long long seq = *dctr;
+  HostResult* out = ring + (seq & (RES_RING - 1));
   out->sel0 = s0;
   out->sel1 = s1;
   out->flag = f;
   out->cancelled = cx;
   __threadfence_system();
-  __hip_atomic_store(&out->seq, *dctr, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 struct VerArgs {
@@ -2684,12 +2696,14 @@ __global__ __launch_bounds__(256) void k_sfinish(SfinArgs F) {
     F.sel[0] = c;
     F.sel[1] = a;
     if (F.pub) {
-      F.pub->sel0 = c;
-      F.pub->sel1 = a;
-      F.pub->flag = s_min;
-      F.pub->cancelled = *F.cancel;
+      const long long seq = *F.dctr;
+      HostResult* pub = F.pub + (seq & (RES_RING - 1));  // the step's slot of the result ring
+      pub->sel0 = c;
+      pub->sel1 = a;
+      pub->flag = s_min;
+      pub->cancelled = *F.cancel;
       __threadfence_system();
-      __hip_atomic_store(&F.pub->seq, *F.dctr, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&pub->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }

@@ -67,6 +67,7 @@ SIGNATURES = {
     "sfx_runner_stats": (_I, [_VP] + [C.POINTER(C.c_longlong)] * 3 + [C.POINTER(C.c_double)]),
     "sfx_runner_gate_timeout": (_I, [_VP, _D]),
     "sfx_runner_retried": (_I, [_VP, C.POINTER(C.c_longlong)]),
+    "sfx_runner_recomputed": (_I, [_VP, C.POINTER(C.c_longlong)]),
     "sfx_runner_warm": (_I, [_VP]),
     "sfx_runner_gpi_counters": (_I, [_VP, C.POINTER(C.c_longlong)]),
     "sfx_runner_record": (_I, [_VP, _I]),

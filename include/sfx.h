@@ -278,6 +278,10 @@ int sfx_runner_gate_timeout(sfx_runner_t r, double seconds);
 int sfx_runner_warm(sfx_runner_t r);
 /* Steps issued again after their gate gave up (the step in flight, or steps queued behind it). */
 int sfx_runner_retried(sfx_runner_t r, long long* retried);
+/* Steps whose host rounds found later steps cancelled at their gates: those steps' launches ran
+ * (committing nothing) over the transient buffers the rounds read, so the step's forward and
+ * device rounds were recomputed from its pre-step slot first. */
+int sfx_runner_recomputed(sfx_runner_t r, long long* recomputed);
 /* SF.gpi_counters (features/successor.py:270-272): [T][T] counts of the GPI task per active task
  * (counted only with GPI action selection, as SF.GPI(update_counters=use_gpi), agents/sfdqn.py:41) */
 int sfx_runner_gpi_counters(sfx_runner_t r, long long* out_host /* [T*T] */);

@@ -221,9 +221,9 @@ def test_runner_gate_timeouts_cancel_and_retry(schedule, force):
     it, so the step is cancelled (none of its launches commits -- parameters, moments, step
     counters, w) and re-issued from the same staged inputs.  The results must still be the
     oracle's, step for step.  force = 1: every step also finishes with host rounds on the side
-    stream -- exactly when the next step's gate gives up and its (cancelled) launches would
-    overwrite the transient buffers those rounds read, unless the hold protocol (gate_wait)
-    drains them first."""
+    stream -- after the next step's gate gave up (10 ns) and its cancelled launches ran over the
+    transient buffers those rounds read (activations, speculative next actions): the runner
+    drains them and recomputes the step's forward and device rounds before its host rounds."""
     from sfx.runner import NativeEnvLoop
 
     spec = R.Spec(17, 32, 7, 8, ("relu", "relu"))
@@ -240,6 +240,8 @@ def test_runner_gate_timeouts_cancel_and_retry(schedule, force):
     loop.run(n)
     stats = loop.stats()
     assert stats["retried"] > 0 and stats["prelaunched"] > 0, stats
+    if force >= 0:  # every step's host rounds found the next steps cancelled: recomputed first
+        assert stats["recomputed"] > 0, stats
     recs = loop.records()
     if schedule == "all":
         replay_with_oracle(st, spec, recs, alpha, ev, loop.action())
