@@ -534,7 +534,10 @@ def main():
             dt = sharded["ms_per_step"] * args.steps / 1000.0
             layout = f"shard{world}"
     elif args.shard_steps > 0 and args.schedule == "all":
-        sharded = bench_sharded(args, world, rank, device, barrier, dist)
+        # the same window of training as the headline (its warmup, then its step count), so the two
+        # rates compare like for like (the all-task rate rises as more speculative rounds skip)
+        sharded = bench_sharded(args, world, rank, device, barrier, dist, steps=max(args.steps, args.shard_steps),
+                                warmup=args.warmup)
     elif args.shard_steps > 0 and args.schedule == "tsf":
         sharded = bench_sharded_tsf(args, world, rank, device, barrier, dist)
 
