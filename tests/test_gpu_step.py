@@ -130,3 +130,39 @@ def test_step_without_minibatch_then_active_updates():
         R.sf_update(st, (s, a, r, phi, s1, gamma), i, use_gpi=True)
     params_close(torch.stack([eng.get_head(t) for t in range(T)]), st.online, 1e-2)
     eng.close()
+
+
+def test_paired_forward_tiles_are_bit_exact(monkeypatch):
+    """Two column tiles per forward workgroup (the layer-0+1 forward and the oversubscribed
+    layer-2 forward of the first forward at the C2 shape: 384 tiles -> 192 workgroups) run each
+    tile's MFMA chain in the same k order as one tile per workgroup (SFX_FWD_TPW=1): heads, Adam
+    state, w and every selected action identical bit for bit after several all-task steps."""
+    spec = R.Spec(17, 256, 7, 8, ("relu", "relu"))
+    T, k = 8, 4
+    results = []
+    for tpw in ("1", "2"):
+        monkeypatch.setenv("SFX_FWD_TPW", tpw)  # read when the handle is created
+        eng, st = setup(spec, T)
+        gen = torch.Generator().manual_seed(21)
+        acts = []
+        for j in range(k):
+            B = 32
+            s, s1 = torch.randn(B, spec.n_s, generator=gen), torch.randn(B, spec.n_s, generator=gen)
+            a = torch.randint(0, spec.A, (B,), generator=gen)
+            phi = torch.rand(B, spec.d, generator=gen)
+            gamma = torch.full((B,), 0.9)
+            phi1, r1 = torch.rand(spec.d, generator=gen), torch.rand(1, generator=gen)
+            s_next = torch.randn(1, spec.n_s, generator=gen)
+            eng.step_all(dev(s), dev(a, torch.long), dev(phi), dev(s1), dev(gamma), use_gpi=True, lms_task=j % T,
+                         lms_phi=dev(phi1), lms_r=dev(r1), lms_alpha=0.05, s_next=dev(s_next), task_index=j % T)
+            acts.append(eng.step_finish())
+        heads = torch.stack([eng.get_head(t, 0) for t in range(T)])
+        adam = [eng.get_adam(t) for t in range(T)]
+        w = torch.stack([eng.get_w(t)[0] for t in range(T)])
+        results.append((acts, heads, adam, w))
+        eng.close()
+    (a1, h1, m1, w1), (a2, h2, m2, w2) = results
+    assert a1 == a2
+    assert torch.equal(h1, h2) and torch.equal(w1, w2)
+    for (p, q, s_), (p2, q2, s2) in zip(m1, m2):
+        assert torch.equal(p, p2) and torch.equal(q, q2) and s_ == s2
