@@ -149,6 +149,7 @@ struct sfx_handle {
   // sharded step, sortable int32: maxima buffers xb[2] ([Tg][Mmax][A] ++ q table [Tg][A]) and the
   // pre-step part xge ([Tg][Mmax][A]) of the fused path (shard_fused)
   int *xb[2] = {nullptr, nullptr}, *xge = nullptr;
+  int *qh = nullptr, *qhs = nullptr;  // local heads' own maxima terms (FwdArgs::qh), qhs inside qh's block
   bool shard_qa = true;  // SFX_SHARD_QA=0: maxima by separate k_qmax launches
   struct ShardPending {
     bool active = false;
@@ -167,6 +168,7 @@ struct sfx_handle {
   int* skip = nullptr;            // [T]: the policy repeats the previous round (BwdArgs::skip)
   unsigned long long* skipc = nullptr;  // [0] policies checked, [1] skipped (rounds >= 1)
   bool skip_rounds = true;        // SFX_SKIP=0: every round recomputes every policy
+  bool shard_skip_fwd = true;     // SFX_SHARD_SKIPF=0: sharded rounds skip backward work only
   StepOut* dout = nullptr;  // device
   // set by the runner while it captures a step: the final k_ver (with action selection)
   // publishes to pub_res instead of a separate k_publish; pub_folded reports that it did
@@ -298,6 +300,8 @@ struct FwdExtra {
   int qa_role = -1, qa_M = 0, qa_row = -1, qa_task = 0, qa_use_gpi = 1;
   int *qa_all = nullptr, *qa_ge = nullptr, *qa_lt = nullptr, *qa_sel = nullptr;
   const int* skip = nullptr;  // post-update forward of rounds r >= 1 (FwdArgs::skip; one group)
+  int* qh = nullptr;          // sharded rounds: the local heads' maxima terms (FwdArgs::qh)
+  int* qhs = nullptr;
 };
 
 int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const float* xa, const float* xb,
@@ -310,7 +314,7 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
   F.lms_head = -1;
   F.qa_role = -1;
   F.skip = ex.skip;
-  if (ex.skip && (groups.size() != 1 || ex.flag || ex.lms_head >= 0 || ex.qa_role >= 0 || h->rec))
+  if (ex.skip && (groups.size() != 1 || ex.flag || ex.lms_head >= 0 || (ex.qa_role >= 0 && !ex.qh) || h->rec))
     SFX_FAIL(SFX_E_STATE, "run_fwd: head skipping needs one group and no LMS / flag / maxima");
   int ninst = 0;
   bool uniform = true;  // every group covers heads 0..T-1: XCD-aware grid possible
@@ -362,6 +366,8 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
       F.qa_row = ex.qa_row;
       F.qa_task = ex.qa_task;
       F.qa_use_gpi = ex.qa_use_gpi;
+      F.qh = ex.qh;
+      F.qhs = ex.qhs;
     }
     // the vector path needs K % (256/NW) == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
     const bool aligned = l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0);
@@ -746,7 +752,7 @@ void free_all(sfx_handle* h) {
   for (hipEvent_t e : h->prof_pool) (void)hipEventDestroy(e);
   for (void* p : {(void*)h->online, (void*)h->target, (void*)h->am, (void*)h->av, (void*)h->w, (void*)h->wm,
                   (void*)h->wv, (void*)h->step, (void*)h->dcancel, (void*)h->adamc, (void*)h->round_ctr, (void*)h->act, (void*)h->dz, (void*)h->rowloss, (void*)h->spec_next, (void*)h->skip, (void*)h->skipc,
-                  (void*)h->dout, (void*)h->dxpart, (void*)h->dxctr})
+                  (void*)h->dout, (void*)h->dxpart, (void*)h->dxctr, (void*)h->qh})
     if (p) (void)hipFree(p);
   if (h->hout) (void)hipHostFree(h->hout);
   if (h->on16) (void)hipFree(h->on16);
@@ -990,6 +996,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->shard_qa = !(eqa && eqa[0] == '0');
   const char* edw = std::getenv("SFX_DW_WIDE");
   h->dw_wide = edw && edw[0] == '1';  // opt-in
+  const char* essf = std::getenv("SFX_SHARD_SKIPF");
+  h->shard_skip_fwd = !(essf && essf[0] == '0');
   const char* esk = std::getenv("SFX_SKIP");
   h->skip_rounds = !(esk && esk[0] == '0');
   int off = 0, ptorch = 0;

@@ -385,6 +385,10 @@ struct FwdArgs {
   int* qa_lt;    // max over local heads with global index < policy (post-update rounds)
   int* qa_sel;   // [Tg][A] selection table of row qa_row with w of qa_task (null: none)
   int qa_row, qa_task, qa_use_gpi, pad3_;
+  // sharded rounds: every computed tile also stores its head's terms, qh[head][i][b][a] and the
+  // selection row's qhs[head][a]; a head that skips the round (skip) replays them (q_replay)
+  int* qh;
+  int* qhs;
   // post-update forward of speculative rounds r >= 1: heads whose policy repeats round r-1
   // (BwdArgs::skip) keep the values that round left in the role -- their tiles exit at once
   const int* skip;
@@ -423,9 +427,10 @@ __device__ void q_accumulate(const Geo& G, const FwdArgs& F, int head, int tN, i
     if (all) atomicMax(F.qa_all + o, v);
     if (ge) atomicMax(F.qa_ge + o, v);
     if (lt) atomicMax(F.qa_lt + o, v);
+    if (F.qh) F.qh[(((size_t)head * Tg + i) * F.qa_M + m0 + bl) * Aa + a] = v;
   }
   const int rl = F.qa_row - m0;
-  if (F.qa_sel && rl >= 0 && rl < 32 && (F.qa_use_gpi || tg == F.qa_task))
+  if ((F.qa_sel || F.qhs) && rl >= 0 && rl < 32 && (F.qa_use_gpi || tg == F.qa_task))
     for (int al = tid; al < na; al += nt) {
       const int a = a0 + al;
       if (a >= Aa) continue;
@@ -433,7 +438,31 @@ __device__ void q_accumulate(const Geo& G, const FwdArgs& F, int head, int tN, i
       const float* w = sw + F.qa_task * d;
       float q = 0.f;
       for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], w[k], q);
-      F.qa_sel[(size_t)tg * Aa + a] = sortable(q);
+      const int v = sortable(q);
+      if (F.qa_sel) F.qa_sel[(size_t)tg * Aa + a] = v;
+      if (F.qhs) F.qhs[(size_t)head * Aa + a] = v;
+    }
+}
+
+// A head whose policy repeats the previous round (BwdArgs::skip) has the same post-update ψ as
+// then: its tiles add the terms they stored in that round (q_accumulate's qh / qhs) instead of
+// recomputing them.
+__device__ void q_replay(const Geo& G, const FwdArgs& F, int head, int tN, int tM) {
+  const int d = G.d, Aa = G.A, Tg = F.qa_Tg, tid = threadIdx.x, nt = blockDim.x;
+  const int n0 = tN * 16, m0 = tM * 32, na = 16 / d, a0 = n0 / d, tg = F.qa_off + head;
+  const int mrows = F.qa_M - m0 < 32 ? F.qa_M - m0 : 32;
+  const int per_i = (mrows > 0 ? mrows : 0) * na;
+  for (int it = tid; it < Tg * per_i; it += nt) {
+    const int i = it / per_i, rem = it - i * per_i, bl = rem / na, al = rem - bl * na, a = a0 + al;
+    if (a >= Aa || !F.qa_lt || tg >= i) continue;
+    const int v = F.qh[(((size_t)head * Tg + i) * F.qa_M + m0 + bl) * Aa + a];
+    atomicMax(F.qa_lt + ((size_t)i * F.qa_M + m0 + bl) * Aa + a, v);
+  }
+  const int rl = F.qa_row - m0;
+  if (F.qa_sel && rl >= 0 && rl < 32 && (F.qa_use_gpi || tg == F.qa_task))
+    for (int al = tid; al < na; al += nt) {
+      const int a = a0 + al;
+      if (a < Aa) F.qa_sel[(size_t)tg * Aa + a] = F.qhs[(size_t)head * Aa + a];
     }
 }
 
@@ -769,16 +798,19 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
   if constexpr (TP > 1) tN *= F.tpw;
   bool qa = false;
   int head = 0;
-  if (F.skip) {  // single group: instance y is the head
-    int yy = y;
-    const FwdGroup grp = fwd_group(F, yy);
-    if (__builtin_nontemporal_load(F.skip + grp.head0 + yy)) return;
-  }
   if (F.qa_role >= 0) {  // the sharded step's maxima from this tile (last layer, group role qa_role)
     int yy = y;
     const FwdGroup grp = fwd_group(F, yy);
     qa = grp.role == F.qa_role;
     head = grp.head0 + yy;
+  }
+  if (F.skip) {  // single group: instance y is the head
+    int yy = y;
+    const FwdGroup grp = fwd_group(F, yy);
+    if (__builtin_nontemporal_load(F.skip + grp.head0 + yy)) {
+      if (qa && F.qh) q_replay(G, F, head, tN, tM);  // its maxima terms as that round stored them
+      return;
+    }
   }
   __shared__ float sT[qa_tile_floats(L0)];
   fwd_tile<VEC, NW, L0, false, BF, TP>(G, F, y, tN, tM, qa ? sT : nullptr);
