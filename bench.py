@@ -395,6 +395,12 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
     for buf in ("reference", "host"):
         out[f"reacher17-all-T8-B32-dropin-{buf}-buffer"] = dropin_loop.measure(buf, steps=300, warmup=60,
                                                                                 batch=args.batch, device=device)
+    # the test phase (agents/sfdqn.py:111-115): 8 test tasks one after the other as the reference
+    # runs them, and in lockstep (sfx/lockstep.py, one sfx_test_actions launch set per step)
+    from tools import test_phase
+
+    for ls in (False, True):
+        out[f"reacher-test-phase-E8-{'lockstep' if ls else 'sequential'}"] = test_phase.measure(ls, device=device)
     return out
 
 

@@ -1255,6 +1255,22 @@ int sfx_select_action(sfx_t h, const float* s, int task_index, int use_gpi, floa
   return run_graph(h, key, [&]() -> int { return select_body(h, s, task_index, use_gpi, q, out); });
 }
 
+int sfx_test_actions(sfx_t h, const float* S, int E, const float* W, int w_stride, float* q, int64_t* out) {
+  if (!h || !S || !W || !out || E < 1 || w_stride < h->d) SFX_FAIL(SFX_E_ARG, "bad args");
+  const GraphKey key = make_key(26, {E, w_stride}, h->mask, {S, W, q, out});
+  return run_graph(h, key, [&]() -> int {
+    for (int row0 = 0; row0 < E; row0 += h->Mmax) {
+      const int m = E - row0 < h->Mmax ? E - row0 : h->Mmax;
+      RC(run_fwd(h, {{R_G, P_ONLINE, 1, 0, h->T}}, m, S + (size_t)row0 * h->n_s, nullptr));
+      GpiArgs g = gpi_args(R_G, 0, row0, W, nullptr, q, nullptr, nullptr, out, 0, 1, m);
+      g.w_stride = w_stride;
+      g.sel_stride = 2;
+      RC(run_gpi(h, g));
+    }
+    return SFX_OK;
+  });
+}
+
 int sfx_update(sfx_t h, int policy, const float* S, const int64_t* a, const float* r, const float* phi,
                const float* S1, const float* gamma, int B, int use_gpi, float* losses, int64_t* next) {
   if (!valid_head(h, policy) || !S || !a || !phi || !S1 || !gamma) SFX_FAIL(SFX_E_ARG, "bad args");

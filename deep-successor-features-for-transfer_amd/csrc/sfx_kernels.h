@@ -1966,6 +1966,7 @@ __global__ __launch_bounds__(256) void k_round(Geo G, RoundArgs R) {
 // -------------------------------------------------------------------------------------
 struct GpiArgs {
   int M, role, row0, select_task, use_gpi, rowoff;  // rowoff: first row of the role block used
+  int w_stride, sel_stride;  // > 0: row b's w at w + b*w_stride, its (c, a) at sel_out + b*sel_stride
   const float* w;
   float* psi_out;   // [B, T, A, d] or null  (row b -> row0 + b)
   float* q_out;     // [B, T, A] or null
@@ -2000,6 +2001,8 @@ __device__ void gpi_row(const Geo& G, const GpiArgs& A, int b) {
   const long long ob = (long long)(A.row0 + b);
   const int lb = A.rowoff + b;
   const FDiv fA = fdiv(Aa);
+  const float* wr = A.w + ob * A.w_stride;
+  int64_t* so = A.sel_out ? A.sel_out + ob * A.sel_stride : nullptr;
   if (A.psi_out) {
     const FDiv fO = fdiv(O);
     for (int idx = tid; idx < T * O; idx += 256) {
@@ -2007,11 +2010,11 @@ __device__ void gpi_row(const Geo& G, const GpiArgs& A, int b) {
       A.psi_out[(ob * T + t) * O + o] = G.actp(A.role, t, NLm)[(size_t)lb * O + o];
     }
   }
-  if (TA <= 256 && (d & 3) == 0 && d <= 16 && ((uintptr_t)A.w & 15) == 0) {  // one dot per thread, ψ and w requested together
+  if (TA <= 256 && (d & 3) == 0 && d <= 16 && ((uintptr_t)wr & 15) == 0) {  // one dot per thread, ψ and w requested together
     const int V4 = d >> 2, t = tid / fA, a = tid - t * Aa;
     const bool act = tid < TA;
     const float4* p4 = reinterpret_cast<const float4*>(G.actp(A.role, act ? t : 0, NLm) + (size_t)lb * O + (act ? a * d : 0));
-    const float4* w4 = reinterpret_cast<const float4*>(A.w);
+    const float4* w4 = reinterpret_cast<const float4*>(wr);
     float4 pv[4], wv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -2033,7 +2036,7 @@ __device__ void gpi_row(const Geo& G, const GpiArgs& A, int b) {
       if (A.q_out) A.q_out[(ob * T + t) * Aa + a] = q;
     }
   } else {
-    for (int k = tid; k < d; k += 256) s_w[k] = A.w[k];
+    for (int k = tid; k < d; k += 256) s_w[k] = wr[k];
     __syncthreads();
     for (int idx = tid; idx < TA; idx += 256) {
       const int t = idx / fA, a = idx - t * Aa;
@@ -2070,18 +2073,18 @@ __device__ void gpi_row(const Geo& G, const GpiArgs& A, int b) {
     const int tb = argmax_idx(wave_max(kt)), ab = argmax_idx(wave_max(ka));
     const int c = A.use_gpi ? tb : A.select_task;
     unsigned long long kc = 0ull;
-    if (A.sel_out)
+    if (so)
       for (int a = tid; a < Aa; a += 64) {
         const unsigned long long k = argmax_key(s_q[c * Aa + a], a);
         kc = k > kc ? k : kc;
       }
-    const int act = A.sel_out ? argmax_idx(wave_max(kc)) : 0;
+    const int act = so ? argmax_idx(wave_max(kc)) : 0;
     if (tid == 0) {
       if (A.task_out) A.task_out[ob] = tb;
       if (A.next_out) A.next_out[ob] = ab;
-      if (A.sel_out) {  // sc1 stores: k_ver's last workgroup may publish them in this launch
-        __hip_atomic_store(A.sel_out, (int64_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(A.sel_out + 1, (int64_t)act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (so) {  // sc1 stores: k_ver's last workgroup may publish them in this launch
+        __hip_atomic_store(so, (int64_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(so + 1, (int64_t)act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }

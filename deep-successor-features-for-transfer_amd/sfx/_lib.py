@@ -36,6 +36,7 @@ SIGNATURES = {
     "sfx_gpi": (_I, [_VP, _VP, _I, _VP, _VP, _VP, _VP, _VP]),
     "sfx_successors": (_I, [_VP, _VP, _I, _I, _VP]),
     "sfx_select_action": (_I, [_VP, _VP, _I, _I, _VP, _VP]),
+    "sfx_test_actions": (_I, [_VP, _VP, _I, _VP, _I, _VP, _VP]),
     "sfx_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP]),
     "sfx_update_all": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _VP]),
     "sfx_lms": (_I, [_VP, _I, _VP, _VP, _F]),

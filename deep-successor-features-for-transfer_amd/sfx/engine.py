@@ -211,6 +211,24 @@ class SFEngine:
                                     self._sel.data_ptr()), "sfx_select_action")
         return self._sel
 
+    def test_actions(self, S, W, q_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Greedy GPI actions of E test tasks in one launch set, row e under its own reward
+        weights W[e] (agents/sfdqn.py:125-137 for every test task of a lockstep step).  Returns
+        the device tensor [E, 2] of (c, a) (not synchronized)."""
+        S = self._f(S)
+        if S.dim() == 1:
+            S = S.reshape(1, -1)
+        E = S.shape[0]
+        W = self._f(W).reshape(E, -1)
+        if W.shape[1] != self.d:
+            raise ValueError(f"W must be [{E}, {self.d}]")
+        if q_out is not None:
+            _dev_f32(q_out, self.device)
+        out = torch.empty(E, 2, dtype=torch.long, device=self.device)
+        check(lib.sfx_test_actions(self._h, S.data_ptr(), E, W.data_ptr(), W.stride(0), dptr(q_out),
+                                   out.data_ptr()), "sfx_test_actions")
+        return out
+
     def update(self, policy: int, s, a, r, phi, s1, gamma, use_gpi: bool = True,
                losses: Optional[torch.Tensor] = None, next_actions: Optional[torch.Tensor] = None):
         """One TD update of head `policy` (sfdqn.py:303-371 semantics).  r=None -> no l2 / w step."""

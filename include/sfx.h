@@ -118,6 +118,17 @@ int sfx_select_action(sfx_t h, const float* s_dev, int task_index, int use_gpi, 
                       int64_t* out_dev);
 
 /*
+ * Greedy test-task actions of E test tasks at once, each with its own reward weights
+ * (SFDQN.get_test_action's greedy branch, agents/sfdqn.py:125-137, for every test task of one
+ * lockstep step of agents/sfdqn.py:111-115 / test_agent :139-166):
+ *   q[e,t,a] = ψ_t(S[e])[a,:]·W[e,:];  c_e = argmax_t max_a q[e,t,a];  a_e = argmax_a q[e,c_e,a]
+ * (first index on ties).  S_dev [E, n_s], W_dev rows w_stride >= d floats apart,
+ * out_dev [E, 2] = (c_e, a_e), q_dev [E, T, A] may be NULL.
+ */
+int sfx_test_actions(sfx_t h, const float* S_dev, int E, const float* W_dev, int w_stride, float* q_dev,
+                     int64_t* out_dev);
+
+/*
  * One SF TD update of head `policy` (DeepSF.update_successor, sfdqn.py:303-371 ==
  * features/deep_sequential.py:163-231): GPI (or own-ψ) next actions over S1, targets
  * φ + γ ψ⁻_i(S1)[a'], l1 = MSE(ψ_i(S), merged) [+ l2 = MSE(w_i·φ, r) when r_dev != NULL,

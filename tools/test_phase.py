@@ -1,0 +1,180 @@
+"""The test phase a reference user runs (agents/sfdqn.py:111-115 over test_agent :139-166), over
+the drop-in library -- sequential as the reference runs it, or in lockstep through
+``sfx.lockstep``.  Used by tests/test_gpu_lockstep.py (the two must agree
+draw for draw) and by bench.py's ``other_workloads`` (test-phase env-steps/s, both ways).
+
+``EvalAgent`` carries the SFDQN members the test phase touches, restated as the user's program
+(the way tools/dropin_loop.py restates next_sample): ``get_test_action`` (:125-137),
+``test_agent`` (:139-166), ``update_test_reward_mapper`` (:168-184, SGD lr 0.005, weight decay
+0.01 on a bias-free Linear(d, 1)), ``get_target_reward_mapper_error`` (:208-217), and the test
+reward models initialised as in train (:87-98).
+"""
+from __future__ import annotations
+
+import random
+import time
+
+import numpy as np
+import torch
+
+
+class ActionEnv:
+    """A Reacher-shaped test task whose next state depends on the action (so a wrong action
+    shows in the returns) with its own random stream (tasks own their envs, as tasks/reacher.py's
+    bullet envs do)."""
+
+    def __init__(self, n_s, A, d, seed, device):
+        g = np.random.default_rng(1000 + seed)
+        self.rng = np.random.default_rng(seed)
+        self.M = (0.6 * g.standard_normal((A, n_s, n_s)) / np.sqrt(n_s)).astype(np.float32)
+        self.P = g.standard_normal((d, n_s)).astype(np.float32)
+        self.w = g.standard_normal(d).astype(np.float32)
+        self.n_s, self.A, self.d, self.device = n_s, A, d, device
+        self.s = None
+
+    def action_count(self):
+        return self.A
+
+    def feature_dim(self):
+        return self.d
+
+    def encode_dim(self):
+        return self.n_s
+
+    def get_w(self):
+        return torch.from_numpy(self.w).reshape(-1, 1)
+
+    def initialize(self):
+        self.s = self.rng.standard_normal(self.n_s).astype(np.float32)
+        return torch.from_numpy(self.s).to(self.device)
+
+    def transition(self, a):
+        a = int(a)
+        self.s = (np.tanh(self.M[a] @ self.s) + 0.1 * self.rng.standard_normal(self.n_s)).astype(np.float32)
+        r = float(np.tanh(self.P @ self.s) @ self.w)
+        return torch.from_numpy(self.s).to(self.device), r, False
+
+    def features(self, s, a, s1):
+        return torch.tanh(torch.from_numpy(self.P).to(s1.device) @ s1.reshape(-1))
+
+
+class _Log:
+    def __init__(self):
+        self.lines = []
+
+    def log_target_error_progress(self, d):
+        self.lines.append(d)
+
+
+class EvalAgent:
+    """The SFDQN members of the test phase (agents/sfdqn.py), over the drop-in DeepSF."""
+
+    def __init__(self, sf, n_actions, T, test_tasks, test_epsilon=0.03, device=None):
+        self.sf, self.n_actions, self.T, self.test_epsilon = sf, n_actions, T, test_epsilon
+        self.device = device
+        self.encoding = lambda s: s
+        self.logger = _Log()
+        self.total_training_steps = 0
+        self.test_tasks_weights = []
+        for task in test_tasks:  # agents/sfdqn.py:87-98
+            fit_w = torch.Tensor(1, task.feature_dim()).uniform_(-0.01, 0.01).to(device)
+            w = torch.nn.Linear(task.feature_dim(), 1, bias=False, device=device)
+            with torch.no_grad():
+                w.weight = torch.nn.Parameter(fit_w)
+            self.test_tasks_weights.append(w)
+
+    def get_test_action(self, s_enc, w):
+        with torch.no_grad():
+            if random.random() <= self.test_epsilon:
+                return torch.tensor(random.randrange(self.n_actions)).to(self.device)
+            q = w(self.sf.get_successors(s_enc))[:, :, :, 0]
+            c = torch.squeeze(torch.argmax(torch.max(q, axis=2).values, axis=1))
+            return torch.argmax(q[:, c, :])
+
+    def test_agent(self, task, test_index):
+        R, w = 0.0, self.test_tasks_weights[test_index]
+        s_enc = self.encoding(task.initialize())
+        acc = 0
+        for _ in range(self.T):
+            a = self.get_test_action(s_enc, w)
+            s1, r, done = task.transition(a)
+            s1_enc = self.encoding(s1)
+            acc += self.update_test_reward_mapper(w, task, r, s_enc, a, s1_enc).item()
+            s_enc = s1_enc
+            R += r
+            if done:
+                break
+        self.logger.log_target_error_progress(self.get_target_reward_mapper_error(R, acc, test_index, self.T))
+        return R
+
+    def update_test_reward_mapper(self, w_approx, task, r, s, a, s1):
+        phi = task.features(s, a, s1)
+        optim = torch.optim.SGD(w_approx.parameters(), lr=0.005, weight_decay=0.01)
+        r_t = torch.tensor(r).detach().float().unsqueeze(0).requires_grad_(False).to(self.device)
+        optim.zero_grad()
+        loss = torch.nn.MSELoss()(w_approx(phi), r_t)
+        loss.backward()
+        optim.step()
+        return loss
+
+    def get_target_reward_mapper_error(self, r, loss, task_index, ts):
+        return {"task": task_index, "reward": r, "steps": 500 * (self.total_training_steps // 1000) + ts,
+                "w_error": loss}
+
+
+def make(E=8, T_heads=8, n_s=6, H=256, A=9, d=8, acts=("relu", "relu"), ep_len=50, test_epsilon=0.03, seed=3,
+         device=None):
+    """A drop-in DeepSF with T_heads random heads and an agent over E test tasks."""
+    from sfx.dropin.features.deep import DeepSF
+    from tools.dropin_loop import psi_model_lambda
+
+    device = device or torch.device("cuda", 0)
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    sf = DeepSF(pytorch_model_handle=psi_model_lambda(H, acts, 1e-3, device), hyperparameters={},
+                target_update_ev=1000, max_batch=32)
+    sf.reset()
+    for t in range(T_heads):
+        sf.add_training_task(ActionEnv(n_s, A, d, 100 + t, device))
+    tasks = [ActionEnv(n_s, A, d, 200 + e, device) for e in range(E)]
+    agent = EvalAgent(sf, A, ep_len, tasks, test_epsilon, device)
+    return sf, agent, tasks
+
+
+def run_phase(agent, tasks, lockstep: bool):
+    """One test phase (agents/sfdqn.py:113-115): the E returns."""
+    if lockstep:
+        from sfx.lockstep import test_tasks_lockstep
+        return test_tasks_lockstep(agent, tasks)
+    return [agent.test_agent(task, i) for i, task in enumerate(tasks)]
+
+
+def measure(lockstep: bool, E=8, ep_len=50, phases=4, **kw) -> dict:
+    sf, agent, tasks = make(E=E, ep_len=ep_len, **kw)
+    run_phase(agent, tasks, lockstep)  # warm-up phase (graphs captured)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(phases):
+        run_phase(agent, tasks, lockstep)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    sf._close()
+    n = phases * E * ep_len
+    return {"value": round(n / dt, 2), "unit": "test env steps/s", "ms_per_step": round(1000.0 * dt / n, 4),
+            "steps": n, "dtype": "fp32",
+            "path": ("sfx.lockstep: E test tasks per sfx_test_actions launch set" if lockstep else
+                     "the reference's sequential test_agent loop over the drop-in get_successors") +
+                    f" (E={E} test tasks, {ep_len}-step episodes, T=8 heads, H=256)"}
+
+
+if __name__ == "__main__":
+    import json
+    import os
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "deep-successor-features-for-transfer_amd"))
+    sys.path.insert(0, root)
+    for ls in (False, True):
+        print(json.dumps({"lockstep" if ls else "sequential": measure(ls)}), flush=True)
