@@ -59,11 +59,11 @@ def test_tasks_lockstep(agent, test_tasks: Sequence, indices: Sequence[int] = No
     for j in range(T):
         S = torch.cat([torch.as_tensor(s).to(dev, torch.float32).reshape(1, -1) for s in s_enc])
         W = torch.cat([w.weight.detach().to(dev, torch.float32).reshape(1, -1) for w in ws])
-        sel = eng.test_actions(S, W)
+        greedy = eng.test_actions(S, W)[:, 1].unbind()
         losses = []
         for e, task in enumerate(test_tasks):
             x = sched[e][j]
-            a = torch.tensor(x).to(agent.device) if x >= 0 else sel[e, 1]
+            a = torch.tensor(x).to(agent.device) if x >= 0 else greedy[e]
             s1, r, done = task.transition(a)
             s1_enc = agent.encoding(s1)
             losses.append(agent.update_test_reward_mapper(ws[e], task, r, s_enc[e], a, s1_enc))
