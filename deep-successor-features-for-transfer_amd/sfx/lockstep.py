@@ -41,7 +41,7 @@ def _draw_schedule(E: int, T: int, epsilon: float, n_actions: int) -> List[List[
 
 def test_tasks_lockstep(agent, test_tasks: Sequence, indices: Sequence[int] = None) -> List:
     """``[agent.test_agent(task, i) for i, task in enumerate(test_tasks)]`` of agents/sfdqn.py
-    with the episodes in lockstep.  ``agent`` is the user's SFDQN over ``sfx``'s drop-in
+    (or of the single-file sfdqn.py, :665-721) with the episodes in lockstep.  ``agent`` is the user's SFDQN over ``sfx``'s drop-in
     ``DeepSF`` (``agent.sf``); returns the E returns R (as test_agent does)."""
     E = len(test_tasks)
     if E == 0:
@@ -52,7 +52,12 @@ def test_tasks_lockstep(agent, test_tasks: Sequence, indices: Sequence[int] = No
     sf._flush()
     dev, T = eng.device, int(agent.T)
     sched = _draw_schedule(E, T, float(agent.test_epsilon), int(agent.n_actions))
-    ws = [agent.test_tasks_weights[i] for i in idx]
+    # agents/sfdqn.py keeps w_approx per test task, the single-file sfdqn.py (w_approx, optim)
+    # with an optimizer argument to update_test_reward_mapper (sfdqn.py:652, :723)
+    entries = [agent.test_tasks_weights[i] for i in idx]
+    paired = isinstance(entries[0], tuple)
+    ws = [x[0] for x in entries] if paired else entries
+    adev = getattr(agent, "device", None) or sf._out_device()
     s_enc = [agent.encoding(task.initialize()) for task in test_tasks]
     R = [0.0] * E
     acc = [0] * E
@@ -63,10 +68,14 @@ def test_tasks_lockstep(agent, test_tasks: Sequence, indices: Sequence[int] = No
         losses = []
         for e, task in enumerate(test_tasks):
             x = sched[e][j]
-            a = torch.tensor(x).to(agent.device) if x >= 0 else greedy[e]
+            a = torch.tensor(x).to(adev) if x >= 0 else greedy[e]
             s1, r, done = task.transition(a)
             s1_enc = agent.encoding(s1)
-            losses.append(agent.update_test_reward_mapper(ws[e], task, r, s_enc[e], a, s1_enc))
+            if paired:
+                loss = agent.update_test_reward_mapper(ws[e], entries[e][1], task, r, s_enc[e], a, s1_enc)
+            else:
+                loss = agent.update_test_reward_mapper(ws[e], task, r, s_enc[e], a, s1_enc)
+            losses.append(loss)
             s_enc[e] = s1_enc
             R[e] += r
             if done and j + 1 < T:

@@ -114,3 +114,64 @@ def test_lockstep_refuses_episodes_that_end_early():
     tasks[0].transition = lambda a: real(a)[:2] + (True,)
     with pytest.raises(RuntimeError, match="full-length episodes"):
         test_tasks_lockstep(agent, tasks)
+
+
+class _SingleFileAgent(EvalAgent):
+    """The single-file sfdqn.py's test members (:640-652, :695-738): (w_approx, Adam) per test
+    task, the optimizer passed to update_test_reward_mapper, the module-level device."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.test_tasks_weights = [(w, torch.optim.Adam([{"params": w.parameters(), "lr": 1e-2,
+                                                           "weight_decay": 1e-2}]))
+                                   for w in self.test_tasks_weights]
+        del self.device
+
+    def get_test_action(self, s_enc, w):
+        if random.random() <= self.test_epsilon:
+            return torch.tensor(random.randrange(self.n_actions))
+        q = w(self.sf.get_successors(s_enc))[:, :, :, 0]
+        c = torch.squeeze(torch.argmax(torch.max(q, axis=2).values, axis=1))
+        return torch.argmax(q[:, c, :])
+
+    def test_agent(self, task, test_index):
+        R, (w, optim) = 0.0, self.test_tasks_weights[test_index]
+        s_enc, acc = self.encoding(task.initialize()), 0
+        for _ in range(self.T):
+            a = self.get_test_action(s_enc, w)
+            s1, r, done = task.transition(a)
+            acc += self.update_test_reward_mapper(w, optim, task, r, s_enc, a, s1).item()
+            s_enc = s1
+            R += r
+        self.logger.log_target_error_progress(self.get_target_reward_mapper_error(R, acc, test_index, self.T))
+        return R
+
+    def update_test_reward_mapper(self, w_approx, optim, task, r, s, a, s1):
+        phi = task.features(s, a, s1)
+        r_t = torch.tensor(r).float().unsqueeze(0)
+        optim.zero_grad()
+        loss = torch.nn.MSELoss()(w_approx(phi), r_t)
+        loss.backward()
+        optim.step()
+        return loss
+
+
+def test_lockstep_single_file_sfdqn_shape():
+    from sfx.lockstep import test_tasks_lockstep
+
+    def setup():
+        random.seed(11)
+        torch.manual_seed(11)
+        sf = _SF(_Psi(4, 6, 9, 8))
+        sf._out_device = lambda: torch.device("cpu")
+        tasks = [ActionEnv(6, 9, 8, 70 + e, torch.device("cpu")) for e in range(4)]
+        return sf, _SingleFileAgent(sf, 9, 10, tasks, 0.25, torch.device("cpu")), tasks
+
+    _, ref, tasks0 = setup()
+    want = [[ref.test_agent(t, i) for i, t in enumerate(tasks0)] for _ in range(2)]
+    st = random.getstate()
+    _, agent, tasks1 = setup()
+    assert [test_tasks_lockstep(agent, tasks1) for _ in range(2)] == want
+    assert random.getstate() == st and agent.logger.lines == ref.logger.lines
+    for (wa, _), (wb, _) in zip(agent.test_tasks_weights, ref.test_tasks_weights):
+        assert torch.equal(wa.weight, wb.weight)
