@@ -16,8 +16,12 @@ user's own ``update_test_reward_mapper`` -- the same arithmetic, the same draws,
 actions, the same returns and log lines in the same order as the sequential loop, with one GPU
 round trip per step instead of E.
 
-Precondition: episodes run the full ``agent.T`` steps (tasks/reacher.py:112 never ends one).  An
-episode that ends early would have shifted every later task's draws; the rollout then raises.
+Preconditions: each test task owns its env and its random state (tasks/reacher.py: one bullet
+env with its own ``np_random`` per task), since the lockstep order interleaves the tasks' env calls;
+and episodes run the full ``agent.T`` steps (tasks/reacher.py:112 never ends one) -- an episode that
+ended early would have shifted every later task's draws, so the rollout raises.  The TSF agents'
+test phase (two actions per step, an LR schedule, conditional logs) keeps the sequential loop over
+the HIP test-task calls of ``sfx.dropin.bind``.
 """
 from __future__ import annotations
 
