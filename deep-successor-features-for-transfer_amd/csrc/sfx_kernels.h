@@ -1119,12 +1119,16 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
   const float wk = tid < d ? G.w[(long long)pol * G.dpad + tid] : 0.f;
   const int ab_l = tid < nb ? (int)A.tdg_a[m0 + tid] : 0;
   const float gam_l = tid < nb ? A.tdg_gamma[m0 + tid] : 0.f;
-  float xv[4];
+  int xv[4];  // raw sortable ints: decoded after the barrier, so no wait is placed here
   if (xm) {  // the all-reduced maxima rows of this policy: stage C's output
     const int* xr = A.tdg_xmax + ((size_t)(A.tdg_poloff + pol) * M + m0) * Aa;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) xv[u] = tid + u * 256 < nb * Aa ? unsortable(xr[tid + u * 256]) : 0.f;
+    for (int u = 0; u < 4; ++u) xv[u] = tid + u * 256 < nb * Aa ? xr[tid + u * 256] : 0;
   }
+  // the previous round's next action of this thread's row, requested with the other operands
+  // (stage D compares against it; a load there would cost a dependent round trip)
+  const int64_t* prev = A.tdg_prev ? A.tdg_prev + (size_t)(pol - A.head0) * A.tdg_next_stride + m0 : nullptr;
+  const int64_t prev_l = prev && tid < nb ? prev[tid] : -1;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int i = tid + u * 256;
@@ -1145,7 +1149,7 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
   if (xm) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if (tid + u * 256 < nb * Aa) sm.m[tid + u * 256] = xv[u];
+      if (tid + u * 256 < nb * Aa) sm.m[tid + u * 256] = unsortable(xv[u]);
   }
   // ---- stage B: q = ψ·w, one fmaf chain per dot in k order
 #pragma unroll
@@ -1174,7 +1178,6 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
   }
   __syncthreads();
   // ---- stage D: first argmax over actions
-  const int64_t* prev = A.tdg_prev ? A.tdg_prev + (size_t)(pol - A.head0) * A.tdg_next_stride + m0 : nullptr;
   int differs = prev == nullptr || m0 != 0 || nb != M;  // skipping needs every row of the policy
   for (int bl = tid; bl < nb; bl += 256) {
     const float* mb = sm.m + bl * Aa;
@@ -1186,7 +1189,7 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
         am = a;
       }
     sm.n[bl] = am;
-    if (prev && prev[bl] != am) differs = 1;
+    if (prev && (bl == tid ? prev_l : prev[bl]) != am) differs = 1;
     if (pub && A.tdg_next) A.tdg_next[(size_t)(pol - A.head0) * A.tdg_next_stride + m0 + bl] = am;
   }
   const int same = !__syncthreads_or(differs);
