@@ -401,6 +401,13 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
 
     for ls in (False, True):
         out[f"reacher-test-phase-E8-{'lockstep' if ls else 'sequential'}"] = test_phase.measure(ls, device=device)
+    # the TSF agents' test phase (agents/tsfdqn_sequential.py:385-420) at the Hopper TSF shape:
+    # the per-call drop-in binding vs sfx.lockstep.test_tasks_lockstep_tsf
+    from tools import tsf_test_phase
+
+    for ls in (False, True):
+        out[f"hopper-tsf-test-phase-E8-{'lockstep' if ls else 'sequential'}"] = tsf_test_phase.measure(
+            ls, device=device)
     return out
 
 

@@ -530,12 +530,48 @@ struct TsfTestArgs {
   AdamHP hpw, hpo;
   float* losses;         // [3]: loss, l2, l1 (the reference's return order)
   int64_t* act_out;      // k_tsf_test_act: the greedy action
+  // Lockstep test phase (sfx_tsf_test_actions / sfx_tsf_test_updates): row e of a launch is test
+  // task e -- its state rows s/s1 [E][n_s], ψ row e of the forward, φ [E][d], a/a1 [E], w / ω /
+  // moments at their row strides, losses [E][3], act_out [E]; rowp [E][6] = r, lr_w, wd_w, lr_ω,
+  // wd_ω, step of each task's own optimizer (nullptr: the scalar fields above, E = 1).
+  int w_stride, o_stride, mom_stride, pad3_;
+  const float* rowp;
 };
+
+// The arguments of test task e (row e of a lockstep launch); e = 0 with rowp == nullptr is the
+// single-task call unchanged.
+__device__ inline TsfTestArgs tsf_test_row(const TsfTestArgs& A0, int e) {
+  TsfTestArgs A = A0;
+  if (A.s) A.s += (long long)e * A.n_s;
+  if (A.s1) A.s1 += (long long)e * A.n_s;
+  if (A.gfeat) A.gfeat += (long long)e * 2 * A.T * A.G;
+  if (A.psi) A.psi += (long long)e * A.O;
+  if (A.psi1) A.psi1 += (long long)e * A.O;
+  if (A.phi) A.phi += (long long)e * A.d;
+  if (A.a) A.a += e;
+  if (A.a1) A.a1 += e;
+  if (A.w) A.w += (long long)e * A.w_stride;
+  if (A.omega) A.omega += (long long)e * A.o_stride;
+  if (A.mom) A.mom += (long long)e * A.mom_stride;
+  if (A.losses) A.losses += (long long)e * 3;
+  if (A.act_out) A.act_out += e;
+  if (A.rowp) {
+    const float* p = A.rowp + (long long)e * 6;
+    A.r = p[0];
+    A.hpw.lr = p[1];
+    A.hpw.wd = p[2];
+    A.hpo.lr = p[3];
+    A.hpo.wd = p[4];
+    A.step = (int)p[5];
+  }
+  return A;
+}
 
 // g_t(s), g_t(s1) for every task: one wave per task, lanes 0..31 row s, 32..63 row s1, one state
 // component per lane through the K planar flows (w_k·z by a xor butterfly within the 32-lane
 // half), then Linear(n_s, G) from LDS.
-__global__ __launch_bounds__(64) void k_tsf_test_g(TsfTestArgs A) {
+__global__ __launch_bounds__(64) void k_tsf_test_g(TsfTestArgs A0) {
+  const TsfTestArgs A = tsf_test_row(A0, blockIdx.y);
   const int t = blockIdx.x, lane = threadIdx.x, row = lane >> 5, j = lane & 31, n_s = A.n_s, G = A.G;
   const float* gp = A.g + (long long)t * A.Pg;
   const bool on = j < n_s;
@@ -564,7 +600,8 @@ __global__ __launch_bounds__(64) void k_tsf_test_g(TsfTestArgs A) {
 }
 
 // The greedy test action: argmax_a Σ_k w_k Σ_t ω̂_t ψ_t(s)[a][k] (first index on ties), one WG.
-__global__ __launch_bounds__(256) void k_tsf_test_act(TsfTestArgs A) {
+__global__ __launch_bounds__(256) void k_tsf_test_act(TsfTestArgs A0) {
+  const TsfTestArgs A = tsf_test_row(A0, blockIdx.x);
   __shared__ float s_on[64];
   __shared__ float s_q[256];
   const int tid = threadIdx.x, T = A.T, d = A.d;
@@ -593,7 +630,8 @@ __global__ __launch_bounds__(256) void k_tsf_test_act(TsfTestArgs A) {
 }
 
 // One update_test_reward_mapper step, one WG (T <= 64, d <= 256, G <= 512).
-__global__ __launch_bounds__(256) void k_tsf_test_step(TsfTestArgs A) {
+__global__ __launch_bounds__(256) void k_tsf_test_step(TsfTestArgs A0) {
+  const TsfTestArgs A = tsf_test_row(A0, blockIdx.x);
   const int tid = threadIdx.x, T = A.T, d = A.d, G = A.G;
   __shared__ float s_om[64], s_on[64], s_dn[64];
   __shared__ float s_ws[2][512], s_gws[512];

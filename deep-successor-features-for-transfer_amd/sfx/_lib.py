@@ -104,6 +104,8 @@ SIGNATURES = {
     "sfx_phi_get": (_I, [_VP, _VP]),
     "sfx_phi_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _VP, _VP]),
     "sfx_tsf_test_update": (_I, [_VP, _VP, _VP, _VP, _VP, _F, _VP, _VP, _VP, _VP, _I] + [_F] * 7 + [_VP]),
+    "sfx_tsf_test_actions": (_I, [_VP, _VP, _I, _VP, _I, _VP, _I, _VP]),
+    "sfx_tsf_test_updates": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _VP, _I, _VP, _I, _VP, _F, _F, _F, _VP]),
 }
 
 # env callbacks of sfx_runner_create (include/sfx.h)

@@ -409,6 +409,44 @@ class SFEngine:
                                       losses.data_ptr()), "sfx_tsf_test_update")
         return losses
 
+    def tsf_test_actions(self, S, W: torch.Tensor, Omega: torch.Tensor, out: Optional[torch.Tensor] = None):
+        """tsf_test_action for E test tasks in one launch set (lockstep test phase): S [E, n_s],
+        W [E, d] / Omega [E, T] float32 device tensors with unit column stride.  Returns the
+        int64 device tensor [E] (not synchronized)."""
+        S = self._f(S)
+        E = S.shape[0]
+        _dev_f32(W, self.device)
+        _dev_f32(Omega, self.device)
+        if W.shape != (E, self.d) or Omega.shape != (E, self.T) or W.stride(1) != 1 or Omega.stride(1) != 1:
+            raise ValueError(f"W must be [{E}, {self.d}] and Omega [{E}, {self.T}] with unit column stride")
+        out = torch.empty(E, dtype=torch.long, device=self.device) if out is None else out
+        check(lib.sfx_tsf_test_actions(self._h, S.data_ptr(), E, W.data_ptr(), W.stride(0), Omega.data_ptr(),
+                                       Omega.stride(0), out.data_ptr()), "sfx_tsf_test_actions")
+        return out
+
+    def tsf_test_updates(self, S, S1, a, a1, phi, W: torch.Tensor, Omega: torch.Tensor, adam_state: torch.Tensor,
+                         rowp: torch.Tensor, gamma: float, beta: float, lasso: float,
+                         losses: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """tsf_test_update for E test tasks in one launch set: W [E, d], Omega [E, T],
+        adam_state [E, 2d + 2T] updated in place; rowp [E, 6] device float32 (r, lr_w, wd_w,
+        lr_omega, wd_omega, step per task).  Returns losses [E, 3] = (loss, l2, l1) per row."""
+        S, S1 = self._f(S), self._f(S1)
+        E = S.shape[0]
+        phi = self._f(phi, (E, self.d))
+        a, a1 = self._l(a), self._l(a1)
+        for t in (W, Omega, adam_state, rowp):
+            _dev_f32(t, self.device)
+            if t.stride(-1) != 1 or t.shape[0] != E:
+                raise ValueError("sfx tsf_test_updates: row-major [E, ...] tensors expected")
+        if rowp.shape != (E, 6) or not rowp.is_contiguous():
+            raise ValueError(f"rowp must be a contiguous [{E}, 6] tensor")
+        losses = torch.empty(E, 3, device=self.device) if losses is None else losses
+        check(lib.sfx_tsf_test_updates(self._h, E, S.data_ptr(), S1.data_ptr(), a.data_ptr(), a1.data_ptr(),
+                                       phi.data_ptr(), W.data_ptr(), W.stride(0), Omega.data_ptr(), Omega.stride(0),
+                                       adam_state.data_ptr(), adam_state.stride(0), rowp.data_ptr(), float(gamma),
+                                       float(beta), float(lasso), losses.data_ptr()), "sfx_tsf_test_updates")
+        return losses
+
     def tsf_update(self, policy: int, s, a, r, phi, s1, gamma, use_gpi: bool = True,
                    losses: Optional[torch.Tensor] = None, next_actions: Optional[torch.Tensor] = None):
         """TSFDQN.update_successor (tsfdqn.py:588-709): returns losses [3] = (l1 + beta l2, l1, l2)."""

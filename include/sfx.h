@@ -408,6 +408,21 @@ int sfx_tsf_test_update(sfx_t h, const float* s_dev, const float* s1_dev, const 
                         float r, const float* phi_dev, float* w_dev, float* omega_dev, float* adam_state_dev,
                         int step, float gamma, float beta, float lasso, float lr_w, float wd_w, float lr_omega,
                         float wd_omega, float* losses_dev);
+/* Lockstep test phase (SURVEY §8f rank 3 for the TSF agents: agents/tsfdqn_sequential.py:392-433,
+ * tsfdqn.py:872-915 -- the E test tasks' episodes stepped together).  Row e is test task e:
+ * S_dev / S1_dev [E][n_s], W_dev rows at w_stride (>= d), Omega_dev rows at o_stride (>= T),
+ * adam_state_dev rows at mom_stride (>= 2d + 2T), E <= max_batch.
+ * sfx_tsf_test_actions: a_dev [E] = sfx_tsf_test_action of every row, one launch set.
+ * sfx_tsf_test_updates: sfx_tsf_test_update of every row (a_dev / a1_dev [E], phi_dev [E][d],
+ *   losses_dev [E][3]); rowp_dev [E][6] holds each task's r, lr_w, wd_w, lr_omega, wd_omega and
+ *   its 1-based Adam step (as a float) -- each test task owns its optimizer and LR schedule
+ *   (agents/tsfdqn_sequential.py:333-348). */
+int sfx_tsf_test_actions(sfx_t h, const float* S_dev, int E, const float* W_dev, int w_stride, const float* Omega_dev,
+                         int o_stride, int64_t* a_dev);
+int sfx_tsf_test_updates(sfx_t h, int E, const float* S_dev, const float* S1_dev, const int64_t* a_dev,
+                         const int64_t* a1_dev, const float* phi_dev, float* W_dev, int w_stride, float* Omega_dev,
+                         int o_stride, float* adam_state_dev, int mom_stride, const float* rowp_dev, float gamma,
+                         float beta, float lasso, float* losses_dev);
 
 /* ---------------------------------------------------------------------------------------
  * TSF-DQN with the source-task heads sharded across ranks (BASELINE config C5: tsfdqn_nf.py,

@@ -175,3 +175,113 @@ def test_lockstep_single_file_sfdqn_shape():
     assert random.getstate() == st and agent.logger.lines == ref.logger.lines
     for (wa, _), (wb, _) in zip(agent.test_tasks_weights, ref.test_tasks_weights):
         assert torch.equal(wa.weight, wb.weight)
+
+
+# ---- TSF agents' test phase (sfx.lockstep.test_tasks_lockstep_tsf; tools/tsf_test_phase.py) ----
+
+class _TsfOracleEngine:
+    """The four TSF test-task calls of the engine over the oracle (oracle/ref_cpu.py
+    tsf_test_action / tsf_test_update, pinned by tests/golden/test_tsf*.npz), row by row, with the
+    float32 rounding of the C ABI's scalar arguments: the sequential binding and the lockstep rollout
+    then agree exactly when the host logic (draws, schedules, LR, steps, write-back) does."""
+    device = torch.device("cpu")
+    max_batch = 4
+
+    def __init__(self, st):
+        self.st, self.batched = st, 0
+
+    def tsf_test_action(self, s, w, om):
+        from oracle import ref_cpu as R
+        return torch.tensor(R.tsf_test_action(self.st, torch.as_tensor(s).float(), w, om))
+
+    def tsf_test_update(self, s, s1, a, a1, r, phi, w, om, state, step, gamma, beta, lasso, lr_w, wd_w, lr_o, wd_o):
+        import numpy as np
+        from oracle import ref_cpu as R
+        f = lambda x: float(np.float32(x))  # noqa: E731
+        d, T = w.numel(), om.numel()
+        tm = R.TestMapper(w.clone(), om.clone(), state[:d].clone(), state[d:2 * d].clone(),
+                          state[2 * d:2 * d + T].clone(), state[2 * d + T:].clone(), step - 1)
+        out = R.tsf_test_update(self.st, tm, torch.as_tensor(s).float(), int(a), f(r), torch.as_tensor(phi).float(),
+                                torch.as_tensor(s1).float(), int(a1), gamma=f(gamma), beta=f(beta), lasso=f(lasso),
+                                lr_w=f(lr_w), wd_w=f(wd_w), lr_o=f(lr_o), wd_o=f(wd_o))
+        w.copy_(tm.w)
+        om.copy_(tm.omega)
+        state.copy_(torch.cat([tm.wm, tm.wv, tm.om, tm.ov]))
+        return torch.tensor(out)
+
+    def tsf_test_actions(self, S, W, Om):
+        assert S.shape[0] <= self.max_batch
+        self.batched += 1
+        return torch.stack([self.tsf_test_action(S[e], W[e], Om[e]) for e in range(S.shape[0])])
+
+    def tsf_test_updates(self, S, S1, A, A1, PHI, W, Om, M, rowp, gamma, beta, lasso, losses):
+        self.batched += 1
+        for e in range(S.shape[0]):
+            r, lw, ww, lo, wo, step = rowp[e].tolist()
+            losses[e] = self.tsf_test_update(S[e], S1[e], A[e], A1[e], r, PHI[e], W[e], Om[e], M[e], int(step), gamma,
+                                             beta, lasso, lw, ww, lo, wo)
+        return losses
+
+
+def _tsf_setup(E, ep_len, eps, total=0, seed=11):
+    from oracle import ref_cpu as R
+    from tools import tsf_test_phase as P
+
+    T, n_s, A, d, G, K = 4, 6, 9, 8, 10, 2
+    spec, gs = R.Spec(n_s, 16, A, d), R.GSpec(n_s, G, K)
+    g = torch.Generator().manual_seed(5)
+    online = 0.3 * torch.randn(T, spec.P, generator=g)
+    st = R.TSFState(spec, online, online + 1e-2 * torch.randn(T, spec.P, generator=g), torch.zeros(T, d), gspec=gs,
+                    g=0.3 * torch.randn(T, K * (2 * n_s + 1) + G * n_s + G, generator=g),
+                    h=0.3 * torch.randn(d * G + d, generator=g))
+    _, agent, tasks = P.make(E=E, T_heads=T, n_s=n_s, A=A, d=d, ep_len=ep_len, test_epsilon=eps, seed=seed,
+                             total_training_steps=total, eng=_TsfOracleEngine(st), device=torch.device("cpu"))
+    return agent, tasks
+
+
+def _printed(capsys):
+    import re
+    return sorted(re.sub(r" at 0x[0-9a-f]+", "", x) for x in capsys.readouterr().out.splitlines())
+
+
+@pytest.mark.parametrize("E,eps,total", [(3, 0.05, 0), (6, 0.4, 5000), (2, 1.0, 1000), (5, 0.0, 7)])
+def test_tsf_lockstep_matches_sequential_test_phase(E, eps, total, capsys):
+    """Two phases: returns, fitted w / ω, Adam moments, LR schedules, log lines (only when
+    total_training_steps % 5000 == 0), the diagnostic prints (randint draws when % 1000 == 0)
+    and the random state as the reference's sequential loop; E = 5, 6 run as two lockstep
+    groups (max_batch 4)."""
+    from sfx.lockstep import test_tasks_lockstep_tsf
+
+    ep_len, phases = 6, 2
+    ref, tasks0 = _tsf_setup(E, ep_len, eps, total)
+    R0 = [[ref.test_agent(t, i) for i, t in enumerate(tasks0)] for _ in range(phases)]
+    st0 = random.getstate()
+    out0 = _printed(capsys)
+    agent, tasks1 = _tsf_setup(E, ep_len, eps, total)
+    R1 = [test_tasks_lockstep_tsf(agent, tasks1) for _ in range(phases)]
+    assert random.getstate() == st0
+    assert _printed(capsys) == out0
+    assert R1 == R0
+    assert agent.logger.lines == ref.logger.lines
+    assert bool(agent.logger.lines) == (total % 5000 == 0)
+    for (wa, oa, sa), (wb, ob, sb) in zip(agent.test_tasks_weights, ref.test_tasks_weights):
+        assert torch.equal(wa.weight.detach(), wb.weight.detach())
+        assert oa.param_groups[1]["lr"] == ob.param_groups[1]["lr"]
+    for oa, ob in zip(agent.omegas, ref.omegas):
+        assert torch.equal(oa.detach(), ob.detach())
+    for (ka, va), (kb, vb) in zip(agent.sf._test_state.items(), ref.sf._test_state.items()):
+        assert torch.equal(va[0], vb[0]) and va[1] == vb[1] == phases * ep_len
+    assert agent.sf._eng.batched == phases * ep_len * 3 * ((E + 3) // 4)
+
+
+def test_tsf_enable_binds_lockstep_into_train_loop():
+    """enable() on a TSF agent (it has ``omegas``): the reference's per-task test_agent calls of
+    train (agents/tsfdqn_sequential.py:361-364) return the lockstep returns, in order."""
+    from sfx import lockstep
+
+    ref, tasks0 = _tsf_setup(3, 5, 0.1)
+    R0 = [ref.test_agent(t, i) for i, t in enumerate(tasks0)]
+    agent, tasks1 = _tsf_setup(3, 5, 0.1)
+    agent.train = lambda *a, **k: [agent.test_agent(t, i) for i, t in enumerate(k["test_tasks"])]
+    lockstep.enable(agent)
+    assert agent.train([], 0, test_tasks=tasks1) == R0
