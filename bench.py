@@ -41,6 +41,7 @@ SHAPE = dict(n_s=17, H=256, A=7, d=8, acts=("relu", "relu"))
 # BASELINE.json configs C3 / C5 (one GPU): Hopper-shape TSF-DQN, |s|=11, 27 actions, d=50, 16 source
 # tasks, g_i / h width 100; K planar layers in g_i for tsfdqn_nf.py (reacher.cfg n_coupling_layers=100)
 TSF_SHAPE = dict(n_s=11, H=256, A=27, d=50, acts=("relu", "relu"), G=100)
+C1_SHAPE = dict(n_s=4, H=256, A=2, d=20, acts=("relu", "relu"))  # BASELINE C1 (CartPole-v2)
 WORKLOADS = {"reacher-sf": None, "hopper-tsf": 0, "hopper-tsf-nf": 100}
 KIND_NAMES = {"fwd": "k_fwd", "tdg": "k_tdg", "bwd": "k_bwd", "gpi": "k_gpi", "lms": "k_lms", "ver": "k_ver",
               "round": "k_round", "tsf": "k_tsf"}
@@ -89,6 +90,8 @@ def parse():
 
 
 def shape_of(args):
+    if getattr(args, "c1", False):
+        return C1_SHAPE
     return SHAPE if args.tsf_K is None else TSF_SHAPE
 
 
@@ -355,9 +358,12 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
                                       ("reacher17-all-T8-B32-bf16", "all", None, False, "bf16"),
                                       ("hopper11-tsf-T16-B32", "tsf", 0, False, "fp32"),
                                       ("hopper11-tsf-T16-B32-bf16", "tsf", 0, False, "bf16"),
-                                      ("hopper11-tsf-nf100-T16-B32", "tsf", 100, False, "fp32")):
-        sh = SHAPE if K is None else TSF_SHAPE
-        T = 8 if K is None else 16
+                                      ("hopper11-tsf-nf100-T16-B32", "tsf", 100, False, "fp32"),
+                                      ("cartpole4-all-T2-B32", "all", None, False, "fp32")):
+        # C1: CartPole-v2 SF-DQN (n_s 4, A 2, d 20: configs/cartpole_phi.cfg:52), 2 source tasks
+        c1 = name.startswith("cartpole")
+        sh = C1_SHAPE if c1 else SHAPE if K is None else TSF_SHAPE
+        T = 2 if c1 else 8 if K is None else 16
         eng = SFEngine(T, sh["n_s"], sh["H"], sh["A"], sh["d"], sh["acts"], max_batch=args.batch, device=device)
         if K is None:
             online, w = reference_heads(T, sh["n_s"], sh["H"], sh["A"], sh["d"], sh["acts"], seed=0)
@@ -597,6 +603,12 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, args.cpu_seconds)
+            if args.tsf_K is None and args.schedule == "all" and args.other:
+                # C1 (CartPole shape, 2 source tasks) on the same host cores, beside the headline's
+                c1 = argparse.Namespace(**vars(args))
+                c1.c1, c1.heads = True, 2
+                cpu["c1_cartpole4_all_T2_B32"] = {k: v for k, v in cpu_baseline(c1, 5.0).items()
+                                                  if k in ("value", "unit", "cores", "kind", "sample")}
         other = None
         if world == 1 and args.other and args.tsf_K is None and args.schedule == "all":
             other = bench_other_workloads(args, device)
