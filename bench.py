@@ -430,6 +430,27 @@ def traffic_from_profiles(kind: str, workload: str):
         return None
 
 
+def rocprof_avg_from_profiles(kind: str):
+    """Average duration (µs) of `kind`'s launches in the committed rocprofv3 --kernel-trace --stats
+    summary of the headline workload (profiles/headline_kernel_stats.csv, copied from the latest
+    round-end profile run), or None."""
+    path = os.path.join(ROOT, "profiles", "headline_kernel_stats.csv")
+    if not os.path.exists(path):
+        return None
+    try:
+        import csv
+        base = KIND_NAMES[kind]
+        n = ns = 0.0
+        for r in csv.DictReader(open(path)):
+            name = r["Name"].split("(")[0].split("<")[0].split("::")[-1].strip()
+            if name == base or name.startswith(base + "_"):
+                n += float(r["Calls"])
+                ns += float(r["TotalDurationNs"])
+        return ns / n / 1000.0 if n else None
+    except Exception:
+        return None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -574,6 +595,14 @@ def main():
                     "bytes_per_launch": round(bpl), "avg_launch_us": round(avg_us, 3),
                     "share_of_gpu_time": round(us / max(sum(v[1] for v in stats.values()), 1e-9), 3),
                     "per_kind_avg_us": {KIND_NAMES[k]: round(v[1] / max(v[0], 1), 3) for k, v in stats.items() if v[0]}}
+        if args.tsf_K is None and args.schedule == "all":
+            # the same kind's average in the committed rocprofv3 stats (whole 550-step profiled run,
+            # early steps with fewer skipped rounds included): the conservative fraction beside the live one
+            rp = rocprof_avg_from_profiles(kind)
+            if rp:
+                roofline["rocprof_avg_us"] = round(rp, 3)
+                roofline["rocprof_frac"] = round(bpl / (rp * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)
+                roofline["rocprof_source"] = "profiles/headline_kernel_stats.csv"
         # SURVEY §8(d)'s whole-step figure: the ALGORITHMIC bytes of one env step x env-steps/s / peak,
         # per GPU.  Launched bytes (each launch's own minimum, summed -- speculative re-work included)
         # are reported beside it as a ratio, never as achieved bandwidth.
