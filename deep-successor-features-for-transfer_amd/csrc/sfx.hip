@@ -1271,6 +1271,15 @@ int sfx_test_actions(sfx_t h, const float* S, int E, const float* W, int w_strid
   });
 }
 
+int sfx_test_reward_updates(sfx_t h, int E, const float* phi, const float* r, float* W, int w_stride, double lr,
+                            double wd, float* loss) {
+  if (!h || !phi || !r || !W || !loss || E < 1 || w_stride < h->d) SFX_FAIL(SFX_E_ARG, "bad args");
+  launch(h, K_GPI, 12.0 * E * h->d, k_sf_test_mapper, dim3(cdiv(E, 64)), dim3(64), E, h->d, phi, r, W, w_stride,
+         (float)(-lr), (float)wd, loss);
+  LAUNCHCHK();
+  return SFX_OK;
+}
+
 int sfx_update(sfx_t h, int policy, const float* S, const int64_t* a, const float* r, const float* phi,
                const float* S1, const float* gamma, int B, int use_gpi, float* losses, int64_t* next) {
   if (!valid_head(h, policy) || !S || !a || !phi || !S1 || !gamma) SFX_FAIL(SFX_E_ARG, "bad args");

@@ -2275,6 +2275,32 @@ __global__ void k_lms(float* __restrict__ w, const float* __restrict__ phi, cons
   if (tid < d) w[tid] = __fadd_rn(wk, __fmul_rn(s_e, pk));
 }
 
+// SFDQN.update_test_reward_mapper (agents/sfdqn.py:168-184) for E test tasks, one lane per task:
+// a fresh SGD(lr, weight_decay=wd) step on the bias-free Linear(d, 1) w_e with the loss
+// MSE(w_e(φ_e), r_e) -- y = w·φ, loss = (y - r)², ∂w = 2(y - r) φ (mse_loss_backward: 2/N with
+// N = 1), d_p = ∂w + wd·w, w += -lr·d_p (torch/optim/sgd.py single-tensor, no momentum).  The
+// loss is the pre-step value, as the reference returns it.  lr / wd are narrowed where ATen
+// narrows its Scalar arguments.
+__global__ __launch_bounds__(64) void k_sf_test_mapper(int E, int d, const float* __restrict__ phi,
+                                                       const float* __restrict__ r, float* __restrict__ W,
+                                                       int w_stride, float neg_lr, float wd,
+                                                       float* __restrict__ loss) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const float* f = phi + (long long)e * d;
+  float* w = W + (long long)e * w_stride;
+  float y = 0.f;
+  for (int k = 0; k < d; ++k) y = __builtin_fmaf(w[k], f[k], y);
+  const float diff = __fsub_rn(y, r[e]);
+  const float gy = __fmul_rn(2.f, diff);
+  for (int k = 0; k < d; ++k) {
+    const float wk = w[k];
+    const float dp = __fadd_rn(__fmul_rn(gy, f[k]), __fmul_rn(wd, wk));
+    w[k] = __builtin_fmaf(neg_lr, dp, wk);
+  }
+  loss[e] = __fmul_rn(diff, diff);
+}
+
 }  // namespace sfx
 
 namespace sfx {

@@ -229,6 +229,26 @@ class SFEngine:
                                    out.data_ptr()), "sfx_test_actions")
         return out
 
+    def test_reward_updates(self, phi, r, W: torch.Tensor, lr: float = 0.005, wd: float = 0.01,
+                            losses: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """SFDQN.update_test_reward_mapper (agents/sfdqn.py:168-184) of E test tasks in one launch:
+        a fresh SGD(lr, weight_decay=wd) step on each row of W [E, d] (float32 device tensor with
+        unit column stride, updated in place) against MSE(W[e]·phi[e], r[e]).  Returns the E
+        pre-step losses (device tensor, not synchronized)."""
+        E = W.shape[0]
+        if W.dim() != 2 or W.shape[1] != self.d or W.stride(1) != 1 or W.dtype != torch.float32 \
+                or W.device != self.device:
+            raise ValueError(f"W must be a float32 [{E}, {self.d}] device tensor with unit column stride")
+        phi = self._f(phi, (E, self.d))
+        r = self._f(r, (E,))
+        losses = torch.empty(E, device=self.device) if losses is None else losses
+        _dev_f32(losses, self.device)
+        if losses.numel() != E:
+            raise ValueError(f"losses must hold {E} floats")
+        check(lib.sfx_test_reward_updates(self._h, E, phi.data_ptr(), r.data_ptr(), W.data_ptr(), W.stride(0),
+                                          float(lr), float(wd), losses.data_ptr()), "sfx_test_reward_updates")
+        return losses
+
     def update(self, policy: int, s, a, r, phi, s1, gamma, use_gpi: bool = True,
                losses: Optional[torch.Tensor] = None, next_actions: Optional[torch.Tensor] = None):
         """One TD update of head `policy` (sfdqn.py:303-371 semantics).  r=None -> no l2 / w step."""

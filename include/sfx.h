@@ -129,6 +129,16 @@ int sfx_test_actions(sfx_t h, const float* S_dev, int E, const float* W_dev, int
                      int64_t* out_dev);
 
 /*
+ * The test tasks' reward models of one lockstep step: SFDQN.update_test_reward_mapper
+ * (agents/sfdqn.py:168-184: a fresh SGD(lr=0.005, weight_decay=0.01) step on the bias-free
+ * Linear(d, 1) w_e, loss MSE(w_e(φ_e), r_e)) for E test tasks in one launch.  phi_dev [E, d]
+ * contiguous, r_dev [E], W_dev rows w_stride >= d floats apart (updated in place), loss_dev [E]
+ * = the pre-step losses the reference returns.  Asynchronous on the handle's stream.
+ */
+int sfx_test_reward_updates(sfx_t h, int E, const float* phi_dev, const float* r_dev, float* W_dev, int w_stride,
+                            double lr, double wd, float* loss_dev);
+
+/*
  * One SF TD update of head `policy` (DeepSF.update_successor, sfdqn.py:303-371 ==
  * features/deep_sequential.py:163-231): GPI (or own-ψ) next actions over S1, targets
  * φ + γ ψ⁻_i(S1)[a'], l1 = MSE(ψ_i(S), merged) [+ l2 = MSE(w_i·φ, r) when r_dev != NULL,

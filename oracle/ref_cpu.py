@@ -528,6 +528,25 @@ def tsf_test_update(st: "TSFState", tm: TestMapper, s, a: int, r: float, phi, s1
     return float(loss.detach()), float(l2.detach()), float(l1.detach())
 
 
+def sf_test_reward_update(w: torch.Tensor, phi, r) -> float:
+    """SFDQN.update_test_reward_mapper (agents/sfdqn.py:168-184) on a [1, d] (or [d]) weight
+    tensor, updated in place: a fresh SGD(lr=0.005, weight_decay=0.01) step of
+    MSE(Linear(d, 1, bias=False)(φ), r), by autograd and torch.optim.SGD as the reference runs it.
+    Returns the pre-step loss."""
+    lin = torch.nn.Linear(w.numel(), 1, bias=False)
+    with torch.no_grad():
+        lin.weight.copy_(w.reshape(1, -1))
+    optim = torch.optim.SGD(lin.parameters(), lr=0.005, weight_decay=0.01)
+    r_t = torch.tensor(r).detach().float().unsqueeze(0)
+    optim.zero_grad()
+    loss = torch.nn.MSELoss()(lin(torch.as_tensor(phi).float()), r_t)
+    loss.backward()
+    optim.step()
+    with torch.no_grad():
+        w.copy_(lin.weight.detach().reshape(w.shape))
+    return float(loss.detach())
+
+
 # --------------------------------------------------------------------------------------
 # Learned φ (SURVEY §8f rank 4): features/deep_phi.py DeepSF_PHI.update_successor (:93-224),
 # the library of main_sfdqn_phi_torch.py with agents/sfdqn_phi.py.  φ = phi_net(s ⊕ a ⊕ s1) is an

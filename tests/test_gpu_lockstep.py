@@ -5,7 +5,10 @@
   that q, across launch chunks (E > max_batch).
 * A whole test phase over the drop-in DeepSF, sequential as the reference runs it
   (tools/test_phase.py restates agents/sfdqn.py:139-184) vs in lockstep: the same returns, the
-  same fitted reward models (bit for bit), the same log lines and the same random-stream state.
+  same fitted reward models (bit for bit with the user's torch mapper; within 1e-5 with the
+  device mapper), the same log lines and the same random-stream state.
+* ``sfx_test_reward_updates`` (agents/sfdqn.py:168-184 for E rows) vs the oracle at 1e-4.
+* Episodes that end early: the lockstep entry point runs the sequential loop (decided up front).
 """
 import random
 
@@ -65,6 +68,82 @@ def test_lockstep_phase_matches_sequential(E, eps):
     R1 = [test_phase.run_phase(agent, tasks1, True) for _ in range(phases)]
     assert random.getstate() == st0
     assert R1 == R0
+    for wa, wb in zip(agent.test_tasks_weights, w0):
+        assert torch.equal(wa.weight.detach().cpu(), wb)
+    assert agent.logger.lines == ref.logger.lines
+    sf1._close()
+
+
+@pytest.mark.parametrize("E,d", [(8, 8), (33, 12)])
+def test_sf_test_reward_rows_vs_oracle(E, d):
+    """sfx_test_reward_updates: E test tasks' SGD steps (agents/sfdqn.py:168-184) in one launch vs the
+    oracle's per-task autograd + torch.optim.SGD, 4 steps: losses and w within 1e-4 relative."""
+    _need_gpu()
+    from oracle import ref_cpu as R
+    from sfx.engine import SFEngine
+
+    eng = SFEngine(2, 6, 32, 3, d, ("relu", "relu"), max_batch=16)
+    try:
+        gen = torch.Generator().manual_seed(E + d)
+        w_ref = [torch.empty(1, d).uniform_(-0.01, 0.01, generator=gen) for _ in range(E)]
+        W = torch.cat(w_ref).to(eng.device)
+        for j in range(4):
+            PHI = 2 * torch.rand(E, d, generator=gen) - 0.5
+            r = torch.randn(E, generator=gen)
+            lo = eng.test_reward_updates(PHI.to(eng.device), r.to(eng.device), W).cpu()
+            want = [R.sf_test_reward_update(w_ref[e], PHI[e], float(r[e])) for e in range(E)]
+            rel_close(lo, want, rtol=1e-4, atol=1e-7)
+            rel_close(W.cpu(), torch.cat(w_ref), rtol=1e-4, atol=1e-7)
+    finally:
+        eng.close()
+
+
+def test_lockstep_device_mapper_phase_vs_sequential():
+    """The lockstep test phase with agents/sfdqn.py's reward mapper on the device (one
+    sfx_test_reward_updates launch per step, losses read once per phase) vs the reference's sequential
+    loop with its torch SGD per task and step: the same returns and random state; reward models
+    and logged loss sums within 1e-5."""
+    _need_gpu()
+    from tools import test_phase
+
+    E, ep_len, phases = 8, 25, 2
+    sf0, ref, tasks0 = test_phase.make(E=E, ep_len=ep_len, test_epsilon=0.1, H=64)
+    R0 = [test_phase.run_phase(ref, tasks0, False) for _ in range(phases)]
+    st0 = random.getstate()
+    w0 = [w.weight.detach().cpu() for w in ref.test_tasks_weights]
+    sf0._close()
+    sf1, agent, tasks1 = test_phase.make(E=E, ep_len=ep_len, test_epsilon=0.1, H=64, device_mapper=True)
+    R1 = [test_phase.run_phase(agent, tasks1, True) for _ in range(phases)]
+    assert random.getstate() == st0
+    assert R1 == R0
+    for wa, wb in zip(agent.test_tasks_weights, w0):
+        torch.testing.assert_close(wa.weight.detach().cpu(), wb, rtol=1e-5, atol=1e-8)
+    assert len(agent.logger.lines) == len(ref.logger.lines)
+    for xa, xb in zip(agent.logger.lines, ref.logger.lines):
+        assert xa["reward"] == xb["reward"] and xa["steps"] == xb["steps"] and xa["task"] == xb["task"]
+        assert abs(xa["w_error"] - xb["w_error"]) <= 1e-5 * abs(xb["w_error"]) + 1e-7
+    sf1._close()
+
+
+def test_lockstep_episodes_that_end_run_sequentially():
+    """Test tasks whose episodes end early: sfx.lockstep decides before the first step and runs the
+    sequential loop -- returns, reward models (bit for bit), log lines and random state as the
+    reference's."""
+    _need_gpu()
+    from tests.test_lockstep import _ending
+    from tools import test_phase
+
+    at = [None, 7, None, 3]
+    sf0, ref, tasks0 = test_phase.make(E=4, ep_len=15, test_epsilon=0.2, H=64)
+    _ending(tasks0, at)
+    R0 = [test_phase.run_phase(ref, tasks0, False) for _ in range(2)]
+    st0 = random.getstate()
+    w0 = [w.weight.detach().cpu() for w in ref.test_tasks_weights]
+    sf0._close()
+    sf1, agent, tasks1 = test_phase.make(E=4, ep_len=15, test_epsilon=0.2, H=64, device_mapper=True)
+    _ending(tasks1, at)
+    R1 = [test_phase.run_phase(agent, tasks1, True) for _ in range(2)]
+    assert R1 == R0 and random.getstate() == st0
     for wa, wb in zip(agent.test_tasks_weights, w0):
         assert torch.equal(wa.weight.detach().cpu(), wb)
     assert agent.logger.lines == ref.logger.lines

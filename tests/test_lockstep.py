@@ -41,6 +41,17 @@ class _Engine:
             out.append([int(c), int(torch.argmax(q[:, c, :]))])
         return torch.tensor(out)
 
+    def test_reward_updates(self, phi, r, W, lr=0.005, wd=0.01, losses=None):
+        """sfx_test_reward_updates over the oracle (agents/sfdqn.py:168-184 by autograd + SGD), row
+        by row: bit-identical to the user's own mapper on the CPU."""
+        from oracle import ref_cpu as R
+        self.mapper_calls = getattr(self, "mapper_calls", 0) + 1
+        out = torch.tensor([R.sf_test_reward_update(W[e], phi[e], float(r[e])) for e in range(W.shape[0])])
+        if losses is not None:
+            losses.copy_(out)
+            return losses
+        return out
+
 
 class _SF:
     def __init__(self, psi):
@@ -90,7 +101,7 @@ def test_enable_binds_into_the_reference_train_loop():
 
     E, ep_len = 4, 10
 
-    def train(agent, test_tasks, phases):  # the shape of agents/sfdqn.py:78-123's test phase
+    def train(agent, test_tasks, phases):  # noqa: F811  # the shape of agents/sfdqn.py:78-123's test phase
         out = []
         for _ in range(phases):
             out.append([agent.test_agent(t, i) for i, t in enumerate(test_tasks)])
@@ -106,14 +117,107 @@ def test_enable_binds_into_the_reference_train_loop():
     assert agent.logger.lines == ref.logger.lines
 
 
-def test_lockstep_refuses_episodes_that_end_early():
+def _ending(tasks, at):
+    """Make task e's episodes end after at[e] steps (None: never), as gym's Hopper / CartPole do."""
+    for t, n in zip(tasks, at):
+        real, t._n = t.transition, 0
+
+        def tr(a, t=t, real=real, n=n):
+            s1, r, _ = real(a)
+            t._n += 1
+            return s1, r, n is not None and t._n % n == 0
+        t.transition = tr
+        t.episodes_never_end = n is None
+
+
+@pytest.mark.parametrize("device_mapper", [False, True])
+def test_lockstep_decides_up_front_for_episodes_that_end(device_mapper):
+    """Test tasks whose episodes end early: the lockstep entry point sees that before the first step
+    and runs the reference's sequential loop -- the same returns, reward models, log lines and
+    random state, and no lockstep launch."""
     from sfx.lockstep import test_tasks_lockstep
 
-    sf, agent, tasks = _setup(2, 8, 0.0)
-    real = tasks[0].transition
-    tasks[0].transition = lambda a: real(a)[:2] + (True,)
-    with pytest.raises(RuntimeError, match="full-length episodes"):
-        test_tasks_lockstep(agent, tasks)
+    ep_len, at = 12, [None, 5, None]
+    sf0, ref, tasks0 = _setup(3, ep_len, 0.2)
+    _ending(tasks0, at)
+    R0 = [[ref.test_agent(t, i) for i, t in enumerate(tasks0)] for _ in range(2)]
+    st0 = random.getstate()
+    sf1, agent, tasks1 = _setup(3, ep_len, 0.2)
+    _ending(tasks1, at)
+    if device_mapper:
+        type(agent).update_test_reward_mapper.__sfx_mapper__ = "sgd"
+    try:
+        R1 = [test_tasks_lockstep(agent, tasks1) for _ in range(2)]
+    finally:
+        type(agent).update_test_reward_mapper.__dict__.pop("__sfx_mapper__", None)
+    assert R1 == R0 and random.getstate() == st0
+    assert agent.logger.lines == ref.logger.lines
+    for wa, wb in zip(agent.test_tasks_weights, ref.test_tasks_weights):
+        assert torch.equal(wa.weight, wb.weight)
+    assert sf1.eng.calls == 0 and sf1.flushed == 0  # never started a lockstep step
+
+
+def test_lockstep_declared_endless_task_that_ends_warns_and_finishes():
+    """A task declared endless that ends anyway: no exception mid-phase; it stops (the reference's
+    break), the phase finishes, and the tasks before it match the sequential loop exactly."""
+    from sfx.lockstep import test_tasks_lockstep
+
+    sf0, ref, tasks0 = _setup(3, 10, 0.0)
+    _ending(tasks0, [None, None, 4])
+    want = [ref.test_agent(t, i) for i, t in enumerate(tasks0)]
+    sf1, agent, tasks1 = _setup(3, 10, 0.0)
+    _ending(tasks1, [None, None, 4])
+    with pytest.warns(RuntimeWarning, match="declared never to end"):
+        got = test_tasks_lockstep(agent, tasks1, episodes_end=False)
+    assert got == want  # ε = 0: no draws depend on where task 2 ended
+    assert tasks1[2]._n == 4
+
+
+@pytest.mark.parametrize("E,eps", [(1, 0.03), (5, 0.3), (4, 1.0)])
+def test_lockstep_device_reward_mapper_matches_sequential(E, eps):
+    """agents/sfdqn.py's own reward mapper (SGD on w_approx) is recognised and run as one engine
+    call per step over all E rows (sfx_test_reward_updates, here over the oracle): returns, reward
+    models, log lines (the losses' python sums, read once per phase) and random state as the
+    sequential loop with the user's torch SGD."""
+    from sfx import lockstep
+
+    ep_len, phases = 9, 2
+    sf0, ref, tasks0 = _setup(E, ep_len, eps)
+    R0 = [[ref.test_agent(t, i) for i, t in enumerate(tasks0)] for _ in range(phases)]
+    st0 = random.getstate()
+    sf1, agent, tasks1 = _setup(E, ep_len, eps)
+    assert not lockstep.device_reward_mapper(agent)
+    type(agent).update_test_reward_mapper.__sfx_mapper__ = "sgd"
+    try:
+        assert lockstep.device_reward_mapper(agent)
+        R1 = [lockstep.test_tasks_lockstep(agent, tasks1) for _ in range(phases)]
+    finally:
+        del type(agent).update_test_reward_mapper.__sfx_mapper__
+    assert random.getstate() == st0 and R1 == R0
+    assert agent.logger.lines == ref.logger.lines
+    for wa, wb in zip(agent.test_tasks_weights, ref.test_tasks_weights):
+        assert torch.equal(wa.weight, wb.weight)
+    assert sf1.eng.mapper_calls == phases * ep_len
+
+
+def test_device_reward_mapper_recognises_only_the_reference_method():
+    from sfx.lockstep import device_reward_mapper
+
+    class SFDQN:
+        def update_test_reward_mapper(self, w_approx, task, r, s, a, s1):
+            pass
+    SFDQN.__module__ = "agents.sfdqn"
+    SFDQN.update_test_reward_mapper.__module__ = "agents.sfdqn"
+    SFDQN.update_test_reward_mapper.__qualname__ = "SFDQN.update_test_reward_mapper"
+    assert device_reward_mapper(SFDQN())
+
+    class Mine(SFDQN):
+        def update_test_reward_mapper(self, w_approx, task, r, s, a, s1):
+            pass
+    assert not device_reward_mapper(Mine())
+    x = SFDQN()
+    x.update_test_reward_mapper = lambda *a: None
+    assert not device_reward_mapper(x)
 
 
 class _SingleFileAgent(EvalAgent):
@@ -214,8 +318,9 @@ class _TsfOracleEngine:
         self.batched += 1
         return torch.stack([self.tsf_test_action(S[e], W[e], Om[e]) for e in range(S.shape[0])])
 
-    def tsf_test_updates(self, S, S1, A, A1, PHI, W, Om, M, rowp, gamma, beta, lasso, losses):
+    def tsf_test_updates(self, S, S1, A, A1, PHI, W, Om, M, rowp, gamma, beta, lasso, losses=None):
         self.batched += 1
+        losses = torch.empty(S.shape[0], 3) if losses is None else losses
         for e in range(S.shape[0]):
             r, lw, ww, lo, wo, step = rowp[e].tolist()
             losses[e] = self.tsf_test_update(S[e], S1[e], A[e], A1[e], r, PHI[e], W[e], Om[e], M[e], int(step), gamma,
@@ -285,3 +390,49 @@ def test_tsf_enable_binds_lockstep_into_train_loop():
     agent.train = lambda *a, **k: [agent.test_agent(t, i) for i, t in enumerate(k["test_tasks"])]
     lockstep.enable(agent)
     assert agent.train([], 0, test_tasks=tasks1) == R0
+
+
+def test_tsf_lockstep_decides_up_front_for_episodes_that_end(capsys):
+    """TSF test tasks whose episodes end early (Hopper / CartPole return gym's done): the lockstep
+    entry point runs the sequential loop instead -- returns, w, ω, Adam state, LR schedules, log
+    lines and random state as the reference's, and no lockstep launch."""
+    from sfx.lockstep import test_tasks_lockstep_tsf
+
+    at = [None, 3, None]
+    ref, tasks0 = _tsf_setup(3, 6, 0.3, 5000)
+    _ending(tasks0, at)
+    R0 = [[ref.test_agent(t, i) for i, t in enumerate(tasks0)] for _ in range(2)]
+    st0, out0 = random.getstate(), _printed(capsys)
+    agent, tasks1 = _tsf_setup(3, 6, 0.3, 5000)
+    _ending(tasks1, at)
+    R1 = [test_tasks_lockstep_tsf(agent, tasks1) for _ in range(2)]
+    assert R1 == R0 and random.getstate() == st0 and _printed(capsys) == out0
+    assert agent.logger.lines == ref.logger.lines
+    for (wa, oa, _), (wb, ob, _) in zip(agent.test_tasks_weights, ref.test_tasks_weights):
+        assert torch.equal(wa.weight.detach(), wb.weight.detach())
+        assert oa.param_groups[1]["lr"] == ob.param_groups[1]["lr"]
+    for oa, ob in zip(agent.omegas, ref.omegas):
+        assert torch.equal(oa.detach(), ob.detach())
+    assert agent.sf._eng.batched == 0
+
+
+def test_tsf_lockstep_declared_endless_task_that_ends_stops_there():
+    """A TSF test task declared endless that ends anyway stops at its done (the reference's break:
+    no further env step, Adam step or scheduler step for it) with a warning; with ε = 0 and no
+    diagnostic draws every task still matches the sequential loop."""
+    from sfx.lockstep import test_tasks_lockstep_tsf
+
+    at = [2, None, None]
+    ref, tasks0 = _tsf_setup(3, 5, 0.0, 7)
+    _ending(tasks0, at)
+    R0 = [ref.test_agent(t, i) for i, t in enumerate(tasks0)]
+    agent, tasks1 = _tsf_setup(3, 5, 0.0, 7)
+    _ending(tasks1, at)
+    with pytest.warns(RuntimeWarning, match="declared never to end"):
+        R1 = test_tasks_lockstep_tsf(agent, tasks1, episodes_end=False)
+    assert R1 == R0 and tasks1[0]._n == 2
+    for (wa, oa, _), (wb, ob, _) in zip(agent.test_tasks_weights, ref.test_tasks_weights):
+        assert torch.equal(wa.weight.detach(), wb.weight.detach())
+        assert oa.param_groups[1]["lr"] == ob.param_groups[1]["lr"]
+    for oa, ob in zip(agent.omegas, ref.omegas):
+        assert torch.equal(oa.detach(), ob.detach())

@@ -21,7 +21,8 @@ import torch
 class ActionEnv:
     """A Reacher-shaped test task whose next state depends on the action (so a wrong action
     shows in the returns) with its own random stream (tasks own their envs, as tasks/reacher.py's
-    bullet envs do)."""
+    bullet envs do).  Like tasks/reacher.py (:112), its episodes never end."""
+    episodes_never_end = True
 
     def __init__(self, n_s, A, d, seed, device):
         g = np.random.default_rng(1000 + seed)
@@ -122,9 +123,20 @@ class EvalAgent:
                 "w_error": loss}
 
 
+class RefEvalAgent(EvalAgent):
+    """EvalAgent whose reward mapper (the reference's, restated above) counts as agents/sfdqn.py's
+    own: sfx.lockstep then runs it on the device, as it does for the reference's SFDQN."""
+
+    def update_test_reward_mapper(self, w_approx, task, r, s, a, s1):
+        return EvalAgent.update_test_reward_mapper(self, w_approx, task, r, s, a, s1)
+
+    update_test_reward_mapper.__sfx_mapper__ = "sgd"
+
+
 def make(E=8, T_heads=8, n_s=6, H=256, A=9, d=8, acts=("relu", "relu"), ep_len=50, test_epsilon=0.03, seed=3,
-         device=None):
-    """A drop-in DeepSF with T_heads random heads and an agent over E test tasks."""
+         device=None, device_mapper=False):
+    """A drop-in DeepSF with T_heads random heads and an agent over E test tasks (``device_mapper``:
+    a RefEvalAgent, whose reward mapper the lockstep runs on the device)."""
     from sfx.dropin.features.deep import DeepSF
     from tools.dropin_loop import psi_model_lambda
 
@@ -138,7 +150,7 @@ def make(E=8, T_heads=8, n_s=6, H=256, A=9, d=8, acts=("relu", "relu"), ep_len=5
     for t in range(T_heads):
         sf.add_training_task(ActionEnv(n_s, A, d, 100 + t, device))
     tasks = [ActionEnv(n_s, A, d, 200 + e, device) for e in range(E)]
-    agent = EvalAgent(sf, A, ep_len, tasks, test_epsilon, device)
+    agent = (RefEvalAgent if device_mapper else EvalAgent)(sf, A, ep_len, tasks, test_epsilon, device)
     return sf, agent, tasks
 
 
@@ -151,7 +163,7 @@ def run_phase(agent, tasks, lockstep: bool):
 
 
 def measure(lockstep: bool, E=8, ep_len=50, phases=4, **kw) -> dict:
-    sf, agent, tasks = make(E=E, ep_len=ep_len, **kw)
+    sf, agent, tasks = make(E=E, ep_len=ep_len, device_mapper=lockstep, **kw)
     run_phase(agent, tasks, lockstep)  # warm-up phase (graphs captured)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -163,7 +175,8 @@ def measure(lockstep: bool, E=8, ep_len=50, phases=4, **kw) -> dict:
     n = phases * E * ep_len
     return {"value": round(n / dt, 2), "unit": "test env steps/s", "ms_per_step": round(1000.0 * dt / n, 4),
             "steps": n, "dtype": "fp32",
-            "path": ("sfx.lockstep: E test tasks per sfx_test_actions launch set" if lockstep else
+            "path": ("sfx.lockstep: E test tasks per sfx_test_actions launch set, their reward models' SGD steps in "
+                     "one sfx_test_reward_updates launch" if lockstep else
                      "the reference's sequential test_agent loop over the drop-in get_successors") +
                     f" (E={E} test tasks, {ep_len}-step episodes, T=8 heads, H=256)"}
 
