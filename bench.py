@@ -44,7 +44,7 @@ TSF_SHAPE = dict(n_s=11, H=256, A=27, d=50, acts=("relu", "relu"), G=100)
 C1_SHAPE = dict(n_s=4, H=256, A=2, d=20, acts=("relu", "relu"))  # BASELINE C1 (CartPole-v2)
 WORKLOADS = {"reacher-sf": None, "hopper-tsf": 0, "hopper-tsf-nf": 100}
 KIND_NAMES = {"fwd": "k_fwd", "tdg": "k_tdg", "bwd": "k_bwd", "gpi": "k_gpi", "lms": "k_lms", "ver": "k_ver",
-              "round": "k_round", "tsf": "k_tsf"}
+              "round": "k_round", "tsf": "k_tsf", "pstep": "k_pstep"}
 
 
 def parse():

@@ -31,6 +31,7 @@
 #include "sfx_kernels.h"
 #include "sfx_tsf.h"
 #include "sfx_phi.h"
+#include "sfx_pstep.h"
 #include "../../include/sfx.h"
 
 using namespace sfx;
@@ -136,6 +137,10 @@ struct sfx_handle {
   int Tg = 0, off = 0;
   struct sfx_tsf_state* tsf = nullptr;  // TSF-DQN state (sfx_tsf_setup)
   struct sfx_phi_state* phi = nullptr;  // learned φ (sfx_phi_setup)
+  // persistent all-task step (k_pstep, sfx_pstep.h / sfx_pstep.inc): SFX_PSTEP=1 or sfx_set_pstep
+  int pstep_mode = 0;       // 1: launch_step_all runs k_pstep whenever pstep_use() holds
+  int pstep_census = -1;    // placement check: -1 not run, 0 failed, 1 32 workgroups on each of 8 XCDs
+  struct sfx_pstep_state* ps = nullptr;
   // collective of the sharded step (sfx_comm_init / sfx_set_comm / sfx_set_comm_host): all-reduce
   // (MAX) of fp32 buffers over the ranks that share the source tasks
   int comm_rank = 0, comm_world = 0;  // world 0: no communicator
@@ -218,7 +223,8 @@ void clear_graphs(sfx_handle* h) {
   h->graphs.clear();
 }
 
-enum { K_FWD = 0, K_TDG = 1, K_BWD = 2, K_GPI = 3, K_LMS = 4, K_VER = 5, K_ROUND = 6, K_TSF = 7, K_NKIND = 8 };
+enum { K_FWD = 0, K_TDG = 1, K_BWD = 2, K_GPI = 3, K_LMS = 4, K_VER = 5, K_ROUND = 6, K_TSF = 7, K_PSTEP = 8,
+       K_NKIND = 9 };
 
 hipEvent_t prof_event(sfx_handle* h) {
   if (!h->prof_pool.empty()) {
@@ -896,8 +902,13 @@ int tsf_body(sfx_handle* h, int policy, const float* S, const int64_t* a, const 
              const float* S1, const float* gamma, int B, int use_gpi, float* losses, int64_t* next,
              const int* xmax = nullptr);
 
+bool pstep_use(const sfx_handle* h, const sfx_handle::Pending& p);
+int run_pstep(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, const float* lms_phi, const float* lms_r,
+              float lms_alpha);
+
 int launch_step_all(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, const float* lms_phi, const float* lms_r,
                     float lms_alpha, int rounds) {
+  if (p.update && pstep_use(h, p)) return run_pstep(h, p, lms_task, lms_phi, lms_r, lms_alpha);
   const int T = h->T, B = p.B;
   FwdExtra ex;
   ex.lms_head = lms_task;
@@ -1108,17 +1119,21 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   G.cancel = h->dcancel;
   G.lastOff = h->actOff[h->NL - 1];
   *out = h;
+  const char* eps = std::getenv("SFX_PSTEP");  // the persistent step where it fits and the census passes
+  if (eps && eps[0] == '1') (void)sfx_set_pstep(h, 1);
   return SFX_OK;
 }
 
 void tsf_release(sfx_handle* h);
 void phi_release(sfx_handle* h);
+void pstep_release(sfx_handle* h);
 
 int sfx_destroy(sfx_t h) {
   if (!h) return SFX_OK;
   (void)hipStreamSynchronize(h->stream);
   tsf_release(h);
   phi_release(h);
+  pstep_release(h);
   free_all(h);
   delete h;
   return SFX_OK;
@@ -1415,12 +1430,16 @@ int sfx_step_stats(sfx_t h, long long* steps, long long* fallbacks, long long* r
 
 int sfx_skip_stats(sfx_t h, long long* checked, long long* skipped, int reset) {
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
-  unsigned long long c[2] = {0, 0};
+  unsigned long long c[2] = {0, 0}, ps[4] = {0, 0, 0, 0};
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipMemcpy(c, h->skipc, sizeof(c), hipMemcpyDeviceToHost));
-  if (checked) *checked = (long long)c[0];
-  if (skipped) *skipped = (long long)c[1];
-  if (reset) HIPCHK(hipMemset(h->skipc, 0, sizeof(c)));
+  if (h->ps) HIPCHK(hipMemcpy(ps, h->ps->stats, sizeof(ps), hipMemcpyDeviceToHost));  // k_pstep's own counts
+  if (checked) *checked = (long long)(c[0] + ps[2]);
+  if (skipped) *skipped = (long long)(c[1] + ps[3]);
+  if (reset) {
+    HIPCHK(hipMemset(h->skipc, 0, sizeof(c)));
+    if (h->ps) HIPCHK(hipMemset(h->ps->stats + 2, 0, 2 * sizeof(unsigned long long)));
+  }
   return SFX_OK;
 }
 
@@ -1519,3 +1538,4 @@ int sfx_synchronize(sfx_t h) {
 #include "sfx_runner.inc"
 #include "sfx_tsf.inc"
 #include "sfx_phi.inc"
+#include "sfx_pstep.inc"
