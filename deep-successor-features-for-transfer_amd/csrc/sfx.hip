@@ -1117,6 +1117,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   G.dz = h->dz;
   G.rowloss = h->rowloss;
   G.cancel = h->dcancel;
+  G.nonfin = h->dcancel + 8;  // sticky non-finite TD flag (sfx_nonfinite)
   G.lastOff = h->actOff[h->NL - 1];
   *out = h;
   const char* eps = std::getenv("SFX_PSTEP");  // the persistent step where it fits and the census passes
@@ -1440,6 +1441,16 @@ int sfx_skip_stats(sfx_t h, long long* checked, long long* skipped, int reset) {
     HIPCHK(hipMemset(h->skipc, 0, sizeof(c)));
     if (h->ps) HIPCHK(hipMemset(h->ps->stats + 2, 0, 2 * sizeof(unsigned long long)));
   }
+  return SFX_OK;
+}
+
+int sfx_nonfinite(sfx_t h, int* flag_host, int reset) {
+  if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
+  int v = 0;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(&v, h->G.nonfin, sizeof(int), hipMemcpyDeviceToHost));
+  if (flag_host) *flag_host = v;
+  if (reset) HIPCHK(hipMemset(h->G.nonfin, 0, sizeof(int)));
   return SFX_OK;
 }
 

@@ -194,6 +194,7 @@ struct Geo {
   float* dz;          // [T][actSize]
   float* rowloss;     // [T][MMAX] per-row Σ (c - t)^2 of the last TD target
   const int* cancel;  // runner steps: 1 when the step's gate cancelled it (see step_cancelled)
+  int* nonfin;        // SURVEY §5 failure detection: set (sticky) when a TD error comes out non-finite
   int lastOff;        // offset of the last layer's output inside an activation block
   // bf16 operand mode: bf16 copies of the online [2][T][P] and target [T][P] parameters (the
   // fp32 ones stay the master copy; the Adam epilogue rewrites the copy of every weight it
@@ -984,6 +985,7 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   if (tid < d && aok) {
     const float diff = __fsub_rn(cval, __fadd_rn(phik, __fmul_rn(gam, s_t[an * d + tid])));
     dsq = __fmul_rn(diff, diff);
+    if (!__builtin_isfinite(diff) && G.nonfin) atomicOr(G.nonfin, 1);
   }
   if (tid < d) s_sq[tid] = dsq;
   __syncthreads();
@@ -1208,6 +1210,7 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
                                 : (float)(2.0 / ((double)M * (double)O));
   const FDiv fd = fdiv(d);
   float* sq = sm.q;
+  int nf = 0;
   for (int i = tid; i < nb * d; i += 256) {
     const int bl = i / fd, k = i - bl * d, ab = sm.a[bl];
     float e2 = 0.f;
@@ -1216,10 +1219,11 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
       const float diff = __fsub_rn(sm.tc[bl * O + ab * d + k], tg);
       sm.dz[bl * O + ab * d + k] = __fmul_rn(norm, diff);
       e2 = __fmul_rn(diff, diff);
+      nf |= !__builtin_isfinite(diff);
     }
     sq[i] = e2;
   }
-  __syncthreads();
+  if (__syncthreads_or(nf) && tid == 0 && G.nonfin) atomicOr(G.nonfin, 1);
   if (pub) {
     float4* gout4 = reinterpret_cast<float4*>(G.dzp(pol, NLm) + (size_t)m0 * O);
     for (int i = tid; i < n4; i += 256) {
@@ -2112,7 +2116,8 @@ __global__ __launch_bounds__(256) void k_gpi(Geo G, GpiArgs A) {
 struct HostResult {  // host-coherent; seq written last
   long long sel0, sel1;
   int flag, err;       // err (slot 0 only): a gate timed out (set by the gate itself, system scope)
-  int cancelled, pad_; // the published step was cancelled at its gate: nothing of it committed
+  int cancelled;       // the published step was cancelled at its gate: nothing of it committed
+  int nonfinite;       // the handle's non-finite TD flag (Geo::nonfin) when the step published
   long long seq;
 };
 // Results live in a ring of RES_RING slots, step seq in slot seq % RES_RING: steps queued behind
@@ -2123,7 +2128,7 @@ constexpr int RES_RING = 64;
 // Post the step's result (selected action, speculation verdict) to host-coherent memory;
 // seq is written last (system release).  The inputs are read with coherent (sc1) loads.
 __device__ __forceinline__ void publish_result(const int64_t* sel, const int* flag, HostResult* ring,
-                                               const long long* dctr, const int* cancel) {
+                                               const long long* dctr, const int* cancel, const int* nonfin) {
   const long long s0 = __hip_atomic_load(sel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const long long s1 = __hip_atomic_load(sel + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2134,6 +2139,7 @@ __device__ __forceinline__ void publish_result(const int64_t* sel, const int* fl
   out->sel1 = s1;
   out->flag = f;
   out->cancelled = cx;
+  out->nonfinite = nonfin ? __hip_atomic_load(nonfin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   __threadfence_system();
   __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -2249,7 +2255,7 @@ __global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
       const unsigned prev = __hip_atomic_fetch_add(V.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("" ::: "memory");
       if (prev == (unsigned)V.nblocks - 1) {
-        publish_result(V.g.sel_out, V.flag, V.pub, V.pub_dctr, G.cancel);
+        publish_result(V.g.sel_out, V.flag, V.pub, V.pub_dctr, G.cancel, G.nonfin);
         __hip_atomic_store(V.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -2505,9 +2511,9 @@ __global__ __launch_bounds__(256) void k_gate_replay(ReplayGateArgs A) {
 }
 
 __global__ void k_publish(const int64_t* sel, const int* flag, HostResult* out, const long long* dctr,
-                          const int* cancel) {
+                          const int* cancel, const int* nonfin) {
   PROBE_T(pt0);
-  if (threadIdx.x == 0) publish_result(sel, flag, out, dctr, cancel);
+  if (threadIdx.x == 0) publish_result(sel, flag, out, dctr, cancel, nonfin);
   PROBE_REC(18, pt0);
 }
 
@@ -2722,6 +2728,7 @@ struct SfinArgs {
   HostResult* pub;        // runner steps: publish (flag, sel) to the host (k_publish folded in)
   const long long* dctr;
   const int* cancel;
+  const int* nonfin;      // Geo::nonfin
 };
 
 // One workgroup: verification of the speculated next actions (k_sverify), the env action, and
@@ -2766,6 +2773,7 @@ __global__ __launch_bounds__(256) void k_sfinish(SfinArgs F) {
       pub->sel1 = a;
       pub->flag = s_min;
       pub->cancelled = *F.cancel;
+      pub->nonfinite = F.nonfin ? __hip_atomic_load(F.nonfin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
       __threadfence_system();
       __hip_atomic_store(&pub->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }

@@ -65,7 +65,8 @@ struct PsArgs {
   AdamHP hp;
   PsLayer L[PS_NLMAX];
   // LDS carve (floats), computed by the host (ps_smem)
-  int o_sx, o_phi, o_gam, o_ab, o_w, o_own, o_dz, o_dzn, o_g3, o_ap, o_ac, o_cr, o_qs, o_wc3, o_psi, o_st;
+  int o_sx, o_phi, o_gam, o_ab, o_w, o_own, o_dz, o_dzn, o_g3, o_g3m, o_ap, o_ac, o_cr, o_qs, o_wc3, o_psi, o_pst, o_nb,
+      o_st;
   const float *S, *S1, *phi, *gamma, *s_next, *lms_phi, *lms_r;
   const int64_t* a;
   // workspace: intra-head hand-off buffers (rewritten every launch)
@@ -188,12 +189,20 @@ __device__ __forceinline__ float ps_dot(const float* x, const float* w, int K) {
 // order-preserving u32 of a float (the high word of the selection key)
 __device__ __forceinline__ unsigned ps_ukey(float q) { return (unsigned)sortable(q) ^ 0x80000000u; }
 
+// Per-thread state that every speculative round of a step re-reads is made resident ONCE per step:
+// the Adam state (p, m, v of the read slot) of this rank's rows of every layer and the columns
+// X_l[b][tid] of the step-start activations that the dW sums need live in registers; the weight
+// column slices of the dX products, ψ⁻(s1) and c in LDS; the post-update weights a round produces
+// stay in LDS for that round's forward.  A round then pays only its hand-offs.
+// NH hidden Linear layers (NL = NH + 2), DC = ceil(d / 8) chunks of 8 output rows per rank.
+template <int NH, int DC>
 __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
+  constexpr int NL = NH + 2;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ int s_rank, s_ok, s_flag;
   __shared__ AdamC s_ac;
   const int tid = threadIdx.x;
-  const int T = P.T, B = P.B, A = P.A, d = P.d, O = P.O, NL = P.NL, n_s = P.n_s, K0S = P.K0S;
+  const int T = P.T, B = P.B, A = P.A, d = P.d, O = P.O, n_s = P.n_s, K0S = P.K0S;
   const unsigned ep = __hip_atomic_load(P.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int par = (int)(ep & 1u);
   unsigned* cnt = P.cnt + par * PS_CSET;
@@ -212,38 +221,111 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
     if (gt < PS_RMAX) P.sel[q * PS_RMAX + gt] = 0ull;
   }
   const unsigned xcc = ps_xcc();
-  if (tid == 0) s_rank = xcc < 8 ? (int)__hip_atomic_fetch_add(cnt + 32 * xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : PS_R;
+  if (tid == 0)
+    s_rank = xcc < 8 ? (int)__hip_atomic_fetch_add(cnt + 32 * xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : PS_R;
   __syncthreads();
-  const int head = (int)xcc, rank = s_rank;
+  const int head = (int)xcc, rank = s_rank, hd = head & 7;
   const bool active = head < T && rank < PS_R;
   const int cancelled = step_cancelled(G.cancel);
   const bool work = active && !cancelled;
-  unsigned* hctr = cnt + 32 * (8 + (head & 7));
+  unsigned* hctr = cnt + 32 * (8 + hd);
   unsigned* qctr = cnt + 32 * 16;
   unsigned* fin = cnt + 32 * 17;
   const bool outr = rank < A;  // this rank owns action `rank` of the output layer
   unsigned e = 0;              // intra-head edges completed so far
   int rounds = 0;              // the converged round (the result is round rounds - 1's)
   bool ok = true;
+  int r = 0;                   // current round (PS_MARK0)
+  // LDS carve (sfx_pstep.inc pstep_carve)
   float* sx = sm + P.o_sx;     // [97][K0S]: S | S1 | S1 | s_next
   float* sphi = sm + P.o_phi;  // [32][d]
   float* sgam = sm + P.o_gam;  // [32]
-  int* sab = reinterpret_cast<int*>(sm + P.o_ab);   // [32]
+  int* sab = reinterpret_cast<int*>(sm + P.o_ab);  // [32]
   float* sw = sm + P.o_w;      // [T][d] reward weights (the active task's after LMS)
   float* own = sm + P.o_own;   // [NL-1][32][8]: own columns of the step-start S-row activations
   float* sdz = sm + P.o_dz;    // [32][8]: own columns of the current output gradient
   float* sdzn = sm + P.o_dzn;  // [32][8]: ... of the next (lower) layer
   float* g3 = sm + P.o_g3;     // [32][d]: TD gradient at the taken action
-  int* ap = reinterpret_cast<int*>(sm + P.o_ap);    // [8][32] next actions of the previous round
-  int* ac = reinterpret_cast<int*>(sm + P.o_ac);    // [8][32] ... of this round
+  float* g3m = sm + P.o_g3m;   // [32][d]: the same, zero in rows whose action is not this rank's
+  int* ap = reinterpret_cast<int*>(sm + P.o_ap);  // [8][32] next actions of the previous round
+  int* ac = reinterpret_cast<int*>(sm + P.o_ac);  // [8][32] ... of this round
   float* scr = sm + P.o_cr;    // [32][d] ψ_i(s_b)[a_b]
   float* qs = sm + P.o_qs;     // [8][32] saved post-update q of this rank's action (skip re-publication)
   float* wc3 = sm + P.o_wc3;   // [O][8]: output-layer weights of this rank's hidden columns (read slot)
   float* psi = sm + P.o_psi;   // [33][d]: ψ of this rank's action
-  float* st = sm + P.o_st;     // staging (phase-local)
+  float* pst = sm + P.o_pst;   // [32][O]: ψ⁻(s1) of this head
+  float* nb = sm + P.o_nb;     // [NL-1][8] post-update biases of this rank's hidden units; [NL-1][..] output
+  float* st = sm + P.o_st;     // staging
+  // round-time staging layout: [33][XS] hand-off rows | WcT [NH][8][XS] | Wn [NH][8][XS] | Wno [8 DC][XS] | W0n
+  float* WcT = st + (PS_MB + 1) * PS_XS;
+  float* Wn = WcT + NH * PS_J * PS_XS;
+  float* Wno = Wn + NH * PS_J * PS_XS;
+  float* W0n = Wno + 8 * DC * PS_XS;
   unsigned long long qkey = 0ull;
   int step0 = 0;
+  const int rs = rslot(P.mask, hd), wsl = rs ^ 1;
+  const float* pon = G.online + G.slot_off(rs, hd);  // read slot (pre-step)
+  float* pnew = G.online + G.slot_off(wsl, hd);      // write slot
+  const float* mrd = G.am + G.slot_off(rs, hd);
+  const float* vrd = G.av + G.slot_off(rs, hd);
+  float* mwr = G.am + G.slot_off(wsl, hd);
+  float* vwr = G.av + G.slot_off(wsl, hd);
+  const float* ptg = G.target + (long long)hd * G.P;
+  const int j = tid & 7, g = tid >> 3;  // (hidden column, row group) of the 8-column phases
+  const int c0 = PS_J * (rank & 31);    // this rank's first hidden unit
+  const int arow = (rank & 31) * d;     // this rank's first output row
+  float* xsh = P.xs + (size_t)hd * (NL - 1) * 3 * PS_MB * PS_H;
+  float* dzh = P.dzb + (size_t)hd * (NL - 1) * PS_MB * PS_H;
+  float* xvh = P.xv + (size_t)hd * (NL - 1) * (PS_MB + 1) * PS_H;
+  float* psith = P.psit + (size_t)hd * PS_MB * O;
+  float* crh = P.cr + (size_t)hd * PS_MB * d;
+
+  // ---- register-resident Adam state of this rank's rows (read slot: written by no one in this launch)
+  float pw[NH][PS_J][3];      // hidden layer l = 1..NH, rows c0 + jj, column tid
+  float po[DC][8][3];         // output rows arow + 8c + u, column tid (output ranks)
+  float p0[3] = {0.f, 0.f, 0.f};  // layer 0: entry tid of rows c0.. (8 n_s <= 256 entries)
+  float pb[NL - 1][3];        // threads < 8: bias c0 + tid of layers 0 .. NH
+  float pbo[3] = {0.f, 0.f, 0.f};  // threads < d: output bias arow + tid
+  float xc[NH + 1][PS_MB];    // X_l[b][tid] of the step-start S rows, l = 0 .. NH (X_NH: output ranks)
   if (work) {
+#pragma unroll
+    for (int l = 0; l < NH; ++l)
+#pragma unroll
+      for (int jj = 0; jj < PS_J; ++jj) {
+        const size_t wi = P.L[l + 1].wOff + (size_t)(c0 + jj) * PS_H + tid;
+        pw[l][jj][0] = pon[wi];
+        pw[l][jj][1] = mrd[wi];
+        pw[l][jj][2] = vrd[wi];
+      }
+#pragma unroll
+    for (int c = 0; c < DC; ++c)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const bool okk = outr && 8 * c + u < d;
+        const size_t wi = P.L[NL - 1].wOff + (size_t)(arow + 8 * c + u) * PS_H + tid;
+        po[c][u][0] = okk ? pon[wi] : 0.f;
+        po[c][u][1] = okk ? mrd[wi] : 0.f;
+        po[c][u][2] = okk ? vrd[wi] : 0.f;
+      }
+    if (tid < PS_J * n_s) {
+      const size_t wi = P.L[0].wOff + (size_t)c0 * n_s + tid;
+      p0[0] = pon[wi];
+      p0[1] = mrd[wi];
+      p0[2] = vrd[wi];
+    }
+#pragma unroll
+    for (int l = 0; l < NL - 1; ++l) {
+      const size_t bi = P.L[l].bOff + c0 + (tid & 7);
+      pb[l][0] = tid < PS_J ? pon[bi] : 0.f;
+      pb[l][1] = tid < PS_J ? mrd[bi] : 0.f;
+      pb[l][2] = tid < PS_J ? vrd[bi] : 0.f;
+    }
+    if (outr && tid < d) {
+      const size_t bi = P.L[NL - 1].bOff + arow + tid;
+      pbo[0] = pon[bi];
+      pbo[1] = mrd[bi];
+      pbo[2] = vrd[bi];
+    }
     // ---------------- inputs: S | S1 | S1 | s_next (K padded to K0S), φ, γ, a, w (+ LMS)
     for (int i = tid; i < 97 * K0S; i += 256) {
       const int row = i / K0S, k = i - row * K0S;
@@ -264,7 +346,6 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
       const int t = i / d;
       sw[i] = G.w[(long long)t * G.dpad + (i - t * d)];
     }
-    for (int i = tid; i < (NL - 1) * 256; i += 256) own[i] = 0.f;
     step0 = G.step[head];
     __syncthreads();
     if (P.lms_task >= 0 && tid == 0) {  // features/successor.py:164-167, k_lms's order
@@ -276,21 +357,6 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
     }
     __syncthreads();
   }
-  const int rs = rslot(P.mask, head & 7), wsl = rs ^ 1;
-  const float* pon = G.online + G.slot_off(rs, head & 7);   // read slot (pre-step)
-  float* pnew = G.online + G.slot_off(wsl, head & 7);       // write slot
-  const float* mrd = G.am + G.slot_off(rs, head & 7);
-  const float* vrd = G.av + G.slot_off(rs, head & 7);
-  float* mwr = G.am + G.slot_off(wsl, head & 7);
-  float* vwr = G.av + G.slot_off(wsl, head & 7);
-  const float* ptg = G.target + (long long)(head & 7) * G.P;
-  const int j = tid & 7, g = tid >> 3;   // (hidden column, row group) of the 8-column phases
-  const int c0 = PS_J * rank;            // this rank's first hidden unit
-  float* xsh = P.xs + (size_t)(head & 7) * (NL - 1) * 3 * PS_MB * PS_H;
-  float* dzh = P.dzb + (size_t)(head & 7) * (NL - 1) * PS_MB * PS_H;
-  float* xvh = P.xv + (size_t)(head & 7) * (NL - 1) * (PS_MB + 1) * PS_H;
-  float* psith = P.psit + (size_t)(head & 7) * PS_MB * O;
-  float* crh = P.cr + (size_t)(head & 7) * PS_MB * d;
 
   // ---------------- step-start forward, layer 0 (K = n_s): rows S, S1 (online), S1 (target)
   PS_MARK(0);
@@ -300,15 +366,12 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
     {
       const int n0 = PS_J * n_s;  // the 8 rows are contiguous in the packed head
       for (int i = tid; i < 2 * n0 + 2 * PS_J; i += 256) {
-        float v;
         if (i < 2 * n0) {
           const int which = i >= n0, ii = i - which * n0, jj = ii / n_s, k = ii - jj * n_s;
-          v = (which ? ptg : pon)[L0.wOff + (size_t)c0 * n_s + ii];
-          W0s[(which * PS_J + jj) * K0S + k] = v;
+          W0s[(which * PS_J + jj) * K0S + k] = (which ? ptg : pon)[L0.wOff + (size_t)c0 * n_s + ii];
         } else {
           const int ii = i - 2 * n0;
-          v = (ii >= PS_J ? ptg : pon)[L0.bOff + c0 + (ii & 7)];
-          W0s[2 * PS_J * K0S + ii] = v;
+          W0s[2 * PS_J * K0S + ii] = (ii >= PS_J ? ptg : pon)[L0.bOff + c0 + (ii & 7)];
         }
       }
       __syncthreads();
@@ -335,20 +398,25 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
     if (tid == 64) s_ac = adam_consts(P.hp, step0 + 1);
     PS_MARK(1);
   }
-  // ---------------- step-start forward, hidden layers 1 .. NL-2
-  for (int l = 1; l <= NL - 2 && work && ok; ++l) {
+  // ---------------- step-start forward, hidden layers 1 .. NH
+#pragma unroll
+  for (int l = 1; l <= NH; ++l) {
+    if (work && ok) {
     const PsLayer Ll = P.L[l];
-    float* X = st;                       // [96][PS_XS]
-    float* Wst = st + 96 * PS_XS;        // [16][PS_XS]: online rows c0.., target rows c0..
+    float* X = st;                 // [96][PS_XS]
+    float* Wst = st + 96 * PS_XS;  // [16][PS_XS]: online rows c0.., target rows c0..
     for (int i = tid; i < 16 * 64; i += 256) {  // weight rows first: they do not depend on the hand-off
       const int row = i >> 6, c4 = (i & 63) << 2;
       const float* src = (row < 8 ? pon : ptg) + Ll.wOff + (size_t)(c0 + (row & 7)) * PS_H + c4;
       *reinterpret_cast<float4*>(Wst + row * PS_XS + c4) = *reinterpret_cast<const float4*>(src);
     }
     const float bo = pon[Ll.bOff + c0 + j], bt = ptg[Ll.bOff + c0 + j];
-    if (!(ok = ps_wait(P, hctr, PS_R * e, &s_ok))) break;
+    ok = ps_wait(P, hctr, PS_R * e, &s_ok);
+    if (ok) {
     ps_stage<12>(xsh + (size_t)(l - 1) * 3 * PS_MB * PS_H, 96, X);
     __syncthreads();
+#pragma unroll
+    for (int b = 0; b < PS_MB; ++b) xc[l - 1][b] = X[b * PS_XS + tid];  // X_{l-1}[b][tid], S rows
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
     {
       const float* x0 = X + g * PS_XS;
@@ -381,29 +449,35 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
     ps_arrive(hctr);
     ++e;
     PS_MARK(1 + l);
+    }
+    }
   }
   // ---------------- step-start output layer (rank a < A): c rows, ψ⁻(s1), pre-step maxima
   const PsLayer LO = P.L[NL - 1];
   if (work && ok && outr) {
-    float* X = st;                        // [96][PS_XS]
-    float* Wst = st + 96 * PS_XS;         // [d][PS_XS]: online rows of action `rank`, then target
-    const int arow = rank * d;
+    float* X = st;                 // [96][PS_XS]
+    float* Wst = st + 96 * PS_XS;  // [d][PS_XS]: online rows of action `rank`, then target
     for (int i = tid; i < d * 64; i += 256) {
       const int row = i >> 6, c4 = (i & 63) << 2;
       *reinterpret_cast<float4*>(Wst + row * PS_XS + c4) =
           *reinterpret_cast<const float4*>(pon + LO.wOff + (size_t)(arow + row) * PS_H + c4);
     }
-    float4 tw[8];  // target rows, held until the online rows are done (d <= 32: <= 8 per thread)
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = tid + u * 256;
-      tw[u] = i < d * 64 ? *reinterpret_cast<const float4*>(ptg + LO.wOff + (size_t)(arow + (i >> 6)) * PS_H + ((i & 63) << 2))
-                         : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    // target rows: beside the online rows when the staging holds both (96 + 2d <= 112 rows), else
+    // over them once the online rows are done
+    const bool tw_lds = 96 + 2 * d <= 112;
+    float* Wtg = tw_lds ? Wst + d * PS_XS : Wst;
+    if (tw_lds)
+      for (int i = tid; i < d * 64; i += 256) {
+        const int row = i >> 6, c4 = (i & 63) << 2;
+        *reinterpret_cast<float4*>(Wtg + row * PS_XS + c4) =
+            *reinterpret_cast<const float4*>(ptg + LO.wOff + (size_t)(arow + row) * PS_H + c4);
+      }
     ok = ps_wait(P, hctr, PS_R * e, &s_ok);
     if (ok) {
       ps_stage<12>(xsh + (size_t)(NL - 2) * 3 * PS_MB * PS_H, 96, X);
       __syncthreads();
+#pragma unroll
+      for (int b = 0; b < PS_MB; ++b) xc[NH][b] = X[b * PS_XS + tid];
       for (int i = tid; i < 64 * d; i += 256) {  // online: S rows -> c, S1 rows -> psi
         const int row = i / d, k = i - row * d;
         const float y = __fadd_rn(ps_dot(X + row * PS_XS, Wst + k * PS_XS, PS_H), pon[LO.bOff + arow + k]);
@@ -414,15 +488,17 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
         }
       }
       __syncthreads();
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = tid + u * 256;
-        if (i < d * 64) *reinterpret_cast<float4*>(Wst + (i >> 6) * PS_XS + ((i & 63) << 2)) = tw[u];
+      if (!tw_lds) {
+        for (int i = tid; i < d * 64; i += 256) {
+          const int row = i >> 6, c4 = (i & 63) << 2;
+          *reinterpret_cast<float4*>(Wtg + row * PS_XS + c4) =
+              *reinterpret_cast<const float4*>(ptg + LO.wOff + (size_t)(arow + row) * PS_H + c4);
+        }
+        __syncthreads();
       }
-      __syncthreads();
       for (int i = tid; i < B * d; i += 256) {  // target: ψ⁻(s1_b)[rank][k]
         const int b = i / d, k = i - b * d;
-        const float y = __fadd_rn(ps_dot(X + (64 + b) * PS_XS, Wst + k * PS_XS, PS_H), ptg[LO.bOff + arow + k]);
+        const float y = __fadd_rn(ps_dot(X + (64 + b) * PS_XS, Wtg + k * PS_XS, PS_H), ptg[LO.bOff + arow + k]);
         ps_st(psith + b * O + arow + k, y);
       }
       // pre-step maxima: policy i <= head takes this head through xge, i > head through xq[0]
@@ -437,9 +513,18 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
     }
   }
   PS_MARK(6);
-  // ---------------- speculative rounds
+  // ---------------- operands of every round that do not change from round to round (read slot):
+  // the dX weight slices W_l[:, c0 .. c0+7] (transposed) and W_out[:, c0 .. c0+7]
   if (work && ok) {
-    // persistent operands of every round: the output layer's weights of this rank's hidden columns
+    __syncthreads();  // the step-start staging is dead: WcT overlaps it
+#pragma unroll
+    for (int l = 1; l <= NH; ++l) {
+      const float4* src = reinterpret_cast<const float4*>(pon + P.L[l].wOff + (size_t)tid * PS_H + c0);
+      const float4 lo = src[0], hi = src[1];
+      float* w = WcT + (l - 1) * PS_J * PS_XS;
+      w[0 * PS_XS + tid] = lo.x; w[1 * PS_XS + tid] = lo.y; w[2 * PS_XS + tid] = lo.z; w[3 * PS_XS + tid] = lo.w;
+      w[4 * PS_XS + tid] = hi.x; w[5 * PS_XS + tid] = hi.y; w[6 * PS_XS + tid] = hi.z; w[7 * PS_XS + tid] = hi.w;
+    }
     for (int o = tid; o < O; o += 256) {
       const float4* src = reinterpret_cast<const float4*>(pon + LO.wOff + (size_t)o * PS_H + c0);
       *reinterpret_cast<float4*>(wc3 + o * 8) = src[0];
@@ -449,39 +534,49 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
   const unsigned qper = (unsigned)(T * A);
   __syncthreads();
   const AdamC adc = s_ac;
-  for (int r = 0; work && ok; ++r) {
+  for (r = 0; work && ok; ++r) {
     if (!(ok = ps_wait(P, qctr, qper * (unsigned)(r + 1), &s_ok))) break;
     PS_MARK(8 + 8 * (r < 6 ? r : 5));
     // next actions of every policy (each workgroup the same, from the same maxima): every load
-    // issued before the first compare
+    // issued before the first compare; round 0 also takes ψ⁻(s1) and c of this head into LDS
     int chg = 0, chg_own = 0;
+    if (r == 0) {
+      for (int i = tid; i < B * O; i += 256) pst[i] = ps_ld(psith + i);
+      for (int i = tid; i < B * d; i += 256) scr[i] = ps_ld(crh + i);
+    }
+    {  // the round's maxima of every policy, max(xq[r], xge), into LDS (the staging rows are free)
+      int* mx = reinterpret_cast<int*>(st);
+      const int n = T * PS_MB * A;
+      const int* xr = xq + (size_t)r * n;
+      for (int i0 = 0; i0 < n; i0 += 256 * 8) {
+        int xv[8], gv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + u * 256 + tid;
+          xv[u] = i < n ? ps_ldi(xr + i) : 0;
+          gv[u] = i < n ? ps_ldi(xge + i) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (i0 + u * 256 + tid < n) mx[i0 + u * 256 + tid] = max(xv[u], gv[u]);
+      }
+    }
+    __syncthreads();
     if (tid < T * B) {
       const int pi = tid / B, b = tid - pi * B;
-      const int* xr = xq + ((size_t)r * T * PS_MB + pi * PS_MB + b) * A;
-      const int* gr = xge + (pi * PS_MB + b) * A;
-      int xv[PS_MAXAS], gv[PS_MAXAS];
-#pragma unroll
-      for (int aa = 0; aa < PS_MAXAS; ++aa) {
-        xv[aa] = aa < A ? ps_ldi(xr + aa) : SORT_EMPTY;
-        gv[aa] = aa < A ? ps_ldi(gr + aa) : SORT_EMPTY;
-      }
-      int best = 0, bv = 0;
-#pragma unroll
-      for (int aa = 0; aa < PS_MAXAS; ++aa) {
-        const int v = max(xv[aa], gv[aa]);
-        if (aa < A && (aa == 0 || v > bv)) {
-          bv = v;
+      const int* m = reinterpret_cast<const int*>(st) + (pi * PS_MB + b) * A;
+      int best = 0, bv = m[0];
+      for (int aa = 1; aa < A; ++aa)
+        if (m[aa] > bv) {
+          bv = m[aa];
           best = aa;
         }
-      }
       ac[pi * PS_MB + b] = best;
       if (r > 0 && best != ap[pi * PS_MB + b]) {
         chg = 1;
         chg_own = pi == head;
       }
     }
-    if (r == 0)
-      for (int i = tid; i < B * d; i += 256) scr[i] = ps_ld(crh + i);
     const int any = __syncthreads_or(chg);
     const int own_chg = __syncthreads_or(chg_own);
     if (r > 0 && !any) {
@@ -518,114 +613,80 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
     }
     // ---- TD target and output gradient (k_tdg's arithmetic), every rank the same
     const int* an = ac + head * PS_MB;
+    int nf = 0;
     for (int i = tid; i < PS_MB * d; i += 256) {
       const int b = i / d, k = i - b * d;
       float gv = 0.f;
       if (b < B && sab[b] >= 0 && sab[b] < A) {
-        const float tgt = ps_ld(psith + b * O + an[b] * d + k);
-        const float tg = __fadd_rn(sphi[b * d + k], __fmul_rn(sgam[b], tgt));
-        gv = __fmul_rn(P.norm, __fsub_rn(scr[b * d + k], tg));
+        const float tg = __fadd_rn(sphi[b * d + k], __fmul_rn(sgam[b], pst[b * O + an[b] * d + k]));
+        const float diff = __fsub_rn(scr[b * d + k], tg);
+        gv = __fmul_rn(P.norm, diff);
+        nf |= !__builtin_isfinite(diff);
       }
       g3[i] = gv;
+      g3m[i] = b < B && sab[b] == rank ? gv : 0.f;
     }
-    // dW + Adam operands of the output layer (rank a < A: rows a·d .. a·d+d, column tid)
-    const int arow = rank * d;
-    float xcol[PS_MB];
-    {
-      const float* x2 = xsh + (size_t)(NL - 2) * 3 * PS_MB * PS_H + tid;
-#pragma unroll
-      for (int b = 0; b < PS_MB; ++b) xcol[b] = b < B ? ps_ld(x2 + (size_t)b * PS_H) : 0.f;
-    }
-    __syncthreads();
+    if (__syncthreads_or(nf) && tid == 0 && rank == 0) atomicOr(G.nonfin, 1);
     PS_MARK0(40);
-    // dX of layer NL-2 (sparse: row b's gradient sits at action a_b)
-    {
+    {  // dX of layer NH (sparse: row b's gradient sits at action a_b) -> dZ_NH, published
       float dx = 0.f;
       const int ab = g < B ? sab[g] : -1;
       if (ab >= 0 && ab < A)
         for (int k = 0; k < d; ++k) dx = __builtin_fmaf(g3[g * d + k], wc3[(ab * d + k) * 8 + j], dx);
-      const float z = g < B ? act_bwd(dx, own[((NL - 2) * 32 + g) * 8 + j], P.L[NL - 2].act) : 0.f;
+      const float z = g < B ? act_bwd(dx, own[(NH * 32 + g) * 8 + j], P.L[NH].act) : 0.f;
       sdz[g * 8 + j] = z;
-      if (NL - 2 >= 1) ps_st(dzh + ((size_t)(NL - 2) * PS_MB + g) * PS_H + c0 + j, z);
+      ps_st(dzh + ((size_t)NH * PS_MB + g) * PS_H + c0 + j, z);
     }
-    if (NL - 2 >= 1) {
-      ps_arrive(hctr);
-      ++e;
-    } else {
-      __syncthreads();
-    }
+    ps_arrive(hctr);
+    ++e;
     PS_MARK0(41);
     if (outr) {  // dW / db + Adam of the output rows of action `rank` (read slot -> write slot)
-      for (int k0 = 0; k0 < d; k0 += 8) {
-        float pp[8], mm[8], vv[8];
+#pragma unroll
+      for (int c = 0; c < DC; ++c)
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const size_t wi = LO.wOff + (size_t)(arow + k0 + u) * PS_H + tid;
-          const bool okk = k0 + u < d;
-          pp[u] = okk ? pon[wi] : 0.f;
-          mm[u] = okk ? mrd[wi] : 0.f;
-          vv[u] = okk ? vrd[wi] : 0.f;
-        }
+          const int k = 8 * c + u;
+          if (k < d) {
+            float gw = 0.f;  // rows of other actions hold exact zeros in g3m: the same sum
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int k = k0 + u;
-          if (k >= d) break;
-          float gw = 0.f;
-#pragma unroll
-          for (int b = 0; b < PS_MB; ++b)
-            if (b < B && sab[b] == rank) gw = __builtin_fmaf(g3[b * d + k], xcol[b], gw);
-          adam_apply(pp[u], mm[u], vv[u], gw, adc);
-          const size_t wi = LO.wOff + (size_t)(arow + k) * PS_H + tid;
-          ps_st(pnew + wi, pp[u]);
-          ps_st(mwr + wi, mm[u]);
-          ps_st(vwr + wi, vv[u]);
+            for (int b = 0; b < PS_MB; ++b) gw = __builtin_fmaf(g3m[b * d + k], xc[NH][b], gw);
+            float pp = po[c][u][0], mm = po[c][u][1], vv = po[c][u][2];
+            adam_apply(pp, mm, vv, gw, adc);
+            const size_t wi = LO.wOff + (size_t)(arow + k) * PS_H + tid;
+            pnew[wi] = pp;
+            mwr[wi] = mm;
+            vwr[wi] = vv;
+            Wno[k * PS_XS + tid] = pp;
+          }
         }
-      }
       if (tid < d) {
-        const size_t bi = LO.bOff + arow + tid;
         float gb = 0.f;
         for (int b = 0; b < B; ++b)
           if (sab[b] == rank) gb = __fadd_rn(gb, g3[b * d + tid]);
-        float pp = pon[bi], mm = mrd[bi], vv = vrd[bi];
+        float pp = pbo[0], mm = pbo[1], vv = pbo[2];
         adam_apply(pp, mm, vv, gb, adc);
-        ps_st(pnew + bi, pp);
-        ps_st(mwr + bi, mm);
-        ps_st(vwr + bi, vv);
+        const size_t bi = LO.bOff + arow + tid;
+        pnew[bi] = pp;
+        mwr[bi] = mm;
+        vwr[bi] = vv;
+        nb[(NL - 1) * PS_J + tid] = pp;
       }
     }
     PS_MARK0(42);
-    // ---- hidden layers NL-2 .. 1: dX of layer l-1 (published) || dW + Adam of layer l (own rows)
-    for (int l = NL - 2; l >= 1 && ok; --l) {
+    // ---- hidden layers NH .. 1: dX of layer l-1 (published) || dW + Adam of layer l (own rows)
+#pragma unroll
+    for (int l = NH; l >= 1; --l) {
+      if (ok) {
       const PsLayer Ll = P.L[l];
-      float* DZ = st;                   // [32][PS_XS]
-      float* WcT = st + 32 * PS_XS;     // [8][PS_XS]: W_l[:, c0 + jj] transposed
-      {
-        const float4* src = reinterpret_cast<const float4*>(pon + Ll.wOff + (size_t)tid * PS_H + c0);
-        const float4 lo = src[0], hi = src[1];
-        WcT[0 * PS_XS + tid] = lo.x; WcT[1 * PS_XS + tid] = lo.y;
-        WcT[2 * PS_XS + tid] = lo.z; WcT[3 * PS_XS + tid] = lo.w;
-        WcT[4 * PS_XS + tid] = hi.x; WcT[5 * PS_XS + tid] = hi.y;
-        WcT[6 * PS_XS + tid] = hi.z; WcT[7 * PS_XS + tid] = hi.w;
-      }
-      const float* xin = xsh + (size_t)(l - 1) * 3 * PS_MB * PS_H + tid;
-#pragma unroll
-      for (int b = 0; b < PS_MB; ++b) xcol[b] = b < B ? ps_ld(xin + (size_t)b * PS_H) : 0.f;
-      float pp[PS_J], mm[PS_J], vv[PS_J];  // Adam state of W_l[c0 + jj][tid], requested before the wait
-#pragma unroll
-      for (int jj = 0; jj < PS_J; ++jj) {
-        const size_t wi = Ll.wOff + (size_t)(c0 + jj) * PS_H + tid;
-        pp[jj] = pon[wi];
-        mm[jj] = mrd[wi];
-        vv[jj] = vrd[wi];
-      }
-      PS_MARK0(43 + 4 * (NL - 2 - l));
-      if (!(ok = ps_wait(P, hctr, PS_R * e, &s_ok))) break;
-      PS_MARK(9 + 8 * (r < 6 ? r : 5) + (NL - 2 - l));
+      float* DZ = st;  // [32][PS_XS]
+      PS_MARK0(43 + 4 * (NH - l));
+      ok = ps_wait(P, hctr, PS_R * e, &s_ok);
+      if (ok) {
       ps_stage<8>(dzh + (size_t)l * PS_MB * PS_H, PS_MB, DZ);
       __syncthreads();
-      PS_MARK0(44 + 4 * (NL - 2 - l));
+      PS_MARK0(44 + 4 * (NH - l));
       {  // dX_{l-1}[g][c0 + j]
-        const float dx = ps_dot(DZ + g * PS_XS, WcT + j * PS_XS, PS_H);
+        const float dx = ps_dot(DZ + g * PS_XS, WcT + ((l - 1) * PS_J + j) * PS_XS, PS_H);
         const float z = g < B ? act_bwd(dx, own[((l - 1) * 32 + g) * 8 + j], P.L[l - 1].act) : 0.f;
         sdzn[g * 8 + j] = z;
         if (l - 1 >= 1) ps_st(dzh + ((size_t)(l - 1) * PS_MB + g) * PS_H + c0 + j, z);
@@ -636,68 +697,66 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
       } else {
         __syncthreads();
       }
-      PS_MARK0(45 + 4 * (NL - 2 - l));
-      // dW_l[c0 + jj][tid] = Σ_b dZ_l[b][c0 + jj] X_{l-1}[b][tid], db_l; Adam
+      PS_MARK0(45 + 4 * (NH - l));
+      // dW_l[c0 + jj][tid] = Σ_b dZ_l[b][c0 + jj] X_{l-1}[b][tid], db_l; Adam from registers
 #pragma unroll
       for (int jj = 0; jj < PS_J; ++jj) {
-        const size_t wi = Ll.wOff + (size_t)(c0 + jj) * PS_H + tid;
-        float gw = 0.f;
+        float gw = 0.f;  // rows past B hold exact zeros in sdz
 #pragma unroll
-        for (int b = 0; b < PS_MB; ++b)
-          if (b < B) gw = __builtin_fmaf(sdz[b * 8 + jj], xcol[b], gw);
-        adam_apply(pp[jj], mm[jj], vv[jj], gw, adc);
-        ps_st(pnew + wi, pp[jj]);
-        ps_st(mwr + wi, mm[jj]);
-        ps_st(vwr + wi, vv[jj]);
+        for (int b = 0; b < PS_MB; ++b) gw = __builtin_fmaf(sdz[b * 8 + jj], xc[l - 1][b], gw);
+        float pp = pw[l - 1][jj][0], mm = pw[l - 1][jj][1], vv = pw[l - 1][jj][2];
+        adam_apply(pp, mm, vv, gw, adc);
+        const size_t wi = Ll.wOff + (size_t)(c0 + jj) * PS_H + tid;
+        pnew[wi] = pp;
+        mwr[wi] = mm;
+        vwr[wi] = vv;
+        Wn[((l - 1) * PS_J + jj) * PS_XS + tid] = pp;
       }
       if (tid < PS_J) {
-        const size_t bi = Ll.bOff + c0 + tid;
         float gb = 0.f;
         for (int b = 0; b < B; ++b) gb = __fadd_rn(gb, sdz[b * 8 + tid]);
-        float pp = pon[bi], mm = mrd[bi], vv = vrd[bi];
+        float pp = pb[l][0], mm = pb[l][1], vv = pb[l][2];
         adam_apply(pp, mm, vv, gb, adc);
-        ps_st(pnew + bi, pp);
-        ps_st(mwr + bi, mm);
-        ps_st(vwr + bi, vv);
+        const size_t bi = Ll.bOff + c0 + tid;
+        pnew[bi] = pp;
+        mwr[bi] = mm;
+        vwr[bi] = vv;
+        nb[l * PS_J + tid] = pp;
       }
       __syncthreads();
-      PS_MARK0(46 + 4 * (NL - 2 - l));
-      for (int i = tid; i < 256; i += 256) sdz[i] = sdzn[i];
+      PS_MARK0(46 + 4 * (NH - l));
+      sdz[tid] = sdzn[tid];
       __syncthreads();
+      }
+      }
     }
     if (!ok) break;
     // ---- layer 0: dW0 + Adam of rows c0.., then the post-update forward of S1 ++ s_next
     {
       const PsLayer L0 = P.L[0];
-      float* W0n = st;  // [8][K0S] new rows, then bias [8]
-      for (int i = tid; i < PS_J * K0S; i += 256) {
-        const int jj = i / K0S, k = i - jj * K0S;
-        float nv = 0.f;
-        if (k < n_s) {
-          const size_t wi = L0.wOff + (size_t)(c0 + jj) * n_s + k;
-          float pp = pon[wi], mm = mrd[wi], vv = vrd[wi];
-          float gw = 0.f;
+      if (tid < PS_J * n_s) {
+        const int jj = tid / n_s, k = tid - jj * n_s;
+        float gw = 0.f;
 #pragma unroll
-          for (int b = 0; b < PS_MB; ++b)
-            if (b < B) gw = __builtin_fmaf(sdz[b * 8 + jj], sx[b * K0S + k], gw);
-          adam_apply(pp, mm, vv, gw, adc);
-          ps_st(pnew + wi, pp);
-          ps_st(mwr + wi, mm);
-          ps_st(vwr + wi, vv);
-          nv = pp;
-        }
-        W0n[i] = nv;
+        for (int b = 0; b < PS_MB; ++b) gw = __builtin_fmaf(sdz[b * 8 + jj], sx[b * K0S + k], gw);
+        float pp = p0[0], mm = p0[1], vv = p0[2];
+        adam_apply(pp, mm, vv, gw, adc);
+        const size_t wi = L0.wOff + (size_t)c0 * n_s + tid;
+        pnew[wi] = pp;
+        mwr[wi] = mm;
+        vwr[wi] = vv;
+        W0n[jj * K0S + k] = pp;
       }
       if (tid < PS_J) {
-        const size_t bi = L0.bOff + c0 + tid;
-        float pp = pon[bi], mm = mrd[bi], vv = vrd[bi];
         float gb = 0.f;
         for (int b = 0; b < B; ++b) gb = __fadd_rn(gb, sdz[b * 8 + tid]);
+        float pp = pb[0][0], mm = pb[0][1], vv = pb[0][2];
         adam_apply(pp, mm, vv, gb, adc);
-        ps_st(pnew + bi, pp);
-        ps_st(mwr + bi, mm);
-        ps_st(vwr + bi, vv);
-        W0n[PS_J * K0S + tid] = pp;
+        const size_t bi = L0.bOff + c0 + tid;
+        pnew[bi] = pp;
+        mwr[bi] = mm;
+        vwr[bi] = vv;
+        nb[tid] = pp;
       }
       __syncthreads();
       PS_MARK0(51);
@@ -706,75 +765,51 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
         const float* xr = sx + (row < PS_MB ? 32 + row : 96) * K0S;
         float acc = 0.f;
         for (int k = 0; k < n_s; ++k) acc = __builtin_fmaf(xr[k], W0n[jj * K0S + k], acc);
-        ps_st(xvh + (size_t)row * PS_H + c0 + jj, act_fwd(__fadd_rn(acc, W0n[PS_J * K0S + jj]), L0.act));
+        ps_st(xvh + (size_t)row * PS_H + c0 + jj, act_fwd(__fadd_rn(acc, nb[jj]), L0.act));
       }
       ps_arrive(hctr);
       ++e;
       PS_MARK(12 + 8 * (r < 6 ? r : 5));
     }
-    // ---- post-update forward, hidden layers 1 .. NL-2 (own rows from the write slot)
-    for (int l = 1; l <= NL - 2 && ok; ++l) {
+    // ---- post-update forward, hidden layers 1 .. NH (own rows from LDS)
+#pragma unroll
+    for (int l = 1; l <= NH; ++l) {
+      if (ok) {
       const PsLayer Ll = P.L[l];
-      float* X = st;                        // [33][PS_XS]
-      float* Wn = st + (PS_MB + 1) * PS_XS; // [8][PS_XS]
-      {
-        const __amdgpu_buffer_rsrc_t rw = ps_rsrc(pnew + Ll.wOff + (size_t)c0 * PS_H, PS_J * PS_H * 4u);
-        float4 v[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) v[u] = ps_ld4(rw, (tid + u * 256) * 16);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int i = tid + u * 256;
-          *reinterpret_cast<float4*>(Wn + (i >> 6) * PS_XS + ((i & 63) << 2)) = v[u];
-        }
-      }
-      const float bn = ps_ld(pnew + Ll.bOff + c0 + j);
+      float* X = st;  // [33][PS_XS]
       PS_MARK0(53 + 3 * (l - 1));
-      if (!(ok = ps_wait(P, hctr, PS_R * e, &s_ok))) break;
+      ok = ps_wait(P, hctr, PS_R * e, &s_ok);
+      if (ok) {
       ps_stage<9>(xvh + (size_t)(l - 1) * (PS_MB + 1) * PS_H, PS_MB + 1, X);
       __syncthreads();
       PS_MARK0(54 + 3 * (l - 1));
+      const float bn = nb[l * PS_J + j];
       for (int row = g; row < PS_MB + 1; row += 32) {
-        const float y = act_fwd(__fadd_rn(ps_dot(X + row * PS_XS, Wn + j * PS_XS, PS_H), bn), Ll.act);
+        const float y = act_fwd(__fadd_rn(ps_dot(X + row * PS_XS, Wn + ((l - 1) * PS_J + j) * PS_XS, PS_H), bn), Ll.act);
         ps_st(xvh + ((size_t)l * (PS_MB + 1) + row) * PS_H + c0 + j, y);
       }
       ps_arrive(hctr);
       ++e;
       PS_MARK0(55 + 3 * (l - 1));
+      }
+      }
     }
     if (!ok) break;
     // ---- post-update output layer (rank a < A): this round's maxima for policies > head, selection key
     if (outr) {
-      float* X = st;                          // [33][PS_XS]
-      float* Wn = st + (PS_MB + 1) * PS_XS;   // [d][PS_XS]
-      {
-        const __amdgpu_buffer_rsrc_t rw = ps_rsrc(pnew + LO.wOff + (size_t)arow * PS_H, (unsigned)d * PS_H * 4u);
-        float4 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int i = tid + u * 256;
-          v[u] = i < d * 64 ? ps_ld4(rw, i * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int i = tid + u * 256;
-          if (i < d * 64) *reinterpret_cast<float4*>(Wn + (i >> 6) * PS_XS + ((i & 63) << 2)) = v[u];
-        }
-      }
-      if (tid < d) psi[PS_MB * d + tid] = ps_ld(pnew + LO.bOff + arow + tid);  // bias, parked in row 32's slot
+      float* X = st;  // [33][PS_XS]
       PS_MARK0(59);
       if (!(ok = ps_wait(P, hctr, PS_R * e, &s_ok))) break;
       PS_MARK(13 + 8 * (r < 6 ? r : 5));
-      ps_stage<9>(xvh + (size_t)(NL - 2) * (PS_MB + 1) * PS_H, PS_MB + 1, X);
+      ps_stage<9>(xvh + (size_t)NH * (PS_MB + 1) * PS_H, PS_MB + 1, X);
       __syncthreads();
       float yv[5];
 #pragma unroll
       for (int u = 0; u < 5; ++u) {
         const int i = tid + u * 256;
         const int row = i / d, k = i - row * d;
-        yv[u] = i < (PS_MB + 1) * d ? __fadd_rn(ps_dot(X + row * PS_XS, Wn + k * PS_XS, PS_H), psi[PS_MB * d + k]) : 0.f;
+        yv[u] = i < (PS_MB + 1) * d ? __fadd_rn(ps_dot(X + row * PS_XS, Wno + k * PS_XS, PS_H), nb[(NL - 1) * PS_J + k]) : 0.f;
       }
-      __syncthreads();
 #pragma unroll
       for (int u = 0; u < 5; ++u)
         if (tid + u * 256 < (PS_MB + 1) * d) psi[tid + u * 256] = yv[u];
@@ -837,6 +872,7 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
       out->sel1 = a;
       out->flag = flag;
       out->cancelled = cancelled;
+      out->nonfinite = __hip_atomic_load(G.nonfin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __threadfence_system();
       __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -850,7 +886,6 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
       __hip_atomic_store(P.epoch, ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
-
 
 // Placement census (host check before the persistent step is used): per XCC_ID, how many of a
 // 256-workgroup launch with k_pstep's LDS footprint landed there.

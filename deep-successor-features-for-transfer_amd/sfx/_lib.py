@@ -40,6 +40,8 @@ SIGNATURES = {
     "sfx_set_pstep": (_I, [_VP, _I]),
     "sfx_get_pstep": (_I, [_VP]),
     "sfx_pstep_stats": (_I, [_VP, _VP]),
+    "sfx_nonfinite": (_I, [_VP, _VP, _I]),
+    "sfx_runner_nonfinite": (_I, [_VP, _VP]),
     "sfx_pstep_trace": (_I, [_VP, _VP]),
     "sfx_pstep_timeline": (_I, [_VP, _VP]),
     "sfx_test_reward_updates": (_I, [_VP, _I, _VP, _VP, _VP, _I, C.c_double, C.c_double, _VP]),

@@ -331,6 +331,12 @@ class SFEngine:
                       for t in range(self.T)}
         return conv, out
 
+    def nonfinite(self, reset: bool = False) -> bool:
+        """SURVEY §5 failure detection: whether any TD error since the last reset was NaN / Inf."""
+        v = C.c_int()
+        check(lib.sfx_nonfinite(self._h, C.byref(v), int(bool(reset))), "sfx_nonfinite")
+        return bool(v.value)
+
     PRECISIONS = {"fp32": 0, "bf16": 1}
 
     def set_precision(self, precision: str):

@@ -333,10 +333,12 @@ class NativeEnvLoop:
         self._check(self._lib.sfx_runner_stats(self._r, C.byref(a), C.byref(b), C.byref(c), C.byref(w)),
                     "sfx_runner_stats")
         self._check(self._lib.sfx_runner_retried(self._r, C.byref(rt)), "sfx_runner_retried")
-        rc = C.c_longlong()
+        rc, nf = C.c_longlong(), C.c_longlong()
         self._check(self._lib.sfx_runner_recomputed(self._r, C.byref(rc)), "sfx_runner_recomputed")
+        self._check(self._lib.sfx_runner_nonfinite(self._r, C.byref(nf)), "sfx_runner_nonfinite")
         return {"env_steps": a.value, "prelaunched": b.value, "host_round_steps": c.value,
-                "host_wait_us": round(w.value, 1), "retried": rt.value, "recomputed": rc.value}
+                "host_wait_us": round(w.value, 1), "retried": rt.value, "recomputed": rc.value,
+                "nonfinite_steps": nf.value}
 
     def gpi_counters(self) -> np.ndarray:
         T = self.eng.T_glob if self.schedule == "sharded" else self.eng.T

@@ -204,6 +204,15 @@ int sfx_step_stats(sfx_t h, long long* steps, long long* fallbacks, long long* r
 int sfx_skip_stats(sfx_t h, long long* checked, long long* skipped, int reset);
 
 /*
+ * Failure detection (the reference only prints NaN/Inf diagnostics,
+ * features/deep_phi.py:185-192): every TD-target kernel sets a sticky device flag when a TD error
+ * c - (φ + γ ψ⁻) comes out non-finite (NaN or Inf in φ, γ, the ψ heads or the target heads).  The
+ * native runner publishes the flag with each step's result and fails the run at the first such
+ * step; sfx_nonfinite reads it (flag_host = 0 / 1) and optionally resets it.
+ */
+int sfx_nonfinite(sfx_t h, int* flag_host, int reset);
+
+/*
  * The persistent all-task step (k_pstep): the whole env step of agents/sfdqn.py:57-60 over
  * features/deep.py:93-131 -- LMS, forwards, every speculative round until verified, action
  * selection and (runner steps) publication -- as ONE launch of 256 workgroups, head t on XCD t.
@@ -326,6 +335,9 @@ int sfx_runner_retried(sfx_runner_t r, long long* retried);
  * (committing nothing) over the transient buffers the rounds read, so the step's forward and
  * device rounds were recomputed from its pre-step slot first. */
 int sfx_runner_recomputed(sfx_runner_t r, long long* recomputed);
+/* Steps whose published result carried the non-finite TD flag (sfx_nonfinite); the runner returns
+ * SFX_E_STATE at the first one. */
+int sfx_runner_nonfinite(sfx_runner_t r, long long* steps);
 /* SF.gpi_counters (features/successor.py:270-272): [T][T] counts of the GPI task per active task
  * (counted only with GPI action selection, as SF.GPI(update_counters=use_gpi), agents/sfdqn.py:41) */
 int sfx_runner_gpi_counters(sfx_runner_t r, long long* out_host /* [T*T] */);
