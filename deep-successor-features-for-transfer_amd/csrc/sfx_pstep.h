@@ -282,7 +282,12 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
 
   // ---- register-resident Adam state of this rank's rows (read slot: written by no one in this launch)
   float pw[NH][PS_J][3];      // hidden layer l = 1..NH, rows c0 + jj, column tid
-  float po[DC][8][3];         // output rows arow + 8c + u, column tid (output ranks)
+  // output rows arow + 8c + u, column tid (output ranks): registers for DC = 1 only; wider output
+  // slices read their (read-slot) Adam state at the update instead -- at DC >= 2 the resident copy
+  // pushed the kernel into heavy register spilling, and the DC = 3 build lost resident state
+  // (tests/test_gpu_pstep.py caught it at d = 20)
+  constexpr bool PO_REG = DC == 1;
+  float po[PO_REG ? DC : 1][8][3];
   float p0[3] = {0.f, 0.f, 0.f};  // layer 0: entry tid of rows c0.. (8 n_s <= 256 entries)
   float pb[NL - 1][3];        // threads < 8: bias c0 + tid of layers 0 .. NH
   float pbo[3] = {0.f, 0.f, 0.f};  // threads < d: output bias arow + tid
@@ -297,16 +302,16 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
         pw[l][jj][1] = mrd[wi];
         pw[l][jj][2] = vrd[wi];
       }
-#pragma unroll
-    for (int c = 0; c < DC; ++c)
+    if constexpr (PO_REG) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const bool okk = outr && 8 * c + u < d;
-        const size_t wi = P.L[NL - 1].wOff + (size_t)(arow + 8 * c + u) * PS_H + tid;
-        po[c][u][0] = okk ? pon[wi] : 0.f;
-        po[c][u][1] = okk ? mrd[wi] : 0.f;
-        po[c][u][2] = okk ? vrd[wi] : 0.f;
+        const bool okk = outr && u < d;
+        const size_t wi = P.L[NL - 1].wOff + (size_t)(arow + u) * PS_H + tid;
+        po[0][u][0] = okk ? pon[wi] : 0.f;
+        po[0][u][1] = okk ? mrd[wi] : 0.f;
+        po[0][u][2] = okk ? vrd[wi] : 0.f;
       }
+    }
     if (tid < PS_J * n_s) {
       const size_t wi = P.L[0].wOff + (size_t)c0 * n_s + tid;
       p0[0] = pon[wi];
@@ -641,8 +646,18 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
     ++e;
     PS_MARK0(41);
     if (outr) {  // dW / db + Adam of the output rows of action `rank` (read slot -> write slot)
+#pragma unroll 1
+      for (int c = 0; c < DC; ++c) {  // rolled: an unrolled DC >= 2 body spills
+        float pl[8][3];  // DC >= 2: this chunk's read-slot Adam state, all loads issued up front
+        if constexpr (!PO_REG) {
 #pragma unroll
-      for (int c = 0; c < DC; ++c)
+          for (int u = 0; u < 8; ++u) {
+            const size_t wi = LO.wOff + (size_t)(arow + (8 * c + u < d ? 8 * c + u : 0)) * PS_H + tid;
+            pl[u][0] = pon[wi];
+            pl[u][1] = mrd[wi];
+            pl[u][2] = vrd[wi];
+          }
+        }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int k = 8 * c + u;
@@ -650,7 +665,16 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
             float gw = 0.f;  // rows of other actions hold exact zeros in g3m: the same sum
 #pragma unroll
             for (int b = 0; b < PS_MB; ++b) gw = __builtin_fmaf(g3m[b * d + k], xc[NH][b], gw);
-            float pp = po[c][u][0], mm = po[c][u][1], vv = po[c][u][2];
+            float pp, mm, vv;
+            if constexpr (PO_REG) {
+              pp = po[0][u][0];
+              mm = po[0][u][1];
+              vv = po[0][u][2];
+            } else {
+              pp = pl[u][0];
+              mm = pl[u][1];
+              vv = pl[u][2];
+            }
             adam_apply(pp, mm, vv, gw, adc);
             const size_t wi = LO.wOff + (size_t)(arow + k) * PS_H + tid;
             pnew[wi] = pp;
@@ -659,6 +683,7 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
             Wno[k * PS_XS + tid] = pp;
           }
         }
+      }
       if (tid < d) {
         float gb = 0.f;
         for (int b = 0; b < B; ++b)

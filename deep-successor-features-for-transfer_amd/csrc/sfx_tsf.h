@@ -8,42 +8,52 @@
 // l2 = MSE(w_i·φ̃, r); loss = l1 + β l2 and one Adam step over {ψ_i, w_i, g_i, h}.
 //
 // The ψ part runs through the SF-DQN kernels with φ̃ as the features; these kernels do the rest:
-//   k_tsf_fwd<LPR>  before the TD target: φ̃, the saved flow states / tanh outputs / g features,
+//   k_tsf_fwd<NP>   before the TD target: φ̃, the saved flow states / tanh outputs / g features,
 //                   and a snapshot of g_i, h, w_i as they were before the step.  A workgroup
-//                   owns PB batch indices (their s and s1 rows); a row's planar-flow chain runs
-//                   on LPR lanes (one state component per lane, butterfly reduction of w_k·z).
-//   k_tsf_bwd<LPR>  after the ψ backward, one launch of four workgroup roles that all read the
+//                   owns TSF_PB batch indices (their s and s1 rows); a row's planar-flow chain
+//                   runs in ONE lane (z in NP registers, w_k·z as packed FMAs in three
+//                   independent chains, flow parameters as wave-uniform scalar loads), so a
+//                   flow step holds no cross-lane reduction.  NP = n_s rounded up to 4.
+//   k_tsf_bwd<NP>   after the ψ backward, one launch of four workgroup roles that all read the
 //                   snapshot (so no role sees another's Adam writes):
-//                     flow rows  FR rows each: dg, then the reverse flow chain on LPR lanes per
-//                                row with the flow states staged in LDS; each row's terms of the
+//                     flow rows  TSF_FR rows each: dg, then the reverse flow chain, one lane per
+//                                row, the flow states staged in LDS; each row's terms of the
 //                                flow-parameter gradients into `part`
 //                     h          256 parameters of the shared h each: gradient + Adam
 //                     g-Linear   TSF_QS output columns of g_i's Linear each: dg, gradient + Adam
 //                     w          l2, the w_i gradient + Adam, the loss row
 //   k_tsf_flow      flow parameters: sum of the per-row terms (fixed order) + Adam (K > 0).
-// Limits (checked by sfx_tsf_setup, see tsf_geometry_ok): n_s <= 32, B <= 64, d*G <= 8192,
-// 2B*G <= 8192, B*d <= 4096, K(2 n_s + 1) + G(n_s + 1) <= 4096, and the flow-row staging
-// FR*(K+1)*n_s <= TSF_ZS, FR*K <= TSF_TS, FR*G <= 2048, FR*d <= 2048.
+// Limits (checked by sfx_tsf_setup): n_s <= 32, B <= 64, d <= 128, d*G <= 8192, 2B*G <= 8192,
+// B*d <= 4096, K(2 n_s + 1) + G(n_s + 1) <= 4096, 2 TSF_PB G <= 4096, and the flow-row staging
+// TSF_FR (K+1) NP <= TSF_ZS, TSF_FR K <= TSF_TS, TSF_FR G <= 2048, TSF_FR d <= 2048.
 #pragma once
 
 namespace sfx {
 
-constexpr int TSF_NS = 32;     // max n_s (one lane per state component, LPR <= 32)
+constexpr int TSF_NS = 32;     // max n_s
 constexpr int TSF_LDS = 8192;  // floats per staged operand (flows, W_h, g features)
-constexpr int TSF_ZS = 12288;  // flow states staged per flow-row workgroup: FR x (K+1) x n_s
-constexpr int TSF_TS = 1024;   // tanh outputs staged per flow-row workgroup: FR x K
+constexpr int TSF_ZS = 12288;  // flow states staged per flow-row workgroup: TSF_FR x (K+1) x NP
+constexpr int TSF_TS = 1024;   // tanh outputs staged per flow-row workgroup: TSF_FR x K
 constexpr int TSF_QS = 16;     // g-Linear output columns per backward workgroup
-constexpr int TSF_SM = TSF_ZS + TSF_TS + TSF_LDS / 2 + TSF_LDS + 3 * 2048;  // k_tsf_bwd LDS (floats)
+constexpr int TSF_PB = 8;      // forward: batch indices per workgroup (2 TSF_PB flow rows)
+constexpr int TSF_FR = 8;      // backward: flow rows per flow-row workgroup
+constexpr int TSF_SCR = 64 * TSF_NS;  // TsfArgs::scratch floats (one row per chain lane)
+constexpr int TSF_FA = 8192;   // flows staged in the chain layout: K x tsf_fst(NP)
+constexpr int TSF_SM = TSF_ZS + TSF_TS + TSF_LDS / 2 + TSF_LDS + 3 * 2048 + TSF_FA;  // k_tsf_bwd LDS (floats)
 
-// lanes per flow row and the row groups they imply (256-thread workgroups)
-__host__ __device__ constexpr int tsf_lpr(int n_s) { return n_s <= 16 ? 16 : 32; }
-__host__ __device__ constexpr int tsf_rpw(int lpr) { return 256 / lpr; }  // forward rows per WG
-__host__ __device__ constexpr int tsf_fr(int lpr) { return 128 / lpr; }   // backward flow rows per WG
+// NP: n_s rounded up to 4 -- the register width of a flow row and the row stride of the saved
+// flow states (zs [K+1][2B][NP], 16-byte rows); the per-row gradient terms `part` are
+// [K][2B][tsf_pst(NP)]: da·z_k at [0, NP), dz·t at [NP, 2NP), da at 2NP.
+__host__ __device__ constexpr int tsf_np(int n_s) { return (n_s + 3) & ~3; }
+__host__ __device__ constexpr int tsf_pst(int np) { return 2 * np + 4; }
+// a flow in the chain layout (LDS): w at [0, NP), u at [NP, 2NP), b at 2NP, zeros elsewhere
+__host__ __device__ constexpr int tsf_fst(int np) { return 2 * np + 4; }
 
 struct TsfArgs {
   int pol, B, n_s, G, K, d, Pg, Ph, O, lastOff;
   float beta;
-  int nflow, nh, nlin, pad_;  // k_tsf_bwd roles: flow-row / h / g-Linear workgroups, then one w workgroup
+  int nflow, nh, nlin;  // k_tsf_bwd roles: flow-row / h / g-Linear workgroups, then one w workgroup
+  int np;               // tsf_np(n_s)
   const float* S;
   const float* S1;
   const float* phi;
@@ -55,13 +65,13 @@ struct TsfArgs {
   float* hp;  // [Ph]: W_h[d][G] then b_h[d]
   float* hm;  // [T][Ph] (each task's optimizer keeps its own moments of the shared h)
   float* hv;
-  float* zs;     // [K+1][2B][n_s] flow states (rows 0..B-1: s, B..2B-1: s1)
+  float* zs;     // [K+1][2B][NP] flow states (rows 0..B-1: s, B..2B-1: s1)
   float* ts;     // [K][2B] tanh outputs
   float* gfeat;  // [2B][G]
   float* tphi;   // [B][d]
-  float* part;   // [K][2B][2n_s+1] per-row flow-parameter gradient terms
+  float* part;   // [K][2B][tsf_pst(NP)] per-row flow-parameter gradient terms
+  float* scratch;  // [TSF_SCR]: stores of flow-chain lanes past the batch (never read)
   float* snap;   // [Pg + Ph + d]: g_i, h, w_i before this step (written by k_tsf_fwd)
-  float* trash;  // one word written by lanes whose store is unused (branch-free store loops)
   float* losses; // [3]: [1] = l1 (written by the ψ tail); [0], [2] written here
   const float* dzlast;  // output gradient of the policy's ψ head [B][O] (written by K2)
   const int* step;      // Adam step of the policy (already bumped by the ψ path)
@@ -89,20 +99,62 @@ __device__ __forceinline__ float tsf_tanh(float x) {
   return copysignf(ax < 0.625f ? small : large, x);
 }
 
-// Sum over a flow row's LPR lanes, the same value in every lane: quad_perm xor 1, xor 2,
-// row_half_mirror, row_mirror (DPP, no LDS round trip; each step pairs lanes symmetrically so
-// every lane adds the same two partials), then xor 16 across the two DPP rows when LPR = 32.
-template <int LPR>
-__device__ __forceinline__ float tsf_row_sum(float v) {
-#define SFX_DPP_ADD(ctrl) \
-  v = __fadd_rn(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false)))
-  SFX_DPP_ADD(0xB1);   // quad_perm [1,0,3,2]
-  SFX_DPP_ADD(0x4E);   // quad_perm [2,3,0,1]
-  SFX_DPP_ADD(0x141);  // row_half_mirror
-  SFX_DPP_ADD(0x140);  // row_mirror
-#undef SFX_DPP_ADD
-  if (LPR == 32) v = __fadd_rn(v, __shfl_xor(v, 16, 32));
-  return v;
+typedef float tsf_f2 __attribute__((ext_vector_type(2)));
+typedef float tsf_f4 __attribute__((ext_vector_type(4)));
+
+// One planar flow's parameters (chain layout, see tsf_fst), read from LDS: every lane of the
+// wave reads the same words (broadcast), 16 bytes at a time.
+template <int NP>
+struct TsfFlow {
+  float w[NP], u[NP], b;
+};
+
+template <int NP>
+__device__ __forceinline__ void tsf_flow_ld(TsfFlow<NP>& F, const float* f) {
+#pragma unroll
+  for (int q = 0; q < NP / 4; ++q) {
+    const tsf_f4 w4 = *(const tsf_f4*)(f + 4 * q), u4 = *(const tsf_f4*)(f + NP + 4 * q);
+    F.w[4 * q] = w4.x; F.w[4 * q + 1] = w4.y; F.w[4 * q + 2] = w4.z; F.w[4 * q + 3] = w4.w;
+    F.u[4 * q] = u4.x; F.u[4 * q + 1] = u4.y; F.u[4 * q + 2] = u4.z; F.u[4 * q + 3] = u4.w;
+  }
+  F.b = f[2 * NP];
+}
+
+// x·y over NP components: NP/2 packed FMAs in (up to) three independent chains, then the three
+// pair sums.
+template <int NP>
+__device__ __forceinline__ float tsf_dot(const tsf_f2 (&x)[NP / 2], const float (&y)[NP]) {
+  tsf_f2 c0 = {0.f, 0.f}, c1 = {0.f, 0.f}, c2 = {0.f, 0.f};
+#pragma unroll
+  for (int p = 0; p < NP / 2; ++p) {
+    const tsf_f2 yy = {y[2 * p], y[2 * p + 1]};
+    if (p % 3 == 0)
+      c0 = __builtin_elementwise_fma(x[p], yy, c0);
+    else if (p % 3 == 1)
+      c1 = __builtin_elementwise_fma(x[p], yy, c1);
+    else
+      c2 = __builtin_elementwise_fma(x[p], yy, c2);
+  }
+  return __fadd_rn(__fadd_rn(__fadd_rn(c0.x, c0.y), __fadd_rn(c1.x, c1.y)), __fadd_rn(c2.x, c2.y));
+}
+
+// x += s·y (packed)
+template <int NP>
+__device__ __forceinline__ void tsf_axpy(tsf_f2 (&x)[NP / 2], float s, const float (&y)[NP]) {
+  const tsf_f2 ss = {s, s};
+#pragma unroll
+  for (int p = 0; p < NP / 2; ++p) x[p] = __builtin_elementwise_fma((tsf_f2){y[2 * p], y[2 * p + 1]}, ss, x[p]);
+}
+
+// dst[0, NP) = s·x (16-byte stores)
+template <int NP>
+__device__ __forceinline__ void tsf_store_scaled(float* dst, const tsf_f2 (&x)[NP / 2], float s) {
+  const tsf_f2 ss = {s, s};
+#pragma unroll
+  for (int q = 0; q < NP / 4; ++q) {
+    const tsf_f2 lo = x[2 * q] * ss, hi = x[2 * q + 1] * ss;
+    *(tsf_f4*)(dst + 4 * q) = (tsf_f4){lo.x, lo.y, hi.x, hi.y};
+  }
 }
 
 typedef __attribute__((address_space(3))) void* tsf_lds_t;
@@ -116,6 +168,30 @@ __device__ __forceinline__ void glds(float* dst, int n, F src) {
   for (int c = threadIdx.x >> 6; c * 64 < n; c += nw) {
     const int j = c * 64 + lane;
     if (j < n) __builtin_amdgcn_global_load_lds((const void*)src(j), (tsf_lds_t)(dst + c * 64), 4, 0, 0);
+  }
+}
+
+// The K flows of g (packed: flow k at k(2 n_s + 1): w[n_s], b, u[n_s]) -> LDS in the chain layout
+// (tsf_fst); the padding words are zeroed by plain LDS stores (disjoint from the DMA'd words).
+// Complete at the caller's next __syncthreads().
+template <int NP>
+__device__ __forceinline__ void tsf_stage_flows(float* dst, const float* src, int K, int n_s) {
+  constexpr int FA = tsf_fst(NP);
+  const int fs = tsf_flow_stride(n_s), n = K * FA;
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  for (int c = threadIdx.x >> 6; c * 64 < n; c += nw) {
+    const int j = c * 64 + lane, k = j / FA, e = j - k * FA;
+    int o = -1;
+    if (e < NP)
+      o = e < n_s ? e : -1;
+    else if (e < 2 * NP)
+      o = e - NP < n_s ? n_s + 1 + (e - NP) : -1;
+    else if (e == 2 * NP)
+      o = n_s;
+    if (j < n && o >= 0)
+      __builtin_amdgcn_global_load_lds((const void*)(src + k * fs + o), (tsf_lds_t)(dst + c * 64), 4, 0, 0);
+    else if (j < n)
+      dst[j] = 0.f;
   }
 }
 
@@ -171,39 +247,85 @@ __device__ float tsf_stage_daff(const TsfArgs& A, int n, BMap bmap, float* s_tp,
   return se;
 }
 
-// grid cdiv(B, PB), 256 threads; PB = RPW / 2 batch indices (their s rows and s1 rows) per WG.
-template <int LPR>
-__global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A) {
-  constexpr int RPW = tsf_rpw(LPR), PB = RPW / 2;
+// dst[0, NP) = x (16-byte stores)
+template <int NP>
+__device__ __forceinline__ void tsf_store(float* dst, const tsf_f2 (&x)[NP / 2]) {
+#pragma unroll
+  for (int q = 0; q < NP / 4; ++q) *(tsf_f4*)(dst + 4 * q) = (tsf_f4){x[2 * q].x, x[2 * q].y, x[2 * q + 1].x, x[2 * q + 1].y};
+}
+
+// grid cdiv(B, TSF_PB), 256 threads; TSF_PB batch indices (their s rows and s1 rows) per WG.
+// gfl = A.g + pol Pg (g_i).  The flow rows wait for the staging (their flow parameters come from
+// LDS: LDS reads are counted apart from the rows' global stores, so a flow step never waits on
+// memory), then wave 0 runs them while waves 1-3 write the snapshot.
+template <int NP>
+__global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A, const float* __restrict__ gfl) {
+  constexpr int PB = TSF_PB, RPW = 2 * PB;
   __shared__ float s_fl[TSF_LDS / 2];  // flows, then the Linear of g
   __shared__ float s_whT[TSF_LDS];     // W_h transposed: [G][d]
   __shared__ float s_gf[TSF_LDS / 2];  // g features of this workgroup's rows [RPW][G]
   __shared__ float s_ph[1024];         // φ rows of this workgroup's batch indices [PB][d]
   __shared__ float s_z[RPW * TSF_NS];  // z_K of this workgroup's rows
   __shared__ float s_bh[256], s_wv[256];
+  __shared__ __attribute__((aligned(16))) float s_fa[TSF_FA];  // flows, chain layout
   const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
   const int fs = tsf_flow_stride(n_s), nfl = K * fs, nlin = G * n_s + G;
+  constexpr int FA = tsf_fst(NP);
   const int b0 = blockIdx.x * PB, nb = min(PB, B - b0);
   PROBE_T(t0_);
-  const float* gp = A.g + (long long)A.pol * A.Pg;
-  const int rl = tid / LPR, li = tid - rl * LPR;
-  const bool s1row = rl >= PB;
-  const int b = b0 + (s1row ? rl - PB : rl);
-  const bool valid = b < B;
-  const int row = s1row ? B + b : b;
-  float z = 0.f;
-  if (valid && li < n_s) z = (s1row ? A.S1 : A.S)[(size_t)b * n_s + li];
   const FDiv fd = fdiv(d), fG = fdiv(G);
-  glds(s_fl, nfl + nlin, [&](int j) { return gp + j; });
+  glds(s_fl, nfl + nlin, [&](int j) { return gfl + j; });
   glds(s_whT, d * G, [&](int j) { const int q = j / fd; return A.hp + (j - q * d) * G + q; });
   glds(s_bh, d, [&](int j) { return A.hp + d * G + j; });
   glds(s_wv, d, [&](int j) { return A.w + j; });
   glds(s_ph, nb * d, [&](int j) { return A.phi + (size_t)b0 * d + j; });
+  tsf_stage_flows<NP>(s_fa, gfl, K, n_s);
+  // the flow rows' initial states (plain loads, in flight with the staging)
+  const bool s1row = tid >= PB;
+  const int b = b0 + (s1row ? tid - PB : tid);
+  const bool valid = tid < RPW && b < B;
+  const int row = s1row ? B + b : b;
+  tsf_f2 z[NP / 2];
+  if (tid < RPW) {
+    const float* src = (s1row ? A.S1 : A.S) + (size_t)(valid ? b : 0) * n_s;
+#pragma unroll
+    for (int p = 0; p < NP / 2; ++p)
+      z[p] = (tsf_f2){valid && 2 * p < n_s ? src[2 * p] : 0.f, valid && 2 * p + 1 < n_s ? src[2 * p + 1] : 0.f};
+  }
   __syncthreads();
-  {  // this workgroup's slice of the pre-step snapshot of g_i, h, w_i (read by k_tsf_bwd)
+  if (tid < RPW) {
+    // planar flows, one lane per row: lanes 0..PB-1 the s rows of batch indices b0.., PB.. the s1 rows
+    // rows past the batch write their (unused) flow states to a scratch row, so the loop body is
+    // one basic block: its LDS reads for step k + 1 issue at the top and are waited for only at
+    // the bottom, after step k's arithmetic
+    float* zrow = valid ? A.zs + (size_t)row * NP : A.scratch + tid * TSF_NS;
+    float* trow = valid ? A.ts + row : A.scratch + tid * TSF_NS + NP;
+    const size_t zstep = valid ? (size_t)R2 * NP : 0, tstep = valid ? (size_t)R2 : 0;
+    PROBE_AT(1);
+    TsfFlow<NP> F, Fn;
+    if (K > 0) tsf_flow_ld<NP>(F, s_fa);
+    for (int k = 0; k < K; ++k) {
+      tsf_flow_ld<NP>(Fn, s_fa + min(k + 1, K - 1) * FA);  // next flow, off the chain
+      const float t = tsf_tanh(__fadd_rn(tsf_dot<NP>(z, F.w), F.b));
+      tsf_store<NP>(zrow, z);
+      *trow = t;
+      zrow += zstep;
+      trow += tstep;
+      tsf_axpy<NP>(z, t, F.u);
+      F = Fn;
+    }
+    tsf_store<NP>(zrow, z);
+#pragma unroll
+    for (int p = 0; p < NP / 2; ++p) {
+      s_z[tid * TSF_NS + 2 * p] = z[p].x;
+      s_z[tid * TSF_NS + 2 * p + 1] = z[p].y;
+    }
+  } else if (tid >= 64) {
+    // waves 1-3, beside the flow rows: this workgroup's slice of the pre-step snapshot of g_i,
+    // h, w_i (read by k_tsf_bwd)
     const int S = A.Pg + A.Ph + d, per = (S + gridDim.x - 1) / gridDim.x;
     const int lo = blockIdx.x * per, hi = min(S, lo + per);
-    for (int j = lo + tid; j < hi; j += 256) {
+    for (int j = lo + tid - 64; j < hi; j += 192) {
       float v;
       if (j < A.Pg) {
         v = s_fl[j];
@@ -218,35 +340,6 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A) {
       A.snap[j] = v;
     }
   }
-  // planar flows: lane li carries z[li]; w_k·z by a butterfly over the row's LPR lanes
-  const int lc = li < n_s ? li : 0;  // lanes past n_s carry z = 0 and weight 0
-  const float lm = li < n_s ? 1.f : 0.f;
-  float fw = K > 0 ? __fmul_rn(lm, s_fl[lc]) : 0.f, fb = K > 0 ? s_fl[n_s] : 0.f;
-  float fu = K > 0 ? __fmul_rn(lm, s_fl[n_s + 1 + lc]) : 0.f;
-  float* zp = A.zs + (size_t)row * n_s + lc;
-  float* tp = A.ts + row;
-  PROBE_AT(1);
-  // z·w_k is formed one step ahead, so z's load is waited for before the loop and the loop body
-  // holds no wait on global memory (its stores stay in flight)
-  float zw = __fmul_rn(z, fw);
-  const bool zok = valid && li < n_s, tok = valid && li == 0;
-  for (int k = 0; k < K; ++k) {
-    const float b_k = fb, u_k = fu;
-    if (k + 1 < K) {  // next flow's parameters, off the chain
-      const float* f = s_fl + (k + 1) * fs;
-      fw = __fmul_rn(lm, f[lc]);
-      fb = f[n_s];
-      fu = __fmul_rn(lm, f[n_s + 1 + lc]);
-    }
-    const float p = tsf_row_sum<LPR>(zw);
-    const float t = tsf_tanh(__fadd_rn(p, b_k));
-    *(zok ? zp + (size_t)k * R2 * n_s : A.trash) = z;  // lanes with nothing to save write the trash word
-    *(tok ? tp + (size_t)k * R2 : A.trash) = t;
-    z = __fadd_rn(z, __fmul_rn(u_k, t));
-    zw = __fmul_rn(z, fw);
-  }
-  if (valid && li < n_s) A.zs[((size_t)K * R2 + row) * n_s + li] = z;
-  s_z[rl * TSF_NS + li] = z;
   __syncthreads();
   PROBE_AT(2);
   // Linear(n_s, G) of g for this workgroup's rows
@@ -277,37 +370,40 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A) {
   PROBE_REC(10, t0_);
 }
 
-// flow-row role: rows [f FR, (f+1) FR) of the 2B rows; waves 0-1 run the reverse flow chains
-template <int LPR>
-__device__ void tsf_bwd_flows(const TsfArgs& A, float* sm, float* s_dr, float* s_w, float* s_r, int* s_ab, int f) {
-  constexpr int FR = tsf_fr(LPR);
+// flow-row role: rows [f FR, (f+1) FR) of the 2B rows; lanes 0..FR-1 of wave 0 run the reverse
+// flow chains (one row each).  sfl = A.snap (the pre-step g_i first).
+template <int NP>
+__device__ void tsf_bwd_flows(const TsfArgs& A, const float* __restrict__ sfl, float* sm, float* s_dr, float* s_w,
+                              float* s_r, int* s_ab, int f) {
+  constexpr int FR = TSF_FR, PST = tsf_pst(NP);
   const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
   const int fs = tsf_flow_stride(n_s), nfl = K * fs, nlin = G * n_s + G;
-  float* s_z = sm;                                  // [K+1][FR][n_s]
+  float* s_z = sm;                                  // [K+1][FR][NP] (16-byte rows)
   float* s_t = sm + TSF_ZS;                         // [K][FR]
-  float* s_fl = s_t + TSF_TS;                       // flows + Linear of g (pre-step)
+  float* s_fl = s_t + TSF_TS;                       // Linear of g (pre-step)
   float* s_wh = s_fl + TSF_LDS / 2;                 // W_h (pre-step)
   float* s_dg = s_wh + TSF_LDS;                     // [FR][G] (φ̃ rows while staging)
   float* s_da = s_dg + 2048;                        // [FR][d]
-  float* s_gc = s_da + 2048;                        // [FR][d] ψ output gradient rows
-  const float* snap = A.snap;
+  float* s_gc = s_da + 2048;                        // [FR][d] ψ output gradient rows, then dz_K [FR][NP]
+  float* s_fa = s_gc + 2048;                        // [K][tsf_fst(NP)] flows, chain layout
+  constexpr int FA = tsf_fst(NP);
   PROBE_T(t0_);
   const int r0 = f * FR;
   const int nr = min(FR, R2 - r0);
   // stage everything up front (LDS-DMA, all in flight together)
-  const int zr = FR * n_s;
-  const FDiv fzr = fdiv(zr);
-  const int nzv = nr * n_s;
+  constexpr int zr = FR * NP;
+  const int nzv = nr * NP;
   glds(s_z, (K + 1) * zr, [&](int j) {
-    const int k = j / fzr, e = j - k * zr;
-    return A.zs + ((size_t)k * R2 + r0) * n_s + (e < nzv ? e : 0);  // rows past 2B: finite copies, zero dg
+    const int k = j / zr, e = j - k * zr;
+    return A.zs + ((size_t)k * R2 + r0) * NP + (e < nzv ? e : 0);  // rows past 2B: finite copies, zero dg
   });
   glds(s_t, K * FR, [&](int j) {
     const int k = j / FR, e = j - k * FR;
     return A.ts + (size_t)k * R2 + r0 + (e < nr ? e : 0);
   });
-  glds(s_fl, nfl + nlin, [&](int j) { return snap + j; });
-  glds(s_wh, d * G, [&](int j) { return snap + A.Pg + j; });
+  glds(s_fl, nlin, [&](int j) { return sfl + nfl + j; });
+  glds(s_wh, d * G, [&](int j) { return sfl + A.Pg + j; });
+  tsf_stage_flows<NP>(s_fa, sfl, K, n_s);
   (void)tsf_stage_daff(A, nr, [&](int rl) { const int row = r0 + rl; return row < B ? row : row - B; }, s_dg, s_da,
                        s_gc, s_dr, s_w, s_r, s_ab);
   PROBE_AT(1);
@@ -321,56 +417,77 @@ __device__ void tsf_bwd_flows(const TsfArgs& A, float* sm, float* s_dr, float* s
     s_dg[j] = acc;
   }
   __syncthreads();
+  // dz_K = dg W_lin (zero past n_s), one thread per (row, component)
+  float* s_dz = s_gc;
+  if (tid < FR * NP) {
+    const int rl = tid / NP, i = tid - rl * NP;
+    float dz = 0.f;
+    if (i < n_s)
+      for (int q = 0; q < G; ++q) dz = __builtin_fmaf(s_dg[rl * G + q], s_fl[q * n_s + i], dz);
+    s_dz[tid] = dz;
+  }
+  __syncthreads();
   PROBE_AT(2);
-  if (tid >= 128) return;
-  const int rl = tid / LPR, li = tid - rl * LPR;
-  const float* Wl = s_fl + nfl;
-  float dz = 0.f;
-  if (li < n_s)
-    for (int q = 0; q < G; ++q) dz = __builtin_fmaf(s_dg[rl * G + q], Wl[q * n_s + li], dz);
-  // reverse chain; each row stores its own parameter-gradient terms (summed in k_tsf_flow).  The
-  // next step's operands are read from LDS one step ahead, off the chain.
-  const int row = r0 + rl;
+  if (tid >= FR) return;
+  // reverse chain of row r0 + tid; each row stores its own parameter-gradient terms (summed in
+  // k_tsf_flow).  The next step's operands (flow parameters, z_k, t_k) are read one step ahead.
+  const int rl = tid, row = r0 + rl;
   const bool valid = row < R2;
-  const int lc = li < n_s ? li : 0;
-  const float lm = li < n_s ? 1.f : 0.f;
-  float* pr = A.part + (size_t)row * fs;
-  auto ld = [&](int k, float& t, float& zk, float& uk, float& wk) {
-    const float* fp = s_fl + k * fs;
+  tsf_f2 dz[NP / 2];
+#pragma unroll
+  for (int p = 0; p < NP / 2; ++p) dz[p] = (tsf_f2){s_dz[rl * NP + 2 * p], s_dz[rl * NP + 2 * p + 1]};
+  float* pr = A.part + (size_t)row * PST;
+  auto ldz = [&](int k, tsf_f2 (&zk)[NP / 2], float& t) {
+    const float* zp = s_z + (k * FR + rl) * NP;
+#pragma unroll
+    for (int q = 0; q < NP / 4; ++q) {
+      const tsf_f4 v = *(const tsf_f4*)(zp + 4 * q);
+      zk[2 * q] = (tsf_f2){v.x, v.y};
+      zk[2 * q + 1] = (tsf_f2){v.z, v.w};
+    }
     t = s_t[k * FR + rl];
-    zk = __fmul_rn(lm, s_z[(k * FR + rl) * n_s + lc]);
-    uk = __fmul_rn(lm, fp[n_s + 1 + lc]);
-    wk = __fmul_rn(lm, fp[lc]);
   };
   PROBE_AT(3);
-  const bool zok = valid && li < n_s, bok = valid && li == 0;
-  float nt = 0.f, nz = 0.f, nu = 0.f, nw = 0.f;
-  if (K > 0) ld(K - 1, nt, nz, nu, nw);
+  TsfFlow<NP> F, Fn;
+  tsf_f2 zk[NP / 2], zn[NP / 2];
+  float t = 0.f, tn = 0.f;
+  if (K > 0) {
+    tsf_flow_ld<NP>(F, s_fa + (K - 1) * FA);
+    ldz(K - 1, zk, t);
+  }
+  // rows past 2B write to a scratch row (one basic block per step, as in k_tsf_fwd)
+  float* pk = valid ? pr + (size_t)(K - 1) * R2 * PST : A.scratch + tid * TSF_NS;
+  const size_t pstep = valid ? (size_t)R2 * PST : 0;
   for (int k = K - 1; k >= 0; --k) {
-    const float t = nt, zk = nz, uk = nu, wk = nw;
-    if (k > 0) ld(k - 1, nt, nz, nu, nw);
-    const float su = tsf_row_sum<LPR>(__fmul_rn(dz, uk));
+    const int kn = max(k - 1, 0);
+    tsf_flow_ld<NP>(Fn, s_fa + kn * FA);
+    ldz(kn, zn, tn);
+    const float su = tsf_dot<NP>(dz, F.u);
     const float da = __fmul_rn(su, __fsub_rn(1.f, __fmul_rn(t, t)));
-    float* pk = pr + (size_t)k * R2 * fs;
-    *(zok ? pk + li : A.trash) = __fmul_rn(da, zk);
-    *(zok ? pk + n_s + 1 + li : A.trash) = __fmul_rn(dz, t);
-    *(bok ? pk + n_s : A.trash) = da;
-    dz = __fadd_rn(dz, __fmul_rn(da, wk));
+    tsf_store_scaled<NP>(pk, zk, da);
+    tsf_store_scaled<NP>(pk + NP, dz, t);
+    *(tsf_f4*)(pk + 2 * NP) = (tsf_f4){da, 0.f, 0.f, 0.f};
+    pk -= pstep;
+    tsf_axpy<NP>(dz, da, F.w);
+    F = Fn;
+#pragma unroll
+    for (int p = 0; p < NP / 2; ++p) zk[p] = zn[p];
+    t = tn;
   }
   PROBE_REC(11, t0_);
 }
 
 // grid nflow + nh + nlin + 1, 256 threads (roles: see the header comment)
-template <int LPR>
-__global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A) {
-  __shared__ float sm[TSF_SM];
+template <int NP>
+__global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A, const float* __restrict__ sfl) {
+  __shared__ __attribute__((aligned(16))) float sm[TSF_SM];
   __shared__ float s_dr[64], s_r[64], s_w[256], s_red[256];
   __shared__ int s_ab[64];
   const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
   const int fs = tsf_flow_stride(n_s), nfl = K * fs;
   int role = blockIdx.x;
   if (role < A.nflow) {
-    tsf_bwd_flows<LPR>(A, sm, s_dr, s_w, s_r, s_ab, role);
+    tsf_bwd_flows<NP>(A, sfl, sm, s_dr, s_w, s_r, s_ab, role);
     return;
   }
   role -= A.nflow;
@@ -387,7 +504,7 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A) {
   const bool wrole = role == A.nh + A.nlin;
   float* s_gf = sm + TSF_LDS / 2;       // h role: [2B][G]
   float* s_whs = sm + TSF_LDS / 2;      // g-Linear role: [d][TSF_QS] pre-step W_h columns
-  float* s_zk = s_whs + TSF_LDS / 2;    // g-Linear role: [2B][n_s] z_K (<= 4096)
+  float* s_zk = s_whs + TSF_LDS / 2;    // g-Linear role: [2B][NP] z_K (<= 4096)
   float* s_dg = sm + 5 * (TSF_LDS / 2); // g-Linear role: [B][TSF_QS] (after the φ̃ / gradient rows)
   const int q0 = (role - A.nh) * TSF_QS, nq = min(TSF_QS, G - q0);
   if (!wrole && role < A.nh) {
@@ -397,7 +514,7 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A) {
       const int c = j / TSF_QS, qq = j - c * TSF_QS;
       return snap + A.Pg + c * G + q0 + (qq < nq ? qq : 0);  // columns past G: zeroed below
     });
-    glds(s_zk, R2 * n_s, [&](int j) { return A.zs + (size_t)K * R2 * n_s + j; });
+    glds(s_zk, R2 * NP, [&](int j) { return A.zs + (size_t)K * R2 * NP + j; });
   }
   const float se = tsf_stage_daff(A, B, [](int rl) { return rl; }, s_tp, s_da, s_gc, s_dr, s_w, s_r, s_ab);
   PROBE_AT(1);
@@ -458,8 +575,8 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A) {
     if (i < n_s) {  // dW = dgᵀ z_K(s) + dgᵀ z_K(s1)
       float g0 = 0.f, g1 = 0.f;
       for (int b = 0; b < B; ++b) {
-        g0 = __builtin_fmaf(s_dg[b * TSF_QS + qq], s_zk[b * n_s + i], g0);
-        g1 = __builtin_fmaf(s_dg[b * TSF_QS + qq], s_zk[(B + b) * n_s + i], g1);
+        g0 = __builtin_fmaf(s_dg[b * TSF_QS + qq], s_zk[b * NP + i], g0);
+        g1 = __builtin_fmaf(s_dg[b * TSF_QS + qq], s_zk[(B + b) * NP + i], g1);
       }
       g = __fadd_rn(g0, g1);
       o = nfl + (q0 + qq) * n_s + i;
@@ -478,14 +595,16 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A) {
 // g_backward calls of the reference), then Adam.  grid cdiv(K (2 n_s + 1), 256).  All 2B loads
 // of a thread are issued before the first add.
 __global__ __launch_bounds__(256) void k_tsf_flow(TsfArgs A) {
-  const int fs = tsf_flow_stride(A.n_s), nfl = A.K * fs, B = A.B, R2 = 2 * B;
+  const int n_s = A.n_s, fs = tsf_flow_stride(n_s), nfl = A.K * fs, B = A.B, R2 = 2 * B, NP = A.np;
+  const int PST = tsf_pst(NP);
   PROBE_T(t0_);
   const int j0 = blockIdx.x * 256 + threadIdx.x, j = j0 < nfl ? j0 : nfl - 1;
   const int k = j / fs, e = j - k * fs;
-  const float* pk = A.part + (size_t)k * R2 * fs + e;
+  const int off = e < n_s ? e : (e == n_s ? 2 * NP : NP + e - n_s - 1);  // w_i | b | u_i terms
+  const float* pk = A.part + (size_t)k * R2 * PST + off;
   float v[128];
 #pragma unroll
-  for (int r = 0; r < 128; ++r) v[r] = r < R2 ? pk[(size_t)r * fs] : 0.f;
+  for (int r = 0; r < 128; ++r) v[r] = r < R2 ? pk[(size_t)r * PST] : 0.f;
   float g0 = 0.f, g1 = 0.f;
 #pragma unroll
   for (int r = 0; r < 128; ++r) {
