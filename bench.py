@@ -270,6 +270,7 @@ def bench_sharded(args, world, rank, device, barrier, dist, steps=None, warmup=N
     else:
         init_comm(eng, rank, world)
     loop = NativeEnvLoop(eng, batch=B, seed=1, schedule="sharded")
+    loop.set_wait_timeout(30.0)  # a collective that never completes: abort + error, not a hang
     loop.prefill(1000)
     loop.set_task(0)
     loop.warm()
@@ -285,6 +286,8 @@ def bench_sharded(args, world, rank, device, barrier, dist, steps=None, warmup=N
         dt = float(t.item())
     st = loop.stats()
     st.update(eng.step_stats())
+    eng_comm = eng.comm_state()
+    eng_comm["rccl_forced_world1"] = os.environ.get("SFX_RCCL_WORLD1") == "1"
     loop.close()
     eng.close()
     v = steps / dt
@@ -292,6 +295,7 @@ def bench_sharded(args, world, rank, device, barrier, dist, steps=None, warmup=N
             "steps": steps, "warmup": warmup, "heads_total": Tg, "heads_per_gpu": T_loc,
             "head_updates_per_s": round(v * Tg, 1), "parallelism": f"heads sharded over {world} GPU(s)",
             "loop": "native C++ runner (sfx_runner schedule sharded): one pre-launched graph per env step",
+            "comm": eng_comm,
             "collective": ("gloo via host (rehearsal)" if args.via_host else "RCCL (library-owned communicator)") +
                           " all-reduce(MAX): GPI maxima [T_glob,B,A] per speculative round, then verification "
                           "maxima ++ the env action's q table [T_glob,A] in one call",
@@ -564,7 +568,7 @@ def main():
             n_, us_, by_ = stats[kd]
             stats[kd] = (n_, us_, max(0.0, by_ - nsk * per))
 
-    sharded = replicas = None
+    sharded = replicas = sharded_rccl1 = None
     layout = "single" if world == 1 else f"replica{world}"
     if world > 1 and args.schedule == "all" and args.tsf_K is None and args.layout == "sharded":
         # the headline at N > 1 is config C4's layout, timed with the same W / K; the replicas just
@@ -585,6 +589,17 @@ def main():
         # rates compare like for like (the all-task rate rises as more speculative rounds skip)
         sharded = bench_sharded(args, world, rank, device, barrier, dist, steps=max(args.steps, args.shard_steps),
                                 warmup=args.warmup)
+        if world == 1 and not args.via_host:
+            # the per-step cost the N > 1 headline pays: the same stream with real (captured)
+            # ncclAllReduce calls at one rank, pipelined through the host rounds' split communicator
+            os.environ["SFX_RCCL_WORLD1"] = "1"
+            try:
+                sharded_rccl1 = bench_sharded(args, world, rank, device, barrier, dist,
+                                              steps=max(args.steps, args.shard_steps), warmup=args.warmup)
+            except Exception as e:  # an error return (a bounded collective), not a hang
+                sharded_rccl1 = {"error": repr(e)[:400]}
+            finally:
+                os.environ.pop("SFX_RCCL_WORLD1", None)
     elif args.shard_steps > 0 and args.schedule == "tsf":
         sharded = bench_sharded_tsf(args, world, rank, device, barrier, dist)
 
@@ -686,6 +701,7 @@ def main():
             "repeats": {"values": repeats, "steps_each": args.steps} if repeats else None,
             "speculation": spec_stats,
             "sharded": sharded,
+            "sharded_rccl_world1": sharded_rccl1,
             "replicas": replicas,
             "other_workloads": other,
             "cpu_baseline": cpu,

@@ -14,6 +14,7 @@
 // arguments, including the slot mask) and replayed afterwards; SFX_GRAPHS=0 disables graphs.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <cmath>
@@ -37,6 +38,50 @@
 using namespace sfx;
 
 static thread_local std::string g_err;
+
+// RCCL is resolved at run time (dlopen), on the first communicator call: libsfx.so loads -- and
+// runs every single-rank path -- on a host without RCCL; only the sharded collectives need it.
+struct RcclApi {
+  bool ok = false;
+  std::string why;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;
+  ncclResult_t (*CommSplit)(ncclComm_t, int, int, ncclComm_t*, ncclConfig_t*) = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+static const RcclApi& rccl() {
+  static const RcclApi api = [] {
+    RcclApi a;
+    void* lib = nullptr;
+    for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1", "/opt/rocm/lib/librccl.so"})
+      if ((lib = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+    if (!lib) {
+      a.why = "RCCL not found (dlopen librccl.so.1)";
+      return a;
+    }
+    bool all = true;
+    auto sym = [&](auto& f, const char* n) {
+      f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(lib, n));
+      all = all && f != nullptr;
+    };
+    sym(a.GetUniqueId, "ncclGetUniqueId");
+    sym(a.CommInitRank, "ncclCommInitRank");
+    sym(a.AllReduce, "ncclAllReduce");
+    sym(a.CommDestroy, "ncclCommDestroy");
+    sym(a.CommAbort, "ncclCommAbort");
+    sym(a.CommGetAsyncError, "ncclCommGetAsyncError");
+    sym(a.CommSplit, "ncclCommSplit");
+    sym(a.GetErrorString, "ncclGetErrorString");
+    a.ok = all;
+    if (!all) a.why = "RCCL lacks a needed entry point";
+    return a;
+  }();
+  return api;
+}
 
 #define SFX_FAIL(code, msg) \
   do {                      \
@@ -146,6 +191,14 @@ struct sfx_handle {
   int comm_rank = 0, comm_world = 0;  // world 0: no communicator
   ncclComm_t comm = nullptr;
   bool comm_owned = false;
+  // host rounds' own communicator (ncclCommSplit of comm, always owned): the collectives of a
+  // step's host rounds (side stream) and of the pre-launched next step (step stream) never share
+  // a communicator, so the runner pre-launches at N > 1 too
+  ncclComm_t comm_rounds = nullptr;
+  bool rounds_comm = false;  // coll_max uses comm_rounds (set while the runner runs host rounds)
+  bool comm_dead = false;    // aborted after a collective timed out (sfx_runner_wait_timeout)
+  std::string comm_err;
+  long long* dstall = nullptr;  // test hook (sfx_debug_stall): one-shot stall of the sharded finish
   bool comm_force = false;  // SFX_RCCL_WORLD1=1: call RCCL even with one rank (tests)
   int (*host_ar)(void*, int32_t*, int) = nullptr;  // host transport: (ctx, host buffer, count)
   void* host_ar_ctx = nullptr;
@@ -766,7 +819,9 @@ void free_all(sfx_handle* h) {
   if (h->host_ar_buf) (void)hipHostFree(h->host_ar_buf);
   for (int* p : {h->xb[0], h->xb[1]})  // xge lives in xb[0]'s block
     if (p) (void)hipFree(p);
-  if (h->comm && h->comm_owned) (void)ncclCommDestroy(h->comm);
+  if (h->comm_rounds) (void)rccl().CommDestroy(h->comm_rounds);
+  if (h->comm && h->comm_owned) (void)rccl().CommDestroy(h->comm);
+  if (h->dstall) (void)hipFree(h->dstall);
   if (h->cap) (void)hipStreamDestroy(h->cap);
 }
 

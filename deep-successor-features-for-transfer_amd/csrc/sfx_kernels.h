@@ -2729,6 +2729,7 @@ struct SfinArgs {
   const long long* dctr;
   const int* cancel;
   const int* nonfin;      // Geo::nonfin
+  long long* stall;       // test hook (sfx_debug_stall): one-shot delay before the publication
 };
 
 // One workgroup: verification of the speculated next actions (k_sverify), the env action, and
@@ -2766,6 +2767,14 @@ __global__ __launch_bounds__(256) void k_sfinish(SfinArgs F) {
     *F.flag = s_min;
     F.sel[0] = c;
     F.sel[1] = a;
+    if (F.stall) {  // bounded by the host's value (<= 60 s), consumed once
+      const long long n = *F.stall;
+      if (n > 0) {
+        *F.stall = 0;
+        const long long t0 = wall_clock64();
+        while (wall_clock64() - t0 < n) __builtin_amdgcn_s_sleep(127);
+      }
+    }
     if (F.pub) {
       const long long seq = *F.dctr;
       HostResult* pub = F.pub + (seq & (RES_RING - 1));  // the step's slot of the result ring

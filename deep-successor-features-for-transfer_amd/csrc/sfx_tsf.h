@@ -23,30 +23,32 @@
 //                     g-Linear   TSF_QS output columns of g_i's Linear each: dg, gradient + Adam
 //                     w          l2, the w_i gradient + Adam, the loss row
 //   k_tsf_flow      flow parameters: sum of the per-row terms (fixed order) + Adam (K > 0).
-// Limits (checked by sfx_tsf_setup): n_s <= 32, B <= 64, d <= 128, d*G <= 8192, 2B*G <= 8192,
-// B*d <= 4096, K(2 n_s + 1) + G(n_s + 1) <= 4096, 2 TSF_PB G <= 4096, and the flow-row staging
-// TSF_FR (K+1) NP <= TSF_ZS, TSF_FR K <= TSF_TS, TSF_FR G <= 2048, TSF_FR d <= 2048.
+// Limits (checked by sfx_tsf_setup): n_s <= 32, B <= 64, d <= 128, G <= 256, d*G4 <= 8192 (G4: G
+// rounded up to 4), 2B*G <= 8192, B*d <= 4096, K(2 n_s + 1) + G(n_s + 1) <= 4096, G*NP <= 4096,
+// K tsf_fst(NP) <= TSF_FA, and the flow-row staging TSF_FR K <= TSF_TS, TSF_FR G <= 2048,
+// TSF_FR d <= 2048.
 #pragma once
 
 namespace sfx {
 
 constexpr int TSF_NS = 32;     // max n_s
 constexpr int TSF_LDS = 8192;  // floats per staged operand (flows, W_h, g features)
-constexpr int TSF_ZS = 12288;  // flow states staged per flow-row workgroup: TSF_FR x (K+1) x NP
 constexpr int TSF_TS = 1024;   // tanh outputs staged per flow-row workgroup: TSF_FR x K
 constexpr int TSF_QS = 16;     // g-Linear output columns per backward workgroup
 constexpr int TSF_PB = 8;      // forward: batch indices per workgroup (2 TSF_PB flow rows)
 constexpr int TSF_FR = 8;      // backward: flow rows per flow-row workgroup
 constexpr int TSF_SCR = 64 * TSF_NS;  // TsfArgs::scratch floats (one row per chain lane)
 constexpr int TSF_FA = 8192;   // flows staged in the chain layout: K x tsf_fst(NP)
-constexpr int TSF_SM = TSF_ZS + TSF_TS + TSF_LDS / 2 + TSF_LDS + 3 * 2048 + TSF_FA;  // k_tsf_bwd LDS (floats)
+constexpr int TSF_SM = TSF_TS + TSF_LDS / 2 + TSF_LDS + 3 * 2048 + TSF_FA;  // k_tsf_bwd LDS (floats)
 
 // NP: n_s rounded up to 4 -- the register width of a flow row and the row stride of the saved
 // flow states (zs [K+1][2B][NP], 16-byte rows); the per-row gradient terms `part` are
-// [K][2B][tsf_pst(NP)]: da·z_k at [0, NP), dz·t at [NP, 2NP), da at 2NP.
+// [K][2B][tsf_pst(NP)]: dz_{k+1} (the gradient reaching z_{k+1}) at [0, NP), da_k at NP --
+// k_tsf_flow forms the w / u terms da_k z_k and dz_{k+1} t_k from them and the saved states.
 __host__ __device__ constexpr int tsf_np(int n_s) { return (n_s + 3) & ~3; }
-__host__ __device__ constexpr int tsf_pst(int np) { return 2 * np + 4; }
-// a flow in the chain layout (LDS): w at [0, NP), u at [NP, 2NP), b at 2NP, zeros elsewhere
+__host__ __device__ constexpr int tsf_pst(int np) { return np + 4; }
+// a flow in the chain layout (LDS): w at [0, NP), u at [NP, 2NP), b at 2NP, c at 2NP + 1, zeros
+// elsewhere
 __host__ __device__ constexpr int tsf_fst(int np) { return 2 * np + 4; }
 
 struct TsfArgs {
@@ -69,7 +71,8 @@ struct TsfArgs {
   float* ts;     // [K][2B] tanh outputs
   float* gfeat;  // [2B][G]
   float* tphi;   // [B][d]
-  float* part;   // [K][2B][tsf_pst(NP)] per-row flow-parameter gradient terms
+  float* part;   // [K][2B][tsf_pst(NP)] per-row flow gradients (dz_{k+1}, da_k)
+  float* cst;    // [K] c_k = w_{k+1}·u_k of the pre-step flows (written by k_tsf_fwd)
   float* scratch;  // [TSF_SCR]: stores of flow-chain lanes past the batch (never read)
   float* snap;   // [Pg + Ph + d]: g_i, h, w_i before this step (written by k_tsf_fwd)
   float* losses; // [3]: [1] = l1 (written by the ψ tail); [0], [2] written here
@@ -80,6 +83,7 @@ struct TsfArgs {
   float* wm;
   float* wv;
   AdamHP hpw, hpg, hph;
+  AdamHP hpf;  // the planar flows' Adam (hpg, or lr = 0 when frozen: sfx_tsf_freeze_flows)
 };
 
 __device__ __forceinline__ int tsf_flow_stride(int n_s) { return 2 * n_s + 1; }
@@ -102,11 +106,12 @@ __device__ __forceinline__ float tsf_tanh(float x) {
 typedef float tsf_f2 __attribute__((ext_vector_type(2)));
 typedef float tsf_f4 __attribute__((ext_vector_type(4)));
 
-// One planar flow's parameters (chain layout, see tsf_fst), read from LDS: every lane of the
-// wave reads the same words (broadcast), 16 bytes at a time.
+// One planar flow's parameters in the chain layout (tsf_fst): w, u, b and the look-ahead
+// coefficient c_k = w_{k+1}·u_k, read from LDS (every lane of the wave reads the same words:
+// broadcast, 16 bytes at a time).
 template <int NP>
 struct TsfFlow {
-  float w[NP], u[NP], b;
+  float w[NP], u[NP], b, c;
 };
 
 template <int NP>
@@ -117,7 +122,9 @@ __device__ __forceinline__ void tsf_flow_ld(TsfFlow<NP>& F, const float* f) {
     F.w[4 * q] = w4.x; F.w[4 * q + 1] = w4.y; F.w[4 * q + 2] = w4.z; F.w[4 * q + 3] = w4.w;
     F.u[4 * q] = u4.x; F.u[4 * q + 1] = u4.y; F.u[4 * q + 2] = u4.z; F.u[4 * q + 3] = u4.w;
   }
-  F.b = f[2 * NP];
+  const tsf_f4 bc = *(const tsf_f4*)(f + 2 * NP);
+  F.b = bc.x;
+  F.c = bc.y;
 }
 
 // x·y over NP components: NP/2 packed FMAs in (up to) three independent chains, then the three
@@ -146,53 +153,55 @@ __device__ __forceinline__ void tsf_axpy(tsf_f2 (&x)[NP / 2], float s, const flo
   for (int p = 0; p < NP / 2; ++p) x[p] = __builtin_elementwise_fma((tsf_f2){y[2 * p], y[2 * p + 1]}, ss, x[p]);
 }
 
-// dst[0, NP) = s·x (16-byte stores)
+// dst[0, NP) = x (16-byte stores)
 template <int NP>
-__device__ __forceinline__ void tsf_store_scaled(float* dst, const tsf_f2 (&x)[NP / 2], float s) {
-  const tsf_f2 ss = {s, s};
+__device__ __forceinline__ void tsf_store(float* dst, const tsf_f2 (&x)[NP / 2]) {
 #pragma unroll
-  for (int q = 0; q < NP / 4; ++q) {
-    const tsf_f2 lo = x[2 * q] * ss, hi = x[2 * q + 1] * ss;
-    *(tsf_f4*)(dst + 4 * q) = (tsf_f4){lo.x, lo.y, hi.x, hi.y};
-  }
+  for (int q = 0; q < NP / 4; ++q) *(tsf_f4*)(dst + 4 * q) = (tsf_f4){x[2 * q].x, x[2 * q].y, x[2 * q + 1].x, x[2 * q + 1].y};
+}
+
+// a·b over n4 16-byte groups of two LDS rows, four independent lanes of accumulation
+__device__ __forceinline__ float tsf_dot4(const float* a, const float* b, int n4) {
+  tsf_f4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int q = 0; q < n4; ++q) acc = __builtin_elementwise_fma(*(const tsf_f4*)(a + 4 * q), *(const tsf_f4*)(b + 4 * q), acc);
+  return __fadd_rn(__fadd_rn(acc.x, acc.y), __fadd_rn(acc.z, acc.w));
 }
 
 typedef __attribute__((address_space(3))) void* tsf_lds_t;
 
 // LDS-DMA staging: dst[j] = *src(j) for j < n (global_load_lds_dword; wave-uniform LDS base +
-// lane * 4, per-lane global address, no VGPR destination).  Nothing waits here: the loads of
-// every staging call stay in flight together until the caller's next __syncthreads().
+// lane * 4, per-lane global address, no VGPR destination), by waves [w0, w0 + nw) of the
+// workgroup; src(j) == nullptr marks a padding word, zeroed by a plain LDS store instead.
+// Nothing waits here: the loads of every staging call stay in flight together until the
+// caller's next __syncthreads().
 template <class F>
-__device__ __forceinline__ void glds(float* dst, int n, F src) {
-  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  for (int c = threadIdx.x >> 6; c * 64 < n; c += nw) {
+__device__ __forceinline__ void glds(float* dst, int n, F src, int w0 = 0, int nw = 4) {
+  const int lane = threadIdx.x & 63, wv = (threadIdx.x >> 6) - w0;
+  if (wv < 0 || wv >= nw) return;
+  for (int c = wv; c * 64 < n; c += nw) {
     const int j = c * 64 + lane;
-    if (j < n) __builtin_amdgcn_global_load_lds((const void*)src(j), (tsf_lds_t)(dst + c * 64), 4, 0, 0);
+    const float* p = j < n ? src(j) : nullptr;
+    if (p)
+      __builtin_amdgcn_global_load_lds((const void*)p, (tsf_lds_t)(dst + c * 64), 4, 0, 0);
+    else if (j < n)
+      dst[j] = 0.f;
   }
 }
 
 // The K flows of g (packed: flow k at k(2 n_s + 1): w[n_s], b, u[n_s]) -> LDS in the chain layout
-// (tsf_fst); the padding words are zeroed by plain LDS stores (disjoint from the DMA'd words).
-// Complete at the caller's next __syncthreads().
+// (tsf_fst): w at [0, NP), u at [NP, 2NP), b at 2NP, c (filled by the caller) at 2NP + 1, zeros
+// elsewhere.  Completes at the caller's next __syncthreads().
 template <int NP>
 __device__ __forceinline__ void tsf_stage_flows(float* dst, const float* src, int K, int n_s) {
   constexpr int FA = tsf_fst(NP);
-  const int fs = tsf_flow_stride(n_s), n = K * FA;
-  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  for (int c = threadIdx.x >> 6; c * 64 < n; c += nw) {
-    const int j = c * 64 + lane, k = j / FA, e = j - k * FA;
-    int o = -1;
-    if (e < NP)
-      o = e < n_s ? e : -1;
-    else if (e < 2 * NP)
-      o = e - NP < n_s ? n_s + 1 + (e - NP) : -1;
-    else if (e == 2 * NP)
-      o = n_s;
-    if (j < n && o >= 0)
-      __builtin_amdgcn_global_load_lds((const void*)(src + k * fs + o), (tsf_lds_t)(dst + c * 64), 4, 0, 0);
-    else if (j < n)
-      dst[j] = 0.f;
-  }
+  const int fs = tsf_flow_stride(n_s);
+  glds(dst, K * FA, [&](int j) -> const float* {
+    const int k = j / FA, e = j - k * FA;
+    const float* f = src + k * fs;
+    if (e < NP) return e < n_s ? f + e : nullptr;
+    if (e < 2 * NP) return e - NP < n_s ? f + n_s + 1 + (e - NP) : nullptr;
+    return e == 2 * NP ? f + n_s : nullptr;
+  });
 }
 
 // Rows [0, n) of the minibatch (row rl is batch index bmap(rl)), staged for the backward roles:
@@ -247,40 +256,30 @@ __device__ float tsf_stage_daff(const TsfArgs& A, int n, BMap bmap, float* s_tp,
   return se;
 }
 
-// dst[0, NP) = x (16-byte stores)
-template <int NP>
-__device__ __forceinline__ void tsf_store(float* dst, const tsf_f2 (&x)[NP / 2]) {
-#pragma unroll
-  for (int q = 0; q < NP / 4; ++q) *(tsf_f4*)(dst + 4 * q) = (tsf_f4){x[2 * q].x, x[2 * q].y, x[2 * q + 1].x, x[2 * q + 1].y};
-}
-
 // grid cdiv(B, TSF_PB), 256 threads; TSF_PB batch indices (their s rows and s1 rows) per WG.
-// gfl = A.g + pol Pg (g_i).  The flow rows wait for the staging (their flow parameters come from
-// LDS: LDS reads are counted apart from the rows' global stores, so a flow step never waits on
-// memory), then wave 0 runs them while waves 1-3 write the snapshot.
+// gfl = A.g + pol Pg (g_i).
+//   A  all waves: the flows into LDS (chain layout), then c_k = w_{k+1}·u_k;
+//   B  wave 0, one lane per row: the planar-flow chain.  With q_{k+1} = w_{k+1}·z_k + b_{k+1}
+//      (known before t_k) the next pre-activation is a_{k+1} = q_{k+1} + t_k c_k, so a flow
+//      step's critical path is tanh + one FMA; z_{k+1} = z_k + u_k t_k and the stores of z_k, t_k
+//      run beside it.  Waves 1-3 meanwhile stage the Linear of g, W_h, b_h and φ, and write the
+//      snapshot of g_i, h, w_i (read by k_tsf_bwd) from global memory;
+//   C  Linear(n_s, G) of g for the workgroup's rows, then φ̃ = (h(g(s)) + h(g(s1))) ⊙ φ.
 template <int NP>
 __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A, const float* __restrict__ gfl) {
-  constexpr int PB = TSF_PB, RPW = 2 * PB;
-  __shared__ float s_fl[TSF_LDS / 2];  // flows, then the Linear of g
-  __shared__ float s_whT[TSF_LDS];     // W_h transposed: [G][d]
-  __shared__ float s_gf[TSF_LDS / 2];  // g features of this workgroup's rows [RPW][G]
-  __shared__ float s_ph[1024];         // φ rows of this workgroup's batch indices [PB][d]
-  __shared__ float s_z[RPW * TSF_NS];  // z_K of this workgroup's rows
-  __shared__ float s_bh[256], s_wv[256];
-  __shared__ __attribute__((aligned(16))) float s_fa[TSF_FA];  // flows, chain layout
+  constexpr int PB = TSF_PB, RPW = 2 * PB, FA = tsf_fst(NP);
+  __shared__ __attribute__((aligned(16))) float s_fa[TSF_FA];       // flows, chain layout
+  __shared__ __attribute__((aligned(16))) float s_wl[TSF_LDS / 2];  // Linear of g: [G][NP]
+  __shared__ __attribute__((aligned(16))) float s_wh[TSF_LDS];      // W_h: [d][GP]
+  __shared__ __attribute__((aligned(16))) float s_gf[TSF_LDS / 2];  // g features [RPW][GP]
+  __shared__ __attribute__((aligned(16))) float s_z[RPW * TSF_NS];  // z_K rows [RPW][NP]
+  __shared__ float s_ph[1024];                                      // φ rows [PB][d]
+  __shared__ float s_bl[256], s_bh[256];
   const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
-  const int fs = tsf_flow_stride(n_s), nfl = K * fs, nlin = G * n_s + G;
-  constexpr int FA = tsf_fst(NP);
+  const int fs = tsf_flow_stride(n_s), nfl = K * fs, GP = (G + 3) & ~3;
   const int b0 = blockIdx.x * PB, nb = min(PB, B - b0);
   PROBE_T(t0_);
-  const FDiv fd = fdiv(d), fG = fdiv(G);
-  glds(s_fl, nfl + nlin, [&](int j) { return gfl + j; });
-  glds(s_whT, d * G, [&](int j) { const int q = j / fd; return A.hp + (j - q * d) * G + q; });
-  glds(s_bh, d, [&](int j) { return A.hp + d * G + j; });
-  glds(s_wv, d, [&](int j) { return A.w + j; });
-  glds(s_ph, nb * d, [&](int j) { return A.phi + (size_t)b0 * d + j; });
   tsf_stage_flows<NP>(s_fa, gfl, K, n_s);
-  // the flow rows' initial states (plain loads, in flight with the staging)
   const bool s1row = tid >= PB;
   const int b = b0 + (s1row ? tid - PB : tid);
   const bool valid = tid < RPW && b < B;
@@ -293,76 +292,95 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A, const float* __restr
       z[p] = (tsf_f2){valid && 2 * p < n_s ? src[2 * p] : 0.f, valid && 2 * p + 1 < n_s ? src[2 * p + 1] : 0.f};
   }
   __syncthreads();
+  for (int k = tid; k < K; k += 256) {  // c_k (k = K - 1: no next flow)
+    float c = 0.f;
+    if (k + 1 < K) c = tsf_dot4(s_fa + (k + 1) * FA, s_fa + k * FA + NP, NP / 4);
+    s_fa[k * FA + 2 * NP + 1] = c;
+    if (blockIdx.x == 0) A.cst[k] = c;
+  }
+  __syncthreads();
   if (tid < RPW) {
-    // planar flows, one lane per row: lanes 0..PB-1 the s rows of batch indices b0.., PB.. the s1 rows
-    // rows past the batch write their (unused) flow states to a scratch row, so the loop body is
-    // one basic block: its LDS reads for step k + 1 issue at the top and are waited for only at
-    // the bottom, after step k's arithmetic
+    // rows past the batch write their (unused) states to a scratch row, so the loop body is one
+    // basic block: the LDS reads for step k + 1 issue at its top
     float* zrow = valid ? A.zs + (size_t)row * NP : A.scratch + tid * TSF_NS;
     float* trow = valid ? A.ts + row : A.scratch + tid * TSF_NS + NP;
     const size_t zstep = valid ? (size_t)R2 * NP : 0, tstep = valid ? (size_t)R2 : 0;
     PROBE_AT(1);
-    TsfFlow<NP> F, Fn;
-    if (K > 0) tsf_flow_ld<NP>(F, s_fa);
-    for (int k = 0; k < K; ++k) {
-      tsf_flow_ld<NP>(Fn, s_fa + min(k + 1, K - 1) * FA);  // next flow, off the chain
-      const float t = tsf_tanh(__fadd_rn(tsf_dot<NP>(z, F.w), F.b));
+    // flows k (F0) and k + 1 (F1) in registers; flow k + 2's LDS reads are issued a full step
+    // before their use
+    TsfFlow<NP> F0, F1, F2;
+    float a = 0.f;
+    if (K > 0) {
+      tsf_flow_ld<NP>(F0, s_fa);
+      tsf_flow_ld<NP>(F1, s_fa + min(1, K - 1) * FA);
+      a = __fadd_rn(tsf_dot<NP>(z, F0.w), F0.b);
+    }
+    // one flow step: Fa = flow k, Fb = flow k + 1, Fc <- flow k + 2; the loop rotates the three
+    // register sets by name (unrolled by 3), so no step copies parameters
+    auto step = [&](const TsfFlow<NP>& Fa, const TsfFlow<NP>& Fb, TsfFlow<NP>& Fc, int k) {
+      tsf_flow_ld<NP>(Fc, s_fa + min(k + 2, K - 1) * FA);
+      const float q = __fadd_rn(tsf_dot<NP>(z, Fb.w), Fb.b);  // w_{k+1}·z_k + b_{k+1}: off the critical path
+      const float t = tsf_tanh(a);
       tsf_store<NP>(zrow, z);
       *trow = t;
       zrow += zstep;
       trow += tstep;
-      tsf_axpy<NP>(z, t, F.u);
-      F = Fn;
+      a = __builtin_fmaf(t, Fa.c, q);
+      tsf_axpy<NP>(z, t, Fa.u);
+    };
+    for (int k = 0;;) {
+      if (k >= K) break;
+      step(F0, F1, F2, k++);
+      if (k >= K) break;
+      step(F1, F2, F0, k++);
+      if (k >= K) break;
+      step(F2, F0, F1, k++);
     }
     tsf_store<NP>(zrow, z);
-#pragma unroll
-    for (int p = 0; p < NP / 2; ++p) {
-      s_z[tid * TSF_NS + 2 * p] = z[p].x;
-      s_z[tid * TSF_NS + 2 * p + 1] = z[p].y;
-    }
+    tsf_store<NP>(s_z + tid * NP, z);
+    PROBE_AT(2);
   } else if (tid >= 64) {
-    // waves 1-3, beside the flow rows: this workgroup's slice of the pre-step snapshot of g_i,
-    // h, w_i (read by k_tsf_bwd)
+    const FDiv fnp = fdiv(NP), fgp = fdiv(GP);
+    const float* Wl = gfl + nfl;
+    glds(s_wl, G * NP, [&](int j) -> const float* {
+      const int c = j / fnp, i = j - c * NP;
+      return i < n_s ? Wl + c * n_s + i : nullptr;
+    }, 1, 3);
+    glds(s_bl, G, [&](int j) { return Wl + G * n_s + j; }, 1, 3);
+    glds(s_wh, d * GP, [&](int j) -> const float* {
+      const int c = j / fgp, q = j - c * GP;
+      return q < G ? A.hp + c * G + q : nullptr;
+    }, 1, 3);
+    glds(s_bh, d, [&](int j) { return A.hp + d * G + j; }, 1, 3);
+    glds(s_ph, nb * d, [&](int j) { return A.phi + (size_t)b0 * d + j; }, 1, 3);
+    // this workgroup's slice of the pre-step snapshot of g_i, h, w_i
     const int S = A.Pg + A.Ph + d, per = (S + gridDim.x - 1) / gridDim.x;
     const int lo = blockIdx.x * per, hi = min(S, lo + per);
-    for (int j = lo + tid - 64; j < hi; j += 192) {
-      float v;
-      if (j < A.Pg) {
-        v = s_fl[j];
-      } else if (j < A.Pg + d * G) {
-        const int jj = j - A.Pg, c = jj / fG, q = jj - c * G;
-        v = s_whT[q * d + c];
-      } else if (j < A.Pg + A.Ph) {
-        v = s_bh[j - A.Pg - d * G];
-      } else {
-        v = s_wv[j - A.Pg - A.Ph];
+    for (int j = lo + tid - 64; j < hi; j += 192)
+      A.snap[j] = j < A.Pg ? gfl[j] : (j < A.Pg + A.Ph ? A.hp[j - A.Pg] : A.w[j - A.Pg - A.Ph]);
+  }
+  __syncthreads();
+  {  // Linear(n_s, G) of g for this workgroup's rows (columns past G: zero)
+    const FDiv fgp = fdiv(GP);
+    for (int j = tid; j < RPW * GP; j += 256) {
+      const int r = j / fgp, c = j - r * GP;
+      float v = 0.f;
+      if (c < G) {
+        v = __fadd_rn(tsf_dot4(s_z + r * NP, s_wl + c * NP, NP / 4), s_bl[c]);
+        const int bb = b0 + (r >= PB ? r - PB : r);
+        if (bb < B) A.gfeat[(size_t)(r >= PB ? B + bb : bb) * G + c] = v;
       }
-      A.snap[j] = v;
+      s_gf[j] = v;
     }
   }
   __syncthreads();
-  PROBE_AT(2);
-  // Linear(n_s, G) of g for this workgroup's rows
-  const float* Wl = s_fl + nfl;
-  const float* bl = Wl + G * n_s;
-  for (int j = tid; j < RPW * G; j += 256) {
-    const int r = j / fG, c = j - r * G;
-    float acc = 0.f;
-    for (int i = 0; i < n_s; ++i) acc = __builtin_fmaf(s_z[r * TSF_NS + i], Wl[c * n_s + i], acc);
-    const float v = __fadd_rn(acc, bl[c]);
-    s_gf[j] = v;
-    const int bb = b0 + (r >= PB ? r - PB : r);
-    if (bb < B) A.gfeat[(size_t)(r >= PB ? B + bb : bb) * G + c] = v;
-  }
-  __syncthreads();
-  // φ̃ = (h(g(s)) + h(g(s1))) ⊙ φ  (lanes over c read W_hᵀ rows: conflict-free)
+  PROBE_AT(3);
+  // φ̃ = (h(g(s)) + h(g(s1))) ⊙ φ
+  const FDiv fd = fdiv(d);
   for (int j = tid; j < nb * d; j += 256) {
     const int r = j / fd, c = j - r * d, bb = b0 + r;
-    float h0 = 0.f, h1 = 0.f;
-    for (int q = 0; q < G; ++q) {
-      h0 = __builtin_fmaf(s_gf[r * G + q], s_whT[q * d + c], h0);
-      h1 = __builtin_fmaf(s_gf[(PB + r) * G + q], s_whT[q * d + c], h1);
-    }
+    const float h0 = tsf_dot4(s_gf + r * GP, s_wh + c * GP, GP / 4);
+    const float h1 = tsf_dot4(s_gf + (PB + r) * GP, s_wh + c * GP, GP / 4);
     const float hb = s_bh[c];
     const float aff = __fadd_rn(__fadd_rn(h0, hb), __fadd_rn(h1, hb));
     A.tphi[(size_t)bb * d + c] = __fmul_rn(aff, s_ph[j]);
@@ -371,32 +389,27 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A, const float* __restr
 }
 
 // flow-row role: rows [f FR, (f+1) FR) of the 2B rows; lanes 0..FR-1 of wave 0 run the reverse
-// flow chains (one row each).  sfl = A.snap (the pre-step g_i first).
+// flow chains (one row each).  sfl = A.snap (the pre-step g_i first).  With r_k = dz_{k+1}·u_{k-1}
+// (known before da_k) the next chain value is su_{k-1} = dz_k·u_{k-1} = r_k + da_k c_{k-1}, so a
+// step's critical path is two operations (da_k = su_k (1 - t_k^2), then that FMA); the update
+// dz_k = dz_{k+1} + da_k w_k and the stores of dz_{k+1}, da_k run beside it.
 template <int NP>
 __device__ void tsf_bwd_flows(const TsfArgs& A, const float* __restrict__ sfl, float* sm, float* s_dr, float* s_w,
                               float* s_r, int* s_ab, int f) {
-  constexpr int FR = TSF_FR, PST = tsf_pst(NP);
+  constexpr int FR = TSF_FR, PST = tsf_pst(NP), FA = tsf_fst(NP);
   const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
   const int fs = tsf_flow_stride(n_s), nfl = K * fs, nlin = G * n_s + G;
-  float* s_z = sm;                                  // [K+1][FR][NP] (16-byte rows)
-  float* s_t = sm + TSF_ZS;                         // [K][FR]
+  float* s_t = sm;                                  // [K][FR]
   float* s_fl = s_t + TSF_TS;                       // Linear of g (pre-step)
   float* s_wh = s_fl + TSF_LDS / 2;                 // W_h (pre-step)
   float* s_dg = s_wh + TSF_LDS;                     // [FR][G] (φ̃ rows while staging)
   float* s_da = s_dg + 2048;                        // [FR][d]
   float* s_gc = s_da + 2048;                        // [FR][d] ψ output gradient rows, then dz_K [FR][NP]
-  float* s_fa = s_gc + 2048;                        // [K][tsf_fst(NP)] flows, chain layout
-  constexpr int FA = tsf_fst(NP);
+  float* s_fa = s_gc + 2048;                        // [K][FA] flows, chain layout
   PROBE_T(t0_);
   const int r0 = f * FR;
   const int nr = min(FR, R2 - r0);
   // stage everything up front (LDS-DMA, all in flight together)
-  constexpr int zr = FR * NP;
-  const int nzv = nr * NP;
-  glds(s_z, (K + 1) * zr, [&](int j) {
-    const int k = j / zr, e = j - k * zr;
-    return A.zs + ((size_t)k * R2 + r0) * NP + (e < nzv ? e : 0);  // rows past 2B: finite copies, zero dg
-  });
   glds(s_t, K * FR, [&](int j) {
     const int k = j / FR, e = j - k * FR;
     return A.ts + (size_t)k * R2 + r0 + (e < nr ? e : 0);
@@ -404,6 +417,7 @@ __device__ void tsf_bwd_flows(const TsfArgs& A, const float* __restrict__ sfl, f
   glds(s_fl, nlin, [&](int j) { return sfl + nfl + j; });
   glds(s_wh, d * G, [&](int j) { return sfl + A.Pg + j; });
   tsf_stage_flows<NP>(s_fa, sfl, K, n_s);
+  for (int k = tid; k < K; k += 256) s_fa[k * FA + 2 * NP + 1] = A.cst[k];
   (void)tsf_stage_daff(A, nr, [&](int rl) { const int row = r0 + rl; return row < B ? row : row - B; }, s_dg, s_da,
                        s_gc, s_dr, s_w, s_r, s_ab);
   PROBE_AT(1);
@@ -428,51 +442,43 @@ __device__ void tsf_bwd_flows(const TsfArgs& A, const float* __restrict__ sfl, f
   }
   __syncthreads();
   PROBE_AT(2);
-  if (tid >= FR) return;
-  // reverse chain of row r0 + tid; each row stores its own parameter-gradient terms (summed in
-  // k_tsf_flow).  The next step's operands (flow parameters, z_k, t_k) are read one step ahead.
+  if (tid >= FR || K == 0) return;
   const int rl = tid, row = r0 + rl;
   const bool valid = row < R2;
   tsf_f2 dz[NP / 2];
 #pragma unroll
   for (int p = 0; p < NP / 2; ++p) dz[p] = (tsf_f2){s_dz[rl * NP + 2 * p], s_dz[rl * NP + 2 * p + 1]};
-  float* pr = A.part + (size_t)row * PST;
-  auto ldz = [&](int k, tsf_f2 (&zk)[NP / 2], float& t) {
-    const float* zp = s_z + (k * FR + rl) * NP;
-#pragma unroll
-    for (int q = 0; q < NP / 4; ++q) {
-      const tsf_f4 v = *(const tsf_f4*)(zp + 4 * q);
-      zk[2 * q] = (tsf_f2){v.x, v.y};
-      zk[2 * q + 1] = (tsf_f2){v.z, v.w};
-    }
-    t = s_t[k * FR + rl];
-  };
-  PROBE_AT(3);
-  TsfFlow<NP> F, Fn;
-  tsf_f2 zk[NP / 2], zn[NP / 2];
-  float t = 0.f, tn = 0.f;
-  if (K > 0) {
-    tsf_flow_ld<NP>(F, s_fa + (K - 1) * FA);
-    ldz(K - 1, zk, t);
-  }
   // rows past 2B write to a scratch row (one basic block per step, as in k_tsf_fwd)
-  float* pk = valid ? pr + (size_t)(K - 1) * R2 * PST : A.scratch + tid * TSF_NS;
+  float* pk = valid ? A.part + ((size_t)(K - 1) * R2 + row) * PST : A.scratch + tid * TSF_NS;
   const size_t pstep = valid ? (size_t)R2 * PST : 0;
-  for (int k = K - 1; k >= 0; --k) {
-    const int kn = max(k - 1, 0);
-    tsf_flow_ld<NP>(Fn, s_fa + kn * FA);
-    ldz(kn, zn, tn);
-    const float su = tsf_dot<NP>(dz, F.u);
-    const float da = __fmul_rn(su, __fsub_rn(1.f, __fmul_rn(t, t)));
-    tsf_store_scaled<NP>(pk, zk, da);
-    tsf_store_scaled<NP>(pk + NP, dz, t);
-    *(tsf_f4*)(pk + 2 * NP) = (tsf_f4){da, 0.f, 0.f, 0.f};
+  PROBE_AT(3);
+  // flows k (F0) and k - 1 (F1) in registers; flow k - 2's LDS reads go out a step ahead
+  TsfFlow<NP> F0, F1, F2;
+  tsf_flow_ld<NP>(F0, s_fa + (K - 1) * FA);
+  tsf_flow_ld<NP>(F1, s_fa + max(K - 2, 0) * FA);
+  float t = s_t[(K - 1) * FR + rl];
+  float su = tsf_dot<NP>(dz, F0.u);  // dz_K·u_{K-1}
+  // one reverse step: Fa = flow k, Fb = flow k - 1, Fc <- flow k - 2 (rotated by name, as in
+  // k_tsf_fwd); tb = t_{k-1}, tc <- t_{k-2}
+  float t1 = s_t[max(K - 2, 0) * FR + rl], t2 = 0.f;
+  auto step = [&](const TsfFlow<NP>& Fa, const TsfFlow<NP>& Fb, TsfFlow<NP>& Fc, float ta, float& tc, int k) {
+    tsf_flow_ld<NP>(Fc, s_fa + max(k - 2, 0) * FA);
+    tc = s_t[max(k - 2, 0) * FR + rl];
+    const float rn = tsf_dot<NP>(dz, Fb.u);  // dz_{k+1}·u_{k-1}: off the critical path
+    const float da = __fmul_rn(su, __fsub_rn(1.f, __fmul_rn(ta, ta)));
+    tsf_store<NP>(pk, dz);
+    *(tsf_f4*)(pk + NP) = (tsf_f4){da, 0.f, 0.f, 0.f};
     pk -= pstep;
-    tsf_axpy<NP>(dz, da, F.w);
-    F = Fn;
-#pragma unroll
-    for (int p = 0; p < NP / 2; ++p) zk[p] = zn[p];
-    t = tn;
+    su = __builtin_fmaf(da, Fb.c, rn);
+    tsf_axpy<NP>(dz, da, Fa.w);
+  };
+  for (int k = K - 1;;) {
+    if (k < 0) break;
+    step(F0, F1, F2, t, t2, k--);
+    if (k < 0) break;
+    step(F1, F2, F0, t1, t, k--);
+    if (k < 0) break;
+    step(F2, F0, F1, t2, t1, k--);
   }
   PROBE_REC(11, t0_);
 }
@@ -592,30 +598,41 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A, const float* __restr
 }
 
 // flow parameters: Σ over the s rows + Σ over the s1 rows of the per-row terms (the two
-// g_backward calls of the reference), then Adam.  grid cdiv(K (2 n_s + 1), 256).  All 2B loads
-// of a thread are issued before the first add.
+// g_backward calls of the reference), then Adam.  grid K (one workgroup per flow), 256 threads:
+// the flow's saved states z_k, tanh outputs t_k and the rows' (dz_{k+1}, da_k) into LDS, then
+// thread e of [0, 2 n_s + 1) sums its parameter's terms row by row:
+//   w_i: da_k z_k[i]     b: da_k     u_i: dz_{k+1}[i] t_k
 __global__ __launch_bounds__(256) void k_tsf_flow(TsfArgs A) {
-  const int n_s = A.n_s, fs = tsf_flow_stride(n_s), nfl = A.K * fs, B = A.B, R2 = 2 * B, NP = A.np;
-  const int PST = tsf_pst(NP);
+  __shared__ float s_z[128 * TSF_NS], s_dz[128 * TSF_NS], s_da[128], s_t[128];  // 2B <= 128 rows
+  const int tid = threadIdx.x, n_s = A.n_s, fs = tsf_flow_stride(n_s), B = A.B, R2 = 2 * B, NP = A.np;
+  const int PST = tsf_pst(NP), k = blockIdx.x;
   PROBE_T(t0_);
-  const int j0 = blockIdx.x * 256 + threadIdx.x, j = j0 < nfl ? j0 : nfl - 1;
-  const int k = j / fs, e = j - k * fs;
-  const int off = e < n_s ? e : (e == n_s ? 2 * NP : NP + e - n_s - 1);  // w_i | b | u_i terms
-  const float* pk = A.part + (size_t)k * R2 * PST + off;
-  float v[128];
-#pragma unroll
-  for (int r = 0; r < 128; ++r) v[r] = r < R2 ? pk[(size_t)r * PST] : 0.f;
+  const FDiv fnp = fdiv(NP);
+  glds(s_z, R2 * NP, [&](int j) { return A.zs + (size_t)k * R2 * NP + j; });
+  glds(s_dz, R2 * NP, [&](int j) {
+    const int r = j / fnp;
+    return A.part + ((size_t)k * R2 + r) * PST + (j - r * NP);
+  });
+  glds(s_da, R2, [&](int j) { return A.part + ((size_t)k * R2 + j) * PST + NP; });
+  glds(s_t, R2, [&](int j) { return A.ts + (size_t)k * R2 + j; });
+  __syncthreads();
+  if (tid >= fs) return;
+  const int e = tid;
   float g0 = 0.f, g1 = 0.f;
-#pragma unroll
-  for (int r = 0; r < 128; ++r) {
-    if (r < B)
-      g0 = __fadd_rn(g0, v[r]);
-    else if (r < R2)
-      g1 = __fadd_rn(g1, v[r]);
+  if (e < n_s) {
+    for (int r = 0; r < B; ++r) g0 = __fadd_rn(g0, __fmul_rn(s_da[r], s_z[r * NP + e]));
+    for (int r = B; r < R2; ++r) g1 = __fadd_rn(g1, __fmul_rn(s_da[r], s_z[r * NP + e]));
+  } else if (e == n_s) {
+    for (int r = 0; r < B; ++r) g0 = __fadd_rn(g0, s_da[r]);
+    for (int r = B; r < R2; ++r) g1 = __fadd_rn(g1, s_da[r]);
+  } else {
+    const int i = e - n_s - 1;
+    for (int r = 0; r < B; ++r) g0 = __fadd_rn(g0, __fmul_rn(s_dz[r * NP + i], s_t[r]));
+    for (int r = B; r < R2; ++r) g1 = __fadd_rn(g1, __fmul_rn(s_dz[r * NP + i], s_t[r]));
   }
   const float g = __fadd_rn(g0, g1);
-  const long long go = (long long)A.pol * A.Pg;
-  if (j0 < nfl && !step_cancelled(A.cancel)) adam_el(A.g + go + j, A.gm + go + j, A.gv + go + j, g, adam_consts(A.hpg, *A.step));
+  const long long go = (long long)A.pol * A.Pg + (long long)k * fs + e;
+  if (!step_cancelled(A.cancel)) adam_el(A.g + go, A.gm + go, A.gv + go, g, adam_consts(A.hpf, *A.step));
   PROBE_REC(15, t0_);
 }
 

@@ -75,6 +75,7 @@ SIGNATURES = {
     "sfx_runner_action": (_I, [_VP, C.POINTER(C.c_int64)]),
     "sfx_runner_stats": (_I, [_VP] + [C.POINTER(C.c_longlong)] * 3 + [C.POINTER(C.c_double)]),
     "sfx_runner_gate_timeout": (_I, [_VP, _D]),
+    "sfx_runner_wait_timeout": (_I, [_VP, _D]),
     "sfx_runner_retried": (_I, [_VP, C.POINTER(C.c_longlong)]),
     "sfx_runner_recomputed": (_I, [_VP, C.POINTER(C.c_longlong)]),
     "sfx_runner_warm": (_I, [_VP]),
@@ -87,6 +88,9 @@ SIGNATURES = {
     "sfx_comm_init": (_I, [_VP, _VP, _I, _I]),
     "sfx_set_comm": (_I, [_VP, _VP, _I, _I]),
     "sfx_set_comm_host": (_I, [_VP, _VP, _VP, _I, _I]),
+    "sfx_comm_state": (_I, [_VP, _VP]),
+    "sfx_tsf_freeze_flows": (_I, [_VP, _I]),
+    "sfx_debug_stall": (_I, [_VP, _D]),
     "sfx_shard_setup": (_I, [_VP, _I, _I]),
     "sfx_shard_begin": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP, _F, _VP]),
     "sfx_shard_td_maxima": (_I, [_VP, _I, _VP]),

@@ -60,14 +60,28 @@ def tsf_get_test_action(self, s_enc, w, omegas):
         return self.sf.tsf_test_action(s_enc, w, omegas)
 
 
+def prints_phi_shape(agent) -> bool:
+    """agents/tsfdqn_sequential.py:443 prints ``Phi values {phi.shape}`` on every call of its
+    reward mapper; tsfdqn.py / tsfdqn_nf.py do not."""
+    return type(agent).__module__.split(".")[-1] == "tsfdqn_sequential"
+
+
 def tsf_update_test_reward_mapper(self, w_approx, omegas, optim, task, r, s, a, s1, a1):
-    """TSFDQN.update_test_reward_mapper (tsfdqn.py:917-997) as one library call
-    (sfx_tsf_test_update): φ from the user's task, the learning rates and weight decays read from
-    the agent's optimizer groups (its LambdaLR keeps decaying ω's), the Adam step on the device.
-    Returns (loss, l2, l1) as the reference does."""
+    """TSFDQN.update_test_reward_mapper (tsfdqn.py:917-997, agents/tsfdqn_sequential.py:435-520) as
+    one library call (sfx_tsf_test_update): φ from the user's task, the learning rates and weight
+    decays read from the agent's optimizer groups (its LambdaLR keeps decaying ω's), the Adam step
+    on the device.  Returns (loss, l2, l1) as the reference does.
+
+    Console output: agents/tsfdqn_sequential.py's unconditional ``Phi values`` line is printed as
+    the reference does; the occasional diagnostic block (every 1000th training step, when
+    ``random.randint(1, 1000) < 10``) draws from the same random stream but prints ONE line (the
+    task's ω and w) instead of the reference's block of intermediate tensors, and ``omegas.grad`` /
+    ``w_approx.weight.grad`` are not populated (the gradients live on the device only)."""
     if self.h_function is None:
         raise Exception('Affine Function (h) is not initialized')
     phi = task.features(s, a, s1)
+    if prints_phi_shape(self):
+        print(f'Phi values {phi.shape}')
     gw, go = optim.param_groups[0], optim.param_groups[1]
     for grp in (gw, go):
         if tuple(grp.get("betas", (0.9, 0.999))) != (0.9, 0.999) or grp.get("eps", 1e-8) != 1e-8:

@@ -13,8 +13,11 @@ sfx_successors(which = 1).  g_i / h modules are refreshed from the device by
 """
 from __future__ import annotations
 
+import warnings
+
 import numpy as np
 import torch
+from torch.utils.weak import WeakIdKeyDictionary
 
 from sfx.dropin._host import copy_weights as update_models_weights
 from . import deep_sequential as _seq
@@ -24,13 +27,22 @@ def _g_tensors(g):
     """g_i's tensors in the engine's packing (include/sfx.h sfx_tsf_load_g): per planar flow
     weight [1, n_s], bias [1], scale [1, n_s], then the Linear's weight and bias.  Flows are read by
     attribute: tsfdqn_nf.py's PlanarFlow moves its Parameters with .to(device) on a GPU, which
-    leaves them unregistered; they train here either way."""
+    leaves them unregistered -- see _flows_unregistered."""
     mods = list(g) if isinstance(g, torch.nn.Sequential) else [g]
     *flows, lin = mods
     out = []
     for f in flows:
         out += [getattr(f, "weight", None), getattr(f, "bias", None), getattr(f, "scale", None)]
     return out + [getattr(lin, "weight", None), getattr(lin, "bias", None)]
+
+
+def _flows_unregistered(g) -> bool:
+    """True when g_i's planar-flow tensors are not among g.parameters(): tsfdqn_nf.py's
+    PlanarFlow built on a GPU (Parameter(...).to(device) is a copy the module does not register),
+    so the reference's optimizer never updates them."""
+    mods = list(g) if isinstance(g, torch.nn.Sequential) else [g]
+    reg = {id(p) for p in g.parameters()}
+    return any(id(getattr(f, k)) not in reg for f in mods[:-1] for k in ("weight", "bias", "scale"))
 
 
 def _g_geometry(g, n_s):
@@ -74,16 +86,26 @@ def _params_load(m: torch.nn.Module, flat):
 class DeepTSF(_seq.DeepSF):
     TSF_MAX_BATCH = 64  # minibatch rows of the TSF kernels (sfx_tsf.h)
 
-    def __init__(self, pytorch_model_handle, *args, target_update_ev=1000, **kwargs):
+    def __init__(self, pytorch_model_handle, *args, target_update_ev=1000, train_unregistered_flows=False,
+                 **kwargs):
+        """train_unregistered_flows: planar flows that g_i does not register (tsfdqn_nf.py on a
+        GPU) stay fixed by default, as the reference's optimizer leaves them; True trains them
+        anyway (the reference's CPU behaviour)."""
         super().__init__(pytorch_model_handle, *args, target_update_ev=target_update_ev, **kwargs)
         self.max_batch = min(self.max_batch, self.TSF_MAX_BATCH)
+        self.train_unregistered_flows = train_unregistered_flows
 
     def reset(self):
         super().reset()
         self._g = []
         self._h = None
         self._tsf_stale = False
-        self._test_state = {}
+        # Adam state of each test task's {w, ω}, keyed by the ω tensor itself (weakly: it goes
+        # with the agent's tensor).  Not cleared here: the reference keeps that state in the
+        # agent's torch optimizers, which agent.reset() never rebuilds, so a second trial's test
+        # phases continue it.
+        if not isinstance(getattr(self, "_test_state", None), WeakIdKeyDictionary):
+            self._test_state = WeakIdKeyDictionary()
 
     def add_training_task(self, task, source=None, g_function_model={}, h_function_model={}):
         """features/deep_sequential_tsf.py:40-73 (w first, then the ψ networks and the optimizer)."""
@@ -151,6 +173,14 @@ class DeepTSF(_seq.DeepSF):
             for t, g in enumerate(self._g):
                 eng.tsf_load_g(t, _tensors_flat(_g_tensors(g)))
             eng.tsf_load_h(_params_flat(h))
+            if K > 0 and any(_flows_unregistered(g) for g in self._g):
+                freeze = not getattr(self, "train_unregistered_flows", False)
+                warnings.warn("sfx DeepTSF: the planar flows of g_i are not registered parameters of g_i "
+                              "(tsfdqn_nf.py's PlanarFlow on a GPU), so the reference's optimizer never updates "
+                              "them; " + ("they are held fixed here too (train_unregistered_flows=True trains "
+                                          "them)" if freeze else "train_unregistered_flows=True: they train here"),
+                              RuntimeWarning, stacklevel=3)
+                eng.tsf_freeze_flows(freeze)
         return eng
 
     def sync_tsf_modules(self):
@@ -179,7 +209,7 @@ class DeepTSF(_seq.DeepSF):
     # TSFDQN.get_test_action / update_test_reward_mapper (tsfdqn.py:859-997) on the device: the
     # agent's w_approx.weight [1, d] and ω [1, T, 1, 1] are updated in place when they live on the
     # engine's device (staged through it otherwise); the Adam moments of each test task's {w, ω}
-    # live here, keyed by its ω tensor (the reference keeps them in the torch optimizer).
+    # live here, keyed by its ω tensor object (the reference keeps them in the torch optimizer).
     def _on_engine(self, t):
         dev = self._eng.device
         if t.device == dev and t.dtype == torch.float32 and t.is_contiguous():
@@ -196,10 +226,9 @@ class DeepTSF(_seq.DeepSF):
     def tsf_test_update(self, w_approx, omegas, phi, r, s, a, s1, a1, *, gamma, beta, lasso, lr_w, wd_w, lr_o, wd_o):
         eng = self._engine(1)
         self._flush()
-        key = id(omegas)
-        if key not in self._test_state:
-            self._test_state[key] = [torch.zeros(2 * (self.n_features + self.n_tasks), device=eng.device), 0]
-        st = self._test_state[key]
+        st = self._test_state.get(omegas)
+        if st is None:
+            st = self._test_state[omegas] = [torch.zeros(2 * (self.n_features + self.n_tasks), device=eng.device), 0]
         st[1] += 1
         w, w_staged = self._on_engine(w_approx.weight.detach().reshape(-1))
         om, om_staged = self._on_engine(omegas.detach().reshape(-1))

@@ -294,6 +294,19 @@ class SFEngine:
         check(lib.sfx_step_finish(self._h, out), "sfx_step_finish")
         return int(out[0]), int(out[1]), int(out[2])
 
+    def comm_state(self) -> dict:
+        """sfx_comm_state: which communicators the handle holds (RCCL step / host-round split),
+        whether they were aborted after a timed-out collective, or the host transport."""
+        v = C.c_int()
+        check(lib.sfx_comm_state(self._h, C.byref(v)), "sfx_comm_state")
+        return dict(rccl=bool(v.value & 1), rounds_split=bool(v.value & 2), aborted=bool(v.value & 4),
+                    host=bool(v.value & 8))
+
+    def debug_stall(self, seconds: float):
+        """Test hook (sfx_debug_stall): the next sharded runner step stalls on the device before it
+        publishes its result."""
+        check(lib.sfx_debug_stall(self._h, float(seconds)), "sfx_debug_stall")
+
     def debug_force_rerun(self, first_policy: int):
         check(lib.sfx_debug_force_rerun(self._h, int(first_policy)), "sfx_debug_force_rerun")
 
@@ -368,6 +381,10 @@ class SFEngine:
         check(lib.sfx_lms(self._h, int(t), phi.data_ptr(), r.data_ptr(), float(alpha)), "sfx_lms")
 
     # ---------------------------------------------------------------- TSF-DQN (tsfdqn.py / tsfdqn_nf.py)
+    def tsf_freeze_flows(self, freeze: bool = True):
+        """sfx_tsf_freeze_flows: hold the planar flows fixed (the Linear of g_i and h still train)."""
+        check(lib.sfx_tsf_freeze_flows(self._h, int(bool(freeze))), "sfx_tsf_freeze_flows")
+
     def tsf_setup(self, G: int, K: int = 0, beta: float = 1.0, lr_g: float = 1e-3, wd_g: float = 0.0,
                   lr_h: float = 1e-3, wd_h: float = 0.0):
         """Transformed features: g_i = K planar flows + Linear(n_s, G) per task, h = Linear(G, d) shared."""

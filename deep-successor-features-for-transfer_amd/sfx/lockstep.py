@@ -41,7 +41,12 @@ one ``sfx_tsf_test_actions`` launch set for the E actions at s, the E env steps,
 actions at s1, one ``sfx_tsf_test_updates`` launch set fitting the E (w, ω) pairs -- each task's
 own Adam step number, LR (its LambdaLR keeps decaying ω's) and r read per row -- then each task's
 scheduler steps.  The E losses of every step stay on the device until the phase ends (the
-reference's ``loss.item()`` per step is one device read per task and step).
+reference's ``loss.item()`` per step is one device read per task and step).  Console output of the
+TSF phase: the same lines as the sequential loop over the bound reward mapper
+(``sfx.dropin.bind.tsf_update_test_reward_mapper``, which shortens the reference's diagnostic
+block to one line), but a step's lines are printed for all live tasks together, so across tasks
+their order interleaves where the sequential loop prints task by task; the SF phase prints in the
+reference's order.
 """
 from __future__ import annotations
 
@@ -266,17 +271,20 @@ def test_tasks_lockstep_tsf(agent, test_tasks: Sequence, indices: Sequence[int] 
 
 def _tsf_group(agent, eng, test_tasks, entries, omegas, sched, idx):
     """One lockstep group of E <= max_batch TSF test tasks: (returns, per-task [steps][3] losses)."""
+    from sfx.dropin.bind import prints_phi_shape
+
     sf, E, T = agent.sf, len(test_tasks), int(agent.T)
     dev, d, nt = eng.device, int(sf.n_features), int(sf.n_tasks)
+    phi_line = prints_phi_shape(agent)
     hp = agent.hyperparameters
     beta, lasso, gamma = hp['beta_loss_coefficient'], hp['omegas_l1_coefficient'], agent.gamma
     W = torch.stack([w.weight.detach().reshape(-1).to(dev, torch.float32) for w, _, _ in entries]).contiguous()
     Om = torch.stack([o.detach().reshape(-1).to(dev, torch.float32) for o in omegas]).contiguous()
     states = []
     for o in omegas:
-        st = sf._test_state.get(id(o))
+        st = sf._test_state.get(o)
         if st is None:
-            st = sf._test_state[id(o)] = [torch.zeros(2 * (d + nt), device=dev), 0]
+            st = sf._test_state[o] = [torch.zeros(2 * (d + nt), device=dev), 0]
         states.append(st)
     M = torch.stack([st[0] for st in states]).contiguous()
     L = torch.zeros(T, E, 3, device=dev)
@@ -300,14 +308,16 @@ def _tsf_group(agent, eng, test_tasks, entries, omegas, sched, idx):
         Wl, Oml, Ml = (W[lr_].contiguous(), Om[lr_].contiguous(), M[lr_].contiguous()) if part else (W, Om, M)
         S = torch.cat([torch.as_tensor(s_enc[e]).to(dev, torch.float32).reshape(1, -1) for e in live])
         greedy = eng.tsf_test_actions(S, Wl, Oml).to(adev).unbind()
-        acts, s1_enc, phis, rows, ended = [], {}, [], [], []
+        acts, s1_enc, phis, rows, ended, shapes = [], {}, [], [], [], []
         for k, e in enumerate(live):
             task = test_tasks[e]
             xa = sched[e][j][0]
             a = torch.tensor(xa).to(adev) if xa >= 0 else greedy[k]
             s1, r, done = task.transition(a)
             s1e = agent.encoding(s1)
-            phis.append(torch.as_tensor(task.features(s_enc[e], a, s1e)).to(dev, torch.float32).reshape(1, -1))
+            phi = torch.as_tensor(task.features(s_enc[e], a, s1e))
+            shapes.append(phi.shape)
+            phis.append(phi.to(dev, torch.float32).reshape(1, -1))
             acts.append(a.reshape(()).to(dev, torch.long))
             s1_enc[e] = s1e
             states[e][1] += 1
@@ -328,6 +338,9 @@ def _tsf_group(agent, eng, test_tasks, entries, omegas, sched, idx):
                                   lasso, losses=None if part else L[j])
         if part:
             W[lr_], Om[lr_], M[lr_], L[j, lr_] = Wl, Oml, Ml, Lj
+        if phi_line:  # agents/tsfdqn_sequential.py:443, once per task and step (bind.prints_phi_shape)
+            for shp in shapes:
+                print(f'Phi values {shp}')
         printed = [e for e in live if sched[e][j][2]]
         if printed:  # the binding's diagnostic print (bind.tsf_update_test_reward_mapper)
             write_back(printed)

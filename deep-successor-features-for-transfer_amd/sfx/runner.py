@@ -327,6 +327,12 @@ class NativeEnvLoop:
         """Bound of each step's gate wait; a step released later is cancelled and re-issued."""
         self._check(self._lib.sfx_runner_gate_timeout(self._r, float(seconds)), "sfx_runner_gate_timeout")
 
+    def set_wait_timeout(self, seconds: float):
+        """Bound of the host's wait on a step's result (sfx_runner_wait_timeout): past it the
+        queued steps are cancelled and drained; a sharded step stuck in a collective gets its
+        communicators aborted and the call raises instead of hanging."""
+        self._check(self._lib.sfx_runner_wait_timeout(self._r, float(seconds)), "sfx_runner_wait_timeout")
+
     def stats(self) -> dict:
         C = self._C
         a, b, c, w, rt = C.c_longlong(), C.c_longlong(), C.c_longlong(), C.c_double(), C.c_longlong()

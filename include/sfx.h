@@ -323,6 +323,13 @@ int sfx_runner_stats(sfx_runner_t r, long long* env_steps, long long* prelaunche
  * the host are cancelled the same way before the error returns: the heads hold the last
  * completed step and the runner stays usable. */
 int sfx_runner_gate_timeout(sfx_runner_t r, double seconds);
+/* Bound of the host's wait on a step's published result (default 10 s).  Past it the runner
+ * cancels the queued steps and drains the device queue (bounded); when the queue does not drain
+ * -- a sharded step's collective waiting for a peer that is gone -- it reads RCCL's asynchronous
+ * error (ncclCommGetAsyncError), aborts the handle's communicators (ncclCommAbort; a borrowed
+ * sfx_set_comm communicator too) and returns SFX_E_STATE; every later collective of the handle
+ * fails with that error, and a runner whose queue never drained fails every call. */
+int sfx_runner_wait_timeout(sfx_runner_t r, double seconds);
 /* While the host runs host rounds of a step (speculation not verified on the device), the next
  * step's gate does not give up (hold protocol) -- for at most max(bound, 20 s). */
 /* Instantiate the step graphs of the current schedule and task ahead of the first steps (every
@@ -369,6 +376,14 @@ int sfx_comm_unique_id(void* id_out /* sfx_comm_id_bytes() bytes */);
 int sfx_comm_init(sfx_t h, const void* unique_id, int rank, int world);
 int sfx_set_comm(sfx_t h, void* rccl_comm, int rank, int world);
 int sfx_set_comm_host(sfx_t h, sfx_host_allreduce_fn fn, void* ctx, int rank, int world);
+/* Communicator state: bit 0 step communicator, bit 1 the host rounds' communicator (split off by
+ * sfx_comm_init / sfx_set_comm with ncclCommSplit; with it the runner pipelines sharded steps at
+ * N > 1 too), bit 2 aborted after a timed-out collective, bit 3 host transport.  RCCL is loaded
+ * at run time (dlopen) by the first RCCL call. */
+int sfx_comm_state(sfx_t h, int* state);
+/* test hook: the next runner step of the sharded schedule stalls `seconds` (<= 60) on the device
+ * after its collectives and before it publishes its result (exercises sfx_runner_wait_timeout). */
+int sfx_debug_stall(sfx_t h, double seconds);
 
 /* ---------------------------------------------------------------------------------------
  * Heads sharded across ranks (BASELINE config C4: 64 tasks, 8 per GPU).
@@ -405,6 +420,10 @@ int sfx_shard_finish(sfx_t h, int rounds_run);
  * weight[G][n_s], bias[G].  h packing: weight[d][G], bias[d].  K = 0: tsfdqn.py's g.
  * ------------------------------------------------------------------------------------- */
 int sfx_tsf_setup(sfx_t h, int G, int K, float beta, double lr_g, double wd_g, double lr_h, double wd_h);
+/* Planar flows held fixed (Adam with lr = 0 on the flow parameters; the Linear of g_i and h still
+ * train): mirrors tsfdqn_nf.py on a GPU, where PlanarFlow's Parameter(...).to(device) leaves the
+ * flows unregistered, so the reference's optimizer never updates them. */
+int sfx_tsf_freeze_flows(sfx_t h, int freeze);
 int sfx_tsf_load_g(sfx_t h, int t, const float* g_host);
 int sfx_tsf_get_g(sfx_t h, int t, float* g_host, float* gm_host, float* gv_host);
 int sfx_tsf_load_h(sfx_t h, const float* h_host);

@@ -38,7 +38,7 @@ def _need_gpu():
         pytest.skip("no HIP device")
 
 
-def _run_rank(rank, cfg, comm):
+def _run_rank(rank, cfg, comm, force_rerun=None):
     from sfx.engine import SFEngine
     from sfx.init import reference_heads
     from sfx.runner import NativeEnvLoop
@@ -62,6 +62,8 @@ def _run_rank(rank, cfg, comm):
         set_host_comm(eng, rank, world)
     loop = NativeEnvLoop(eng, batch=b, capacity=500, gamma=0.9, epsilon=cfg["eps"], alpha_w=ALPHA,
                          episode_len=cfg["ep"], seed=17, schedule="sharded")
+    if force_rerun is not None:
+        eng.debug_force_rerun(force_rerun)  # every step's device rounds count as failed: host rounds
     loop.prefill(cfg["prefill"])  # the first steps run without a minibatch
     loop.set_task(Tg - 1)
     loop.record(cfg["steps"])
@@ -114,6 +116,68 @@ def test_native_sharded_single_rank_rccl(fused, force, monkeypatch):
     assert stats["prelaunched"] >= (cfg["steps"] - 1 if force else cfg["steps"] // 2), stats
     assert counters.sum() == cfg["steps"]
     _oracle_check(cfg, recs, final, heads, targets, ws)
+
+
+def test_native_sharded_rccl_host_rounds_pipelined(monkeypatch):
+    """Host rounds on the split communicator while the next step is pre-launched: RCCL forced at
+    world 1, every step's device rounds treated as failed (sfx_debug_force_rerun), so each step's
+    host rounds all-reduce on the host-round communicator (side stream) while the next step's
+    graph -- with its own all-reduces on the step communicator -- already waits at its gate.
+    The oracle replay must still reproduce every env action and the parameters."""
+    monkeypatch.setenv("SFX_RCCL_WORLD1", "1")
+    cfg = dict(SMALL, world=1, t_loc=4)
+    recs, final, heads, targets, ws, stats, counters = _run_rank(0, cfg, "rccl", force_rerun=1)
+    assert stats["host_round_steps"] >= 4, stats
+    assert stats["prelaunched"] >= cfg["steps"] // 2, stats
+    _oracle_check(cfg, recs, final, heads, targets, ws)
+
+
+def test_native_sharded_wait_bound_aborts_communicators(monkeypatch):
+    """a sharded step whose result never arrives (here: a one-shot 4 s stall
+    of the finish kernel, after the step's all-reduces) is bounded by sfx_runner_wait_timeout --
+    the runner cancels and drains what it can, reads RCCL's async error, aborts both
+    communicators and raises; later collectives fail fast instead of hanging, and the handle
+    still closes."""
+    import time
+
+    from sfx._lib import SFXError
+    from sfx.engine import SFEngine
+    from sfx.init import reference_heads
+    from sfx.runner import NativeEnvLoop
+    from sfx.shard import init_comm
+
+    monkeypatch.setenv("SFX_RCCL_WORLD1", "1")
+    monkeypatch.setenv("SFX_RUNNER_PIPELINE", "0")  # nothing queued behind the stalled step
+    sp = SMALL["spec"]
+    T = 2
+    online, w = reference_heads(T, sp["n_s"], sp["H"], sp["A"], sp["d"], sp["acts"], seed=3)
+    eng = SFEngine(T, sp["n_s"], sp["H"], sp["A"], sp["d"], sp["acts"], max_batch=16)
+    eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
+    eng.shard_setup(T, 0)
+    for t in range(T):
+        eng.load_head(t, online[t], 0)
+        eng.load_head(t, online[t], 1)
+        eng.load_w(t, w[t])
+    init_comm(eng, 0, 1)
+    assert eng.comm_state() == dict(rccl=True, rounds_split=True, aborted=False, host=False)
+    loop = NativeEnvLoop(eng, batch=16, capacity=200, gamma=0.9, epsilon=0.2, alpha_w=ALPHA, episode_len=50,
+                         seed=5, schedule="sharded")
+    loop.prefill(20)
+    loop.set_task(0)
+    loop.run(3)
+    loop.set_wait_timeout(1.0)
+    eng.debug_stall(4.0)
+    t0 = time.time()
+    with pytest.raises(SFXError, match="did not complete within 1 s.*communicators aborted"):
+        loop.run(3)
+    assert time.time() - t0 < 20.0
+    assert eng.comm_state()["aborted"]
+    t0 = time.time()
+    with pytest.raises(SFXError, match="aborted after a collective timed out"):
+        loop.run(1)
+    assert time.time() - t0 < 5.0
+    loop.close()
+    eng.close()
 
 
 def _worker(rank, port, q, cfg):

@@ -436,3 +436,35 @@ def test_tsf_lockstep_declared_endless_task_that_ends_stops_there():
         assert oa.param_groups[1]["lr"] == ob.param_groups[1]["lr"]
     for oa, ob in zip(agent.omegas, ref.omegas):
         assert torch.equal(oa.detach(), ob.detach())
+
+
+def test_tsf_test_state_survives_sf_reset():
+    """the Adam state of each TSF test task's {w, ω} is keyed by the ω tensor object
+    (weakly) and survives DeepTSF.reset() -- agent.reset() of a second trial; the reference keeps
+    it in the agent's torch optimizers, which reset() never rebuilds."""
+    from torch.utils.weak import WeakIdKeyDictionary
+
+    from sfx.dropin.features.deep_sequential_tsf import DeepTSF
+    from sfx.lockstep import test_tasks_lockstep_tsf
+
+    agent, tasks = _tsf_setup(3, 4, 0.1)
+    test_tasks_lockstep_tsf(agent, tasks)
+    st = agent.sf._test_state
+    assert isinstance(st, WeakIdKeyDictionary) and len(st) == 3
+    assert all(st[o][1] == 4 for o in agent.omegas)
+
+    def lam(n_in, n_out, shape, axis=1):
+        m = torch.nn.Sequential(torch.nn.Linear(n_in, 8), torch.nn.Linear(8, n_out))
+        return m, torch.nn.MSELoss(), torch.optim.Adam(m.parameters())
+
+    sf = DeepTSF(lam)
+    sf.reset()  # agent.reset() of the first trial
+    om = torch.ones(1, 3, 1, 1)
+    state = [torch.arange(4.0), 7]
+    sf._test_state[om] = state
+    sf.reset()
+    assert sf._test_state.get(om) is state
+    del om
+    import gc
+    gc.collect()
+    assert len(sf._test_state) == 0  # weak: goes with the agent's tensor

@@ -35,9 +35,11 @@ class TsfSF:
     an engine whose heads, g_t and h were loaded directly)."""
 
     def __init__(self, eng, d, T):
+        from torch.utils.weak import WeakIdKeyDictionary
+
         from sfx.dropin.features.deep_sequential_tsf import DeepTSF
 
-        self._eng, self._test_state, self.n_features, self.n_tasks = eng, {}, d, T
+        self._eng, self._test_state, self.n_features, self.n_tasks = eng, WeakIdKeyDictionary(), d, T
         for name in ("tsf_test_action", "tsf_test_update", "_on_engine"):
             setattr(self, name, getattr(DeepTSF, name).__get__(self))
 
