@@ -621,10 +621,12 @@ class PhiState:
             self.since_target = [0] * self.online.shape[0]
 
 
-def phi_update(st: PhiState, batch, i: int, *, use_gpi: bool = True, lr: float = 1e-3, target_update_ev: int = 1000):
+def phi_update(st: PhiState, batch, i: int, *, use_gpi: bool = True, lr: float = 1e-3, target_update_ev: int = 1000,
+               next_actions=None):
     """DeepSF_PHI.update_successor(transitions, phis_model, i, loss_coefficient, use_gpi) ->
     (loss, psi_loss, phi_loss, λ_i) and the next actions; st is updated in place.  Gradients by
-    autograd, as the reference's loss.backward()."""
+    autograd, as the reference's loss.backward().  next_actions: use these instead of the argmax
+    (a float64 replay following an fp32 run's actions, tests/test_gpu_phi.py error budget)."""
     s, a, r, _, s1, gamma = batch
     spec = st.spec
     B = s.shape[0]
@@ -637,6 +639,8 @@ def phi_update(st: PhiState, batch, i: int, *, use_gpi: bool = True, lr: float =
         else:
             q1 = torch.matmul(forward(st.online[i], spec, s1)[0], st.w[i].reshape(-1, 1))[..., 0] + st.wb[i]
             nxt = torch.argmax(q1, dim=1)
+        if next_actions is not None:
+            nxt = torch.as_tensor(next_actions)
         tpsi = forward(st.target[i], spec, s1)[0]
     pt = st.online[i].clone().requires_grad_(True)
     ph = st.phi.clone().requires_grad_(True)

@@ -109,6 +109,61 @@ def test_phi_update_full_c2_vs_oracle(use_gpi):
     np.testing.assert_equal(k, 5)
 
 
+def test_phi_error_budget_vs_float64():
+    """what the learned-φ parameters are worth.  Five full-C2 updates on the GPU,
+    in the fp32 oracle (the reference's ATen arithmetic) and in a float64 oracle following the
+    same next actions.  The fresh Adam's first step moves an entry by ±lr whatever the size of
+    its gradient, so an entry whose gradient is at rounding level may go either way: measured
+    against float64, the GPU must flip no more entries than 2x the fp32 reference does (plus a
+    floor of 2e-4 of the entries), every group; the losses within 1e-5 of float64."""
+    from sfx.init import reference_heads
+
+    spec = R.Spec(17, 256, 7, 8, ("relu", "relu"))
+    T, B, k = 8, 32, 5
+    online, w = reference_heads(T, spec.n_s, spec.H, spec.A, spec.d, spec.acts, seed=4)
+    ps = R.PhiSpec(spec.n_s, spec.d)
+    gen = torch.Generator().manual_seed(5)
+    phi0 = torch.empty(ps.P).uniform_(-0.15, 0.15, generator=gen)
+    wb0 = torch.empty(T).uniform_(-0.3, 0.3, generator=gen)
+    st = R.PhiState(spec, ps, online.clone(), online.clone(), w.clone(), wb0.clone(), phi0.clone(), torch.ones(T))
+    s64 = R.PhiState(spec, ps, online.double(), online.double(), w.double(), wb0.double(), phi0.double(),
+                     torch.ones(T, dtype=torch.float64))
+    eng = engine_of(st, 3)
+    rows = []
+    for j in range(k):
+        i = (5 * j) % T
+        s, s1 = torch.randn(B, spec.n_s, generator=gen), torch.randn(B, spec.n_s, generator=gen)
+        a = torch.randint(0, spec.A, (B,), generator=gen)
+        r = torch.rand(B, 1, generator=gen)
+        gamma = torch.where(torch.rand(B, generator=gen) < 0.1, 0.0, 0.9)
+        l32 = R.phi_update(st, (s, a, r, None, s1, gamma), i, use_gpi=True, target_update_ev=3)
+        l64 = R.phi_update(s64, (s.double(), a, r.double(), None, s1.double(), gamma.double()), i, use_gpi=True,
+                           target_update_ev=3, next_actions=l32[4])
+        lo = update(eng, i, s, a, r, s1, gamma, True).cpu().double()
+        for q in range(4):
+            ref = float(l64[q])
+            assert abs(float(lo[q]) - ref) <= 1e-5 * abs(ref) + 1e-9, (j, q, float(lo[q]), ref)
+
+    def flips(x, ref64):
+        x = torch.as_tensor(x).double().cpu().reshape(-1)
+        ref64 = ref64.reshape(-1)
+        bad = (x - ref64).abs() > 1e-5 + 1e-4 * ref64.abs()
+        return float(bad.double().mean()), float((x - ref64).abs().max())
+
+    groups = [("psi online", torch.stack([eng.get_head(t, 0) for t in range(T)]), st.online, s64.online),
+              ("psi target", torch.stack([eng.get_head(t, 1) for t in range(T)]), st.target, s64.target),
+              ("w", torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, s64.w),
+              ("phi net", eng.phi_get(), st.phi, s64.phi),
+              ("w bias", eng.test_wb, st.wb, s64.wb)]
+    for name, gpu, ref32, ref64 in groups:
+        (fg, mg), (fr, mr) = flips(gpu, ref64), flips(ref32, ref64)
+        rows.append((name, fg, fr, mg, mr))
+        print(f"{name:10s} flipped vs float64: GPU {fg:.2e}  reference fp32 {fr:.2e}   max |diff| {mg:.2e} / {mr:.2e}")
+        assert fg <= max(2.0 * fr, 2e-4), (name, fg, fr)
+        assert mg <= 2.0 * 1e-3 * k + 1e-5, (name, mg)
+    eng.close()
+
+
 class _Task:
     """tasks/task.py interface, enough for add_training_task."""
 
