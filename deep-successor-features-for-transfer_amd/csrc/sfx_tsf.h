@@ -41,11 +41,13 @@ constexpr int TSF_SCR = 64 * TSF_NS;  // TsfArgs::scratch floats (one row per ch
 constexpr int TSF_FA = 8192;   // flows staged in the chain layout: K x tsf_fst(NP)
 constexpr int TSF_SM = TSF_TS + TSF_LDS / 2 + TSF_LDS + 3 * 2048 + TSF_FA;  // k_tsf_bwd LDS (floats)
 
-// NP: n_s rounded up to 4 -- the register width of a flow row and the row stride of the saved
-// flow states (zs [K+1][2B][NP], 16-byte rows); the per-row gradient terms `part` are
+// NP: n_s rounded up to a power of two >= 4 -- the width of a flow row (spread over tsf_lpr(NP)
+// lanes) and the row stride of the saved flow states (zs [K+1][2B][NP], 16-byte rows); the per-row gradient terms `part` are
 // [K][2B][tsf_pst(NP)]: dz_{k+1} (the gradient reaching z_{k+1}) at [0, NP), da_k at NP --
 // k_tsf_flow forms the w / u terms da_k z_k and dz_{k+1} t_k from them and the saved states.
-__host__ __device__ constexpr int tsf_np(int n_s) { return (n_s + 3) & ~3; }
+__host__ __device__ constexpr int tsf_np(int n_s) { return n_s <= 4 ? 4 : n_s <= 8 ? 8 : n_s <= 16 ? 16 : 32; }
+// lanes per flow row (each holds NP / lanes = 4 or 8 state components)
+__host__ __device__ constexpr int tsf_lpr(int np) { return np / 4 < 4 ? np / 4 : 4; }
 __host__ __device__ constexpr int tsf_pst(int np) { return np + 4; }
 // a flow in the chain layout (LDS): w at [0, NP), u at [NP, 2NP), b at 2NP, c at 2NP + 1, zeros
 // elsewhere
@@ -72,7 +74,6 @@ struct TsfArgs {
   float* gfeat;  // [2B][G]
   float* tphi;   // [B][d]
   float* part;   // [K][2B][tsf_pst(NP)] per-row flow gradients (dz_{k+1}, da_k)
-  float* cst;    // [K] c_k = w_{k+1}·u_k of the pre-step flows (written by k_tsf_fwd)
   float* scratch;  // [TSF_SCR]: stores of flow-chain lanes past the batch (never read)
   float* snap;   // [Pg + Ph + d]: g_i, h, w_i before this step (written by k_tsf_fwd)
   float* losses; // [3]: [1] = l1 (written by the ψ tail); [0], [2] written here
@@ -106,34 +107,36 @@ __device__ __forceinline__ float tsf_tanh(float x) {
 typedef float tsf_f2 __attribute__((ext_vector_type(2)));
 typedef float tsf_f4 __attribute__((ext_vector_type(4)));
 
-// One planar flow's parameters in the chain layout (tsf_fst): w, u, b and the look-ahead
-// coefficient c_k = w_{k+1}·u_k, read from LDS (every lane of the wave reads the same words:
-// broadcast, 16 bytes at a time).
-template <int NP>
+// A flow row runs on LPR = tsf_lpr(NP) neighbouring lanes, lane j holding NL = NP / LPR
+// components [j NL, (j+1) NL) of the state.  One planar flow's parameters as lane j needs them
+// (chain layout, tsf_fst): its parts of w and u, b and the look-ahead coefficient
+// c_k = w_{k+1}·u_k; LDS reads at the same addresses for every row (broadcast), 16 bytes at a time.
+template <int NL>
 struct TsfFlow {
-  float w[NP], u[NP], b, c;
+  float w[NL], u[NL], b, c;
 };
 
-template <int NP>
-__device__ __forceinline__ void tsf_flow_ld(TsfFlow<NP>& F, const float* f) {
+template <int NL, int NP>
+__device__ __forceinline__ void tsf_flow_ld(TsfFlow<NL>& F, const float* f, int j) {
+  const float* fw = f + j * NL;
+  const float* fu = f + NP + j * NL;
 #pragma unroll
-  for (int q = 0; q < NP / 4; ++q) {
-    const tsf_f4 w4 = *(const tsf_f4*)(f + 4 * q), u4 = *(const tsf_f4*)(f + NP + 4 * q);
+  for (int q = 0; q < NL / 4; ++q) {
+    const tsf_f4 w4 = *(const tsf_f4*)(fw + 4 * q), u4 = *(const tsf_f4*)(fu + 4 * q);
     F.w[4 * q] = w4.x; F.w[4 * q + 1] = w4.y; F.w[4 * q + 2] = w4.z; F.w[4 * q + 3] = w4.w;
     F.u[4 * q] = u4.x; F.u[4 * q + 1] = u4.y; F.u[4 * q + 2] = u4.z; F.u[4 * q + 3] = u4.w;
   }
-  const tsf_f4 bc = *(const tsf_f4*)(f + 2 * NP);
+  const tsf_f2 bc = *(const tsf_f2*)(f + 2 * NP);
   F.b = bc.x;
   F.c = bc.y;
 }
 
-// x·y over NP components: NP/2 packed FMAs in (up to) three independent chains, then the three
-// pair sums.
-template <int NP>
-__device__ __forceinline__ float tsf_dot(const tsf_f2 (&x)[NP / 2], const float (&y)[NP]) {
+// this lane's part of x·y: NL/2 packed FMAs in (up to) three independent chains
+template <int NL>
+__device__ __forceinline__ float tsf_dot(const tsf_f2 (&x)[NL / 2], const float (&y)[NL]) {
   tsf_f2 c0 = {0.f, 0.f}, c1 = {0.f, 0.f}, c2 = {0.f, 0.f};
 #pragma unroll
-  for (int p = 0; p < NP / 2; ++p) {
+  for (int p = 0; p < NL / 2; ++p) {
     const tsf_f2 yy = {y[2 * p], y[2 * p + 1]};
     if (p % 3 == 0)
       c0 = __builtin_elementwise_fma(x[p], yy, c0);
@@ -145,19 +148,44 @@ __device__ __forceinline__ float tsf_dot(const tsf_f2 (&x)[NP / 2], const float 
   return __fadd_rn(__fadd_rn(__fadd_rn(c0.x, c0.y), __fadd_rn(c1.x, c1.y)), __fadd_rn(c2.x, c2.y));
 }
 
-// x += s·y (packed)
-template <int NP>
-__device__ __forceinline__ void tsf_axpy(tsf_f2 (&x)[NP / 2], float s, const float (&y)[NP]) {
-  const tsf_f2 ss = {s, s};
-#pragma unroll
-  for (int p = 0; p < NP / 2; ++p) x[p] = __builtin_elementwise_fma((tsf_f2){y[2 * p], y[2 * p + 1]}, ss, x[p]);
+// the row's full sum from its LPR lanes' parts (DPP quad_perm xor 1, then xor 2: every lane of
+// the row gets the same value, as IEEE addition commutes)
+template <int LPR>
+__device__ __forceinline__ float tsf_row_sum(float v) {
+  if (LPR >= 2) v = __fadd_rn(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));
+  if (LPR >= 4) v = __fadd_rn(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));
+  return v;
 }
 
-// dst[0, NP) = x (16-byte stores)
-template <int NP>
-__device__ __forceinline__ void tsf_store(float* dst, const tsf_f2 (&x)[NP / 2]) {
+// x += s·y (packed)
+template <int NL>
+__device__ __forceinline__ void tsf_axpy(tsf_f2 (&x)[NL / 2], float s, const float (&y)[NL]) {
+  const tsf_f2 ss = {s, s};
 #pragma unroll
-  for (int q = 0; q < NP / 4; ++q) *(tsf_f4*)(dst + 4 * q) = (tsf_f4){x[2 * q].x, x[2 * q].y, x[2 * q + 1].x, x[2 * q + 1].y};
+  for (int p = 0; p < NL / 2; ++p) x[p] = __builtin_elementwise_fma((tsf_f2){y[2 * p], y[2 * p + 1]}, ss, x[p]);
+}
+
+// dst[0, NL) = x (16-byte stores)
+template <int NL>
+__device__ __forceinline__ void tsf_store(float* dst, const tsf_f2 (&x)[NL / 2]) {
+#pragma unroll
+  for (int q = 0; q < NL / 4; ++q) *(tsf_f4*)(dst + 4 * q) = (tsf_f4){x[2 * q].x, x[2 * q].y, x[2 * q + 1].x, x[2 * q + 1].y};
+}
+
+// c_k = w_{k+1}·u_k (c_{K-1} = 0) into the chain layout, by ALL 64 lanes of one wave (lane per
+// flow); the wave's own later LDS reads see these stores (in-order LDS queue per wave)
+template <int NP>
+__device__ __forceinline__ void tsf_lookahead(float* s_fa, int K) {
+  constexpr int FA = tsf_fst(NP);
+  for (int k = threadIdx.x & 63; k < K; k += 64) {
+    float c = 0.f;
+    if (k + 1 < K)
+      for (int i = 0; i < NP; ++i) c = __builtin_fmaf(s_fa[(k + 1) * FA + i], s_fa[k * FA + NP + i], c);
+    s_fa[k * FA + 2 * NP + 1] = c;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // a·b over n4 16-byte groups of two LDS rows, four independent lanes of accumulation
@@ -280,65 +308,86 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A, const float* __restr
   const int b0 = blockIdx.x * PB, nb = min(PB, B - b0);
   PROBE_T(t0_);
   tsf_stage_flows<NP>(s_fa, gfl, K, n_s);
-  const bool s1row = tid >= PB;
-  const int b = b0 + (s1row ? tid - PB : tid);
-  const bool valid = tid < RPW && b < B;
+  // flow row rl = tid / LPR on lanes [LPR rl, LPR rl + LPR) (components [hf NL, hf NL + NL) each):
+  // rows 0..PB-1 the s rows of batch indices b0.., PB.. the s1 rows
+  constexpr int LPR = tsf_lpr(NP), NL = NP / LPR;
+  const int rl = tid / LPR, hf = tid % LPR;
+  const bool s1row = rl >= PB;
+  const int b = b0 + (s1row ? rl - PB : rl);
+  const bool valid = rl < RPW && b < B;
   const int row = s1row ? B + b : b;
-  tsf_f2 z[NP / 2];
-  if (tid < RPW) {
+  tsf_f2 z[NL / 2];
+  if (rl < RPW) {
     const float* src = (s1row ? A.S1 : A.S) + (size_t)(valid ? b : 0) * n_s;
 #pragma unroll
-    for (int p = 0; p < NP / 2; ++p)
-      z[p] = (tsf_f2){valid && 2 * p < n_s ? src[2 * p] : 0.f, valid && 2 * p + 1 < n_s ? src[2 * p + 1] : 0.f};
+    for (int p = 0; p < NL / 2; ++p) {
+      const int i = hf * NL + 2 * p;
+      z[p] = (tsf_f2){valid && i < n_s ? src[i] : 0.f, valid && i + 1 < n_s ? src[i + 1] : 0.f};
+    }
   }
   __syncthreads();
-  for (int k = tid; k < K; k += 256) {  // c_k (k = K - 1: no next flow)
-    float c = 0.f;
-    if (k + 1 < K) c = tsf_dot4(s_fa + (k + 1) * FA, s_fa + k * FA + NP, NP / 4);
-    s_fa[k * FA + 2 * NP + 1] = c;
-    if (blockIdx.x == 0) A.cst[k] = c;
-  }
-  __syncthreads();
-  if (tid < RPW) {
-    // rows past the batch write their (unused) states to a scratch row, so the loop body is one
-    // basic block: the LDS reads for step k + 1 issue at its top
-    float* zrow = valid ? A.zs + (size_t)row * NP : A.scratch + tid * TSF_NS;
-    float* trow = valid ? A.ts + row : A.scratch + tid * TSF_NS + NP;
-    const size_t zstep = valid ? (size_t)R2 * NP : 0, tstep = valid ? (size_t)R2 : 0;
-    PROBE_AT(1);
-    // flows k (F0) and k + 1 (F1) in registers; flow k + 2's LDS reads are issued a full step
-    // before their use
-    TsfFlow<NP> F0, F1, F2;
-    float a = 0.f;
-    if (K > 0) {
-      tsf_flow_ld<NP>(F0, s_fa);
-      tsf_flow_ld<NP>(F1, s_fa + min(1, K - 1) * FA);
-      a = __fadd_rn(tsf_dot<NP>(z, F0.w), F0.b);
+  if (tid < 64) {
+    tsf_lookahead<NP>(s_fa, K);
+    if (rl < RPW) {
+      // rows past the batch write their (unused) states to a scratch row, so the loop body is one
+      // basic block: the LDS reads for step k + 2 issue at its top
+      float* zrow = valid ? A.zs + (size_t)row * NP + hf * NL : A.scratch + rl * TSF_NS + hf * NL;
+      float* trow = valid ? A.ts + row : A.scratch + rl * TSF_NS + NP;  // both lanes: the same t
+      const size_t zstep = valid ? (size_t)R2 * NP : 0, tstep = valid ? (size_t)R2 : 0;
+      PROBE_AT(1);
+      // flows k (F0) and k + 1 (F1) in registers; flow k + 2's LDS reads are issued a full step
+      // before their use
+      TsfFlow<NL> F0, F1, F2;
+      float a = 0.f;
+      if (K > 0) {
+        tsf_flow_ld<NL, NP>(F0, s_fa, hf);
+        tsf_flow_ld<NL, NP>(F1, s_fa + min(1, K - 1) * FA, hf);
+        a = __fadd_rn(tsf_row_sum<LPR>(tsf_dot<NL>(z, F0.w)), F0.b);
+      }
+      // one flow step: Fa = flow k, Fb = flow k + 1, Fc <- flow k + 2; the loop rotates the three
+      // register sets by name (unrolled by 3), so no step copies parameters
+      auto step = [&](const TsfFlow<NL>& Fa, const TsfFlow<NL>& Fb, TsfFlow<NL>& Fc, int k) {
+        tsf_flow_ld<NL, NP>(Fc, s_fa + min(k + 2, K - 1) * FA, hf);
+        // w_{k+1}·z_k + b_{k+1}: off the critical path
+        const float q = __fadd_rn(tsf_row_sum<LPR>(tsf_dot<NL>(z, Fb.w)), Fb.b);
+        const float t = tsf_tanh(a);
+        tsf_store<NL>(zrow, z);
+        *trow = t;
+        zrow += zstep;
+        trow += tstep;
+        a = __builtin_fmaf(t, Fa.c, q);
+        tsf_axpy<NL>(z, t, Fa.u);
+      };
+      // K mod 3 steps first, then groups of three with no exit between their steps (an exit
+      // branch lets the compiler sink each step's flow reads past it, next to their use)
+      int k = 0;
+      const int rem = K % 3;
+      if (rem == 0) {
+        for (; k < K; k += 3) {
+          step(F0, F1, F2, k);
+          step(F1, F2, F0, k + 1);
+          step(F2, F0, F1, k + 2);
+        }
+      } else if (rem == 1) {
+        step(F0, F1, F2, k++);
+        for (; k < K; k += 3) {
+          step(F1, F2, F0, k);
+          step(F2, F0, F1, k + 1);
+          step(F0, F1, F2, k + 2);
+        }
+      } else {
+        step(F0, F1, F2, k++);
+        step(F1, F2, F0, k++);
+        for (; k < K; k += 3) {
+          step(F2, F0, F1, k);
+          step(F0, F1, F2, k + 1);
+          step(F1, F2, F0, k + 2);
+        }
+      }
+      tsf_store<NL>(zrow, z);
+      tsf_store<NL>(s_z + rl * NP + hf * NL, z);
+      PROBE_AT(2);
     }
-    // one flow step: Fa = flow k, Fb = flow k + 1, Fc <- flow k + 2; the loop rotates the three
-    // register sets by name (unrolled by 3), so no step copies parameters
-    auto step = [&](const TsfFlow<NP>& Fa, const TsfFlow<NP>& Fb, TsfFlow<NP>& Fc, int k) {
-      tsf_flow_ld<NP>(Fc, s_fa + min(k + 2, K - 1) * FA);
-      const float q = __fadd_rn(tsf_dot<NP>(z, Fb.w), Fb.b);  // w_{k+1}·z_k + b_{k+1}: off the critical path
-      const float t = tsf_tanh(a);
-      tsf_store<NP>(zrow, z);
-      *trow = t;
-      zrow += zstep;
-      trow += tstep;
-      a = __builtin_fmaf(t, Fa.c, q);
-      tsf_axpy<NP>(z, t, Fa.u);
-    };
-    for (int k = 0;;) {
-      if (k >= K) break;
-      step(F0, F1, F2, k++);
-      if (k >= K) break;
-      step(F1, F2, F0, k++);
-      if (k >= K) break;
-      step(F2, F0, F1, k++);
-    }
-    tsf_store<NP>(zrow, z);
-    tsf_store<NP>(s_z + tid * NP, z);
-    PROBE_AT(2);
   } else if (tid >= 64) {
     const FDiv fnp = fdiv(NP), fgp = fdiv(GP);
     const float* Wl = gfl + nfl;
@@ -417,7 +466,6 @@ __device__ void tsf_bwd_flows(const TsfArgs& A, const float* __restrict__ sfl, f
   glds(s_fl, nlin, [&](int j) { return sfl + nfl + j; });
   glds(s_wh, d * G, [&](int j) { return sfl + A.Pg + j; });
   tsf_stage_flows<NP>(s_fa, sfl, K, n_s);
-  for (int k = tid; k < K; k += 256) s_fa[k * FA + 2 * NP + 1] = A.cst[k];
   (void)tsf_stage_daff(A, nr, [&](int rl) { const int row = r0 + rl; return row < B ? row : row - B; }, s_dg, s_da,
                        s_gc, s_dr, s_w, s_r, s_ab);
   PROBE_AT(1);
@@ -442,43 +490,66 @@ __device__ void tsf_bwd_flows(const TsfArgs& A, const float* __restrict__ sfl, f
   }
   __syncthreads();
   PROBE_AT(2);
-  if (tid >= FR || K == 0) return;
-  const int rl = tid, row = r0 + rl;
+  constexpr int LPR = tsf_lpr(NP), NL = NP / LPR;
+  if (tid >= 64 || K == 0) return;
+  tsf_lookahead<NP>(s_fa, K);  // all 64 lanes of wave 0 (a lane per flow)
+  if (tid >= LPR * FR) return;
+  // row rl on lanes [LPR rl, LPR rl + LPR) (components [hf NL, hf NL + NL) each)
+  const int rl = tid / LPR, hf = tid % LPR, row = r0 + rl;
   const bool valid = row < R2;
-  tsf_f2 dz[NP / 2];
+  tsf_f2 dz[NL / 2];
 #pragma unroll
-  for (int p = 0; p < NP / 2; ++p) dz[p] = (tsf_f2){s_dz[rl * NP + 2 * p], s_dz[rl * NP + 2 * p + 1]};
+  for (int p = 0; p < NL / 2; ++p) dz[p] = *(const tsf_f2*)(s_dz + rl * NP + hf * NL + 2 * p);
   // rows past 2B write to a scratch row (one basic block per step, as in k_tsf_fwd)
-  float* pk = valid ? A.part + ((size_t)(K - 1) * R2 + row) * PST : A.scratch + tid * TSF_NS;
+  float* pk = valid ? A.part + ((size_t)(K - 1) * R2 + row) * PST + hf * NL : A.scratch + rl * TSF_NS + hf * NL;
+  float* pda = valid ? A.part + ((size_t)(K - 1) * R2 + row) * PST + NP : A.scratch + rl * TSF_NS + NP;
   const size_t pstep = valid ? (size_t)R2 * PST : 0;
   PROBE_AT(3);
   // flows k (F0) and k - 1 (F1) in registers; flow k - 2's LDS reads go out a step ahead
-  TsfFlow<NP> F0, F1, F2;
-  tsf_flow_ld<NP>(F0, s_fa + (K - 1) * FA);
-  tsf_flow_ld<NP>(F1, s_fa + max(K - 2, 0) * FA);
+  TsfFlow<NL> F0, F1, F2;
+  tsf_flow_ld<NL, NP>(F0, s_fa + (K - 1) * FA, hf);
+  tsf_flow_ld<NL, NP>(F1, s_fa + max(K - 2, 0) * FA, hf);
   float t = s_t[(K - 1) * FR + rl];
-  float su = tsf_dot<NP>(dz, F0.u);  // dz_K·u_{K-1}
+  float su = tsf_row_sum<LPR>(tsf_dot<NL>(dz, F0.u));  // dz_K·u_{K-1}
   // one reverse step: Fa = flow k, Fb = flow k - 1, Fc <- flow k - 2 (rotated by name, as in
   // k_tsf_fwd); tb = t_{k-1}, tc <- t_{k-2}
   float t1 = s_t[max(K - 2, 0) * FR + rl], t2 = 0.f;
-  auto step = [&](const TsfFlow<NP>& Fa, const TsfFlow<NP>& Fb, TsfFlow<NP>& Fc, float ta, float& tc, int k) {
-    tsf_flow_ld<NP>(Fc, s_fa + max(k - 2, 0) * FA);
+  auto step = [&](const TsfFlow<NL>& Fa, const TsfFlow<NL>& Fb, TsfFlow<NL>& Fc, float ta, float& tc, int k) {
+    tsf_flow_ld<NL, NP>(Fc, s_fa + max(k - 2, 0) * FA, hf);
     tc = s_t[max(k - 2, 0) * FR + rl];
-    const float rn = tsf_dot<NP>(dz, Fb.u);  // dz_{k+1}·u_{k-1}: off the critical path
+    const float rn = tsf_row_sum<LPR>(tsf_dot<NL>(dz, Fb.u));  // dz_{k+1}·u_{k-1}: off the critical path
     const float da = __fmul_rn(su, __fsub_rn(1.f, __fmul_rn(ta, ta)));
-    tsf_store<NP>(pk, dz);
-    *(tsf_f4*)(pk + NP) = (tsf_f4){da, 0.f, 0.f, 0.f};
+    tsf_store<NL>(pk, dz);
+    *pda = da;  // both lanes: the same value
     pk -= pstep;
+    pda -= pstep;
     su = __builtin_fmaf(da, Fb.c, rn);
-    tsf_axpy<NP>(dz, da, Fa.w);
+    tsf_axpy<NL>(dz, da, Fa.w);
   };
-  for (int k = K - 1;;) {
-    if (k < 0) break;
+  // K mod 3 steps first, then groups of three (as in k_tsf_fwd)
+  int k = K - 1;
+  const int rem = K % 3;
+  if (rem == 0) {
+    for (; k >= 0; k -= 3) {
+      step(F0, F1, F2, t, t2, k);
+      step(F1, F2, F0, t1, t, k - 1);
+      step(F2, F0, F1, t2, t1, k - 2);
+    }
+  } else if (rem == 1) {
     step(F0, F1, F2, t, t2, k--);
-    if (k < 0) break;
+    for (; k >= 0; k -= 3) {
+      step(F1, F2, F0, t1, t, k);
+      step(F2, F0, F1, t2, t1, k - 1);
+      step(F0, F1, F2, t, t2, k - 2);
+    }
+  } else {
+    step(F0, F1, F2, t, t2, k--);
     step(F1, F2, F0, t1, t, k--);
-    if (k < 0) break;
-    step(F2, F0, F1, t2, t1, k--);
+    for (; k >= 0; k -= 3) {
+      step(F2, F0, F1, t2, t1, k);
+      step(F0, F1, F2, t, t2, k - 1);
+      step(F1, F2, F0, t1, t, k - 2);
+    }
   }
   PROBE_REC(11, t0_);
 }
