@@ -447,13 +447,14 @@ __device__ void tsf_bwd_flows(const TsfArgs& A, const float* __restrict__ sfl, f
                               float* s_r, int* s_ab, int f) {
   constexpr int FR = TSF_FR, PST = tsf_pst(NP), FA = tsf_fst(NP);
   const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
-  const int fs = tsf_flow_stride(n_s), nfl = K * fs, nlin = G * n_s + G;
+  const int fs = tsf_flow_stride(n_s), nfl = K * fs;
+  const int D4 = (d + 3) & ~3, G4 = (G + 3) & ~3;   // rows padded to 16 bytes (zeros)
   float* s_t = sm;                                  // [K][FR]
-  float* s_fl = s_t + TSF_TS;                       // Linear of g (pre-step)
-  float* s_wh = s_fl + TSF_LDS / 2;                 // W_h (pre-step)
-  float* s_dg = s_wh + TSF_LDS;                     // [FR][G] (φ̃ rows while staging)
+  float* s_wlT = s_t + TSF_TS;                      // Linear of g (pre-step), transposed: [NP][G4]
+  float* s_whT = s_wlT + TSF_LDS / 2;               // W_h (pre-step), transposed: [G][D4]
+  float* s_dg = s_whT + TSF_LDS;                    // [FR][G4] (φ̃ rows while staging)
   float* s_da = s_dg + 2048;                        // [FR][d]
-  float* s_gc = s_da + 2048;                        // [FR][d] ψ output gradient rows, then dz_K [FR][NP]
+  float* s_gc = s_da + 2048;                        // ψ output gradient rows; daff [FR][D4]; dz_K [FR][NP]
   float* s_fa = s_gc + 2048;                        // [K][FA] flows, chain layout
   PROBE_T(t0_);
   const int r0 = f * FR;
@@ -463,30 +464,42 @@ __device__ void tsf_bwd_flows(const TsfArgs& A, const float* __restrict__ sfl, f
     const int k = j / FR, e = j - k * FR;
     return A.ts + (size_t)k * R2 + r0 + (e < nr ? e : 0);
   });
-  glds(s_fl, nlin, [&](int j) { return sfl + nfl + j; });
-  glds(s_wh, d * G, [&](int j) { return sfl + A.Pg + j; });
+  {
+    const FDiv fg4 = fdiv(G4), fd4 = fdiv(D4);
+    glds(s_wlT, NP * G4, [&](int j) -> const float* {
+      const int i = j / fg4, q = j - i * G4;
+      return i < n_s && q < G ? sfl + nfl + q * n_s + i : nullptr;
+    });
+    glds(s_whT, G * D4, [&](int j) -> const float* {
+      const int q = j / fd4, c = j - q * D4;
+      return c < d ? sfl + A.Pg + c * G + q : nullptr;
+    });
+  }
   tsf_stage_flows<NP>(s_fa, sfl, K, n_s);
   (void)tsf_stage_daff(A, nr, [&](int rl) { const int row = r0 + rl; return row < B ? row : row - B; }, s_dg, s_da,
                        s_gc, s_dr, s_w, s_r, s_ab);
   PROBE_AT(1);
-  const FDiv fG = fdiv(G);
-  // dg = daff W_h (the same for a batch index's s row and s1 row); rows past nr are zero
-  for (int j = tid; j < FR * G; j += 256) {
-    const int rl = j / fG, q = j - rl * G;
-    float acc = 0.f;
-    if (rl < nr)
-      for (int c = 0; c < d; ++c) acc = __builtin_fmaf(s_da[rl * d + c], s_wh[c * G + q], acc);
-    s_dg[j] = acc;
+  // daff rows in 16-byte rows (rows past nr: zero)
+  float* s_dap = s_gc;
+  for (int j = tid; j < FR * D4; j += 256) {
+    const int rl = j / D4, c = j - rl * D4;
+    s_dap[j] = rl < nr && c < d ? s_da[rl * d + c] : 0.f;
+  }
+  __syncthreads();
+  // dg = daff W_h (the same for a batch index's s row and s1 row)
+  {
+    const FDiv fg4 = fdiv(G4);
+    for (int j = tid; j < FR * G4; j += 256) {
+      const int rl = j / fg4, q = j - rl * G4;
+      s_dg[j] = q < G ? tsf_dot4(s_dap + rl * D4, s_whT + q * D4, D4 / 4) : 0.f;
+    }
   }
   __syncthreads();
   // dz_K = dg W_lin (zero past n_s), one thread per (row, component)
   float* s_dz = s_gc;
   if (tid < FR * NP) {
     const int rl = tid / NP, i = tid - rl * NP;
-    float dz = 0.f;
-    if (i < n_s)
-      for (int q = 0; q < G; ++q) dz = __builtin_fmaf(s_dg[rl * G + q], s_fl[q * n_s + i], dz);
-    s_dz[tid] = dz;
+    s_dz[tid] = i < n_s ? tsf_dot4(s_dg + rl * G4, s_wlT + i * G4, G4 / 4) : 0.f;
   }
   __syncthreads();
   PROBE_AT(2);
