@@ -167,6 +167,7 @@ struct sfx_handle {
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> prof_pool;
   // pending fused step (sfx_step_all -> sfx_step_finish)
+  bool lazy_finish = false;  // sfx_update_all enqueued a step whose verdict settle() collects
   struct Pending {
     bool active = false, update = false, sel = false;
     int B = 0, use_gpi = 1, task = 0, sel_use_gpi = 1;
@@ -985,6 +986,16 @@ int launch_step_all(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, c
 
 }  // namespace
 
+// sfx_update_all returns once its step is enqueued; the speculation verdict -- and host rounds,
+// should the device rounds leave a policy unverified -- is collected by the next API call on the
+// handle (every entry point settles first), so the host never waits on a step it has not asked
+// a result of.
+static int settle(sfx_handle* h) {
+  if (!h || !h->lazy_finish) return SFX_OK;
+  h->lazy_finish = false;
+  return sfx_step_finish(h, nullptr);
+}
+
 extern "C" {
 
 const char* sfx_version(void) { return "sfx 0.3 gfx950 fp32-mfma graphs speculative-gpi"; }
@@ -1186,6 +1197,7 @@ void pstep_release(sfx_handle* h);
 
 int sfx_destroy(sfx_t h) {
   if (!h) return SFX_OK;
+  (void)settle(h);
   (void)hipStreamSynchronize(h->stream);
   tsf_release(h);
   phi_release(h);
@@ -1196,12 +1208,14 @@ int sfx_destroy(sfx_t h) {
 }
 
 int sfx_set_stream(sfx_t h, void* stream) {
+  RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   h->stream = (hipStream_t)stream;
   return SFX_OK;
 }
 
 int sfx_set_graphs(sfx_t h, int enable) {
+  RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   h->use_graphs = enable != 0;
   if (!h->use_graphs) clear_graphs(h);
@@ -1212,6 +1226,7 @@ int sfx_head_numel(sfx_t h) { return h ? h->Ptorch : SFX_E_ARG; }
 
 int sfx_set_adam(sfx_t h, double lr_psi, double wd_psi, double lr_w, double wd_w, double beta1, double beta2,
                  double eps) {
+  RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   h->hp_psi = AdamHP{lr_psi, wd_psi, beta1, beta2, eps};
   h->hp_w = AdamHP{lr_w, wd_w, beta1, beta2, eps};
@@ -1220,6 +1235,7 @@ int sfx_set_adam(sfx_t h, double lr_psi, double wd_psi, double lr_w, double wd_w
 }
 
 int sfx_load_head(sfx_t h, int t, int which, const float* params_host) {
+  RC(settle(h));
   if (!valid_head(h, t) || !params_host) SFX_FAIL(SFX_E_ARG, "bad head / pointer");
   std::vector<float> buf(h->P);
   pack_head(h, params_host, buf.data());
@@ -1232,6 +1248,7 @@ int sfx_load_head(sfx_t h, int t, int which, const float* params_host) {
 }
 
 int sfx_get_head(sfx_t h, int t, int which, float* params_host) {
+  RC(settle(h));
   if (!valid_head(h, t) || !params_host) SFX_FAIL(SFX_E_ARG, "bad head / pointer");
   std::vector<float> buf(h->P);
   HIPCHK(hipMemcpyAsync(buf.data(), which ? h->target_of(t) : h->online_cur(t), sizeof(float) * h->P,
@@ -1242,6 +1259,7 @@ int sfx_get_head(sfx_t h, int t, int which, float* params_host) {
 }
 
 int sfx_load_adam(sfx_t h, int t, const float* m_host, const float* v_host, int step) {
+  RC(settle(h));
   if (!valid_head(h, t) || !m_host || !v_host || step < 0) SFX_FAIL(SFX_E_ARG, "bad args");
   std::vector<float> bm(h->P), bv(h->P);
   pack_head(h, m_host, bm.data());
@@ -1256,6 +1274,7 @@ int sfx_load_adam(sfx_t h, int t, const float* m_host, const float* v_host, int 
 }
 
 int sfx_get_adam(sfx_t h, int t, float* m_host, float* v_host, int* step) {
+  RC(settle(h));
   if (!valid_head(h, t)) SFX_FAIL(SFX_E_ARG, "bad head");
   std::vector<float> bm(h->P), bv(h->P);
   int st = 0;
@@ -1270,6 +1289,7 @@ int sfx_get_adam(sfx_t h, int t, float* m_host, float* v_host, int* step) {
 }
 
 int sfx_load_w(sfx_t h, int t, const float* w_host) {
+  RC(settle(h));
   if (!valid_w(h, t) || !w_host) SFX_FAIL(SFX_E_ARG, "bad args");
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipMemcpyAsync(h->w + (size_t)t * h->dpad, w_host, sizeof(float) * h->d, hipMemcpyHostToDevice, h->stream));
@@ -1278,6 +1298,7 @@ int sfx_load_w(sfx_t h, int t, const float* w_host) {
 }
 
 int sfx_get_w(sfx_t h, int t, float* w_host, float* wm_host, float* wv_host) {
+  RC(settle(h));
   if (!valid_w(h, t)) SFX_FAIL(SFX_E_ARG, "bad head");
   const size_t o = (size_t)t * h->dpad, n = sizeof(float) * h->d;
   if (w_host) HIPCHK(hipMemcpyAsync(w_host, h->w + o, n, hipMemcpyDeviceToHost, h->stream));
@@ -1288,12 +1309,14 @@ int sfx_get_w(sfx_t h, int t, float* w_host, float* wm_host, float* wv_host) {
 }
 
 int sfx_w_ptr(sfx_t h, int t, float** w_dev) {
+  RC(settle(h));
   if (!valid_w(h, t) || !w_dev) SFX_FAIL(SFX_E_ARG, "bad args");
   *w_dev = h->w + (size_t)t * h->dpad;
   return SFX_OK;
 }
 
 int sfx_gpi(sfx_t h, const float* S, int B, const float* w, float* psi, float* q, int64_t* task, int64_t* next) {
+  RC(settle(h));
   if (!h || !S || !w || B < 1) SFX_FAIL(SFX_E_ARG, "bad args");
   const GraphKey key = make_key(1, {B}, h->mask, {S, w, psi, q, task, next});
   return run_graph(h, key, [&]() -> int {
@@ -1307,6 +1330,7 @@ int sfx_gpi(sfx_t h, const float* S, int B, const float* w, float* psi, float* q
 }
 
 int sfx_successors(sfx_t h, const float* S, int B, int which, float* psi) {
+  RC(settle(h));
   if (!h || !S || !psi || B < 1 || (which != 0 && which != 1)) SFX_FAIL(SFX_E_ARG, "bad args");
   const GraphKey key = make_key(21, {B, which}, h->mask, {S, psi});
   return run_graph(h, key, [&]() -> int {
@@ -1320,6 +1344,7 @@ int sfx_successors(sfx_t h, const float* S, int B, int which, float* psi) {
 }
 
 int sfx_select_action(sfx_t h, const float* s, int task_index, int use_gpi, float* q, int64_t* out) {
+  RC(settle(h));
   if (!h || !s || !out || task_index < 0 || task_index >= h->T) SFX_FAIL(SFX_E_ARG, "bad args");
   use_gpi = use_gpi ? 1 : 0;
   const GraphKey key = make_key(2, {task_index, use_gpi}, h->mask, {s, q, out});
@@ -1327,6 +1352,7 @@ int sfx_select_action(sfx_t h, const float* s, int task_index, int use_gpi, floa
 }
 
 int sfx_test_actions(sfx_t h, const float* S, int E, const float* W, int w_stride, float* q, int64_t* out) {
+  RC(settle(h));
   if (!h || !S || !W || !out || E < 1 || w_stride < h->d) SFX_FAIL(SFX_E_ARG, "bad args");
   const GraphKey key = make_key(26, {E, w_stride}, h->mask, {S, W, q, out});
   return run_graph(h, key, [&]() -> int {
@@ -1344,6 +1370,7 @@ int sfx_test_actions(sfx_t h, const float* S, int E, const float* W, int w_strid
 
 int sfx_test_reward_updates(sfx_t h, int E, const float* phi, const float* r, float* W, int w_stride, double lr,
                             double wd, float* loss) {
+  RC(settle(h));
   if (!h || !phi || !r || !W || !loss || E < 1 || w_stride < h->d) SFX_FAIL(SFX_E_ARG, "bad args");
   launch(h, K_GPI, 12.0 * E * h->d, k_sf_test_mapper, dim3(cdiv(E, 64)), dim3(64), E, h->d, phi, r, W, w_stride,
          (float)(-lr), (float)wd, loss);
@@ -1353,6 +1380,7 @@ int sfx_test_reward_updates(sfx_t h, int E, const float* phi, const float* r, fl
 
 int sfx_update(sfx_t h, int policy, const float* S, const int64_t* a, const float* r, const float* phi,
                const float* S1, const float* gamma, int B, int use_gpi, float* losses, int64_t* next) {
+  RC(settle(h));
   if (!valid_head(h, policy) || !S || !a || !phi || !S1 || !gamma) SFX_FAIL(SFX_E_ARG, "bad args");
   if (B < 1 || B > h->Mmax) SFX_FAIL(SFX_E_ARG, "batch exceeds max_batch");
   use_gpi = use_gpi ? 1 : 0;
@@ -1366,6 +1394,7 @@ int sfx_update(sfx_t h, int policy, const float* S, const int64_t* a, const floa
 int sfx_step_all(sfx_t h, const float* S, const int64_t* a, const float* phi, const float* S1, const float* gamma,
                  int B, int use_gpi, int lms_task, const float* lms_phi, const float* lms_r, float lms_alpha,
                  const float* s_next, int task_index, int sel_use_gpi, float* losses) {
+  RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   if (h->pend.active) SFX_FAIL(SFX_E_STATE, "sfx_step_all: previous step not finished");
   const bool update = B > 0;
@@ -1400,6 +1429,7 @@ int sfx_step_all(sfx_t h, const float* S, const int64_t* a, const float* phi, co
 }
 
 int sfx_step_finish(sfx_t h, int64_t* out_host) {
+  RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   if (!h->pend.active) SFX_FAIL(SFX_E_STATE, "sfx_step_finish without sfx_step_all");
   sfx_handle::Pending p = h->pend;
@@ -1444,6 +1474,7 @@ int sfx_step_finish(sfx_t h, int64_t* out_host) {
 }
 
 int sfx_set_precision(sfx_t h, int precision) {
+  RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   if (precision != SFX_PREC_FP32 && precision != SFX_PREC_BF16) SFX_FAIL(SFX_E_ARG, "unknown precision");
   const bool want = precision == SFX_PREC_BF16;
@@ -1470,12 +1501,14 @@ int sfx_set_precision(sfx_t h, int precision) {
 int sfx_get_precision(sfx_t h) { return h ? (h->bf16 ? SFX_PREC_BF16 : SFX_PREC_FP32) : SFX_E_ARG; }
 
 int sfx_set_spec_rounds(sfx_t h, int rounds) {
+  RC(settle(h));
   if (!h || rounds < 1) SFX_FAIL(SFX_E_ARG, "bad args");
   h->spec_rounds = rounds;
   return SFX_OK;
 }
 
 int sfx_step_stats(sfx_t h, long long* steps, long long* fallbacks, long long* rerun_policies, long long* rounds) {
+  RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   if (rounds) *rounds = h->rounds_total;
   if (steps) *steps = h->steps_spec;
@@ -1485,6 +1518,7 @@ int sfx_step_stats(sfx_t h, long long* steps, long long* fallbacks, long long* r
 }
 
 int sfx_skip_stats(sfx_t h, long long* checked, long long* skipped, int reset) {
+  RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   unsigned long long c[2] = {0, 0}, ps[4] = {0, 0, 0, 0};
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -1500,6 +1534,7 @@ int sfx_skip_stats(sfx_t h, long long* checked, long long* skipped, int reset) {
 }
 
 int sfx_nonfinite(sfx_t h, int* flag_host, int reset) {
+  RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   int v = 0;
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -1510,6 +1545,7 @@ int sfx_nonfinite(sfx_t h, int* flag_host, int reset) {
 }
 
 int sfx_debug_force_rerun(sfx_t h, int first_policy) {
+  RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   h->force_rerun_from = first_policy;
   return SFX_OK;
@@ -1519,11 +1555,14 @@ int sfx_update_all(sfx_t h, const float* S, const int64_t* a, const float* phi, 
                    int B, float* losses) {
   if (!h || !S || !a || !phi || !S1 || !gamma) SFX_FAIL(SFX_E_ARG, "bad args");
   if (B < 1 || B > h->Mmax) SFX_FAIL(SFX_E_ARG, "batch exceeds max_batch");
+  RC(settle(h));
   RC(sfx_step_all(h, S, a, phi, S1, gamma, B, 1, -1, nullptr, nullptr, 0.f, nullptr, 0, 1, losses));
-  return sfx_step_finish(h, nullptr);
+  h->lazy_finish = true;  // the verdict is collected by the next call (settle)
+  return SFX_OK;
 }
 
 int sfx_lms(sfx_t h, int t, const float* phi, const float* r, float alpha) {
+  RC(settle(h));
   if (!valid_w(h, t) || !phi || !r) SFX_FAIL(SFX_E_ARG, "bad args");
   launch(h, K_LMS, 4.0 * (3.0 * h->d + 1), k_lms, dim3(1), dim3(256), h->w + (size_t)t * h->dpad, phi, r, alpha,
          h->d);
@@ -1532,36 +1571,42 @@ int sfx_lms(sfx_t h, int t, const float* phi, const float* r, float alpha) {
 }
 
 int sfx_set_target_update_ev(sfx_t h, int ev) {
+  RC(settle(h));
   if (!h || ev < 1) SFX_FAIL(SFX_E_ARG, "bad args");
   h->target_update_ev = ev;
   return SFX_OK;
 }
 
 int sfx_get_since_target(sfx_t h, int t, int* count) {
+  RC(settle(h));
   if (!valid_head(h, t) || !count) SFX_FAIL(SFX_E_ARG, "bad args");
   *count = h->since_target[t];
   return SFX_OK;
 }
 
 int sfx_set_since_target(sfx_t h, int t, int count) {
+  RC(settle(h));
   if (!valid_head(h, t) || count < 0) SFX_FAIL(SFX_E_ARG, "bad args");
   h->since_target[t] = count;
   return SFX_OK;
 }
 
 int sfx_sync_target(sfx_t h, int t) {
+  RC(settle(h));
   if (!valid_head(h, t)) SFX_FAIL(SFX_E_ARG, "bad head");
   HIPCHK(hipMemcpyAsync(h->target_of(t), h->online_cur(t), sizeof(float) * h->P, hipMemcpyDeviceToDevice, h->stream));
   return SFX_OK;
 }
 
 int sfx_prof_enable(sfx_t h, int enable) {
+  RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   h->prof = enable != 0;
   return SFX_OK;
 }
 
 int sfx_prof_collect(sfx_t h, int kind, int* count, double* total_us, double* bytes) {
+  RC(settle(h));
   if (!h || kind < 0 || kind >= K_NKIND) SFX_FAIL(SFX_E_ARG, "bad args");
   HIPCHK(hipStreamSynchronize(h->stream));
   int n = 0;
@@ -1581,6 +1626,7 @@ int sfx_prof_collect(sfx_t h, int kind, int* count, double* total_us, double* by
 }
 
 int sfx_prof_reset(sfx_t h) {
+  RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   HIPCHK(hipStreamSynchronize(h->stream));
   for (auto& r : h->prof_recs) {
@@ -1592,6 +1638,7 @@ int sfx_prof_reset(sfx_t h) {
 }
 
 int sfx_synchronize(sfx_t h) {
+  RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   HIPCHK(hipStreamSynchronize(h->stream));
   return SFX_OK;

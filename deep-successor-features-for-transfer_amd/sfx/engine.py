@@ -87,14 +87,45 @@ class SFEngine:
         return self._h
 
     # ---------------------------------------------------------------- helpers
+    # Host inputs (numpy / CPU tensors, as the reference's agents pass them) reach the device
+    # through a ring of pinned staging slots and one non-blocking copy each on the engine's
+    # stream (torch's stream at creation), instead of a synchronous pageable copy per argument;
+    # a slot is reused only after its copy's event has completed.
+    _PIN_SLOTS, _PIN_BYTES = 32, 1 << 16
+
+    def _h2d(self, x, dtype) -> torch.Tensor:
+        t = torch.as_tensor(x)
+        if t.device.type != "cpu":
+            return t.to(device=self.device, dtype=dtype)
+        t = t.to(dtype).contiguous()
+        nbytes = t.numel() * t.element_size()
+        if nbytes > self._PIN_BYTES or nbytes == 0:
+            return t.to(device=self.device)
+        if not hasattr(self, "_pin"):
+            self._pin = torch.empty(self._PIN_SLOTS, self._PIN_BYTES, dtype=torch.uint8, pin_memory=True)
+            self._pin_ev = [None] * self._PIN_SLOTS
+            self._pin_i = 0
+        i = self._pin_i
+        self._pin_i = (i + 1) % self._PIN_SLOTS
+        ev = self._pin_ev[i]
+        if ev is not None:
+            ev.synchronize()
+        slot = self._pin[i, :nbytes].view(dtype)
+        slot.copy_(t.reshape(-1))
+        out = torch.empty(t.shape, dtype=dtype, device=self.device)
+        out.copy_(slot.view(t.shape), non_blocking=True)
+        ev = self._pin_ev[i] = ev or torch.cuda.Event()
+        ev.record()
+        return out
+
     def _f(self, x, shape=None) -> torch.Tensor:
-        t = torch.as_tensor(x).to(device=self.device, dtype=torch.float32)
+        t = self._h2d(x, torch.float32)
         if shape is not None:
             t = t.reshape(shape)
         return t.contiguous()
 
     def _l(self, x) -> torch.Tensor:
-        return torch.as_tensor(x).to(device=self.device, dtype=torch.long).reshape(-1).contiguous()
+        return self._h2d(x, torch.long).reshape(-1).contiguous()
 
     # ---------------------------------------------------------------- configuration
     def set_adam(self, lr_psi=1e-3, wd_psi=0.0, lr_w=1e-3, wd_w=0.0, betas=(0.9, 0.999), eps=1e-8):

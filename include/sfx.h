@@ -154,6 +154,10 @@ int sfx_update(sfx_t h, int policy, const float* S_dev, const int64_t* a_dev, co
  * All-task update (agents/sfdqn.py:57-60 looping features/deep.py:93-131 over every
  * head in index order, each GPI seeing the heads already updated in this call).
  * loss = l1 only, w_i not trained (LMS w).  losses_dev [T, 3] (may be NULL).
+ * Returns once the step is enqueued on the handle's stream: the speculation verdict (and host
+ * rounds, should the device rounds leave a policy unverified) is collected by the next call on
+ * the handle -- every entry point does that first -- so losses_dev is complete in stream order and
+ * any result read through the API reflects the whole update.
  */
 int sfx_update_all(sfx_t h, const float* S_dev, const int64_t* a_dev, const float* phi_dev,
                    const float* S1_dev, const float* gamma_dev, int B, float* losses_dev);
