@@ -243,10 +243,12 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
   int* sab = reinterpret_cast<int*>(sm + P.o_ab);  // [32]
   float* sw = sm + P.o_w;      // [T][d] reward weights (the active task's after LMS)
   float* own = sm + P.o_own;   // [NL-1][32][8]: own columns of the step-start S-row activations
-  float* sdz = sm + P.o_dz;    // [32][8]: own columns of the current output gradient
-  float* sdzn = sm + P.o_dzn;  // [32][8]: ... of the next (lower) layer
+  // dZ columns and the masked output gradient are stored transposed (row b contiguous per column)
+  // so the dW sums read 4 rows per 16-byte LDS read
+  float* sdz = sm + P.o_dz;    // [8][32]: own columns of the current output gradient
+  float* sdzn = sm + P.o_dzn;  // [8][32]: ... of the next (lower) layer
   float* g3 = sm + P.o_g3;     // [32][d]: TD gradient at the taken action
-  float* g3m = sm + P.o_g3m;   // [32][d]: the same, zero in rows whose action is not this rank's
+  float* g3m = sm + P.o_g3m;   // [d][32] (transposed): the same, zero in rows whose action is not this rank's
   int* ap = reinterpret_cast<int*>(sm + P.o_ap);  // [8][32] next actions of the previous round
   int* ac = reinterpret_cast<int*>(sm + P.o_ac);  // [8][32] ... of this round
   float* scr = sm + P.o_cr;    // [32][d] ψ_i(s_b)[a_b]
@@ -629,7 +631,7 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
         nf |= !__builtin_isfinite(diff);
       }
       g3[i] = gv;
-      g3m[i] = b < B && sab[b] == rank ? gv : 0.f;
+      g3m[k * PS_MB + b] = b < B && sab[b] == rank ? gv : 0.f;
     }
     if (__syncthreads_or(nf) && tid == 0 && rank == 0) atomicOr(G.nonfin, 1);
     PS_MARK0(40);
@@ -639,7 +641,7 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
       if (ab >= 0 && ab < A)
         for (int k = 0; k < d; ++k) dx = __builtin_fmaf(g3[g * d + k], wc3[(ab * d + k) * 8 + j], dx);
       const float z = g < B ? act_bwd(dx, own[(NH * 32 + g) * 8 + j], P.L[NH].act) : 0.f;
-      sdz[g * 8 + j] = z;
+      sdz[j * PS_MB + g] = z;
       ps_st(dzh + ((size_t)NH * PS_MB + g) * PS_H + c0 + j, z);
     }
     ps_arrive(hctr);
@@ -664,7 +666,13 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
           if (k < d) {
             float gw = 0.f;  // rows of other actions hold exact zeros in g3m: the same sum
 #pragma unroll
-            for (int b = 0; b < PS_MB; ++b) gw = __builtin_fmaf(g3m[b * d + k], xc[NH][b], gw);
+            for (int b = 0; b < PS_MB; b += 4) {
+              const float4 gg = *reinterpret_cast<const float4*>(g3m + k * PS_MB + b);
+              gw = __builtin_fmaf(gg.x, xc[NH][b], gw);
+              gw = __builtin_fmaf(gg.y, xc[NH][b + 1], gw);
+              gw = __builtin_fmaf(gg.z, xc[NH][b + 2], gw);
+              gw = __builtin_fmaf(gg.w, xc[NH][b + 3], gw);
+            }
             float pp, mm, vv;
             if constexpr (PO_REG) {
               pp = po[0][u][0];
@@ -686,8 +694,11 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
       }
       if (tid < d) {
         float gb = 0.f;
-        for (int b = 0; b < B; ++b)
-          if (sab[b] == rank) gb = __fadd_rn(gb, g3[b * d + tid]);
+#pragma unroll
+        for (int b = 0; b < PS_MB; b += 4) {  // other actions' rows and rows past B: exact zeros
+          const float4 g4 = *reinterpret_cast<const float4*>(g3m + tid * PS_MB + b);
+          gb = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(gb, g4.x), g4.y), g4.z), g4.w);
+        }
         float pp = pbo[0], mm = pbo[1], vv = pbo[2];
         adam_apply(pp, mm, vv, gb, adc);
         const size_t bi = LO.bOff + arow + tid;
@@ -713,7 +724,7 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
       {  // dX_{l-1}[g][c0 + j]
         const float dx = ps_dot(DZ + g * PS_XS, WcT + ((l - 1) * PS_J + j) * PS_XS, PS_H);
         const float z = g < B ? act_bwd(dx, own[((l - 1) * 32 + g) * 8 + j], P.L[l - 1].act) : 0.f;
-        sdzn[g * 8 + j] = z;
+        sdzn[j * PS_MB + g] = z;
         if (l - 1 >= 1) ps_st(dzh + ((size_t)(l - 1) * PS_MB + g) * PS_H + c0 + j, z);
       }
       if (l - 1 >= 1) {
@@ -728,7 +739,13 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
       for (int jj = 0; jj < PS_J; ++jj) {
         float gw = 0.f;  // rows past B hold exact zeros in sdz
 #pragma unroll
-        for (int b = 0; b < PS_MB; ++b) gw = __builtin_fmaf(sdz[b * 8 + jj], xc[l - 1][b], gw);
+        for (int b = 0; b < PS_MB; b += 4) {
+          const float4 z4 = *reinterpret_cast<const float4*>(sdz + jj * PS_MB + b);
+          gw = __builtin_fmaf(z4.x, xc[l - 1][b], gw);
+          gw = __builtin_fmaf(z4.y, xc[l - 1][b + 1], gw);
+          gw = __builtin_fmaf(z4.z, xc[l - 1][b + 2], gw);
+          gw = __builtin_fmaf(z4.w, xc[l - 1][b + 3], gw);
+        }
         float pp = pw[l - 1][jj][0], mm = pw[l - 1][jj][1], vv = pw[l - 1][jj][2];
         adam_apply(pp, mm, vv, gw, adc);
         const size_t wi = Ll.wOff + (size_t)(c0 + jj) * PS_H + tid;
@@ -739,7 +756,11 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
       }
       if (tid < PS_J) {
         float gb = 0.f;
-        for (int b = 0; b < B; ++b) gb = __fadd_rn(gb, sdz[b * 8 + tid]);
+#pragma unroll
+        for (int b = 0; b < PS_MB; b += 4) {  // rows past B: exact zeros (the same sum)
+          const float4 z4 = *reinterpret_cast<const float4*>(sdz + tid * PS_MB + b);
+          gb = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(gb, z4.x), z4.y), z4.z), z4.w);
+        }
         float pp = pb[l][0], mm = pb[l][1], vv = pb[l][2];
         adam_apply(pp, mm, vv, gb, adc);
         const size_t bi = Ll.bOff + c0 + tid;
@@ -763,7 +784,13 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
         const int jj = tid / n_s, k = tid - jj * n_s;
         float gw = 0.f;
 #pragma unroll
-        for (int b = 0; b < PS_MB; ++b) gw = __builtin_fmaf(sdz[b * 8 + jj], sx[b * K0S + k], gw);
+        for (int b = 0; b < PS_MB; b += 4) {
+          const float4 z4 = *reinterpret_cast<const float4*>(sdz + jj * PS_MB + b);
+          gw = __builtin_fmaf(z4.x, sx[b * K0S + k], gw);
+          gw = __builtin_fmaf(z4.y, sx[(b + 1) * K0S + k], gw);
+          gw = __builtin_fmaf(z4.z, sx[(b + 2) * K0S + k], gw);
+          gw = __builtin_fmaf(z4.w, sx[(b + 3) * K0S + k], gw);
+        }
         float pp = p0[0], mm = p0[1], vv = p0[2];
         adam_apply(pp, mm, vv, gw, adc);
         const size_t wi = L0.wOff + (size_t)c0 * n_s + tid;
@@ -774,7 +801,11 @@ __global__ __launch_bounds__(256) void k_pstep(Geo G, PsArgs P) {
       }
       if (tid < PS_J) {
         float gb = 0.f;
-        for (int b = 0; b < B; ++b) gb = __fadd_rn(gb, sdz[b * 8 + tid]);
+#pragma unroll
+        for (int b = 0; b < PS_MB; b += 4) {  // rows past B: exact zeros (the same sum)
+          const float4 z4 = *reinterpret_cast<const float4*>(sdz + tid * PS_MB + b);
+          gb = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(gb, z4.x), z4.y), z4.z), z4.w);
+        }
         float pp = pb[0][0], mm = pb[0][1], vv = pb[0][2];
         adam_apply(pp, mm, vv, gb, adc);
         const size_t bi = L0.bOff + c0 + tid;
