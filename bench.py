@@ -367,6 +367,8 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
                                       ("reacher17-all-T8-B32-device-replay", "all", None, True, "fp32"),
                                       ("reacher17-all-T8-B32-fp32", "all", None, False, "fp32"),
                                       ("reacher17-all-T8-B32-bf16", "all", None, False, "bf16"),
+                                      # the opt-in persistent step (k_pstep: one launch per env step)
+                                      ("reacher17-all-T8-B32-persistent", "all", None, False, "fp32"),
                                       ("hopper11-tsf-T16-B32", "tsf", 0, False, "fp32"),
                                       ("hopper11-tsf-T16-B32-bf16", "tsf", 0, False, "bf16"),
                                       ("hopper11-tsf-nf100-T16-B32", "tsf", 100, False, "fp32"),
@@ -392,6 +394,9 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
         eng.set_target_update_ev(1000)
         eng.set_spec_rounds(args.spec_rounds)
         eng.set_precision(prec)
+        persistent = name.endswith("-persistent")
+        if persistent:
+            eng.set_pstep(True)
         loop = NativeEnvLoop(eng, batch=args.batch, seed=1, schedule=sched, p_end=0.0 if K is None else 0.01,
                              device_replay=dev)
         loop.prefill(1000)
@@ -404,6 +409,9 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
         dt = time.perf_counter() - t0
         out[name] = {"value": round(steps / dt, 2), "unit": "env steps/s", "ms_per_step": round(1000.0 * dt / steps, 4),
                      "steps": steps, "dtype": prec}
+        if persistent:
+            st = eng.pstep_stats()
+            out[name]["pstep_rounds_per_step"] = round(st["rounds"] / max(1, st["steps"]), 3)
         loop.close()
         eng.close()
     # the drop-in: features.deep.DeepSF under the reference user's Python agent loop (tools/dropin_loop.py)

@@ -88,21 +88,19 @@ class SFEngine:
 
     # ---------------------------------------------------------------- helpers
     # Host inputs (numpy / CPU tensors, as the reference's agents pass them) reach the device
-    # through a ring of pinned staging slots and one non-blocking copy each on the engine's
-    # stream (torch's stream at creation), instead of a synchronous pageable copy per argument;
-    # a slot is reused only after its copy's event has completed.
+    # through a ring of pinned staging slots: all host arguments of one call are packed into one
+    # slot (16-byte aligned) and go over in ONE non-blocking copy on torch's current stream,
+    # instead of a synchronous pageable copy per argument; a slot is reused only after its copy's
+    # event has completed.
     _PIN_SLOTS, _PIN_BYTES = 32, 1 << 16
 
-    def _h2d(self, x, dtype) -> torch.Tensor:
-        t = torch.as_tensor(x)
-        if t.device.type != "cpu":
-            return t.to(device=self.device, dtype=dtype)
-        t = t.to(dtype).contiguous()
-        nbytes = t.numel() * t.element_size()
-        if nbytes > self._PIN_BYTES or nbytes == 0:
-            return t.to(device=self.device)
+    _NP = {torch.float32: np.float32, torch.long: np.int64}
+
+    def _pin_slot(self):
+        """The next staging slot (numpy view of pinned memory), once its last copy has completed."""
         if not hasattr(self, "_pin"):
             self._pin = torch.empty(self._PIN_SLOTS, self._PIN_BYTES, dtype=torch.uint8, pin_memory=True)
+            self._pin_np = self._pin.numpy()
             self._pin_ev = [None] * self._PIN_SLOTS
             self._pin_i = 0
         i = self._pin_i
@@ -110,12 +108,54 @@ class SFEngine:
         ev = self._pin_ev[i]
         if ev is not None:
             ev.synchronize()
-        slot = self._pin[i, :nbytes].view(dtype)
-        slot.copy_(t.reshape(-1))
-        out = torch.empty(t.shape, dtype=dtype, device=self.device)
-        out.copy_(slot.view(t.shape), non_blocking=True)
-        ev = self._pin_ev[i] = ev or torch.cuda.Event()
+        return i
+
+    def _pin_copy(self, i, nbytes) -> torch.Tensor:
+        """One non-blocking copy of slot i's first nbytes into a fresh device buffer."""
+        out = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        out.copy_(self._pin[i, :nbytes], non_blocking=True)
+        ev = self._pin_ev[i] = self._pin_ev[i] or torch.cuda.Event()
         ev.record()
+        return out
+
+    @staticmethod
+    def _host_array(x, npdt):
+        if torch.is_tensor(x):
+            x = x.detach()
+            if x.device.type != "cpu":
+                return None
+            x = x.numpy()
+        return np.asarray(x, dtype=npdt)
+
+    def _h2d(self, x, dtype) -> torch.Tensor:
+        return self._h2d_many([(x, dtype)])[0]
+
+    def _h2d_many(self, items):
+        """Host inputs [(x, dtype)] -> device tensors of their shapes, staged together through ONE
+        pinned slot and ONE non-blocking copy (a step's s, a, φ, s1, γ are one copy, not five).
+        Device tensors are converted in place of staging."""
+        arrs = [self._host_array(x, self._NP[dt]) for x, dt in items]
+        offs, tot = [], 0
+        for a in arrs:
+            offs.append(tot)
+            if a is not None:
+                tot += (a.nbytes + 15) & ~15
+        if tot > self._PIN_BYTES or any(a is not None and a.nbytes == 0 for a in arrs):
+            return [torch.as_tensor(x).to(device=self.device, dtype=dt) for x, dt in items]
+        dev = None
+        if tot:
+            i = self._pin_slot()
+            row = self._pin_np[i]
+            for a, o in zip(arrs, offs):
+                if a is not None:
+                    row[o:o + a.nbytes].view(a.dtype)[:] = a.reshape(-1)
+            dev = self._pin_copy(i, tot)
+        out = []
+        for (x, dt), a, o in zip(items, arrs, offs):
+            if a is None:
+                out.append(torch.as_tensor(x).to(device=self.device, dtype=dt))
+            else:
+                out.append(dev[o:o + a.nbytes].view(dt).view(a.shape))
         return out
 
     def _f(self, x, shape=None) -> torch.Tensor:
@@ -126,6 +166,17 @@ class SFEngine:
 
     def _l(self, x) -> torch.Tensor:
         return self._h2d(x, torch.long).reshape(-1).contiguous()
+
+    def _batch_in(self, s, s1, a, phi, gamma, r=None):
+        """A minibatch's device inputs (s, s1 [B, n_s], a [B] int64, φ [B, d], γ [B], r [B] or None),
+        one staged copy for all of them."""
+        items = [(s, torch.float32), (s1, torch.float32), (a, torch.long), (phi, torch.float32),
+                 (gamma, torch.float32)] + ([] if r is None else [(r, torch.float32)])
+        t = self._h2d_many(items)
+        B = t[0].shape[0]
+        out = [t[0].contiguous(), t[1].contiguous(), t[2].reshape(-1).contiguous(),
+               t[3].reshape(B, self.d).contiguous(), t[4].reshape(B).contiguous()]
+        return out + [None if r is None else t[5].reshape(B).contiguous()]
 
     # ---------------------------------------------------------------- configuration
     def set_adam(self, lr_psi=1e-3, wd_psi=0.0, lr_w=1e-3, wd_w=0.0, betas=(0.9, 0.999), eps=1e-8):
@@ -270,8 +321,8 @@ class SFEngine:
         if W.dim() != 2 or W.shape[1] != self.d or W.stride(1) != 1 or W.dtype != torch.float32 \
                 or W.device != self.device:
             raise ValueError(f"W must be a float32 [{E}, {self.d}] device tensor with unit column stride")
-        phi = self._f(phi, (E, self.d))
-        r = self._f(r, (E,))
+        phi, r = self._h2d_many([(phi, torch.float32), (r, torch.float32)])
+        phi, r = phi.reshape(E, self.d).contiguous(), r.reshape(E).contiguous()
         losses = torch.empty(E, device=self.device) if losses is None else losses
         _dev_f32(losses, self.device)
         if losses.numel() != E:
@@ -283,12 +334,8 @@ class SFEngine:
     def update(self, policy: int, s, a, r, phi, s1, gamma, use_gpi: bool = True,
                losses: Optional[torch.Tensor] = None, next_actions: Optional[torch.Tensor] = None):
         """One TD update of head `policy` (sfdqn.py:303-371 semantics).  r=None -> no l2 / w step."""
-        s, s1 = self._f(s), self._f(s1)
+        s, s1, a, phi, gamma, rr = self._batch_in(s, s1, a, phi, gamma, r)
         B = s.shape[0]
-        a = self._l(a)
-        phi = self._f(phi, (B, self.d))
-        gamma = self._f(gamma, (B,))
-        rr = None if r is None else self._f(r, (B,))
         if losses is None:
             losses = torch.empty(3, device=self.device)
         check(lib.sfx_update(self._h, int(policy), s.data_ptr(), a.data_ptr(), dptr(rr), phi.data_ptr(),
@@ -298,11 +345,8 @@ class SFEngine:
 
     def update_all(self, s, a, phi, s1, gamma, losses: Optional[torch.Tensor] = None):
         """All-task update (agents/sfdqn.py:57-60 over features/deep.py:93-131)."""
-        s, s1 = self._f(s), self._f(s1)
+        s, s1, a, phi, gamma, _ = self._batch_in(s, s1, a, phi, gamma)
         B = s.shape[0]
-        a = self._l(a)
-        phi = self._f(phi, (B, self.d))
-        gamma = self._f(gamma, (B,))
         if losses is None:
             losses = torch.empty(self.T, 3, device=self.device)
         check(lib.sfx_update_all(self._h, s.data_ptr(), a.data_ptr(), phi.data_ptr(), s1.data_ptr(),
@@ -402,13 +446,8 @@ class SFEngine:
         return {"policies_checked": c.value, "policies_skipped": s.value}
 
     def lms(self, t: int, phi, r, alpha: float):
-        phi, r = torch.as_tensor(phi), torch.as_tensor(r)
-        if phi.device.type == "cpu" and r.device.type == "cpu":  # host values: one copy to the device
-            pr = self._f(torch.cat([phi.reshape(-1).float(), r.reshape(1).float()]))
-            phi, r = pr[:-1], pr[-1:]
-        else:
-            phi = self._f(phi, (-1,))
-            r = self._f(r, (1,))
+        phi, r = self._h2d_many([(phi, torch.float32), (r, torch.float32)])  # host values: one copy
+        phi, r = phi.reshape(-1).contiguous(), r.reshape(1).contiguous()
         check(lib.sfx_lms(self._h, int(t), phi.data_ptr(), r.data_ptr(), float(alpha)), "sfx_lms")
 
     # ---------------------------------------------------------------- TSF-DQN (tsfdqn.py / tsfdqn_nf.py)
@@ -469,11 +508,12 @@ class SFEngine:
         """DeepSF_PHI.update_successor (features/deep_phi.py:93-224): losses [4] = (loss, psi_loss,
         phi_loss, λ after the step); bias / lam: one-element float32 device tensors (the policy's
         reward-model bias and loss coefficient), updated in place."""
-        s, s1 = self._f(s), self._f(s1)
+        s, s1, a, gamma, r = self._h2d_many([(s, torch.float32), (s1, torch.float32), (a, torch.long),
+                                             (gamma, torch.float32), (r, torch.float32)])
+        s, s1 = s.contiguous(), s1.contiguous()
         B = s.shape[0]
-        a = self._l(a)
-        gamma = self._f(gamma, (B,))
-        r = self._f(r, (B,))
+        a = a.reshape(-1).contiguous()
+        gamma, r = gamma.reshape(B).contiguous(), r.reshape(B).contiguous()
         if losses is None:
             losses = torch.empty(4, device=self.device)
         check(lib.sfx_phi_update(self._h, int(policy), s.data_ptr(), a.data_ptr(), r.data_ptr(), s1.data_ptr(),
@@ -497,9 +537,8 @@ class SFEngine:
                         losses: Optional[torch.Tensor] = None) -> torch.Tensor:
         """TSFDQN.update_test_reward_mapper (tsfdqn.py:917-997): updates w, omega and adam_state
         ([2d + 2T], zeros initially) in place; returns losses [3] = (loss, l2, l1)."""
-        s, s1 = self._f(s, (-1,)), self._f(s1, (-1,))
-        phi = self._f(phi, (-1,))
-        a, a1 = self._l(a), self._l(a1)
+        s, s1, phi, a, a1 = (t.reshape(-1).contiguous() for t in self._h2d_many(
+            [(s, torch.float32), (s1, torch.float32), (phi, torch.float32), (a, torch.long), (a1, torch.long)]))
         if losses is None:
             losses = torch.empty(3, device=self.device)
         check(lib.sfx_tsf_test_update(self._h, s.data_ptr(), s1.data_ptr(), a.data_ptr(), a1.data_ptr(), float(r),
@@ -530,10 +569,12 @@ class SFEngine:
         """tsf_test_update for E test tasks in one launch set: W [E, d], Omega [E, T],
         adam_state [E, 2d + 2T] updated in place; rowp [E, 6] device float32 (r, lr_w, wd_w,
         lr_omega, wd_omega, step per task).  Returns losses [E, 3] = (loss, l2, l1) per row."""
-        S, S1 = self._f(S), self._f(S1)
+        S, S1, phi, a, a1 = self._h2d_many([(S, torch.float32), (S1, torch.float32), (phi, torch.float32),
+                                            (a, torch.long), (a1, torch.long)])
+        S, S1 = S.contiguous(), S1.contiguous()
         E = S.shape[0]
-        phi = self._f(phi, (E, self.d))
-        a, a1 = self._l(a), self._l(a1)
+        phi = phi.reshape(E, self.d).contiguous()
+        a, a1 = a.reshape(-1).contiguous(), a1.reshape(-1).contiguous()
         for t in (W, Omega, adam_state, rowp):
             _dev_f32(t, self.device)
             if t.stride(-1) != 1 or t.shape[0] != E:
@@ -550,12 +591,8 @@ class SFEngine:
     def tsf_update(self, policy: int, s, a, r, phi, s1, gamma, use_gpi: bool = True,
                    losses: Optional[torch.Tensor] = None, next_actions: Optional[torch.Tensor] = None):
         """TSFDQN.update_successor (tsfdqn.py:588-709): returns losses [3] = (l1 + beta l2, l1, l2)."""
-        s, s1 = self._f(s), self._f(s1)
+        s, s1, a, phi, gamma, r = self._batch_in(s, s1, a, phi, gamma, r)
         B = s.shape[0]
-        a = self._l(a)
-        phi = self._f(phi, (B, self.d))
-        gamma = self._f(gamma, (B,))
-        r = self._f(r, (B,))
         if losses is None:
             losses = torch.empty(3, device=self.device)
         check(lib.sfx_tsf_update(self._h, int(policy), s.data_ptr(), a.data_ptr(), r.data_ptr(), phi.data_ptr(),

@@ -98,7 +98,9 @@ class RefReplay:
 
 
 class HostReplay:
-    """A numpy ring sampled on the host; one host->device copy per field per replay."""
+    """A numpy ring sampled on the host.  The minibatch stays on the host: DeepSF.update_successor
+    hands host arrays to the engine, which stages all five fields through one pinned slot and
+    one non-blocking copy (a .to(device) per field would be five synchronous pageable copies)."""
 
     def __init__(self, capacity, batch, device, n_s, d):
         self.s = np.zeros((capacity, n_s), np.float32)
@@ -119,10 +121,8 @@ class HostReplay:
         if self.size < self.batch:
             return None
         idx = np.random.randint(0, self.size, size=self.batch)
-        dev = self.device
-        return (torch.from_numpy(self.s[idx]).to(dev), torch.from_numpy(self.a[idx]).to(dev),
-                torch.from_numpy(self.phi[idx]).to(dev), torch.from_numpy(self.s1[idx]).to(dev),
-                torch.from_numpy(self.g[idx]).to(dev))
+        return (torch.from_numpy(self.s[idx]), torch.from_numpy(self.a[idx]), torch.from_numpy(self.phi[idx]),
+                torch.from_numpy(self.s1[idx]), torch.from_numpy(self.g[idx]))
 
 
 class DropinLoop:
