@@ -544,6 +544,10 @@ struct BwdExtra {
   const float* v_xn = nullptr;
   bool skip_fwd = false;      // in: the caller skips the post-update forward of skipped heads
   bool* skip_armed = nullptr; // out: this round's launches decide and honour BwdArgs::skip
+  // launch `li` (tiles `ntile` of one head, grid dim3(ntile)) issued by the caller instead, with
+  // extra workgroups of its own riding along (TSF: k_bwd_tsf); returns true when it launched.
+  // tail_at: the launch holding the loss tail and (not fused) the Adam step bump
+  std::function<bool(int li, int tail_at, const BwdArgs& A, int ntile, double bytes)> ride;
 };
 
 bool can_fuse_v0(const sfx_handle* h, int vM) { return h->fuse_v0 && h->L[0].K <= KFUSE && vM * h->L[0].K <= VFUSE; }
@@ -664,7 +668,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
       launch(h, K_BWD, by, k_bwd_tdg<2, 8>, grid, dim3(256), h->G, A);
     else if (A.tdg)
       launch(h, K_BWD, by, k_bwd_tdg<4, 4>, grid, dim3(256), h->G, A);
-    else
+    else if (!(ex.ride && nhead == 1 && !A.xcd && ex.ride(li, tail_at, A, ntile, by)))
       launch(h, K_BWD, by, h->bf16 ? k_bwd<true> : k_bwd<false>, grid, dim3(256), h->G, A);
     if (ex.hook && li == ex.hook_after && !h->rec) RC(ex.hook());
   }
@@ -691,8 +695,9 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     h->rec->bytes.push_back(nhead * (dw_bytes(1) + dw_bytes(0)));
     return SFX_OK;
   }
-  launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), h->bf16 ? k_bwd<true> : k_bwd<false>,
-         A.xcd ? dim3(8 * cdiv(nhead, 8) * ntile) : dim3(ntile, nhead), dim3(256), h->G, A);
+  if (!(ex.ride && nhead == 1 && !A.xcd && ex.ride(h->NL - 1, tail_at, A, ntile, nhead * (dw_bytes(1) + dw_bytes(0)))))
+    launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), h->bf16 ? k_bwd<true> : k_bwd<false>,
+           A.xcd ? dim3(8 * cdiv(nhead, 8) * ntile) : dim3(ntile, nhead), dim3(256), h->G, A);
   LAUNCHCHK();
   if (ex.hook && ex.hook_after >= h->NL - 1) RC(ex.hook());  // fewer launches than hook_after + 1
   return SFX_OK;

@@ -1461,7 +1461,7 @@ __device__ void role_v0_only(const Geo& G, const BwdArgs& A, int head, const Rol
 }
 
 template <bool C = false, bool BF = false>
-__device__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile, bool fuse) {
+__device__ __forceinline__ void role_dw(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile, bool fuse) {
   const int N = L.N, K = L.K, M = A.M;
   const int ntk = (K + 63) >> 6;
   const int kt = tile % ntk, nt = tile / ntk;
@@ -1754,7 +1754,7 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // loss finalisation, optional w step, Adam step counter (one workgroup per head).  The host
 // drops the tail when it has nothing to do (no losses requested, no w step, step bumped in
 // the fused TD launch).
-__device__ void role_tail(const Geo& G, const BwdArgs& A, int head) {
+__device__ __forceinline__ void role_tail(const Geo& G, const BwdArgs& A, int head) {
   const int M = A.M, d = G.d, tid = threadIdx.x;
   __shared__ float s_e[MMAX];
   __shared__ float s_red[256];
@@ -1807,15 +1807,10 @@ __device__ void role_tail(const Geo& G, const BwdArgs& A, int head) {
   }
 }
 
-template <bool BF = false>
-__global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
-  __shared__ floatx4 red[4][2][64];
+// tile bx of head `head` of a backward launch (k_bwd; k_bwd_tsf after its TSF blocks)
+template <bool BF>
+__device__ __forceinline__ void bwd_body(const Geo& G, const BwdArgs& A, int head, int bx, floatx4 (*red)[2][64]) {
   PROBE_T(pt0);
-  int head = A.head0 + blockIdx.y, bx = blockIdx.x;
-  if (A.xcd) {
-    if (!xcd_decode(blockIdx.x, A.nhead, A.na + A.nb + A.nc + A.tail, head, bx)) return;
-    head += A.head0;
-  }
   PROBE_MARKA();
   const bool skip = A.skip && __builtin_nontemporal_load(A.skip + head) != 0;  // repeats round r-1
   // tiles of a head in dispatch order, longest first so they request their operands before the
@@ -1847,6 +1842,17 @@ __global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
     return;
   }
   role_tail(G, A, head);
+}
+
+template <bool BF = false>
+__global__ __launch_bounds__(256) void k_bwd(Geo G, BwdArgs A) {
+  __shared__ floatx4 red[4][2][64];
+  int head = A.head0 + blockIdx.y, bx = blockIdx.x;
+  if (A.xcd) {
+    if (!xcd_decode(blockIdx.x, A.nhead, A.na + A.nb + A.nc + A.tail, head, bx)) return;
+    head += A.head0;
+  }
+  bwd_body<BF>(G, A, head, bx, red);
 }
 
 // First backward launch with K2 fused: dX of the last layer only (A.na tiles per head).

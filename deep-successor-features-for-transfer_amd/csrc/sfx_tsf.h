@@ -89,6 +89,49 @@ struct TsfArgs {
 
 __device__ __forceinline__ int tsf_flow_stride(int n_s) { return 2 * n_s + 1; }
 
+// LDS carve of the backward roles (float offsets, 16-byte aligned), from the geometry: the
+// flow-row role, the h / g-Linear / w roles and k_tsf_flow's flows each start at 0 of the same
+// buffer.  k_tsf_bwd holds TSF_SM floats (enough for every geometry sfx_tsf_setup accepts);
+// k_bwd_tsf, which shares its workgroups' LDS with the ψ backward tiles, holds TSFX_SM, and the
+// host rides the TSF backward along only when the carve fits (tsf_bwd_lds(...).total).
+constexpr int TSFX_SM = 20480;
+__host__ __device__ constexpr int tsf_r4(int n) { return (n + 3) & ~3; }
+__host__ __device__ constexpr int tsf_imax(int a, int b) { return a > b ? a : b; }
+struct TsfBwdLds {
+  int t, wlT, whT, dg, da, gc, fa, flow_total;  // flow-row role
+  int rda, rgf, rzk, rtp, rgc, rdg, role_total;  // h / g-Linear / w roles
+  int fdz, fda, ft, fk_total;                    // k_tsf_flow (s_z at 0)
+  int total;
+};
+__host__ __device__ inline TsfBwdLds tsf_bwd_lds(int K, int np, int G, int d, int B) {
+  TsfBwdLds L{};
+  const int FR = TSF_FR, G4 = tsf_r4(G), D4 = tsf_r4(d), R2 = 2 * B;
+  int o = 0;
+  L.t = o;   o += tsf_r4(K * FR);
+  L.wlT = o; o += np * G4;
+  L.whT = o; o += G * D4;
+  L.dg = o;  o += tsf_r4(tsf_imax(FR * G4, FR * d));  // φ̃ rows while staging
+  L.da = o;  o += tsf_r4(FR * d);
+  L.gc = o;  o += tsf_imax(FR * D4, FR * np);
+  L.fa = o;  o += K * tsf_fst(np);
+  L.flow_total = K > 0 ? o : 0;
+  o = 0;
+  L.rda = o; o += tsf_r4(B * d);
+  L.rgf = o;                                            // h role: [2B][G]; g-Linear: W_h columns, z_K
+  L.rzk = o + tsf_r4(d * TSF_QS);
+  o += tsf_imax(tsf_r4(R2 * G), tsf_r4(d * TSF_QS) + R2 * np);
+  L.rtp = o; o += tsf_r4(B * d);
+  L.rgc = o; o += tsf_r4(B * d);
+  L.rdg = o; o += B * TSF_QS;
+  L.role_total = o;
+  L.fdz = R2 * np;
+  L.fda = 2 * R2 * np;
+  L.ft = L.fda + tsf_r4(R2);
+  L.fk_total = K > 0 ? L.ft + tsf_r4(R2) : 0;
+  L.total = tsf_imax(tsf_imax(L.flow_total, L.role_total), L.fk_total);
+  return L;
+}
+
 // tanh without branches: for |x| < 0.625 the same odd minimax polynomial (same coefficients,
 // same operation order) as the device library's tanhf, else 1 − 2 / (e^{2|x|} + 1) by v_exp /
 // v_rcp; both are evaluated and selected, so a flow step's chain has no exec-mask branches.
@@ -443,19 +486,20 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A, const float* __restr
 // step's critical path is two operations (da_k = su_k (1 - t_k^2), then that FMA); the update
 // dz_k = dz_{k+1} + da_k w_k and the stores of dz_{k+1}, da_k run beside it.
 template <int NP>
-__device__ void tsf_bwd_flows(const TsfArgs& A, const float* __restrict__ sfl, float* sm, float* s_dr, float* s_w,
+__device__ __forceinline__ void tsf_bwd_flows(const TsfArgs& A, const float* __restrict__ sfl, float* sm, float* s_dr, float* s_w,
                               float* s_r, int* s_ab, int f) {
   constexpr int FR = TSF_FR, PST = tsf_pst(NP), FA = tsf_fst(NP);
   const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
   const int fs = tsf_flow_stride(n_s), nfl = K * fs;
   const int D4 = (d + 3) & ~3, G4 = (G + 3) & ~3;   // rows padded to 16 bytes (zeros)
-  float* s_t = sm;                                  // [K][FR]
-  float* s_wlT = s_t + TSF_TS;                      // Linear of g (pre-step), transposed: [NP][G4]
-  float* s_whT = s_wlT + TSF_LDS / 2;               // W_h (pre-step), transposed: [G][D4]
-  float* s_dg = s_whT + TSF_LDS;                    // [FR][G4] (φ̃ rows while staging)
-  float* s_da = s_dg + 2048;                        // [FR][d]
-  float* s_gc = s_da + 2048;                        // ψ output gradient rows; daff [FR][D4]; dz_K [FR][NP]
-  float* s_fa = s_gc + 2048;                        // [K][FA] flows, chain layout
+  const TsfBwdLds L = tsf_bwd_lds(K, NP, G, d, B);
+  float* s_t = sm + L.t;                            // [K][FR]
+  float* s_wlT = sm + L.wlT;                        // Linear of g (pre-step), transposed: [NP][G4]
+  float* s_whT = sm + L.whT;                        // W_h (pre-step), transposed: [G][D4]
+  float* s_dg = sm + L.dg;                          // [FR][G4] (φ̃ rows while staging)
+  float* s_da = sm + L.da;                          // [FR][d]
+  float* s_gc = sm + L.gc;                          // ψ output gradient rows; daff [FR][D4]; dz_K [FR][NP]
+  float* s_fa = sm + L.fa;                          // [K][FA] flows, chain layout
   PROBE_T(t0_);
   const int r0 = f * FR;
   const int nr = min(FR, R2 - r0);
@@ -567,15 +611,13 @@ __device__ void tsf_bwd_flows(const TsfArgs& A, const float* __restrict__ sfl, f
   PROBE_REC(11, t0_);
 }
 
-// grid nflow + nh + nlin + 1, 256 threads (roles: see the header comment)
+// workgroup `role` of the backward (grid nflow + nh + nlin + 1, 256 threads; roles: see the
+// header comment); sm holds tsf_bwd_lds(...).total floats
 template <int NP>
-__global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A, const float* __restrict__ sfl) {
-  __shared__ __attribute__((aligned(16))) float sm[TSF_SM];
-  __shared__ float s_dr[64], s_r[64], s_w[256], s_red[256];
-  __shared__ int s_ab[64];
+__device__ __forceinline__ void tsf_bwd_block(const TsfArgs& A, const float* __restrict__ sfl, float* sm, float* s_dr, float* s_r,
+                              float* s_w, float* s_red, int* s_ab, int role) {
   const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
   const int fs = tsf_flow_stride(n_s), nfl = K * fs;
-  int role = blockIdx.x;
   if (role < A.nflow) {
     tsf_bwd_flows<NP>(A, sfl, sm, s_dr, s_w, s_r, s_ab, role);
     return;
@@ -586,16 +628,16 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A, const float* __restr
   const int step = *A.step;
   const int cx = step_cancelled(A.cancel);
   const FDiv fG = fdiv(G);
-  // LDS: daff [0, 4096) | role operands [4096, 12288) | φ̃ rows [12288, 16384) | ψ gradient rows
-  // [16384, 20480) | g-Linear dg [20480, 21504)
-  float* s_da = sm;
-  float* s_tp = sm + 3 * (TSF_LDS / 2);
-  float* s_gc = sm + 4 * (TSF_LDS / 2);
+  // LDS (tsf_bwd_lds): daff | role operands | φ̃ rows | ψ gradient rows | g-Linear dg
+  const TsfBwdLds L = tsf_bwd_lds(K, NP, G, d, B);
+  float* s_da = sm + L.rda;
+  float* s_tp = sm + L.rtp;
+  float* s_gc = sm + L.rgc;
   const bool wrole = role == A.nh + A.nlin;
-  float* s_gf = sm + TSF_LDS / 2;       // h role: [2B][G]
-  float* s_whs = sm + TSF_LDS / 2;      // g-Linear role: [d][TSF_QS] pre-step W_h columns
-  float* s_zk = s_whs + TSF_LDS / 2;    // g-Linear role: [2B][NP] z_K (<= 4096)
-  float* s_dg = sm + 5 * (TSF_LDS / 2); // g-Linear role: [B][TSF_QS] (after the φ̃ / gradient rows)
+  float* s_gf = sm + L.rgf;   // h role: [2B][G]
+  float* s_whs = sm + L.rgf;  // g-Linear role: [d][TSF_QS] pre-step W_h columns
+  float* s_zk = sm + L.rzk;   // g-Linear role: [2B][NP] z_K
+  float* s_dg = sm + L.rdg;   // g-Linear role: [B][TSF_QS]
   const int q0 = (role - A.nh) * TSF_QS, nq = min(TSF_QS, G - q0);
   if (!wrole && role < A.nh) {
     glds(s_gf, R2 * G, [&](int j) { return A.gfeat + j; });
@@ -681,15 +723,25 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A, const float* __restr
   PROBE_REC(13, t0_);
 }
 
+template <int NP>
+__global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A, const float* __restrict__ sfl) {
+  __shared__ __attribute__((aligned(16))) float sm[TSF_SM];
+  __shared__ float s_dr[64], s_r[64], s_w[256], s_red[256];
+  __shared__ int s_ab[64];
+  tsf_bwd_block<NP>(A, sfl, sm, s_dr, s_r, s_w, s_red, s_ab, blockIdx.x);
+}
+
 // flow parameters: Σ over the s rows + Σ over the s1 rows of the per-row terms (the two
 // g_backward calls of the reference), then Adam.  grid K (one workgroup per flow), 256 threads:
 // the flow's saved states z_k, tanh outputs t_k and the rows' (dz_{k+1}, da_k) into LDS, then
 // thread e of [0, 2 n_s + 1) sums its parameter's terms row by row:
 //   w_i: da_k z_k[i]     b: da_k     u_i: dz_{k+1}[i] t_k
-__global__ __launch_bounds__(256) void k_tsf_flow(TsfArgs A) {
-  __shared__ float s_z[128 * TSF_NS], s_dz[128 * TSF_NS], s_da[128], s_t[128];  // 2B <= 128 rows
+// sm: tsf_bwd_lds(...).fk_total floats
+__device__ __forceinline__ void tsf_flow_block(const TsfArgs& A, float* sm, int k) {
   const int tid = threadIdx.x, n_s = A.n_s, fs = tsf_flow_stride(n_s), B = A.B, R2 = 2 * B, NP = A.np;
-  const int PST = tsf_pst(NP), k = blockIdx.x;
+  const int PST = tsf_pst(NP);
+  const TsfBwdLds L = tsf_bwd_lds(A.K, NP, A.G, A.d, B);
+  float *s_z = sm, *s_dz = sm + L.fdz, *s_da = sm + L.fda, *s_t = sm + L.ft;
   PROBE_T(t0_);
   const FDiv fnp = fdiv(NP);
   glds(s_z, R2 * NP, [&](int j) { return A.zs + (size_t)k * R2 * NP + j; });
@@ -718,6 +770,35 @@ __global__ __launch_bounds__(256) void k_tsf_flow(TsfArgs A) {
   const long long go = (long long)A.pol * A.Pg + (long long)k * fs + e;
   if (!step_cancelled(A.cancel)) adam_el(A.g + go, A.gm + go, A.gv + go, g, adam_consts(A.hpf, *A.step));
   PROBE_REC(15, t0_);
+}
+
+__global__ __launch_bounds__(256) void k_tsf_flow(TsfArgs A) {
+  __shared__ __attribute__((aligned(16))) float sm[2 * 128 * TSF_NS + 256];  // 2B <= 128 rows
+  tsf_flow_block(A, sm, blockIdx.x);
+}
+
+// A ψ backward launch (k_bwd's tiles) with TSF-DQN's backward riding along in the same grid
+// (sfx_tsf.inc): blocks [0, ntsf) run TSF work -- mode 1 k_tsf_bwd's roles, mode 2 k_tsf_flow's
+// flows -- and the rest k_bwd's tiles of one head.  The TSF chains (≈24 µs at K = 100) then run
+// beside the ψ tiles instead of as launches of their own on the step's critical path; the LDS
+// of the two halves is allocated side by side (k_bwd's + TSFX_SM floats), so the host rides
+// along only when the TSF carve fits and the grid stays within one workgroup per CU.
+template <int NP, bool BF>
+__global__ __launch_bounds__(256) void k_bwd_tsf(Geo G, BwdArgs A, TsfArgs T, const float* __restrict__ sfl,
+                                                  int mode, int ntsf) {
+  __shared__ floatx4 red[4][2][64];
+  __shared__ __attribute__((aligned(16))) float sm[TSFX_SM];
+  __shared__ float s_dr[64], s_r[64], s_w[256], s_red[256];
+  __shared__ int s_ab[64];
+  const int bx = blockIdx.x;
+  if (bx < ntsf) {
+    if (mode == 1)
+      tsf_bwd_block<NP>(T, sfl, sm, s_dr, s_r, s_w, s_red, s_ab, bx);
+    else
+      tsf_flow_block(T, sm, bx);
+    return;
+  }
+  bwd_body<BF>(G, A, A.head0, bx - ntsf, red);
 }
 
 // -------------------------------------------------------------------------------------
