@@ -362,6 +362,10 @@ struct FwdExtra {
   const int* skip = nullptr;  // post-update forward of rounds r >= 1 (FwdArgs::skip; one group)
   int* qh = nullptr;          // sharded rounds: the local heads' maxima terms (FwdArgs::qh)
   int* qhs = nullptr;
+  // the first launch when it is the fused layer-0+1 one (k_fwd<true, 8, true, BF>, one column
+  // tile per workgroup): issued by the caller instead, with workgroups of its own riding along
+  // (TSF: k_fwd_tsf); returns true when it launched
+  std::function<bool(const FwdArgs& F, dim3 grid, double bytes)> ride_l0;
 };
 
 int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const float* xa, const float* xb,
@@ -453,10 +457,11 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
       h->rec->bytes.push_back(by);
       h->rec->fvec = h->rec->fvec && (L.K % 64) == 0 && aligned && !l0;
     } else if (l0) {
-      launch(h, K_FWD, by,
-             tp2 ? (h->bf16 ? k_fwd<true, 8, true, true, 2> : k_fwd<true, 8, true, false, 2>)
-                 : (h->bf16 ? k_fwd<true, 8, true, true> : k_fwd<true, 8, true>),
-             grid, dim3(512), h->G, F);
+      if (!(ex.ride_l0 && !tp2 && !F.xcd && ex.ride_l0(F, grid, by)))
+        launch(h, K_FWD, by,
+               tp2 ? (h->bf16 ? k_fwd<true, 8, true, true, 2> : k_fwd<true, 8, true, false, 2>)
+                   : (h->bf16 ? k_fwd<true, 8, true, true> : k_fwd<true, 8, true>),
+               grid, dim3(512), h->G, F);
     } else if (h->fwd_waves == 8) {
       const bool vec = (L.K % 32) == 0 && aligned;
       launch(h, K_FWD, by,

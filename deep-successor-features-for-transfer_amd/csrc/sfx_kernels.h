@@ -782,13 +782,14 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
 
 constexpr int qa_tile_floats(bool L0) { return L0 ? 1 : 32 * 16; }  // L0 launches never accumulate
 
-template <bool VEC, int NW, bool L0, bool BF = false, int TP = 1>
-__global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
+// workgroup (bx, by, bz) of a forward launch's grid (k_fwd; k_fwd_tsf after its TSF blocks)
+template <bool VEC, int NW, bool L0, bool BF, int TP>
+__device__ __forceinline__ void fwd_body(const Geo& G, const FwdArgs& F, int bx, int by, int bz) {
   PROBE_T(pt0);
-  int y = blockIdx.y, tN = blockIdx.x, tM = blockIdx.z;
+  int y = by, tN = bx, tM = bz;
   const int ntNb = TP > 1 ? (F.ntN + F.tpw - 1) / F.tpw : F.ntN;  // workgroups along N
   if (F.xcd) {  // head h's tiles on the XCD of slot h % 8 (see xcd_decode)
-    const int b = blockIdx.x, hp = (F.nh + 7) >> 3, k = b >> 3;
+    const int b = bx, hp = (F.nh + 7) >> 3, k = b >> 3;
     const int r = hp == 1 ? k : k / fdiv(hp), hd = (b & 7) + 8 * (k - r * hp);
     const int rN = r / fdiv(ntNb), gi = rN / fdiv(F.ntM);
     tN = r - rN * ntNb;
@@ -816,11 +817,16 @@ __global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
   __shared__ float sT[qa_tile_floats(L0)];
   fwd_tile<VEC, NW, L0, false, BF, TP>(G, F, y, tN, tM, qa ? sT : nullptr);
   if (qa) q_accumulate(G, F, head, tN, tM, sT);
-  if (tN == 0 && tM == 0 && blockIdx.y == 0 && (F.xcd ? blockIdx.x == 0 : true)) {
+  if (tN == 0 && tM == 0 && by == 0 && (F.xcd ? bx == 0 : true)) {
     if (F.flag && threadIdx.x == 0) *F.flag = F.flag_value;
     if (F.lms_head >= 0) lms_block(G, F);
   }
   PROBE_REC(L0 ? 2 : 1, pt0);
+}
+
+template <bool VEC, int NW, bool L0, bool BF = false, int TP = 1>
+__global__ __launch_bounds__(64 * NW) void k_fwd(Geo G, FwdArgs F) {
+  fwd_body<VEC, NW, L0, BF, TP>(G, F, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // K1b  Forward of a wide layer (N >= GEMV_N) for a few rows (M <= GEMV_M: the B = 1 action

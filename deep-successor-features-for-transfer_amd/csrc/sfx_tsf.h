@@ -132,6 +132,29 @@ __host__ __device__ inline TsfBwdLds tsf_bwd_lds(int K, int np, int G, int d, in
   return L;
 }
 
+// LDS carve of k_tsf_fwd (float offsets, 16-byte aligned), from the geometry; k_fwd_tsf (the
+// forward riding along in the ψ forward's first launch) holds TSFXF_SM floats of it.
+constexpr int TSFXF_SM = 20480;
+struct TsfFwdLds {
+  int fa, wl, wh, gf, z, ph, bl, bh, total;
+};
+__host__ __device__ inline TsfFwdLds tsf_fwd_lds(int K, int np, int G, int d) {
+  TsfFwdLds L{};
+  const int GP = tsf_r4(G), RPW = 2 * TSF_PB;
+  int o = 0;
+  L.fa = o; o += K * tsf_fst(np);  // flows, chain layout
+  L.wl = o; o += G * np;           // Linear of g: [G][NP]
+  L.wh = o; o += d * GP;           // W_h: [d][GP]
+  L.gf = o; o += RPW * GP;         // g features [RPW][GP]
+  L.z = o;  o += RPW * np;         // z_K rows [RPW][NP]
+  L.ph = o; o += tsf_r4(TSF_PB * d);  // φ rows [PB][d]
+  L.bl = o; o += tsf_r4(G);
+  L.bh = o; o += tsf_r4(d);
+  L.total = o;
+  return L;
+}
+constexpr int TSF_FWD_SM = TSF_FA + TSF_LDS / 2 + TSF_LDS + TSF_LDS / 2 + 2 * TSF_PB * TSF_NS + 1024 + 512;
+
 // tanh without branches: for |x| < 0.625 the same odd minimax polynomial (same coefficients,
 // same operation order) as the device library's tanhf, else 1 − 2 / (e^{2|x|} + 1) by v_exp /
 // v_rcp; both are evaluated and selected, so a flow step's chain has no exec-mask branches.
@@ -336,19 +359,18 @@ __device__ float tsf_stage_daff(const TsfArgs& A, int n, BMap bmap, float* s_tp,
 //      run beside it.  Waves 1-3 meanwhile stage the Linear of g, W_h, b_h and φ, and write the
 //      snapshot of g_i, h, w_i (read by k_tsf_bwd) from global memory;
 //   C  Linear(n_s, G) of g for the workgroup's rows, then φ̃ = (h(g(s)) + h(g(s1))) ⊙ φ.
+// workgroup blk of nblk (threads past 256 of a wider workgroup -- k_fwd_tsf's -- only join the
+// barriers); sm holds tsf_fwd_lds(...).total floats
 template <int NP>
-__global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A, const float* __restrict__ gfl) {
+__device__ __forceinline__ void tsf_fwd_body(const TsfArgs& A, const float* __restrict__ gfl, float* sm, int blk,
+                                             int nblk) {
   constexpr int PB = TSF_PB, RPW = 2 * PB, FA = tsf_fst(NP);
-  __shared__ __attribute__((aligned(16))) float s_fa[TSF_FA];       // flows, chain layout
-  __shared__ __attribute__((aligned(16))) float s_wl[TSF_LDS / 2];  // Linear of g: [G][NP]
-  __shared__ __attribute__((aligned(16))) float s_wh[TSF_LDS];      // W_h: [d][GP]
-  __shared__ __attribute__((aligned(16))) float s_gf[TSF_LDS / 2];  // g features [RPW][GP]
-  __shared__ __attribute__((aligned(16))) float s_z[RPW * TSF_NS];  // z_K rows [RPW][NP]
-  __shared__ float s_ph[1024];                                      // φ rows [PB][d]
-  __shared__ float s_bl[256], s_bh[256];
   const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
   const int fs = tsf_flow_stride(n_s), nfl = K * fs, GP = (G + 3) & ~3;
-  const int b0 = blockIdx.x * PB, nb = min(PB, B - b0);
+  const TsfFwdLds L = tsf_fwd_lds(K, NP, G, d);
+  float *s_fa = sm + L.fa, *s_wl = sm + L.wl, *s_wh = sm + L.wh, *s_gf = sm + L.gf, *s_z = sm + L.z;
+  float *s_ph = sm + L.ph, *s_bl = sm + L.bl, *s_bh = sm + L.bh;
+  const int b0 = blk * PB, nb = min(PB, B - b0);
   PROBE_T(t0_);
   tsf_stage_flows<NP>(s_fa, gfl, K, n_s);
   // flow row rl = tid / LPR on lanes [LPR rl, LPR rl + LPR) (components [hf NL, hf NL + NL) each):
@@ -431,7 +453,7 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A, const float* __restr
       tsf_store<NL>(s_z + rl * NP + hf * NL, z);
       PROBE_AT(2);
     }
-  } else if (tid >= 64) {
+  } else if (tid < 256) {
     const FDiv fnp = fdiv(NP), fgp = fdiv(GP);
     const float* Wl = gfl + nfl;
     glds(s_wl, G * NP, [&](int j) -> const float* {
@@ -446,13 +468,13 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A, const float* __restr
     glds(s_bh, d, [&](int j) { return A.hp + d * G + j; }, 1, 3);
     glds(s_ph, nb * d, [&](int j) { return A.phi + (size_t)b0 * d + j; }, 1, 3);
     // this workgroup's slice of the pre-step snapshot of g_i, h, w_i
-    const int S = A.Pg + A.Ph + d, per = (S + gridDim.x - 1) / gridDim.x;
-    const int lo = blockIdx.x * per, hi = min(S, lo + per);
+    const int S = A.Pg + A.Ph + d, per = (S + nblk - 1) / nblk;
+    const int lo = blk * per, hi = min(S, lo + per);
     for (int j = lo + tid - 64; j < hi; j += 192)
       A.snap[j] = j < A.Pg ? gfl[j] : (j < A.Pg + A.Ph ? A.hp[j - A.Pg] : A.w[j - A.Pg - A.Ph]);
   }
   __syncthreads();
-  {  // Linear(n_s, G) of g for this workgroup's rows (columns past G: zero)
+  if (tid < 256) {  // Linear(n_s, G) of g for this workgroup's rows (columns past G: zero)
     const FDiv fgp = fdiv(GP);
     for (int j = tid; j < RPW * GP; j += 256) {
       const int r = j / fgp, c = j - r * GP;
@@ -469,7 +491,7 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A, const float* __restr
   PROBE_AT(3);
   // φ̃ = (h(g(s)) + h(g(s1))) ⊙ φ
   const FDiv fd = fdiv(d);
-  for (int j = tid; j < nb * d; j += 256) {
+  for (int j = tid; j < (tid < 256 ? nb * d : 0); j += 256) {
     const int r = j / fd, c = j - r * d, bb = b0 + r;
     const float h0 = tsf_dot4(s_gf + r * GP, s_wh + c * GP, GP / 4);
     const float h1 = tsf_dot4(s_gf + (PB + r) * GP, s_wh + c * GP, GP / 4);
@@ -478,6 +500,12 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A, const float* __restr
     A.tphi[(size_t)bb * d + c] = __fmul_rn(aff, s_ph[j]);
   }
   PROBE_REC(10, t0_);
+}
+
+template <int NP>
+__global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A, const float* __restrict__ gfl) {
+  __shared__ __attribute__((aligned(16))) float sm[TSF_FWD_SM];
+  tsf_fwd_body<NP>(A, gfl, sm, blockIdx.x, gridDim.x);
 }
 
 // flow-row role: rows [f FR, (f+1) FR) of the 2B rows; lanes 0..FR-1 of wave 0 run the reverse
@@ -799,6 +827,22 @@ __global__ __launch_bounds__(256) void k_bwd_tsf(Geo G, BwdArgs A, TsfArgs T, co
     return;
   }
   bwd_body<BF>(G, A, A.head0, bx - ntsf, red);
+}
+
+// The ψ forward's first launch (layers 0 + 1 from the states, k_fwd<true, 8, true, BF>) with
+// k_tsf_fwd's workgroups riding along first in the same grid: the flow chains run beside the ψ
+// tiles.  (gx, gy) = the ψ launch's own grid; its workgroup r is (r % gx, r / gx % gy, r / gx gy).
+template <int NP, bool BF>
+__global__ __launch_bounds__(512) void k_fwd_tsf(Geo G, FwdArgs F, TsfArgs T, const float* __restrict__ gfl,
+                                                  int ntsf, int gx, int gy) {
+  __shared__ __attribute__((aligned(16))) float sm[TSFXF_SM];
+  const int b = blockIdx.x;
+  if (b < ntsf) {
+    tsf_fwd_body<NP>(T, gfl, sm, b, ntsf);
+    return;
+  }
+  const int r = b - ntsf;
+  fwd_body<true, 8, true, BF, 1>(G, F, r % gx, (r / gx) % gy, r / (gx * gy));
 }
 
 // -------------------------------------------------------------------------------------
