@@ -38,7 +38,7 @@ def _need_gpu():
         pytest.skip("no HIP device")
 
 
-def _run_rank(rank, cfg, comm, force_rerun=None):
+def _run_rank(rank, cfg, comm, force_rerun=None, gate_timeout=None):
     from sfx.engine import SFEngine
     from sfx.init import reference_heads
     from sfx.runner import NativeEnvLoop
@@ -66,6 +66,8 @@ def _run_rank(rank, cfg, comm, force_rerun=None):
         eng.debug_force_rerun(force_rerun)  # every step's device rounds count as failed: host rounds
     loop.prefill(cfg["prefill"])  # the first steps run without a minibatch
     loop.set_task(Tg - 1)
+    if gate_timeout is not None:
+        loop.set_gate_timeout(gate_timeout)
     loop.record(cfg["steps"])
     loop.run(cfg["steps"])
     recs = loop.records()
@@ -129,6 +131,20 @@ def test_native_sharded_rccl_host_rounds_pipelined(monkeypatch):
     recs, final, heads, targets, ws, stats, counters = _run_rank(0, cfg, "rccl", force_rerun=1)
     assert stats["host_round_steps"] >= 4, stats
     assert stats["prelaunched"] >= cfg["steps"] // 2, stats
+    _oracle_check(cfg, recs, final, heads, targets, ws)
+
+
+def test_native_sharded_one_rank_gate_timeouts_recompute():
+    """one rank, no collective, a 10 ns gate bound and every step's device rounds
+    treated as failed: each step's host rounds find the next pre-launched steps cancelled at their
+    gates (their launches ran over the step's transient buffers), so the runner recomputes the
+    step's forward and device rounds from the pre-step slot before its host rounds -- as the
+    all-task schedule does -- instead of failing the run.  The oracle replay must still reproduce
+    every env action and the parameters."""
+    cfg = dict(SMALL, world=1, t_loc=4)
+    recs, final, heads, targets, ws, stats, counters = _run_rank(0, cfg, "rccl", force_rerun=1, gate_timeout=1e-8)
+    assert stats["retried"] > 0 and stats["recomputed"] > 0, stats
+    assert counters.sum() == cfg["steps"]
     _oracle_check(cfg, recs, final, heads, targets, ws)
 
 
