@@ -1,12 +1,22 @@
 #!/bin/bash
-# Host-side AddressSanitizer + UndefinedBehaviorSanitizer build of the runner driver with libsfx's
-# sources compiled in.  Every -fsanitize= follows -Xarch_host: only host code is instrumented (the
-# GPU kernels are built as in csrc/Makefile).  Output: tools/hostsan/runner_hostsan (git-ignored).
-# Run on the GPU box:  ASAN_OPTIONS=detect_leaks=0:verify_asan_link_order=0 tools/hostsan/runner_hostsan
+# Host-side sanitizer builds of the runner driver with libsfx's sources compiled in.  Every
+# -fsanitize= follows -Xarch_host: only host code is instrumented (the GPU kernels are built as in
+# csrc/Makefile).  Outputs (git-ignored) in tools/hostsan/:
+#   runner_asan   AddressSanitizer                       (default)
+#   runner_ubsan  UndefinedBehaviorSanitizer, no recover ("ubsan")
+# Run on the GPU box:
+#   ASAN_OPTIONS=detect_leaks=0:verify_asan_link_order=0 tools/hostsan/runner_asan
+#   UBSAN_OPTIONS=print_stacktrace=1 tools/hostsan/runner_ubsan
 set -e
 cd "$(dirname "$0")"
 CSRC=../../deep-successor-features-for-transfer_amd/csrc
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -g -std=c++17 -ffp-contract=off -fno-omit-frame-pointer \
-  -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined \
-  -I"$CSRC" -o runner_hostsan runner_hostsan.cpp "$CSRC/sfx.hip" -ldl
-echo built tools/hostsan/runner_hostsan
+F="--offload-arch=gfx950 -O3 -g -std=c++17 -ffp-contract=off -fno-omit-frame-pointer -I$CSRC"
+if [ "${1:-asan}" = ubsan ]; then
+  /opt/rocm/bin/hipcc $F -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize=function,vptr \
+    -Xarch_host -fno-sanitize-recover=undefined -o runner_ubsan runner_hostsan.cpp "$CSRC/sfx.hip" -ldl
+  echo built tools/hostsan/runner_ubsan
+else
+  /opt/rocm/bin/hipcc $F -Xarch_host -fsanitize=address -Xarch_host -fsanitize-address-use-after-return=never \
+    -o runner_asan runner_hostsan.cpp "$CSRC/sfx.hip" -ldl
+  echo built tools/hostsan/runner_asan
+fi
