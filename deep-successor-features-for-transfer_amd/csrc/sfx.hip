@@ -1307,6 +1307,19 @@ int sfx_load_w(sfx_t h, int t, const float* w_host) {
   return SFX_OK;
 }
 
+// w_t with its Adam moments (the sfdqn.py l2 path's w optimizer state; checkpoint resume)
+int sfx_load_w_state(sfx_t h, int t, const float* w_host, const float* wm_host, const float* wv_host) {
+  RC(settle(h));
+  if (!valid_w(h, t) || !w_host || !wm_host || !wv_host) SFX_FAIL(SFX_E_ARG, "bad args");
+  HIPCHK(hipStreamSynchronize(h->stream));
+  const size_t o = (size_t)t * h->dpad, n = sizeof(float) * h->d;
+  HIPCHK(hipMemcpyAsync(h->w + o, w_host, n, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->wm + o, wm_host, n, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->wv + o, wv_host, n, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return SFX_OK;
+}
+
 int sfx_get_w(sfx_t h, int t, float* w_host, float* wm_host, float* wv_host) {
   RC(settle(h));
   if (!valid_w(h, t)) SFX_FAIL(SFX_E_ARG, "bad head");

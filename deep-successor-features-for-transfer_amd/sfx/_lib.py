@@ -32,6 +32,7 @@ SIGNATURES = {
     "sfx_get_adam": (_I, [_VP, _I, _FP, _FP, _IP]),
     "sfx_load_w": (_I, [_VP, _I, _FP]),
     "sfx_get_w": (_I, [_VP, _I, _FP, _FP, _FP]),
+    "sfx_load_w_state": (_I, [_VP, _I, _FP, _FP, _FP]),
     "sfx_w_ptr": (_I, [_VP, _I, C.POINTER(_VP)]),
     "sfx_gpi": (_I, [_VP, _VP, _I, _VP, _VP, _VP, _VP, _VP]),
     "sfx_successors": (_I, [_VP, _VP, _I, _I, _VP]),

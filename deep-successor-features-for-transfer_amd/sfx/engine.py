@@ -54,6 +54,8 @@ class SFEngine:
         self._sel = torch.zeros(2, dtype=torch.long, device=self.device)
         self.T_glob, self.head_offset = T, 0
         self._refresh_w_ptrs(T)
+        # the library's Adam defaults (sfx_set_adam replaces them); kept for checkpoints
+        self.adam_hp = dict(lr_psi=1e-3, wd_psi=0.0, lr_w=1e-3, wd_w=0.0, betas=(0.9, 0.999), eps=1e-8)
 
     def shard_setup(self, T_glob: int, head_offset: int):
         """This engine's T heads become the global heads [head_offset, head_offset + T) of T_glob;
@@ -182,6 +184,8 @@ class SFEngine:
     def set_adam(self, lr_psi=1e-3, wd_psi=0.0, lr_w=1e-3, wd_w=0.0, betas=(0.9, 0.999), eps=1e-8):
         check(lib.sfx_set_adam(self._h, float(lr_psi), float(wd_psi), float(lr_w), float(wd_w),
                                float(betas[0]), float(betas[1]), float(eps)), "sfx_set_adam")
+        self.adam_hp = dict(lr_psi=float(lr_psi), wd_psi=float(wd_psi), lr_w=float(lr_w), wd_w=float(wd_w),
+                            betas=(float(betas[0]), float(betas[1])), eps=float(eps))
 
     def set_graphs(self, enable: bool):
         check(lib.sfx_set_graphs(self._h, int(bool(enable))), "sfx_set_graphs")
@@ -218,6 +222,14 @@ class SFEngine:
         if a.size != self.d:
             raise ValueError("w must have d entries")
         check(lib.sfx_load_w(self._h, t, fptr(a)), "sfx_load_w")
+
+    def load_w_state(self, t: int, w, wm, wv):
+        """w_t with its Adam moments (the sfdqn.py l2 path's w optimizer state)."""
+        a = [np.ascontiguousarray(torch.as_tensor(x).detach().cpu().reshape(-1).numpy(), dtype=np.float32)
+             for x in (w, wm, wv)]
+        if any(x.size != self.d for x in a):
+            raise ValueError("w and its moments must have d entries")
+        check(lib.sfx_load_w_state(self._h, t, fptr(a[0]), fptr(a[1]), fptr(a[2])), "sfx_load_w_state")
 
     def get_w(self, t: int):
         w, m, v = (np.empty(self.d, dtype=np.float32) for _ in range(3))

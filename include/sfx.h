@@ -86,6 +86,9 @@ int sfx_get_adam(sfx_t h, int t, float* m_host, float* v_host, int* step);
  * or the Linear(d,1,bias=False) weight of sfdqn.py:196-204. */
 int sfx_load_w(sfx_t h, int t, const float* w_host);
 int sfx_get_w(sfx_t h, int t, float* w_host, float* wm_host, float* wv_host);
+/* w_t and its Adam moments (sfdqn.py:196-204's w optimizer state), e.g. to resume from a
+ * checkpoint (sfx/checkpoint.py). */
+int sfx_load_w_state(sfx_t h, int t, const float* w_host, const float* wm_host, const float* wv_host);
 /* Device pointer to w row t (d floats), stable for the handle's lifetime. */
 int sfx_w_ptr(sfx_t h, int t, float** w_dev);
 

@@ -1,0 +1,73 @@
+"""GPU round trip of sfx.checkpoint (SURVEY.md §5 checkpoint / resume) on the engine: train a few
+all-task steps (agents/sfdqn.py:47-60, LMS w) and active-task updates with sfdqn.py's Adam-trained w
+(its moments non-zero), save, restore into a fresh engine of the same geometry, and continue both
+with the same inputs -- heads, targets, Adam moments and step counts, w and its moments, target-sync
+counters and the selected actions must be identical (same kernels from the same state: bit for bit)."""
+import pytest
+import torch
+
+from oracle import ref_cpu as R
+from tests.conftest import gpu_available
+from tests.test_gpu_step import dev, setup
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if not gpu_available():
+        pytest.skip("no HIP device")
+
+
+def _train(eng, spec, T, k, seed):
+    gen = torch.Generator().manual_seed(seed)
+    B, out = 32, []
+    l3 = torch.empty(3, device="cuda")
+    for j in range(k):
+        s, s1 = torch.randn(B, spec.n_s, generator=gen), torch.randn(B, spec.n_s, generator=gen)
+        a = torch.randint(0, spec.A, (B,), generator=gen)
+        phi, r = torch.rand(B, spec.d, generator=gen), torch.rand(B, generator=gen)
+        gamma = torch.where(torch.rand(B, generator=gen) < 0.1, 0.0, 0.9)
+        phi1, r1 = torch.rand(spec.d, generator=gen), torch.rand(1, generator=gen)
+        s_next = torch.randn(1, spec.n_s, generator=gen)
+        eng.step_all(dev(s), dev(a, torch.long), dev(phi), dev(s1), dev(gamma), use_gpi=True, lms_task=j % T,
+                     lms_phi=dev(phi1), lms_r=dev(r1), lms_alpha=0.05, s_next=dev(s_next), task_index=j % T)
+        out.append(tuple(eng.step_finish()))
+        eng.update(j % T, dev(s), dev(a, torch.long), dev(r), dev(phi), dev(s1), dev(gamma), True, losses=l3)
+        out.append(tuple(l3.tolist()))
+    return out
+
+
+def _state(eng, T):
+    return ([eng.get_head(t, 0) for t in range(T)], [eng.get_head(t, 1) for t in range(T)],
+            [eng.get_adam(t) for t in range(T)], [eng.get_w(t) for t in range(T)],
+            [eng.since_target(t) for t in range(T)])
+
+
+def _same(x, y):
+    if isinstance(x, (list, tuple)):
+        return len(x) == len(y) and all(_same(a, b) for a, b in zip(x, y))
+    if isinstance(x, torch.Tensor):
+        return torch.equal(x, y)
+    return x == y
+
+
+def test_checkpoint_resume_is_bit_exact(tmp_path):
+    from sfx import checkpoint
+
+    spec = R.Spec(17, 256, 7, 8, ("relu", "relu"))
+    T = 4
+    eng, _ = setup(spec, T, seed=2, ev=3)
+    _train(eng, spec, T, 4, seed=11)
+    path = str(tmp_path / "sfx.pt")
+    checkpoint.save(eng, path)
+    eng2, _ = setup(spec, T, seed=9, ev=3)  # other weights: everything must come from the file
+    checkpoint.load(eng2, path)
+    s1, s2 = _state(eng, T), _state(eng2, T)
+    assert _same(s1, s2)
+    assert any(int(st[2]) > 0 for st in s1[2]) and any(bool(w[1].abs().sum() > 0) for w in s1[3])
+    # the same inputs from the same state: the same results, bit for bit
+    assert _train(eng, spec, T, 3, seed=12) == _train(eng2, spec, T, 3, seed=12)
+    assert _same(_state(eng, T), _state(eng2, T))
+    eng.close()
+    eng2.close()
