@@ -8,8 +8,14 @@ for the current state (B=1), ε-greedy, a synthetic Reacher-shape transition (|s
 Default schedule "all" is the main_sfdqn_torch.py path (agents/sfdqn.py:47-60 over
 features/deep.py): every one of the 8 heads is updated per env step.
 
-Multi-GPU: one process per GPU (torchrun).  Weak scaling: each rank owns 8 heads; ranks
-run independent replicas of the env/replay stream.
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` (N > 1, no WORLD_SIZE in the env) is
+its own launcher: the parent starts N rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR
+127.0.0.1 / MASTER_PORT) before anything touches the GPU, waits for them and exits with their
+status; rank 0 prints the line.  Under `torch.distributed.run` (WORLD_SIZE set) it runs as that
+rank.  The N > 1 headline is BASELINE config C4's layout: 8 heads per GPU, 8N source
+tasks, ONE env stream replicated on every rank, GPI maxima all-reduced (MAX) over RCCL inside the
+step graphs -- weak scaling in source tasks; N independent 8-head replicas are timed beside it
+(`replicas`).  See DESIGN.md §7.
 
 `other_workloads` (N=1 only; --no-other skips it) times the other one-GPU BASELINE configs through
 the same native runner: the active-task schedule of sfdqn.py (C2 shape), Hopper TSF-DQN (C3) and
@@ -49,7 +55,8 @@ KIND_NAMES = {"fwd": "k_fwd", "tdg": "k_tdg", "bwd": "k_bwd", "gpi": "k_gpi", "l
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU); N > 1 without WORLD_SIZE: this process launches the N ranks")
     p.add_argument("--steps", type=int, default=2000)
     p.add_argument("--warmup", type=int, default=200)
     p.add_argument("--schedule", choices=["all", "active"], default="all")
@@ -287,6 +294,9 @@ def bench_sharded(args, world, rank, device, barrier, dist, steps=None, warmup=N
     st = loop.stats()
     st.update(eng.step_stats())
     eng_comm = eng.comm_state()
+    eng_comm.update(eng.comm_size())
+    if world > 1 and not args.via_host and eng_comm["rccl_world"] != world:
+        raise RuntimeError(f"RCCL communicator reports world {eng_comm['rccl_world']}, expected {world}")
     eng_comm["rccl_forced_world1"] = os.environ.get("SFX_RCCL_WORLD1") == "1"
     loop.close()
     eng.close()
@@ -470,9 +480,60 @@ def rocprof_avg_from_profiles(kind: str):
         return None
 
 
+def launch_ranks(n: int, argv=None, dry_run: bool = False) -> int:
+    """`bench.py --gpus N` as its own launcher (N > 1 and no WORLD_SIZE in the environment): start
+    N rank processes of this script, one per GPU, with the torch.distributed env contract
+    (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT),
+    wait for all of them and return the first nonzero exit status (0 if all succeed).  The parent
+    never initialises the GPU (no torch.cuda call happens before this point), so the ranks own
+    their devices; a rank that fails ends the others (their exact PIDs).  dry_run: the children
+    print their rank env as one JSON line and exit (tests/test_bench_launch.py)."""
+    import socket
+    import subprocess
+
+    argv = sys.argv[1:] if argv is None else list(argv)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if dry_run:
+            env["SFX_BENCH_DRYRUN"] = "1"
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                print(f"bench launcher: rank {procs.index(p)} exited with {code}; stopping the others",
+                      file=sys.stderr, flush=True)
+                for q in pending:
+                    q.terminate()
+        if pending:
+            time.sleep(0.05)
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is None:
+        args.gpus = world
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if os.environ.get("SFX_BENCH_DRYRUN") == "1":  # launcher test: report the rank env, touch no GPU
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                         "MASTER_PORT")} | {"gpus": args.gpus}), flush=True)
+        return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # SFX_BENCH_BACKEND=gloo rehearses the multi-rank path on a box with fewer GPUs than ranks
@@ -709,6 +770,7 @@ def main():
             "repeats": {"values": repeats, "steps_each": args.steps} if repeats else None,
             "speculation": spec_stats,
             "sharded": sharded,
+            "comm": (sharded or {}).get("comm") if world > 1 else None,
             "sharded_rccl_world1": sharded_rccl1,
             "replicas": replicas,
             "other_workloads": other,

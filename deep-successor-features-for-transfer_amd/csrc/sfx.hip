@@ -51,6 +51,8 @@ struct RcclApi {
   ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
   ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;
   ncclResult_t (*CommSplit)(ncclComm_t, int, int, ncclComm_t*, ncclConfig_t*) = nullptr;
+  ncclResult_t (*CommCount)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*CommUserRank)(const ncclComm_t, int*) = nullptr;
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
 };
 static const RcclApi& rccl() {
@@ -75,6 +77,8 @@ static const RcclApi& rccl() {
     sym(a.CommAbort, "ncclCommAbort");
     sym(a.CommGetAsyncError, "ncclCommGetAsyncError");
     sym(a.CommSplit, "ncclCommSplit");
+    sym(a.CommCount, "ncclCommCount");
+    sym(a.CommUserRank, "ncclCommUserRank");
     sym(a.GetErrorString, "ncclGetErrorString");
     a.ok = all;
     if (!all) a.why = "RCCL lacks a needed entry point";

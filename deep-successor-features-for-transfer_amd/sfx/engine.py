@@ -112,12 +112,27 @@ class SFEngine:
             ev.synchronize()
         return i
 
+    def _on_stream(self):
+        """Context that makes the handle's stream torch's current one: the staging buffers are
+        allocated, copied into and recorded on the stream the library's kernels read them on (the
+        caching allocator then reuses a freed block only in that stream's order)."""
+        import contextlib
+
+        if self.stream == torch.cuda.current_stream(self.device).cuda_stream:
+            return contextlib.nullcontext()
+        st = getattr(self, "_xstream", None)
+        if st is None:
+            st = self._xstream = torch.cuda.ExternalStream(self.stream, device=self.device)
+        return torch.cuda.stream(st)
+
     def _pin_copy(self, i, nbytes) -> torch.Tensor:
-        """One non-blocking copy of slot i's first nbytes into a fresh device buffer."""
-        out = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
-        out.copy_(self._pin[i, :nbytes], non_blocking=True)
-        ev = self._pin_ev[i] = self._pin_ev[i] or torch.cuda.Event()
-        ev.record()
+        """One non-blocking copy of slot i's first nbytes into a fresh device buffer, on the
+        handle's stream."""
+        with self._on_stream():
+            out = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            out.copy_(self._pin[i, :nbytes], non_blocking=True)
+            ev = self._pin_ev[i] = self._pin_ev[i] or torch.cuda.Event()
+            ev.record()
         return out
 
     @staticmethod
@@ -363,6 +378,11 @@ class SFEngine:
             losses = torch.empty(self.T, 3, device=self.device)
         check(lib.sfx_update_all(self._h, s.data_ptr(), a.data_ptr(), phi.data_ptr(), s1.data_ptr(),
                                  gamma.data_ptr(), B, losses.data_ptr()), "sfx_update_all")
+        # sfx_update_all returns with the step's verdict pending: host rounds, if the device rounds
+        # leave a policy unverified, run inside the NEXT library call (settle) and read these inputs
+        # and write these losses -- keep them alive until then (replaced after the next update_all,
+        # whose own call has settled this step)
+        self._lazy_keep = (s, s1, a, phi, gamma, losses)
         return losses
 
     def step_all(self, s=None, a=None, phi=None, s1=None, gamma=None, *, use_gpi: bool = True, lms_task: int = -1,
@@ -388,6 +408,13 @@ class SFEngine:
         check(lib.sfx_comm_state(self._h, C.byref(v)), "sfx_comm_state")
         return dict(rccl=bool(v.value & 1), rounds_split=bool(v.value & 2), aborted=bool(v.value & 4),
                     host=bool(v.value & 8))
+
+    def comm_size(self) -> dict:
+        """sfx_comm_size: rank / world the handle was given and what its RCCL communicator reports
+        (ncclCommUserRank / ncclCommCount; -1 / 0 without one)."""
+        v = [C.c_int() for _ in range(4)]
+        check(lib.sfx_comm_size(self._h, *[C.byref(x) for x in v]), "sfx_comm_size")
+        return dict(rank=v[0].value, world=v[1].value, rccl_rank=v[2].value, rccl_world=v[3].value)
 
     def debug_stall(self, seconds: float):
         """Test hook (sfx_debug_stall): the next sharded runner step stalls on the device before it

@@ -388,6 +388,9 @@ int sfx_set_comm_host(sfx_t h, sfx_host_allreduce_fn fn, void* ctx, int rank, in
  * N > 1 too), bit 2 aborted after a timed-out collective, bit 3 host transport.  RCCL is loaded
  * at run time (dlopen) by the first RCCL call. */
 int sfx_comm_state(sfx_t h, int* state);
+/* Rank / world the handle was given, and what its RCCL communicator itself reports
+ * (ncclCommUserRank / ncclCommCount; -1 / 0 without an RCCL communicator). */
+int sfx_comm_size(sfx_t h, int* rank, int* world, int* rccl_rank, int* rccl_world);
 /* test hook: the next runner step of the sharded schedule stalls `seconds` (<= 60) on the device
  * after its collectives and before it publishes its result (exercises sfx_runner_wait_timeout). */
 int sfx_debug_stall(sfx_t h, double seconds);

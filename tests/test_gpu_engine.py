@@ -181,6 +181,39 @@ def test_update_all_vs_golden(golden):
     eng.close()
 
 
+def test_update_all_host_rounds_with_temporary_inputs():
+    """sfx_update_all returns with its verdict pending; the host rounds of a step whose device
+    rounds are treated as failed (sfx_debug_force_rerun) run inside the NEXT call.  The caller's
+    inputs are temporaries and the losses are dropped at once, as the drop-in does:
+    the engine must keep them alive until that call, so every step trains on its own minibatch."""
+    from sfx.init import reference_heads
+
+    spec, T, B = R.Spec(17, 64, 7, 8), 4, 32
+    online, w = reference_heads(T, spec.n_s, spec.H, spec.A, spec.d, spec.acts, seed=3)
+    eng = engine_for(spec, T)
+    for t in range(T):
+        eng.load_head(t, online[t], 0)
+        eng.load_head(t, online[t], 1)
+        eng.load_w(t, w[t])
+    eng.debug_force_rerun(1)
+    st = R.SFState(spec, online.clone(), online.clone(), w.clone())
+    gen = torch.Generator().manual_seed(11)
+    batches = [(torch.randn(B, 17, generator=gen), torch.randint(0, 7, (B,), generator=gen),
+                torch.rand(B, 8, generator=gen), torch.randn(B, 17, generator=gen), torch.full((B,), 0.9))
+               for _ in range(4)]
+
+    def step(b):  # every argument is a fresh host tensor that dies with this frame
+        eng.update_all(*(x.clone().numpy() for x in b))
+
+    for b in batches:
+        step(b)
+        R.deep_all_task_step(st, b)
+    stats = eng.step_stats()
+    assert stats["host_round_steps"] == len(batches)
+    params_close(torch.stack([eng.get_head(t) for t in range(T)]), st.online, 4e-3)
+    eng.close()
+
+
 def test_full_size_update_vs_oracle():
     """BASELINE C2 shape (H=256, T=8): one active-task and one all-task step against the oracle."""
     from tests.golden.recipe import SHAPES, full_size_heads
