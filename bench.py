@@ -50,7 +50,7 @@ TSF_SHAPE = dict(n_s=11, H=256, A=27, d=50, acts=("relu", "relu"), G=100)
 C1_SHAPE = dict(n_s=4, H=256, A=2, d=20, acts=("relu", "relu"))  # BASELINE C1 (CartPole-v2)
 WORKLOADS = {"reacher-sf": None, "hopper-tsf": 0, "hopper-tsf-nf": 100}
 KIND_NAMES = {"fwd": "k_fwd", "tdg": "k_tdg", "bwd": "k_bwd", "gpi": "k_gpi", "lms": "k_lms", "ver": "k_ver",
-              "round": "k_round", "tsf": "k_tsf", "pstep": "k_pstep"}
+              "tsf": "k_tsf"}
 
 
 def parse():
@@ -377,8 +377,6 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
                                       ("reacher17-all-T8-B32-device-replay", "all", None, True, "fp32"),
                                       ("reacher17-all-T8-B32-fp32", "all", None, False, "fp32"),
                                       ("reacher17-all-T8-B32-bf16", "all", None, False, "bf16"),
-                                      # the opt-in persistent step (k_pstep: one launch per env step)
-                                      ("reacher17-all-T8-B32-persistent", "all", None, False, "fp32"),
                                       ("hopper11-tsf-T16-B32", "tsf", 0, False, "fp32"),
                                       ("hopper11-tsf-T16-B32-bf16", "tsf", 0, False, "bf16"),
                                       ("hopper11-tsf-nf100-T16-B32", "tsf", 100, False, "fp32"),
@@ -404,9 +402,6 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
         eng.set_target_update_ev(1000)
         eng.set_spec_rounds(args.spec_rounds)
         eng.set_precision(prec)
-        persistent = name.endswith("-persistent")
-        if persistent:
-            eng.set_pstep(True)
         loop = NativeEnvLoop(eng, batch=args.batch, seed=1, schedule=sched, p_end=0.0 if K is None else 0.01,
                              device_replay=dev)
         loop.prefill(1000)
@@ -419,9 +414,6 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
         dt = time.perf_counter() - t0
         out[name] = {"value": round(steps / dt, 2), "unit": "env steps/s", "ms_per_step": round(1000.0 * dt / steps, 4),
                      "steps": steps, "dtype": prec}
-        if persistent:
-            st = eng.pstep_stats()
-            out[name]["pstep_rounds_per_step"] = round(st["rounds"] / max(1, st["steps"]), 3)
         loop.close()
         eng.close()
     # the drop-in: features.deep.DeepSF under the reference user's Python agent loop (tools/dropin_loop.py)

@@ -32,7 +32,6 @@
 #include "sfx_kernels.h"
 #include "sfx_tsf.h"
 #include "sfx_phi.h"
-#include "sfx_pstep.h"
 #include "../../include/sfx.h"
 
 using namespace sfx;
@@ -187,10 +186,6 @@ struct sfx_handle {
   int Tg = 0, off = 0;
   struct sfx_tsf_state* tsf = nullptr;  // TSF-DQN state (sfx_tsf_setup)
   struct sfx_phi_state* phi = nullptr;  // learned φ (sfx_phi_setup)
-  // persistent all-task step (k_pstep, sfx_pstep.h / sfx_pstep.inc): SFX_PSTEP=1 or sfx_set_pstep
-  int pstep_mode = 0;       // 1: launch_step_all runs k_pstep whenever pstep_use() holds
-  int pstep_census = -1;    // placement check: -1 not run, 0 failed, 1 32 workgroups on each of 8 XCDs
-  struct sfx_pstep_state* ps = nullptr;
   // collective of the sharded step (sfx_comm_init / sfx_set_comm / sfx_set_comm_host): all-reduce
   // (MAX) of fp32 buffers over the ranks that share the source tasks
   int comm_rank = 0, comm_world = 0;  // world 0: no communicator
@@ -239,14 +234,11 @@ struct sfx_handle {
   const long long* pub_dctr = nullptr;
   bool pub_folded = false;
   bool fold_publish = true;  // SFX_FOLD_PUBLISH=0: always a separate k_publish
-  // k_round (one launch per speculative round, see sfx_kernels.h); SFX_ROUND=1 turns it on
-  bool use_round = false;
   // bf16 operand mode (sfx_set_precision): bf16 copies of the online [2][T][P] / target [T][P]
   // parameters feed the forward and dX MFMAs; fp32 master weights, moments and accumulators
   bool bf16 = false;
   __bf16* on16 = nullptr;
   __bf16* tg16 = nullptr;
-  unsigned* round_ctr = nullptr;  // [T] per-head arrival counters
   // split-N dX of wide layers (run_bwd): partial tiles and per-(head, tile) arrival counters
   int dxs_max = 1, dx_ntile = 1;
   float* dxpart = nullptr;
@@ -254,14 +246,6 @@ struct sfx_handle {
   bool split_dx = true;  // SFX_SPLIT_DX=0: one workgroup reduces all of N
   bool gemv_fwd = true;  // SFX_GEMV_FWD=0: wide layers of a <= 4-row forward through the MFMA tiles
   bool dw_wide = false;  // SFX_DW_WIDE=1: 64 x 64 dW tiles for wide hidden layers (measured: no gain)
-  struct RoundRec {               // launch arguments recorded instead of launched
-    std::vector<BwdArgs> b;
-    std::vector<FwdArgs> f;
-    std::vector<double> bytes;
-    bool fvec = true;
-    int tdg = 0;
-  };
-  RoundRec* rec = nullptr;
   StepOut* hout = nullptr;  // pinned host
 
   int slot(int head) const { return (int)((mask >> head) & 1ull); }
@@ -281,8 +265,7 @@ void clear_graphs(sfx_handle* h) {
   h->graphs.clear();
 }
 
-enum { K_FWD = 0, K_TDG = 1, K_BWD = 2, K_GPI = 3, K_LMS = 4, K_VER = 5, K_ROUND = 6, K_TSF = 7, K_PSTEP = 8,
-       K_NKIND = 9 };
+enum { K_FWD = 0, K_TDG = 1, K_BWD = 2, K_GPI = 3, K_LMS = 4, K_VER = 5, K_TSF = 6, K_NKIND = 7 };
 
 hipEvent_t prof_event(sfx_handle* h) {
   if (!h->prof_pool.empty()) {
@@ -382,7 +365,7 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
   F.lms_head = -1;
   F.qa_role = -1;
   F.skip = ex.skip;
-  if (ex.skip && (groups.size() != 1 || ex.flag || ex.lms_head >= 0 || (ex.qa_role >= 0 && !ex.qh) || h->rec))
+  if (ex.skip && (groups.size() != 1 || ex.flag || ex.lms_head >= 0 || (ex.qa_role >= 0 && !ex.qh)))
     SFX_FAIL(SFX_E_STATE, "run_fwd: head skipping needs one group and no LMS / flag / maxima");
   int ninst = 0;
   bool uniform = true;  // every group covers heads 0..T-1: XCD-aware grid possible
@@ -444,7 +427,7 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     // half the CUs and fit the chip when paired: C2's first forward of three roles (384 tiles ->
     // 192 workgroups, +1 %); Hopper TSF's 288 tiles stay unpaired (pairing measured 1 % slower)
     const long tiles = (long)F.ntN * F.ntM * ninst;
-    if (!h->rec && !qa && h->fwd_tpw > 1 && h->fwd_waves == 8 && F.ntN > 1 && 2 * tiles >= 3L * h->ncu &&
+    if (!qa && h->fwd_tpw > 1 && h->fwd_waves == 8 && F.ntN > 1 && 2 * tiles >= 3L * h->ncu &&
         tiles <= 2L * h->ncu && (l0 || ((L.K % 32) == 0 && aligned)))
       F.tpw = h->fwd_tpw;
     const int ntNb = cdiv(F.ntN, F.tpw);
@@ -452,14 +435,10 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     double by = 4.0 * ninst * ((double)L.N * L.K + L.N + (double)M * L.K + (double)M * L.N);
     if (l0) by += 4.0 * ninst * ((double)h->L[0].N * h->L[0].K + h->L[0].N + (double)M * h->L[0].K);
     const bool tp2 = F.tpw > 1;
-    const bool gemv = !l0 && !qa && !h->rec && h->gemv_fwd && M <= GEMV_M && L.N >= GEMV_N && L.K % 16 == 0 &&
+    const bool gemv = !l0 && !qa && h->gemv_fwd && M <= GEMV_M && L.N >= GEMV_N && L.K % 16 == 0 &&
                       (l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0));
     if (gemv) {
       launch(h, K_FWD, by, k_fwd_gemv, dim3(cdiv(L.N, 64), ninst), dim3(256), h->G, F);
-    } else if (h->rec) {  // k_round's post-update forward runs 4-wave tiles
-      h->rec->f.push_back(F);
-      h->rec->bytes.push_back(by);
-      h->rec->fvec = h->rec->fvec && (L.K % 64) == 0 && aligned && !l0;
     } else if (l0) {
       if (!(ex.ride_l0 && !tp2 && !F.xcd && ex.ride_l0(F, grid, by)))
         launch(h, K_FWD, by,
@@ -584,7 +563,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.flag = td.flag;
   A.flag_value = h->T;
   A.dz_scale = td.dz_scale;
-  const bool armed = fuse && td.skip && !h->rec && M <= 32;  // k_round's recorded launches never skip
+  const bool armed = fuse && td.skip && M <= 32;
   if (armed) {
     A.tdg_prev = td.prev;
     A.skip = h->skip;
@@ -609,7 +588,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   // opt-in 64 x 64 dW tiles (role_dw_wide) for wide hidden layers when several heads share a
   // launch, which then stays within about one workgroup per CU (measured: no gain)
   auto dw_nw = [&](int l) {
-    return l >= 1 && h->dw_wide && !h->bf16 && !h->rec && nhead >= 4 && h->L[l].N >= 128 &&
+    return l >= 1 && h->dw_wide && !h->bf16 && nhead >= 4 && h->L[l].N >= 128 &&
                    h->L[l].K >= 64
                ? 2
                : 1;
@@ -650,9 +629,9 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     A.ra = geo(l);
     A.na = cdiv(M, 32) * cdiv(h->L[l].K, 16);
     // wide layers: the dX tiles split N in <= 256-wide chunks over workgroups (not in a fused
-    // TD launch, not in k_round's recorded launches)
+    // TD launch)
     A.dxs = 1;
-    if (!A.tdg && !h->rec && h->split_dx && h->dxpart && h->L[l].N > DX_SPLIT_N && M <= 32 * cdiv(h->Mmax, 32) &&
+    if (!A.tdg && h->split_dx && h->dxpart && h->L[l].N > DX_SPLIT_N && M <= 32 * cdiv(h->Mmax, 32) &&
         nhead <= h->T) {
       A.dxs = cdiv(h->L[l].N, DX_SPLIT_N);
       A.dxpart = h->dxpart;
@@ -669,17 +648,13 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     A.tail = li == tail_at && need_tail ? 1 : 0;
     const int ntile = A.tdg ? A.na : A.na + A.nb + A.nc + A.tail;
     const dim3 grid = A.xcd ? dim3(8 * cdiv(nhead, 8) * ntile) : dim3(ntile, nhead);
-    if (h->rec) {
-      h->rec->b.push_back(A);
-      h->rec->bytes.push_back(by);
-      if (A.tdg) h->rec->tdg = tdg_variant(h);
-    } else if (A.tdg && tdg_variant(h) == 1)  // d <= 8
+    if (A.tdg && tdg_variant(h) == 1)  // d <= 8
       launch(h, K_BWD, by, k_bwd_tdg<2, 8>, grid, dim3(256), h->G, A);
     else if (A.tdg)
       launch(h, K_BWD, by, k_bwd_tdg<4, 4>, grid, dim3(256), h->G, A);
     else if (!(ex.ride && nhead == 1 && !A.xcd && ex.ride(li, tail_at, A, ntile, by)))
       launch(h, K_BWD, by, h->bf16 ? k_bwd<true> : k_bwd<false>, grid, dim3(256), h->G, A);
-    if (ex.hook && li == ex.hook_after && !h->rec) RC(ex.hook());
+    if (ex.hook && li == ex.hook_after) RC(ex.hook());
   }
   A.na = 0;
   A.dxs = 1;
@@ -699,11 +674,6 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.v_x = ex.v_x;
   A.v_xn = ex.v_xn;
   const int ntile = A.nb + A.nc + A.tail;
-  if (h->rec) {
-    h->rec->b.push_back(A);
-    h->rec->bytes.push_back(nhead * (dw_bytes(1) + dw_bytes(0)));
-    return SFX_OK;
-  }
   if (!(ex.ride && nhead == 1 && !A.xcd && ex.ride(h->NL - 1, tail_at, A, ntile, nhead * (dw_bytes(1) + dw_bytes(0)))))
     launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), h->bf16 ? k_bwd<true> : k_bwd<false>,
            A.xcd ? dim3(8 * cdiv(nhead, 8) * ntile) : dim3(ntile, nhead), dim3(256), h->G, A);
@@ -825,7 +795,7 @@ void free_all(sfx_handle* h) {
   }
   for (hipEvent_t e : h->prof_pool) (void)hipEventDestroy(e);
   for (void* p : {(void*)h->online, (void*)h->target, (void*)h->am, (void*)h->av, (void*)h->w, (void*)h->wm,
-                  (void*)h->wv, (void*)h->step, (void*)h->dcancel, (void*)h->adamc, (void*)h->round_ctr, (void*)h->act, (void*)h->dz, (void*)h->rowloss, (void*)h->spec_next, (void*)h->skip, (void*)h->skipc,
+                  (void*)h->wv, (void*)h->step, (void*)h->dcancel, (void*)h->adamc, (void*)h->act, (void*)h->dz, (void*)h->rowloss, (void*)h->spec_next, (void*)h->skip, (void*)h->skipc,
                   (void*)h->dout, (void*)h->dxpart, (void*)h->dxctr, (void*)h->qh})
     if (p) (void)hipFree(p);
   if (h->hout) (void)hipHostFree(h->hout);
@@ -843,8 +813,7 @@ void free_all(sfx_handle* h) {
 // Role of round r's post-update forward.  The launches of a round run in stream order, so every
 // round can write the same role (round r's TD launch has read round r-1's values before its
 // forward overwrites them) -- which lets a head whose policy repeats round r-1 skip its forward.
-// k_round's heads progress independently inside one launch: there rounds alternate two roles.
-inline int round_role(const sfx_handle* h, int r) { return h->use_round && (r & 1) ? R_V2 : R_V; }
+inline int round_role(const sfx_handle*, int) { return R_V; }
 // next actions of speculative round r (two buffers: round r reads round r-1's while it writes)
 inline int64_t* spec_buf(sfx_handle* h, int r) { return h->spec_next + (size_t)(r & 1) * h->T * MMAX; }
 
@@ -870,7 +839,7 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
   BwdExtra bx;
   bx.inc_step = r == 0 ? 1 : 0;  // later rounds redo the same optimizer step
   bool armed = false;
-  bx.skip_fwd = !h->use_round;  // one role for every round (round_role)
+  bx.skip_fwd = true;  // one role for every round (round_role)
   bx.skip_armed = &armed;
   // the s_next row rides along in every round that a later round may skip heads after: a skipped
   // head's row must already be in the role when the final round's selection reads it
@@ -880,42 +849,8 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
   bx.v_x = p.S1;
   bx.v_xn = want_sel ? p.s_next : nullptr;
   const int vM = B + (want_sel ? 1 : 0);
-  // the whole round as one k_round launch when its preconditions hold (see RoundArgs)
-  const bool round1 = h->use_round && T <= 8 && bx.fuse_v0 && !p.losses && can_fuse_tdg(h) &&
-                      ((uintptr_t)p.phi & 15) == 0 && h->NL >= 3 && h->NL - 1 <= RF_MAX && h->NL <= RB_MAX;
-  if (round1) {
-    sfx_handle::RoundRec rec;
-    h->rec = &rec;
-    int rc = run_bwd(h, 0, T, B, p.S, p.phi, nullptr, nullptr, td, bx);
-    FwdExtra vx;
-    vx.l0 = 1;
-    if (rc == SFX_OK) rc = run_fwd(h, {{out, P_NEW, 0, 0, T}}, vM, nullptr, nullptr, vx);
-    h->rec = nullptr;
-    RC(rc);
-    if ((int)rec.b.size() != h->NL || (int)rec.f.size() != h->NL - 1 || !rec.b[0].tdg || rec.b.back().tail)
-      SFX_FAIL(SFX_E_STATE, "k_round: unexpected launch sequence");
-    RoundArgs R{};
-    for (size_t i = 0; i < rec.b.size(); ++i) R.b[i] = rec.b[i];
-    for (size_t i = 0; i < rec.f.size(); ++i) R.f[i] = rec.f[i];
-    R.nb = (int)rec.b.size();
-    R.nf = (int)rec.f.size();
-    R.wph = 256 / T < 32 ? 256 / T : 32;
-    R.ctr = h->round_ctr;
-    R.err = &h->dout->flag;
-    R.timeout = 200000000LL;  // 2 s of the 100 MHz clock
-    double by = 0.0;
-    for (double x : rec.bytes) by += x;
-    const dim3 grid(T * R.wph);
-    if (rec.tdg == 1)
-      launch(h, K_ROUND, by, rec.fvec ? k_round<2, 8, true> : k_round<2, 8, false>, grid, dim3(256), h->G, R);
-    else
-      launch(h, K_ROUND, by, rec.fvec ? k_round<4, 4, true> : k_round<4, 4, false>, grid, dim3(256), h->G, R);
-    LAUNCHCHK();
-  } else {
-    RC(run_bwd(h, 0, T, B, p.S, p.phi, nullptr, p.losses, td, bx));
-  }
-  if (round1) {
-  } else if (bx.fuse_v0) {
+  RC(run_bwd(h, 0, T, B, p.S, p.phi, nullptr, p.losses, td, bx));
+  if (bx.fuse_v0) {
     FwdExtra vx;
     vx.l0 = 1;
     vx.skip = armed && r > 0 && bx.skip_fwd ? h->skip : nullptr;
@@ -972,13 +907,9 @@ int tsf_body(sfx_handle* h, int policy, const float* S, const int64_t* a, const 
              const float* S1, const float* gamma, int B, int use_gpi, float* losses, int64_t* next,
              const int* xmax = nullptr);
 
-bool pstep_use(const sfx_handle* h, const sfx_handle::Pending& p);
-int run_pstep(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, const float* lms_phi, const float* lms_r,
-              float lms_alpha);
 
 int launch_step_all(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, const float* lms_phi, const float* lms_r,
                     float lms_alpha, int rounds) {
-  if (p.update && pstep_use(h, p)) return run_pstep(h, p, lms_task, lms_phi, lms_r, lms_alpha);
   const int T = h->T, B = p.B;
   FwdExtra ex;
   ex.lms_head = lms_task;
@@ -1063,8 +994,6 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->fuse_v0 = !(ev0 && ev0[0] == '0');
   const char* efp = std::getenv("SFX_FOLD_PUBLISH");
   h->fold_publish = !(efp && efp[0] == '0');
-  const char* erd = std::getenv("SFX_ROUND");  // opt-in: measured slower than the launches
-  h->use_round = erd && erd[0] == '1';
   const char* ex = std::getenv("SFX_XCD");
   h->xcd = !(ex && ex[0] == '0');
   const char* efw = std::getenv("SFX_FWD_WAVES");
@@ -1141,7 +1070,6 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   alloc((void**)&h->step, sizeof(int) * T);
   alloc((void**)&h->dcancel, 64);
   alloc((void**)&h->adamc, sizeof(AdamC) * T);
-  alloc((void**)&h->round_ctr, sizeof(unsigned) * T);
   {  // split-N dX: every layer's N split into <= 256-wide chunks, tiles of 32 rows x 16 columns
     int nmax = 0, kmax = 0;
     for (const LayerGeo& L : h->L) {
@@ -1200,14 +1128,11 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   G.nonfin = h->dcancel + 8;  // sticky non-finite TD flag (sfx_nonfinite)
   G.lastOff = h->actOff[h->NL - 1];
   *out = h;
-  const char* eps = std::getenv("SFX_PSTEP");  // the persistent step where it fits and the census passes
-  if (eps && eps[0] == '1') (void)sfx_set_pstep(h, 1);
   return SFX_OK;
 }
 
 void tsf_release(sfx_handle* h);
 void phi_release(sfx_handle* h);
-void pstep_release(sfx_handle* h);
 
 int sfx_destroy(sfx_t h) {
   if (!h) return SFX_OK;
@@ -1215,7 +1140,6 @@ int sfx_destroy(sfx_t h) {
   (void)hipStreamSynchronize(h->stream);
   tsf_release(h);
   phi_release(h);
-  pstep_release(h);
   free_all(h);
   delete h;
   return SFX_OK;
@@ -1509,7 +1433,6 @@ int sfx_set_precision(sfx_t h, int precision) {
   HIPCHK(hipStreamSynchronize(h->stream));
   clear_graphs(h);
   if (want) {
-    if (h->use_round) SFX_FAIL(SFX_E_STATE, "sfx_set_precision: bf16 operands do not run in k_round (SFX_ROUND=1)");
     const size_t n = (size_t)h->T * h->P;
     if (!h->on16 && hipMalloc((void**)&h->on16, sizeof(__bf16) * 2 * n) != hipSuccess)
       SFX_FAIL(SFX_E_HIP, "hipMalloc(bf16 copy) failed");
@@ -1547,15 +1470,13 @@ int sfx_step_stats(sfx_t h, long long* steps, long long* fallbacks, long long* r
 int sfx_skip_stats(sfx_t h, long long* checked, long long* skipped, int reset) {
   RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
-  unsigned long long c[2] = {0, 0}, ps[4] = {0, 0, 0, 0};
+  unsigned long long c[2] = {0, 0};
   HIPCHK(hipStreamSynchronize(h->stream));
   HIPCHK(hipMemcpy(c, h->skipc, sizeof(c), hipMemcpyDeviceToHost));
-  if (h->ps) HIPCHK(hipMemcpy(ps, h->ps->stats, sizeof(ps), hipMemcpyDeviceToHost));  // k_pstep's own counts
-  if (checked) *checked = (long long)(c[0] + ps[2]);
-  if (skipped) *skipped = (long long)(c[1] + ps[3]);
+  if (checked) *checked = (long long)c[0];
+  if (skipped) *skipped = (long long)c[1];
   if (reset) {
     HIPCHK(hipMemset(h->skipc, 0, sizeof(c)));
-    if (h->ps) HIPCHK(hipMemset(h->ps->stats + 2, 0, 2 * sizeof(unsigned long long)));
   }
   return SFX_OK;
 }
@@ -1678,4 +1599,3 @@ int sfx_synchronize(sfx_t h) {
 #include "sfx_runner.inc"
 #include "sfx_tsf.inc"
 #include "sfx_phi.inc"
-#include "sfx_pstep.inc"

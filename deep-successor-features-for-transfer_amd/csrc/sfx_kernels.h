@@ -124,8 +124,8 @@ __device__ __forceinline__ bf16x8 ld_bf16x8(const __bf16* p) {  // 16-B aligned
   return *reinterpret_cast<const bf16x8*>(p);
 }
 
-// Loads / stores of data handed between workgroups INSIDE one launch (the round kernel,
-// k_round): C = true makes them coherent -- sc1 (L1-bypassing) dword loads and write-through
+// Loads / stores of data handed between workgroups INSIDE one launch (the split-N dX partial
+// tiles): C = true makes them coherent -- sc1 (L1-bypassing) dword loads and write-through
 // stores, the hand-off form of MI355X_MICROARCH.md's validated table (sc1 stores, every storing
 // wave's vmcnt(0), one agent-scope arrival per workgroup, sc1 poll, barrier, sc1 loads).
 // C = false: plain accesses (data from an earlier launch; the kernel boundary orders it).
@@ -491,9 +491,8 @@ __device__ void lms_block(const Geo& G, const FwdArgs& F) {
 // them for the backward -- and feeds them to the layer-1 MFMAs from LDS: one launch less.
 constexpr int L0_KMAX = 64, L0_NMAX = 256;  // layer-0 fan-in / width handled in-tile
 
-// One 32-row x 16-column output tile of instance y (flattened over the groups).  C: the layer
-// input X, the parameters and the output are handed between workgroups inside the launch
-// (k_round's post-update forward) -- coherent accesses.
+// One 32-row x 16-column output tile of instance y (flattened over the groups).  C: coherent
+// accesses (data handed between workgroups inside the launch).
 // instance y of a forward launch -> its group (y becomes the index inside the group)
 __device__ __forceinline__ FwdGroup fwd_group(const FwdArgs& F, int& y) {
   int gs = 0;
@@ -897,7 +896,7 @@ __global__ __launch_bounds__(256) void k_fwd_gemv(Geo G, FwdArgs F) {
 //   rowloss[i][b] = Σ_k (c[b,a_b,k] - t_b[k])^2
 // Policy i takes ψ_t(s1) of heads t < i from role `guess` and of heads t >= i from R_S1
 // (before the step).  In the reference's in-order loop heads t < i are already updated;
-// guess = R_S1 speculates they did not move, guess = R_V/R_V2 uses the post-update values
+// guess = R_S1 speculates they did not move, guess = R_V uses the post-update values
 // of the previous speculative round (see k_ver).
 // Grid (M, npol), 256 threads.  Policies pol0 .. pol0+npol-1.
 // -------------------------------------------------------------------------------------
@@ -1877,105 +1876,6 @@ __global__ __launch_bounds__(256) void k_bwd_tdg(Geo G, BwdArgs A) {
   PROBE_MARKA();
   role_dx<true, VMAX, U>(G, A, head, bx, red);
   PROBE_REC(3, pt0);
-}
-
-// -------------------------------------------------------------------------------------
-// K3+K1' as ONE launch per speculative round (k_round): the whole per-head chain of a round
-//   fused TD target + last dX -> dX ∥ dW ... -> dW1 ∥ dW0 (+ post-update layer 0)
-//   -> post-update forward layers 1 .. NL-1
-// with the arguments the separate launches would get (b[], f[]).  Workgroup w serves head
-// w % T (blocks b and b + 8 share an XCD, so a head's workgroups share an L2) as slot w / T of
-// wph; a head's phases are separated by a per-head arrival counter instead of a kernel
-// boundary.  Every hand-off inside the launch is coherent: producers store sc1 and wait
-// vmcnt(0) in every wave, one lane per workgroup adds to the head's counter, consumers poll
-// it sc1 and read sc1 (ldc/stc, C = true).  Heads never wait on each other inside a round.
-// Residency: T·wph <= 256 workgroups of 256 threads and > 80 KB LDS, one per CU.  Every wait
-// is bounded (timeout ticks of the 100 MHz clock); on expiry *err is set, the launch drains.
-// -------------------------------------------------------------------------------------
-constexpr int RB_MAX = 5, RF_MAX = 4;  // up to 4 hidden Linear layers
-struct RoundArgs {
-  BwdArgs b[RB_MAX];  // b[0]: fused TD + last dX; b[1..nb-2]: dX ∥ dW; b[nb-1]: dW1 ∥ dW0 (+ v0)
-  FwdArgs f[RF_MAX];  // post-update forward of layers 1 .. NL-1
-  int nb, nf, wph, pad_;
-  unsigned* ctr;  // [T] per-head arrivals; zero at launch, returned to zero by each head's last arrival
-  int* err;       // the speculation flag word: set to -1 when a wait times out (the host fails loudly)
-  long long timeout;
-};
-
-__device__ __forceinline__ void head_sync(const RoundArgs& R, unsigned* ctr, unsigned target, bool probe = false) {
-  if (probe) PROBE_AT(6);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have landed
-  __syncthreads();
-  if (probe) PROBE_AT(7);
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const long long t0 = wall_clock64();
-    unsigned it = 0;
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if ((++it & 63) == 0 && (wall_clock64() - t0 > R.timeout ||
-                               __hip_atomic_load(R.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0)) {
-        atomicMin(R.err, -1);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __syncthreads();
-}
-
-template <int VMAX, int U, bool FVEC>
-__global__ __launch_bounds__(256) void k_round(Geo G, RoundArgs R) {
-  __shared__ floatx4 red[4][2][64];
-  PROBE_T(pt0);
-  const int T = G.T, head = blockIdx.x % T, slot = blockIdx.x / T, wph = R.wph;
-  unsigned* ctr = R.ctr + head;
-  unsigned target = 0;
-  // phase 0: TD target + output gradient + dX of the last layer
-  for (int t = slot; t < R.b[0].na; t += wph) {
-    role_dx<true, VMAX, U, true>(G, R.b[0], head, t, red);
-    __syncthreads();
-  }
-  target += wph;
-  head_sync(R, ctr, target, true);
-  PROBE_AT(1);
-  // backward phases
-  for (int p = 1; p < R.nb; ++p) {
-    const BwdArgs& A = R.b[p];
-    const int n = A.na + A.nb + A.nc;
-    for (int t = slot; t < n; t += wph) {
-      if (t < A.na)
-        role_dx<false, 2, 8, true>(G, A, head, t, red);
-      else if (t < A.na + A.nb)
-        role_dw<true>(G, A, head, A.rb, t - A.na, false);
-      else
-        role_dw<true>(G, A, head, A.rc, t - A.na - A.nb, A.fuse_v0 != 0);
-      __syncthreads();
-    }
-    target += wph;
-    head_sync(R, ctr, target);
-    if (p < 4) PROBE_AT(1 + p);
-  }
-  // post-update forward (instance = head: one group covering heads 0..T-1)
-  for (int p = 0; p < R.nf; ++p) {
-    const FwdArgs& F = R.f[p];
-    const int n = F.ntN * F.ntM;
-    for (int t = slot; t < n; t += wph) {
-      const int tM = t / F.ntN;
-      fwd_tile<FVEC, 4, false, true>(G, F, head, t - tM * F.ntN, tM);
-      __syncthreads();
-    }
-    if (p + 1 < R.nf) {
-      target += wph;
-      head_sync(R, ctr, target);
-      if (p < 1) PROBE_AT(5 + p);
-    }
-  }
-  // the head's last workgroup to finish returns its counter to zero for the next round
-  __syncthreads();
-  if (threadIdx.x == 0 &&
-      __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == target + wph - 1)
-    __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  PROBE_REC(7, pt0);
 }
 
 // -------------------------------------------------------------------------------------

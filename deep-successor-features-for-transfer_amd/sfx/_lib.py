@@ -38,13 +38,8 @@ SIGNATURES = {
     "sfx_successors": (_I, [_VP, _VP, _I, _I, _VP]),
     "sfx_select_action": (_I, [_VP, _VP, _I, _I, _VP, _VP]),
     "sfx_test_actions": (_I, [_VP, _VP, _I, _VP, _I, _VP, _VP]),
-    "sfx_set_pstep": (_I, [_VP, _I]),
-    "sfx_get_pstep": (_I, [_VP]),
-    "sfx_pstep_stats": (_I, [_VP, _VP]),
     "sfx_nonfinite": (_I, [_VP, _VP, _I]),
     "sfx_runner_nonfinite": (_I, [_VP, _VP]),
-    "sfx_pstep_trace": (_I, [_VP, _VP]),
-    "sfx_pstep_timeline": (_I, [_VP, _VP]),
     "sfx_test_reward_updates": (_I, [_VP, _I, _VP, _VP, _VP, _I, C.c_double, C.c_double, _VP]),
     "sfx_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP]),
     "sfx_update_all": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _VP]),

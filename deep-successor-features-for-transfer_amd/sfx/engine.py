@@ -262,7 +262,7 @@ class SFEngine:
     def sync_target(self, t: int):
         check(lib.sfx_sync_target(self._h, t), "sfx_sync_target")
 
-    KINDS = {"fwd": 0, "tdg": 1, "bwd": 2, "gpi": 3, "lms": 4, "ver": 5, "round": 6, "tsf": 7, "pstep": 8}
+    KINDS = {"fwd": 0, "tdg": 1, "bwd": 2, "gpi": 3, "lms": 4, "ver": 5, "tsf": 6}
 
     def prof_enable(self, on: bool):
         check(lib.sfx_prof_enable(self._h, int(bool(on))), "sfx_prof_enable")
@@ -431,32 +431,6 @@ class SFEngine:
         s, f, r, n = C.c_longlong(), C.c_longlong(), C.c_longlong(), C.c_longlong()
         check(lib.sfx_step_stats(self._h, C.byref(s), C.byref(f), C.byref(r), C.byref(n)), "sfx_step_stats")
         return {"steps": s.value, "host_round_steps": f.value, "unverified_policies": r.value, "rounds": n.value}
-
-    def set_pstep(self, enable: bool):
-        """The persistent all-task step (k_pstep: one launch per env step, rounds looped on the
-        device) for sfx_step_all / the native runner's all-task steps where the geometry fits;
-        raises when the device's placement census fails."""
-        check(lib.sfx_set_pstep(self._h, int(bool(enable))), "sfx_set_pstep")
-
-    @property
-    def pstep(self) -> bool:
-        return lib.sfx_get_pstep(self._h) == 1
-
-    def pstep_stats(self):
-        out = (C.c_longlong * 4)()
-        check(lib.sfx_pstep_stats(self._h, out), "sfx_pstep_stats")
-        return {"steps": out[0], "rounds": out[1], "policies_checked": out[2], "policies_skipped": out[3]}
-
-    def pstep_trace(self):
-        """The last persistent step's rounds: (converged round, {round: {head: (computed, next actions [32])}})."""
-        buf = (C.c_int * (10 * 8 * 33 + 1))()
-        check(lib.sfx_pstep_trace(self._h, buf), "sfx_pstep_trace")
-        conv = buf[10 * 8 * 33]
-        out = {}
-        for r in range(conv):
-            out[r] = {t: (buf[(r * 8 + t) * 33 + 32], list(buf[(r * 8 + t) * 33:(r * 8 + t) * 33 + 32]))
-                      for t in range(self.T)}
-        return conv, out
 
     def nonfinite(self, reset: bool = False) -> bool:
         """SURVEY §5 failure detection: whether any TD error since the last reset was NaN / Inf."""

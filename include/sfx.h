@@ -219,29 +219,6 @@ int sfx_skip_stats(sfx_t h, long long* checked, long long* skipped, int reset);
  */
 int sfx_nonfinite(sfx_t h, int* flag_host, int reset);
 
-/*
- * The persistent all-task step (k_pstep): the whole env step of agents/sfdqn.py:57-60 over
- * features/deep.py:93-131 -- LMS, forwards, every speculative round until verified, action
- * selection and (runner steps) publication -- as ONE launch of 256 workgroups, head t on XCD t.
- * Replaces the launch sequence of sfx_step_all / the runner's all-task steps whenever the geometry
- * fits (T <= 8, hidden width 256, 1..4 hidden layers, n_s <= 64, A <= 32, d <= 32, max_batch <= 32,
- * fp32, GPI next actions, no per-step losses).  enable = 1 allocates its workspace and checks that
- * a 256-workgroup launch lands 32 workgroups on each of 8 XCDs (SFX_E_STATE otherwise); the
- * environment variable SFX_PSTEP=1 enables it at sfx_create.  sfx_get_pstep: 1 when enabled.
- * sfx_pstep_stats: [0] steps, [1] speculative rounds computed, [2] policy checks (rounds >= 1),
- * [3] policies that skipped a round.
- */
-int sfx_set_pstep(sfx_t h, int enable);
-int sfx_get_pstep(sfx_t h);
-int sfx_pstep_stats(sfx_t h, long long* out4_host);
-/* Diagnostics of the last persistent step: out_host[(r * 8 + t) * (32 + 1) + b] = the next action
- * head t's policy used in round r for row b, [... + 32] = 1 if head t computed round r (0: it
- * skipped); out_host[10 * 8 * 33] = the round at which every policy verified. */
-int sfx_pstep_trace(sfx_t h, int* out_host);
-/* Phase timeline of the last persistent step (builds with SFX_PSTEP_PROBE=1 in the environment at
- * sfx_set_pstep): out_host[t * 64 + i] = wall clock (100 MHz) of mark i of head t's rank 0. */
-int sfx_pstep_timeline(sfx_t h, long long* out_host);
-
 /* LMS reward fit SF.update_reward (features/successor.py:164-167) on w_t:
  * w <- w + alpha (r - φ·w) φ ;  phi_dev [d], r_dev [1]. */
 int sfx_lms(sfx_t h, int t, const float* phi_dev, const float* r_dev, float alpha);
@@ -255,8 +232,8 @@ int sfx_sync_target(sfx_t h, int t);
 /*
  * Event instrumentation for the benchmark's roofline figure: while enabled, graphs are
  * bypassed and every kernel launch is bracketed by a hipEvent pair.  Kinds:
- * 0 forward, 1 TD target, 2 backward+Adam, 3 GPI, 4 LMS, 5 speculation check, 6 persistent
- * round (k_round), 7 TSF transform (k_tsf_fwd / k_tsf_bwd).  collect() returns the number of
+ * 0 forward, 1 TD target, 2 backward+Adam, 3 GPI, 4 LMS, 5 speculation check, 6 TSF transform
+ * (k_tsf_fwd / k_tsf_bwd) and learned φ.  collect() returns the number of
  * launches of that kind, their summed event-measured duration (us) and their summed
  * ALGORITHMIC bytes (what the launch must read/write at minimum, fp32).
  */

@@ -60,16 +60,12 @@ def check_state(eng, st, T, k):
     rel_close(torch.stack([eng.get_w(t)[0] for t in range(T)]), st.w, rtol=1e-5, atol=1e-7)
 
 
-@pytest.mark.parametrize("pipeline,round_kernel", [(True, False), (False, False), (True, True)])
-def test_runner_matches_oracle(pipeline, round_kernel, monkeypatch):
-    """round_kernel: each speculative round as ONE k_round launch (SFX_ROUND=1, in-launch
-    per-head hand-offs) instead of its 7 launches -- same results."""
+@pytest.mark.parametrize("pipeline", [True, False])
+def test_runner_matches_oracle(pipeline, monkeypatch):
     from sfx.runner import NativeEnvLoop
 
     if not pipeline:
         monkeypatch.setenv("SFX_RUNNER_PIPELINE", "0")
-    if round_kernel:
-        monkeypatch.setenv("SFX_ROUND", "1")
     spec = R.Spec(17, 32, 7, 8, ("relu", "relu"))
     T, ev, alpha, n = 3, 4, 0.05, 24
     eng, st = make(spec, T, ev)

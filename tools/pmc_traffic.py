@@ -13,7 +13,7 @@ import json
 import os
 import sys
 
-KINDS = ("k_bwd", "k_fwd", "k_ver", "k_tdg", "k_gpi", "k_gate", "k_publish", "k_qmax", "k_round")
+KINDS = ("k_bwd", "k_fwd", "k_ver", "k_tdg", "k_gpi", "k_gate", "k_publish", "k_qmax")
 
 
 def load(d, counter):
