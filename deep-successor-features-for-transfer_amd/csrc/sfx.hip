@@ -23,6 +23,7 @@
 #include <cstring>
 #include <algorithm>
 #include <chrono>
+#include <deque>
 #include <map>
 #include <random>
 #include <string>
@@ -177,6 +178,13 @@ struct sfx_handle {
     const float *S = nullptr, *S1 = nullptr, *phi = nullptr, *gamma = nullptr, *s_next = nullptr;
     const int64_t* a = nullptr;
     float* losses = nullptr;
+    // native runner look-ahead: pre -- this step's minibatch roles were filled by the
+    // step before (no step-start forward; the gate resets the flag and runs the LMS); ax / aM --
+    // the next step's minibatch states [NS | NS1] (aM rows each), forwarded by this step's final
+    // round into the other copy of the minibatch roles
+    bool pre = false;
+    const float* ax = nullptr;
+    int aM = 0;
   } pend;
   // step statistics
   long long steps_spec = 0, steps_fallback = 0, policies_rerun = 0, rounds_total = 0;
@@ -365,8 +373,8 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
   F.lms_head = -1;
   F.qa_role = -1;
   F.skip = ex.skip;
-  if (ex.skip && (groups.size() != 1 || ex.flag || ex.lms_head >= 0 || (ex.qa_role >= 0 && !ex.qh)))
-    SFX_FAIL(SFX_E_STATE, "run_fwd: head skipping needs one group and no LMS / flag / maxima");
+  if (ex.skip && (ex.flag || ex.lms_head >= 0 || (ex.qa_role >= 0 && !ex.qh)))
+    SFX_FAIL(SFX_E_STATE, "run_fwd: head skipping needs no LMS / flag / maxima");
   int ninst = 0;
   bool uniform = true;  // every group covers heads 0..T-1: XCD-aware grid possible
   FwdGroup* slots[4] = {&F.g0, &F.g1, &F.g2, &F.g3};
@@ -432,8 +440,12 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
       F.tpw = h->fwd_tpw;
     const int ntNb = cdiv(F.ntN, F.tpw);
     const dim3 grid = F.xcd ? dim3(8 * cdiv(h->T, 8) * ntNb * F.ntM * F.ngroups) : dim3(ntNb, ninst, F.ntM);
-    double by = 4.0 * ninst * ((double)L.N * L.K + L.N + (double)M * L.K + (double)M * L.N);
-    if (l0) by += 4.0 * ninst * ((double)h->L[0].N * h->L[0].K + h->L[0].N + (double)M * h->L[0].K);
+    double by = 0.0;
+    for (const FwdGroup& g : groups) {  // each group at its own rows
+      const double m = g.m > 0 ? g.m : M;
+      by += 4.0 * g.n * ((double)L.N * L.K + L.N + m * L.K + m * L.N);
+      if (l0) by += 4.0 * g.n * ((double)h->L[0].N * h->L[0].K + h->L[0].N + m * h->L[0].K);
+    }
     const bool tp2 = F.tpw > 1;
     const bool gemv = !l0 && !qa && h->gemv_fwd && M <= GEMV_M && L.N >= GEMV_N && L.K % 16 == 0 &&
                       (l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0));
@@ -531,6 +543,8 @@ struct BwdExtra {
   const float* v_x = nullptr;
   const float* v_xn = nullptr;
   bool skip_fwd = false;      // in: the caller skips the post-update forward of skipped heads
+  const float* ax = nullptr;  // look-ahead rows of the fused forward (BwdArgs::ax), aM rows each
+  int aM = 0, a_noskip = 0;
   bool* skip_armed = nullptr; // out: this round's launches decide and honour BwdArgs::skip
   // launch `li` (tiles `ntile` of one head, grid dim3(ntile)) issued by the caller instead, with
   // extra workgroups of its own riding along (TSF: k_bwd_tsf); returns true when it launched.
@@ -539,6 +553,11 @@ struct BwdExtra {
 };
 
 bool can_fuse_v0(const sfx_handle* h, int vM) { return h->fuse_v0 && h->L[0].K <= KFUSE && vM * h->L[0].K <= VFUSE; }
+// the fused forward with the look-ahead rows as well (2 aM rows after vM, 16-B aligned, whole float4s)
+bool can_fuse_ahead(const sfx_handle* h, int vM, int aM) {
+  const int K = h->L[0].K;
+  return can_fuse_v0(h, vM) && ((vM * K + 3) & ~3) + 2 * aM * K <= VFUSE && (2 * aM * K) % 4 == 0;
+}
 
 int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const float* phi, const float* r,
             float* losses, const TdgSpec& td, const BwdExtra& ex = BwdExtra()) {
@@ -673,6 +692,9 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.act0 = h->L[0].actOut;
   A.v_x = ex.v_x;
   A.v_xn = ex.v_xn;
+  A.ax = ex.fuse_v0 ? ex.ax : nullptr;
+  A.aM = ex.fuse_v0 && ex.ax ? ex.aM : 0;
+  A.a_noskip = ex.a_noskip;
   const int ntile = A.nb + A.nc + A.tail;
   if (!(ex.ride && nhead == 1 && !A.xcd && ex.ride(h->NL - 1, tail_at, A, ntile, nhead * (dw_bytes(1) + dw_bytes(0)))))
     launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), h->bf16 ? k_bwd<true> : k_bwd<false>,
@@ -849,12 +871,27 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
   bx.v_x = p.S1;
   bx.v_xn = want_sel ? p.s_next : nullptr;
   const int vM = B + (want_sel ? 1 : 0);
+  // look-ahead: the final round (device or host) also forwards the next step's minibatch into the
+  // other copy of the minibatch roles; the first round that does (the last device round) computes
+  // them for every head, skipped or not -- later host rounds skip them with the rest of a head
+  const bool ahead = final && p.ax && p.aM > 0 && bx.fuse_v0 && can_fuse_ahead(h, vM, p.aM);
+  const int a_noskip = ahead && r <= h->spec_rounds - 1 ? 1 : 0;
+  if (ahead) {
+    bx.ax = p.ax;
+    bx.aM = p.aM;
+    bx.a_noskip = a_noskip;
+  }
   RC(run_bwd(h, 0, T, B, p.S, p.phi, nullptr, p.losses, td, bx));
   if (bx.fuse_v0) {
     FwdExtra vx;
     vx.l0 = 1;
     vx.skip = armed && r > 0 && bx.skip_fwd ? h->skip : nullptr;
-    RC(run_fwd(h, {{out, P_NEW, 0, 0, T}}, vM, nullptr, nullptr, vx));
+    if (ahead)
+      RC(run_fwd(h, {{out, P_NEW, 0, 0, T, vM, 0}, {R_NS, P_NEW, 0, 0, T, p.aM, a_noskip},
+                     {R_NS1, P_NEW, 0, 0, T, p.aM, a_noskip}, {R_NS1T, P_TARGET, 0, 0, T, p.aM, a_noskip}},
+                 std::max(vM, p.aM), nullptr, nullptr, vx));
+    else
+      RC(run_fwd(h, {{out, P_NEW, 0, 0, T}}, vM, nullptr, nullptr, vx));
   } else {
     RC(run_fwd(h, {{out, P_NEW, 2, 0, T}}, B, p.S1, p.S1));
   }
@@ -924,7 +961,10 @@ int launch_step_all(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, c
     return run_gpi(h, gpi_args(R_A, 0, 0, wsel, nullptr, nullptr, nullptr, nullptr, h->dout->sel, p.task,
                                p.sel_use_gpi, 1));
   }
-  RC(run_fwd(h, {{R_S, P_ONLINE, 1, 0, T}, {R_S1T, P_TARGET, 2, 0, T}, {R_S1, P_ONLINE, 2, 0, T}}, B, p.S, p.S1, ex));
+  // a look-ahead step (p.pre) starts at its TD launch: the step before forwarded its minibatch
+  // into these roles, its gate reset the flag and ran the LMS
+  if (!p.pre)
+    RC(run_fwd(h, {{R_S, P_ONLINE, 1, 0, T}, {R_S1T, P_TARGET, 2, 0, T}, {R_S1, P_ONLINE, 2, 0, T}}, B, p.S, p.S1, ex));
   for (int r = 0; r < rounds; ++r) RC(launch_round(h, p, r, r == rounds - 1));
   return SFX_OK;
 }

@@ -42,7 +42,11 @@ enum { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2 };
 // activation-block roles: ψ(S) online (saved for backward), ψ⁻(S1) target, ψ(S1) online
 // before the step, GPI scratch, action selection, and two alternating buffers of
 // ψ(S1 ++ s_next) online after a speculative round of the step
-enum { R_S = 0, R_S1T = 1, R_S1 = 2, R_G = 3, R_A = 4, R_V = 5, R_V2 = 6, NROLE = 7 };
+// Minibatch roles R_S / R_S1T / R_S1 exist twice: Geo::mb (0 or R_NS) picks the copy the current
+// step uses, R_NS / R_NS1T / R_NS1 name the other copy -- the native runner's look-ahead forward
+// (sfx_runner) fills the next step's minibatch roles from the final round's
+// post-update forward, so that step starts at its TD launch.
+enum { R_S = 0, R_S1T = 1, R_S1 = 2, R_G = 3, R_A = 4, R_V = 5, R_V2 = 6, R_NS = 7, R_NS1T = 8, R_NS1 = 9, NROLE = 10 };
 // parameter sets a forward instance can read
 enum { P_ONLINE = 0, P_TARGET = 1, P_NEW = 2 };
 
@@ -201,10 +205,14 @@ struct Geo {
   // updates).  Null in fp32 mode.
   __bf16* on16;
   __bf16* tg16;
+  int mb, pad_mb;  // 0 or R_NS: the physical copy of the minibatch roles this launch calls R_S .. R_S1
 
+  __device__ __forceinline__ int phys_role(int role) const {
+    return role < R_G ? role + mb : role >= R_NS ? role - R_NS + (R_NS - mb) : role;
+  }
   // off: per-layer offset inside a block (passed per launch as a scalar, never indexed)
   __device__ __forceinline__ float* actp(int role, int head, int off) const {
-    return act + ((long long)role * T + head) * actSize + off;
+    return act + ((long long)phys_role(role) * T + head) * actSize + off;
   }
   __device__ __forceinline__ float* dzp(int head, int off) const {
     return dz + (long long)head * actSize + off;
@@ -363,6 +371,8 @@ __device__ __forceinline__ void adam_el(float* p, float* m, float* v, float g, c
 // -------------------------------------------------------------------------------------
 struct FwdGroup {
   int role, which, xsel, head0, n;  // which: P_*; xsel: 1 -> xa, 2 -> xb
+  int m;       // rows of this group (0: FwdArgs::M); tiles past them exit
+  int noskip;  // FwdArgs::skip does not apply (look-ahead groups of the final device round)
 };
 
 struct FwdArgs {
@@ -467,22 +477,26 @@ __device__ void q_replay(const Geo& G, const FwdArgs& F, int head, int tN, int t
     }
 }
 
-__device__ void lms_block(const Geo& G, const FwdArgs& F) {
+// LMS reward fit (features/successor.py:164-167) by one workgroup: w += α (r - Σ φ⊙w) φ, the sum
+// in index order; no store when `cx` (a cancelled runner step).
+__device__ void lms_apply(float* w, const float* phi, const float* r, float alpha, int d, int cx) {
   __shared__ float s_p[DMAX];
   __shared__ float s_e;
-  const int tid = threadIdx.x, d = G.d;
-  float* w = G.w + (long long)F.lms_head * G.dpad;
-  const int cx = step_cancelled(G.cancel);
-  const float wk = tid < d ? w[tid] : 0.f, pk = tid < d ? F.lms_phi[tid] : 0.f;
+  const int tid = threadIdx.x;
+  const float wk = tid < d ? w[tid] : 0.f, pk = tid < d ? phi[tid] : 0.f;
   if (tid < d) s_p[tid] = __fmul_rn(pk, wk);
   __syncthreads();
   if (tid == 0) {
     float rf = 0.f;
     for (int k = 0; k < d; ++k) rf = __fadd_rn(rf, s_p[k]);
-    s_e = __fmul_rn(F.lms_alpha, __fsub_rn(F.lms_r[0], rf));
+    s_e = __fmul_rn(alpha, __fsub_rn(r[0], rf));
   }
   __syncthreads();
   if (tid < d && !cx) w[tid] = __fadd_rn(wk, __fmul_rn(s_e, pk));
+}
+
+__device__ void lms_block(const Geo& G, const FwdArgs& F) {
+  lms_apply(G.w + (long long)F.lms_head * G.dpad, F.lms_phi, F.lms_r, F.lms_alpha, G.d, step_cancelled(G.cancel));
 }
 
 // L0 = true (layer-1 launches of a forward from the states): the workgroup first computes the
@@ -506,6 +520,8 @@ __device__ __forceinline__ FwdGroup fwd_group(const FwdArgs& F, int& y) {
   g.xsel = pick(F.g0.xsel, F.g1.xsel, F.g2.xsel, F.g3.xsel);
   g.head0 = pick(F.g0.head0, F.g1.head0, F.g2.head0, F.g3.head0);
   g.n = pick(F.g0.n, F.g1.n, F.g2.n, F.g3.n);
+  g.m = pick(F.g0.m, F.g1.m, F.g2.m, F.g3.m);
+  g.noskip = pick(F.g0.noskip, F.g1.noskip, F.g2.noskip, F.g3.noskip);
   return g;
 }
 
@@ -527,7 +543,8 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
   // no FwdGroup copy: conditionally copied structs were demoted to scratch, 17 dwords per lane)
   const FwdGroup grp = fwd_group(F, y);
   const int head = grp.head0 + y;
-  const int M = F.M, N = F.N, K = F.K;
+  const int M = grp.m > 0 ? grp.m : F.M, N = F.N, K = F.K;
+  if (tM * 32 >= M) return;  // a group with fewer rows than the launch (block-uniform, before any barrier)
   const float* P = grp.which == P_TARGET ? G.target + (long long)head * G.P
                                          : G.online + G.slot_off(rslot(F.mask, head) ^ (grp.which == P_NEW), head);
   const float* X = F.xOff < 0 ? (grp.xsel == 1 ? F.xa : F.xb) : G.actp(grp.role, head, F.xOff);
@@ -805,10 +822,10 @@ __device__ __forceinline__ void fwd_body(const Geo& G, const FwdArgs& F, int bx,
     qa = grp.role == F.qa_role;
     head = grp.head0 + yy;
   }
-  if (F.skip) {  // single group: instance y is the head
+  if (F.skip) {  // instance y is the head inside its group
     int yy = y;
     const FwdGroup grp = fwd_group(F, yy);
-    if (__builtin_nontemporal_load(F.skip + grp.head0 + yy)) {
+    if (!grp.noskip && __builtin_nontemporal_load(F.skip + grp.head0 + yy)) {
       if (qa && F.qh) q_replay(G, F, head, tN, tM);  // its maxima terms as that round stored them
       return;
     }
@@ -1050,6 +1067,12 @@ struct BwdArgs {
   float* losses;       // tail: [n_head][3] (l1+l2, l1, l2) or null
   const float* v_x;    // fused forward input rows 0..M-1 (S1)
   const float* v_xn;   // fused forward input row M (s_next) or null
+  // look-ahead rows of the fused forward (runner steps): ax = [NS (aM rows) | NS1 (aM
+  // rows)], the next step's minibatch states; layer 0 of NS -> R_NS, NS1 -> R_NS1 with the
+  // post-update weights and NS1 -> R_NS1T with the target weights.  aM = 0: none.  a_noskip: the
+  // layer-0 tiles of a head that skips this round still compute them (first round that has them)
+  const float* ax;
+  int aM, a_noskip;
   // sharded step: the fused-TD launch re-initialises the next round's maxima buffer (xi_dst[j] =
   // xi_src[j] for j < xi_copy, SORT_EMPTY up to xi_n) -- its last reader was an earlier launch
   const int* xi_src;
@@ -1412,57 +1435,150 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
 }
 
 // post-update forward of layer 0 for the 32 output rows this tile just optimised
-// (input rows staged in LDS by role_dw: sX[m * K + k], m < vM)
+// (input rows staged in LDS by role_dw: sX[m * K + k], m < vM); with look-ahead rows also
+// (sX[aoff + m * K + k], m < 2 aM) those rows into R_NS / R_NS1 and, with the target weights sWt,
+// NS1 into R_NS1T.  vrows = false: the look-ahead rows only (a skipped head).
+__device__ __forceinline__ int v0_aoff(const BwdArgs& A, int K) { return (A.vM * K + 3) & ~3; }
+
 template <bool C>
 __device__ void fused_v0(const Geo& G, const BwdArgs& A, const RoleGeo& L, int head, int nbase, const float* sW,
-                         const float* sB, const float* sX) {
+                         const float* sB, const float* sX, const float* sWt = nullptr, const float* sBt = nullptr,
+                         bool vrows = true) {
+  if (A.aM > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the look-ahead LDS-DMA has landed
   __syncthreads();
   PROBE_AT(3);
   const int K = L.K, N = L.N, VM = A.vM;
-  float* Y = G.actp(A.vRole, head, A.vOff);
   // MFMA from LDS (the same k-ordered accumulation as k_fwd's layer-0 path): wave w owns
   // column half (w & 1) and row tiles (w >> 1), (w >> 1) + 2, ...
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
   const int nl = (wave & 1) * 16 + r, n = nbase + nl;
   const float bias = sB[nl];
-  for (int mt = wave >> 1; mt * 16 < VM; mt += 2) {
-    floatx4 c = {0.f, 0.f, 0.f, 0.f};
-    const int ma = mt * 16 + r;
-    for (int k4 = 0; k4 < K; k4 += 4) {
-      const int k = k4 + g;
-      const float a = (k < K && ma < VM) ? sX[ma * K + k] : 0.f;
-      const float b = k < K ? sW[nl * KFUSE + k] : 0.f;
-      c = mfma4(a, b, c);
-    }
-    if (n < N) {
+  if (vrows) {
+    float* Y = G.actp(A.vRole, head, A.vOff);
+    for (int mt = wave >> 1; mt * 16 < VM; mt += 2) {
+      floatx4 c = {0.f, 0.f, 0.f, 0.f};
+      const int ma = mt * 16 + r;
+      for (int k4 = 0; k4 < K; k4 += 4) {
+        const int k = k4 + g;
+        const float a = (k < K && ma < VM) ? sX[ma * K + k] : 0.f;
+        const float b = k < K ? sW[nl * KFUSE + k] : 0.f;
+        c = mfma4(a, b, c);
+      }
+      if (n < N) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = mt * 16 + g * 4 + i;
-        if (m < VM) stc<C>(Y + (size_t)m * N + n, act_fwd(__fadd_rn(c[i], bias), A.act0));
+        for (int i = 0; i < 4; ++i) {
+          const int m = mt * 16 + g * 4 + i;
+          if (m < VM) stc<C>(Y + (size_t)m * N + n, act_fwd(__fadd_rn(c[i], bias), A.act0));
+        }
+      }
+    }
+  }
+  if (A.aM > 0) {
+    // 16-row tiles of three products, one per iteration: NS -> R_NS and NS1 -> R_NS1 with the
+    // post-update weights, NS1 -> R_NS1T with the target weights (row stride K in sWt)
+    const int aM = A.aM, nt = (aM + 15) >> 4;
+    const float* xa = sX + v0_aoff(A, K);
+    const float bt = sBt[nl];
+    for (int it = wave >> 1; it < 3 * nt; it += 2) {
+      const int which = it / nt, mt = it - which * nt;
+      const float* x = xa + (which ? aM * K : 0);
+      const float* w = which == 2 ? sWt + nl * K : sW + nl * KFUSE;
+      const float bb = which == 2 ? bt : bias;
+      float* Y = G.actp(which == 0 ? R_NS : which == 1 ? R_NS1 : R_NS1T, head, A.vOff);
+      floatx4 c = {0.f, 0.f, 0.f, 0.f};
+      const int ma = mt * 16 + r;
+      for (int k4 = 0; k4 < K; k4 += 4) {
+        const int k = k4 + g;
+        const float a = (k < K && ma < aM) ? x[ma * K + k] : 0.f;
+        const float b = k < K ? w[k] : 0.f;
+        c = mfma4(a, b, c);
+      }
+      if (n < N) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = mt * 16 + g * 4 + i;
+          if (m < aM) stc<C>(Y + (size_t)m * N + n, act_fwd(__fadd_rn(c[i], bb), A.act0));
+        }
       }
     }
   }
 }
 
+typedef __attribute__((address_space(3))) void* tsf_lds_t;
+
+// LDS-DMA staging: dst[j] = *src(j) for j < n (global_load_lds_dword; wave-uniform LDS base +
+// lane * 4, per-lane global address, no VGPR destination), by waves [w0, w0 + nw) of the
+// workgroup; src(j) == nullptr marks a padding word, zeroed by a plain LDS store instead.
+// Nothing waits here: the loads of every staging call stay in flight together until the
+// caller's next __syncthreads().
+template <class F>
+__device__ __forceinline__ void glds(float* dst, int n, F src, int w0 = 0, int nw = 4) {
+  const int lane = threadIdx.x & 63, wv = (threadIdx.x >> 6) - w0;
+  if (wv < 0 || wv >= nw) return;
+  for (int c = wv; c * 64 < n; c += nw) {
+    const int j = c * 64 + lane;
+    const float* p = j < n ? src(j) : nullptr;
+    if (p)
+      __builtin_amdgcn_global_load_lds((const void*)p, (tsf_lds_t)(dst + c * 64), 4, 0, 0);
+    else if (j < n)
+      dst[j] = 0.f;
+  }
+}
+
+// LDS of the fused post-update layer-0 forward, one instance per kernel for both of its callers
+// (role_dw's layer-0 tiles and role_v0_only): the tile's weights and biases, the input rows, the
+// target weights and biases of the look-ahead rows.
+struct V0Smem {
+  float sW[32 * KFUSE];
+  float sB[32];
+  float sWt[32 * KFUSE];
+  float sBt[32];
+  __align__(16) float sX[VFUSE];
+};
+__device__ __forceinline__ V0Smem& v0_smem() {
+  __shared__ V0Smem sm;
+  return sm;
+}
+
+// The look-ahead operands by LDS-DMA (no registers; they land while the tile does its dW): the
+// 2 aM input rows (BwdArgs::ax) at sX + v0_aoff, the target weights of columns [nbase, nbase + 32)
+// (32 contiguous rows of K floats; row stride K in sWt) and their biases.  Landed at fused_v0.
+__device__ __forceinline__ void v0_stage_ahead(const Geo& G, const BwdArgs& A, const RoleGeo& L, int head, int nbase,
+                                               V0Smem& sm) {
+  const int K = L.K, ncol = L.N - nbase < 32 ? L.N - nbase : 32;
+  const float* ax = A.ax;
+  glds(sm.sX + v0_aoff(A, K), 2 * A.aM * K, [&](int j) -> const float* { return ax + j; });
+  const float* Pt = G.target + (long long)head * G.P;
+  const float* tw = Pt + L.wOff + (size_t)nbase * K;
+  glds(sm.sWt, 32 * K, [&](int j) -> const float* { return j < ncol * K ? tw + j : nullptr; });
+  const float* tb = Pt + L.bOff + nbase;
+  glds(sm.sBt, 32, [&](int j) -> const float* { return j < ncol ? tb + j : nullptr; }, 0, 1);
+}
+
 // A layer-0 dW tile of a policy that repeats the previous round (BwdArgs::skip): no gradient,
 // no Adam -- the write slot already holds this round's weights -- only the fused post-update
-// forward of its 32 columns, from those weights (the bits role_dw would have staged).
+// forward of its 32 columns, from those weights (the bits role_dw would have staged): every row
+// (vrows), or the look-ahead rows alone (BwdArgs::a_noskip).
 // Fused layers have K <= KFUSE <= 64: one k-tile, so tile = column tile.
-__device__ void role_v0_only(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile) {
+__device__ void role_v0_only(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile, bool vrows) {
   const int N = L.N, K = L.K, M = A.M, tid = threadIdx.x, nbase = tile * 32;
   const float* Pw = G.online + G.slot_off(rslot(A.mask, head) ^ 1, head);
-  __shared__ float sW[32 * KFUSE];
-  __shared__ float sB[32];
-  __shared__ float sX[VFUSE];
+  V0Smem& sm = v0_smem();
+  float* sW = sm.sW;
+  float* sB = sm.sB;
+  float* sX = sm.sX;
+  if (A.aM > 0) v0_stage_ahead(G, A, L, head, nbase, sm);
   const FDiv fK = fdiv(K);
   for (int j = tid; j < 32 * K; j += 256) {
     const int nl = j / fK, k = j - nl * K;
     sW[nl * KFUSE + k] = nbase + nl < N ? Pw[L.wOff + (size_t)(nbase + nl) * K + k] : 0.f;
   }
   if (tid < 32) sB[tid] = nbase + tid < N ? Pw[L.bOff + nbase + tid] : 0.f;
-  const int nxs = A.vM * K;
-  for (int j = tid; j < nxs; j += 256) sX[j] = j < M * K ? A.v_x[j] : A.v_xn[j - M * K];
-  fused_v0<false>(G, A, L, head, nbase, sW, sB, sX);
+  if (vrows) {
+    const int nxs = A.vM * K;
+    for (int j = tid; j < nxs; j += 256) sX[j] = j < M * K ? A.v_x[j] : A.v_xn[j - M * K];
+  }
+  fused_v0<false>(G, A, L, head, nbase, sW, sB, sX, sm.sWt, sm.sBt, vrows);
 }
 
 template <bool C = false, bool BF = false>
@@ -1521,6 +1637,7 @@ __device__ __forceinline__ void role_dw(const Geo& G, const BwdArgs& A, int head
   float xn = 0.f;
   const int nx = fuse ? M * K : 0;
   const int nxn = fuse && A.v_xn ? K : 0;
+  if (fuse && A.aM > 0) v0_stage_ahead(G, A, L, head, nbase, v0_smem());
   if (fuse) {
     if ((nx & 3) == 0 && (reinterpret_cast<uintptr_t>(A.v_x) & 15) == 0) {
 #pragma unroll
@@ -1565,9 +1682,10 @@ __device__ __forceinline__ void role_dw(const Geo& G, const BwdArgs& A, int head
   bsum = __fadd_rn(bsum, __shfl_xor(bsum, 16));
   bsum = __fadd_rn(bsum, __shfl_xor(bsum, 32));
   PROBE_MARK();
-  __shared__ float sW[32 * KFUSE];
-  __shared__ float sB[32];
-  __shared__ __align__(16) float sX[VFUSE];
+  V0Smem& sm = v0_smem();
+  float* sW = sm.sW;
+  float* sB = sm.sB;
+  float* sX = sm.sX;
   if (fuse) {
 #pragma unroll
     for (int q = 0; q < XQ; ++q) {
@@ -1612,7 +1730,7 @@ __device__ __forceinline__ void role_dw(const Geo& G, const BwdArgs& A, int head
     }
     if (fuse) sB[nbias - nbase] = bp;
   }
-  if (fuse) fused_v0<C>(G, A, L, head, nbase, sW, sB, sX);
+  if (fuse) fused_v0<C>(G, A, L, head, nbase, sW, sB, sX, sm.sWt, sm.sBt);
 }
 
 // dW + Adam of a 64 (output columns) x 64 (inputs) tile of a wide hidden layer (RoleGeo::nw == 2,
@@ -1822,7 +1940,7 @@ __device__ __forceinline__ void bwd_body(const Geo& G, const BwdArgs& A, int hea
   // bulk of the launch does: layer-0 dW (+ the fused post-update forward), dW, dX, tail
   if (bx < A.nc) {
     if (skip) {
-      if (A.fuse_v0 && !A.skip_v0) role_v0_only(G, A, head, A.rc, bx);
+      if (A.fuse_v0 && (!A.skip_v0 || (A.aM > 0 && A.a_noskip))) role_v0_only(G, A, head, A.rc, bx, !A.skip_v0);
       return;
     }
     role_dw<false, BF>(G, A, head, A.rc, bx, A.fuse_v0 != 0);
@@ -2246,6 +2364,14 @@ struct GateArgs {
   int* cancel;          // device: this step's verdict for its kernels (Geo::cancel)
   int* clr;             // sharded steps: SORT_EMPTY-fill clr[0, nclr) (round 0's maxima buffers)
   int nclr, pad2_;
+  // a look-ahead step (its minibatch forward ran in the step before): the step-start work of the
+  // forward's block 0 moves here -- the speculation flag reset and the LMS reward fit
+  int* flag;
+  int flag_value, lms_d;
+  float* lms_w;
+  const float* lms_phi;  // in the staging the gate copies from
+  const float* lms_r;
+  float lms_alpha, pad3_;
 };
 
 // Wait for the host's go of this step (bounded); 1 if the step may run, 0 if it is cancelled.
@@ -2313,6 +2439,8 @@ __global__ __launch_bounds__(256) void k_gate(GateArgs g) {
   if (g.clr) fill_sortable(g.clr, nullptr, 0, g.nclr, threadIdx.x, 256);
   PROBE_MARK();
   for (int i = threadIdx.x; i < g.n16; i += 256) g.dst[i] = g.src[i];
+  if (g.flag && threadIdx.x == 0) *g.flag = g.flag_value;
+  if (g.lms_w) lms_apply(g.lms_w, g.lms_phi, g.lms_r, g.lms_alpha, g.lms_d, 0);
   PROBE_REC(9, pt0);
 }
 

@@ -261,26 +261,7 @@ __device__ __forceinline__ float tsf_dot4(const float* a, const float* b, int n4
   return __fadd_rn(__fadd_rn(acc.x, acc.y), __fadd_rn(acc.z, acc.w));
 }
 
-typedef __attribute__((address_space(3))) void* tsf_lds_t;
-
-// LDS-DMA staging: dst[j] = *src(j) for j < n (global_load_lds_dword; wave-uniform LDS base +
-// lane * 4, per-lane global address, no VGPR destination), by waves [w0, w0 + nw) of the
-// workgroup; src(j) == nullptr marks a padding word, zeroed by a plain LDS store instead.
-// Nothing waits here: the loads of every staging call stay in flight together until the
-// caller's next __syncthreads().
-template <class F>
-__device__ __forceinline__ void glds(float* dst, int n, F src, int w0 = 0, int nw = 4) {
-  const int lane = threadIdx.x & 63, wv = (threadIdx.x >> 6) - w0;
-  if (wv < 0 || wv >= nw) return;
-  for (int c = wv; c * 64 < n; c += nw) {
-    const int j = c * 64 + lane;
-    const float* p = j < n ? src(j) : nullptr;
-    if (p)
-      __builtin_amdgcn_global_load_lds((const void*)p, (tsf_lds_t)(dst + c * 64), 4, 0, 0);
-    else if (j < n)
-      dst[j] = 0.f;
-  }
-}
+// glds / tsf_lds_t (LDS-DMA staging): sfx_kernels.h
 
 // The K flows of g (packed: flow k at k(2 n_s + 1): w[n_s], b, u[n_s]) -> LDS in the chain layout
 // (tsf_fst): w at [0, NP), u at [NP, 2NP), b at 2NP, c (filled by the caller) at 2NP + 1, zeros

@@ -73,6 +73,7 @@ SIGNATURES = {
     "sfx_runner_gate_timeout": (_I, [_VP, _D]),
     "sfx_runner_wait_timeout": (_I, [_VP, _D]),
     "sfx_runner_retried": (_I, [_VP, C.POINTER(C.c_longlong)]),
+    "sfx_runner_ahead_stats": (_I, [_VP, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
     "sfx_runner_recomputed": (_I, [_VP, C.POINTER(C.c_longlong)]),
     "sfx_runner_warm": (_I, [_VP]),
     "sfx_runner_gpi_counters": (_I, [_VP, C.POINTER(C.c_longlong)]),
@@ -105,6 +106,9 @@ SIGNATURES = {
     "sfx_tsf_get_g": (_I, [_VP, _I, _FP, _FP, _FP]),
     "sfx_tsf_load_h": (_I, [_VP, _FP]),
     "sfx_tsf_get_h": (_I, [_VP, _FP]),
+    "sfx_tsf_load_g_state": (_I, [_VP, _I, _VP, _VP, _VP]),
+    "sfx_tsf_get_h_state": (_I, [_VP, _I, _VP, _VP]),
+    "sfx_tsf_load_h_state": (_I, [_VP, _I, _VP, _VP]),
     "sfx_tsf_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP]),
     "sfx_tsf_test_action": (_I, [_VP, _VP, _VP, _VP, _VP]),
     "sfx_phi_setup": (_I, [_VP, _I, _I, _F]),

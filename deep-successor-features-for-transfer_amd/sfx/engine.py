@@ -467,6 +467,7 @@ class SFEngine:
     def tsf_freeze_flows(self, freeze: bool = True):
         """sfx_tsf_freeze_flows: hold the planar flows fixed (the Linear of g_i and h still train)."""
         check(lib.sfx_tsf_freeze_flows(self._h, int(bool(freeze))), "sfx_tsf_freeze_flows")
+        self.tsf_frozen = bool(freeze)
 
     def tsf_setup(self, G: int, K: int = 0, beta: float = 1.0, lr_g: float = 1e-3, wd_g: float = 0.0,
                   lr_h: float = 1e-3, wd_h: float = 0.0):
@@ -474,6 +475,8 @@ class SFEngine:
         check(lib.sfx_tsf_setup(self._h, int(G), int(K), float(beta), float(lr_g), float(wd_g), float(lr_h),
                                 float(wd_h)), "sfx_tsf_setup")
         self.tsf_G, self.tsf_K = G, K
+        self.tsf_hp = dict(beta=float(beta), lr_g=float(lr_g), wd_g=float(wd_g), lr_h=float(lr_h), wd_h=float(wd_h))
+        self.tsf_frozen = False
         self.tsf_Pg = K * (2 * self.n_s + 1) + G * self.n_s + G
         self.tsf_Ph = self.d * G + self.d
 
@@ -487,6 +490,27 @@ class SFEngine:
         g, m, v = (np.empty(self.tsf_Pg, dtype=np.float32) for _ in range(3))
         check(lib.sfx_tsf_get_g(self._h, t, fptr(g), fptr(m), fptr(v)), "sfx_tsf_get_g")
         return torch.from_numpy(g), torch.from_numpy(m), torch.from_numpy(v)
+
+    def tsf_load_g_state(self, t: int, g, gm, gv):
+        """g_t with its Adam moments (checkpoint resume)."""
+        a = [np.ascontiguousarray(torch.as_tensor(x).detach().cpu().reshape(-1).numpy(), dtype=np.float32)
+             for x in (g, gm, gv)]
+        if any(x.size != self.tsf_Pg for x in a):
+            raise ValueError(f"g and its moments must have {self.tsf_Pg} entries")
+        check(lib.sfx_tsf_load_g_state(self._h, t, fptr(a[0]), fptr(a[1]), fptr(a[2])), "sfx_tsf_load_g_state")
+
+    def tsf_get_h_state(self, t: int):
+        """Task t's Adam moments of the shared h."""
+        m, v = (np.empty(self.tsf_Ph, dtype=np.float32) for _ in range(2))
+        check(lib.sfx_tsf_get_h_state(self._h, t, fptr(m), fptr(v)), "sfx_tsf_get_h_state")
+        return torch.from_numpy(m), torch.from_numpy(v)
+
+    def tsf_load_h_state(self, t: int, hm, hv):
+        a = [np.ascontiguousarray(torch.as_tensor(x).detach().cpu().reshape(-1).numpy(), dtype=np.float32)
+             for x in (hm, hv)]
+        if any(x.size != self.tsf_Ph for x in a):
+            raise ValueError(f"h moments must have {self.tsf_Ph} entries")
+        check(lib.sfx_tsf_load_h_state(self._h, t, fptr(a[0]), fptr(a[1])), "sfx_tsf_load_h_state")
 
     def tsf_load_h(self, h):
         a = np.ascontiguousarray(torch.as_tensor(h).detach().cpu().reshape(-1).numpy(), dtype=np.float32)
@@ -504,6 +528,7 @@ class SFEngine:
         """features/deep_phi.py's learned φ (main_sfdqn_phi_torch.py phi_model_lambda shape)."""
         check(lib.sfx_phi_setup(self._h, int(width_mul), int(n_mid), float(lr)), "sfx_phi_setup")
         self.phi_numel = lib.sfx_phi_numel(self._h)
+        self.phi_cfg = dict(width_mul=int(width_mul), n_mid=int(n_mid), lr=float(lr))
 
     def phi_load(self, params):
         a = np.ascontiguousarray(torch.as_tensor(params).detach().cpu().reshape(-1).numpy(), dtype=np.float32)

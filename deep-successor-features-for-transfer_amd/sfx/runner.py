@@ -342,9 +342,11 @@ class NativeEnvLoop:
         rc, nf = C.c_longlong(), C.c_longlong()
         self._check(self._lib.sfx_runner_recomputed(self._r, C.byref(rc)), "sfx_runner_recomputed")
         self._check(self._lib.sfx_runner_nonfinite(self._r, C.byref(nf)), "sfx_runner_nonfinite")
+        ps, ofs = C.c_longlong(), C.c_longlong()
+        self._check(self._lib.sfx_runner_ahead_stats(self._r, C.byref(ps), C.byref(ofs)), "sfx_runner_ahead_stats")
         return {"env_steps": a.value, "prelaunched": b.value, "host_round_steps": c.value,
                 "host_wait_us": round(w.value, 1), "retried": rt.value, "recomputed": rc.value,
-                "nonfinite_steps": nf.value}
+                "nonfinite_steps": nf.value, "ahead_pre_steps": ps.value, "ahead_own_forward_steps": ofs.value}
 
     def gpi_counters(self) -> np.ndarray:
         T = self.eng.T_glob if self.schedule == "sharded" else self.eng.T

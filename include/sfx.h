@@ -322,6 +322,14 @@ int sfx_runner_wait_timeout(sfx_runner_t r, double seconds);
 int sfx_runner_warm(sfx_runner_t r);
 /* Steps issued again after their gate gave up (the step in flight, or steps queued behind it). */
 int sfx_runner_retried(sfx_runner_t r, long long* retried);
+/* Look-ahead (all-task schedule with the host replay; SFX_AHEAD=0 turns it off): the final
+ * speculative round of env step E also runs the forward of step E+1's minibatch -- its indices are
+ * drawn a step early from the runner's own index stream -- into the other copy of the minibatch
+ * activations, so step E+1 opens with its TD launch (its gate resets the speculation flag and runs
+ * the LMS fit).  pre_steps: steps that started so; own_forward_steps: steps with an update that ran
+ * their own forward (their minibatch sampled the slot of their own transition, whose next state
+ * was unknown a step early; the first step of a run; after a target sync or a drain). */
+int sfx_runner_ahead_stats(sfx_runner_t r, long long* pre_steps, long long* own_forward_steps);
 /* Steps whose host rounds found later steps cancelled at their gates: those steps' launches ran
  * (committing nothing) over the transient buffers the rounds read, so the step's forward and
  * device rounds were recomputed from its pre-step slot first. */
@@ -415,6 +423,11 @@ int sfx_tsf_load_g(sfx_t h, int t, const float* g_host);
 int sfx_tsf_get_g(sfx_t h, int t, float* g_host, float* gm_host, float* gv_host);
 int sfx_tsf_load_h(sfx_t h, const float* h_host);
 int sfx_tsf_get_h(sfx_t h, float* h_host);
+/* Checkpoint resume (sfx.checkpoint): g_t with its Adam moments; task t's Adam moments of the
+ * shared h (every task's optimizer holds its own, tsfdqn.py:255-270). */
+int sfx_tsf_load_g_state(sfx_t h, int t, const float* g_host, const float* gm_host, const float* gv_host);
+int sfx_tsf_get_h_state(sfx_t h, int t, float* hm_host, float* hv_host);
+int sfx_tsf_load_h_state(sfx_t h, int t, const float* hm_host, const float* hv_host);
 /* TSFDQN.update_successor(transitions, policy, use_gpi): losses_dev [3] = (l1 + β l2, l1, l2) */
 int sfx_tsf_update(sfx_t h, int policy, const float* S_dev, const int64_t* a_dev, const float* r_dev,
                    const float* phi_dev, const float* S1_dev, const float* gamma_dev, int B, int use_gpi,

@@ -3,6 +3,7 @@ reference's ψ Sequential (main_sfdqn_torch.py:44-78) and its torch.optim.Adam e
 continues from the restored state bit for bit, and save -> load(weights_only=True) restores every
 field.  The engine is a host stand-in with SFEngine's state-I/O methods (the GPU round trip is in
 tests/test_gpu_checkpoint.py)."""
+import pytest
 import torch
 
 from sfx import checkpoint as ck
@@ -123,3 +124,153 @@ def test_geometry_mismatch_is_refused():
         assert "geometry" in str(e)
     else:
         raise AssertionError("a checkpoint of another geometry loaded")
+
+
+# ----------------------------------------------------------------------------- TSF-DQN
+G_W, K_FLOWS = 12, 3
+
+
+class PlanarFlow(torch.nn.Module):
+    """The reference's planar layer (tsfdqn_nf.py:331-352): z + scale * tanh(z·weightᵀ + bias),
+    parameters registered in the order weight, bias, scale."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.weight = torch.nn.Parameter(torch.empty(1, dim).uniform_(-0.01, 0.01))
+        self.bias = torch.nn.Parameter(torch.empty(1).uniform_(-0.01, 0.01))
+        self.scale = torch.nn.Parameter(torch.empty(1, dim).uniform_(-0.01, 0.01))
+
+    def forward(self, z):
+        return z + self.scale * torch.tanh(torch.nn.functional.linear(z, self.weight, self.bias))
+
+
+class HostTSFEngine(HostEngine):
+    """HostEngine plus the TSF state surface (g_i with moments, the shared h, per-task h moments)."""
+
+    def __init__(self, T, K):
+        super().__init__(T)
+        self.tsf_G, self.tsf_K = G_W, K
+        self.tsf_Pg = K * (2 * N_S + 1) + G_W * N_S + G_W
+        self.tsf_Ph = D * G_W + D
+        self.tsf_hp = dict(beta=1.0, lr_g=2e-3, wd_g=0.0, lr_h=3e-3, wd_h=0.0)
+        self.tsf_frozen = False
+        self.g, self.gm, self.gv = (torch.zeros(T, self.tsf_Pg) for _ in range(3))
+        self.h = torch.zeros(self.tsf_Ph)
+        self.hm, self.hv = torch.zeros(T, self.tsf_Ph), torch.zeros(T, self.tsf_Ph)
+
+    def tsf_get_g(self, t):
+        return self.g[t].clone(), self.gm[t].clone(), self.gv[t].clone()
+
+    def tsf_load_g_state(self, t, g, gm, gv):
+        self.g[t], self.gm[t], self.gv[t] = (torch.as_tensor(x).reshape(-1) for x in (g, gm, gv))
+
+    def tsf_get_h(self):
+        return self.h.clone()
+
+    def tsf_load_h(self, h):
+        self.h = torch.as_tensor(h).reshape(-1).clone()
+
+    def tsf_get_h_state(self, t):
+        return self.hm[t].clone(), self.hv[t].clone()
+
+    def tsf_load_h_state(self, t, hm, hv):
+        self.hm[t], self.hv[t] = torch.as_tensor(hm).reshape(-1), torch.as_tensor(hv).reshape(-1)
+
+    def tsf_freeze_flows(self, freeze=True):
+        self.tsf_frozen = bool(freeze)
+
+
+def _tsf_modules(seed, K, h_fn):
+    """A TSF task's modules and its 4-group Adam (tsfdqn.py:255-270)."""
+    torch.manual_seed(seed)
+    psi = psi_module(N_S, H, A, D, ACTS)
+    w = torch.nn.Linear(D, 1, bias=False)
+    g = torch.nn.Linear(N_S, G_W) if K == 0 else torch.nn.Sequential(
+        *[PlanarFlow(N_S) for _ in range(K)], torch.nn.Linear(N_S, G_W))
+    opt = torch.optim.Adam([{"params": psi.parameters(), "lr": 1e-3, "weight_decay": 0.0},
+                            {"params": w.parameters(), "lr": 1e-3, "weight_decay": 0.0},
+                            {"params": g.parameters(), "lr": 2e-3, "weight_decay": 0.0},
+                            {"params": h_fn.parameters(), "lr": 3e-3, "weight_decay": 0.0}])
+    return psi, w, g, opt
+
+
+def _tsf_task(seed, K, h_fn):
+    """... after 3 seeded updates."""
+    psi, w, g, opt = _tsf_modules(seed, K, h_fn)
+    for _ in range(3):
+        _tsf_step(psi, w, g, h_fn, opt, torch.randn(8, N_S))
+    return psi, w, g, opt
+
+
+def _tsf_step(psi, w, g, h_fn, opt, x):
+    opt.zero_grad()
+    (psi(x).pow(2).mean() + w(h_fn(g(x))).pow(2).mean()).backward()
+    opt.step()
+
+
+def _flat_state(opt, params, key):
+    return torch.cat([opt.state[p][key].reshape(-1) for p in params])
+
+
+@pytest.mark.parametrize("K", [0, K_FLOWS])
+def test_tsf_export_continues_the_reference_agent(K):
+    """TSF-DQN (VERDICT r3 missing #3): the export of g_i, w_i, the shared h and each task's 4-group
+    Adam loads into the reference's modules and optimizer, which then continue bit for bit."""
+    torch.manual_seed(0)
+    h_fn = torch.nn.Linear(G_W, D)
+    tasks = [_tsf_task(10 + t, K, h_fn) for t in range(2)]
+    eng = HostTSFEngine(2, K)
+    for t, (psi, w, g, opt) in enumerate(tasks):
+        eng.load_head(t, flatten(psi), 0)
+        eng.load_head(t, flatten(psi), 1)
+        eng.load_adam(t, _flat_state(opt, list(psi.parameters()), "exp_avg"),
+                      _flat_state(opt, list(psi.parameters()), "exp_avg_sq"), 6)
+        eng.load_w_state(t, w.weight.detach().reshape(-1), opt.state[w.weight]["exp_avg"].reshape(-1),
+                         opt.state[w.weight]["exp_avg_sq"].reshape(-1))
+        eng.tsf_load_g_state(t, flatten(g), _flat_state(opt, list(g.parameters()), "exp_avg"),
+                             _flat_state(opt, list(g.parameters()), "exp_avg_sq"))
+        eng.tsf_load_h_state(t, _flat_state(opt, list(h_fn.parameters()), "exp_avg"),
+                             _flat_state(opt, list(h_fn.parameters()), "exp_avg_sq"))
+    eng.tsf_load_h(flatten(h_fn))
+    sd = ck.state_dict(eng)
+    # the engine round trip (before the optimizers below take the exported moments over in place)
+    other = HostTSFEngine(2, K)
+    ck.load_state_dict(other, sd)
+    for name in ("g", "gm", "gv", "hm", "hv", "h", "heads", "m", "v", "w", "wm", "wv"):
+        assert torch.equal(getattr(other, name), getattr(eng, name)), name
+    h2 = torch.nn.Linear(G_W, D)
+    h2.load_state_dict(sd["h_model"])
+    x = torch.randn(8, N_S, generator=torch.Generator().manual_seed(5))
+    for t, (psi, w, g, opt) in enumerate(tasks):
+        fp, fw, fg, fo = _tsf_modules(99, K, h2)  # other weights: everything comes from the export
+        fp.load_state_dict(sd["heads"][t]["model"])
+        fw.load_state_dict(sd["heads"][t]["w_model"])
+        fg.load_state_dict(sd["heads"][t]["g_model"])
+        fo.load_state_dict(sd["heads"][t]["optim"])
+        # the task's reference optimizer state carries step 3 (its own updates); the engine's step
+        # counter (6) rides in the export -- align the reference's before comparing a further step
+        for p in opt.state:
+            opt.state[p]["step"] = torch.tensor(6.0)
+        for mods in ((psi, w, g, h_fn, opt), (fp, fw, fg, h2, fo)):  # h is shared by the tasks
+            _tsf_step(*mods, x)
+        for a, b in zip(list(fp.parameters()) + list(fw.parameters()) + list(fg.parameters()),
+                        list(psi.parameters()) + list(w.parameters()) + list(g.parameters())):
+            assert torch.equal(a, b)
+        assert all(torch.equal(a, b) for a, b in zip(h2.parameters(), h_fn.parameters()))
+
+
+def test_tsf_state_is_refused_by_a_plain_engine():
+    eng = HostTSFEngine(1, 0)
+    sd = ck.state_dict(eng)
+    with pytest.raises(ValueError, match="TSF"):
+        ck.load_state_dict(HostEngine(1), sd)
+    with pytest.raises(ValueError, match="TSF"):
+        ck.load_state_dict(HostTSFEngine(1, 0), ck.state_dict(HostEngine(1)))
+
+
+def test_a_sharded_rank_checkpoint_loads_only_into_that_rank():
+    sd = ck.state_dict(_engine_from([_trained_reference(7, 1)]))
+    other = HostEngine(1)
+    other.head_offset = 1
+    with pytest.raises(ValueError, match="geometry"):
+        ck.load_state_dict(other, sd)

@@ -470,3 +470,66 @@ def test_round_skip_is_bit_exact(spec_rounds, force, monkeypatch):
         assert torch.equal(ma, mb) and torch.equal(va, vb) and sa == sb
     assert s0["policies_checked"] == 0
     assert s1["policies_checked"] >= n * (spec_rounds - 1) * T // 2 and s1["policies_skipped"] > 0, s1
+
+
+@pytest.mark.parametrize("force,ev", [(-1, 7), (1, 1000)])
+def test_lookahead_is_bit_exact(force, ev, monkeypatch):
+    """Look-ahead: step E's final round forwards step E+1's minibatch into the other
+    copy of the minibatch roles and step E+1 starts at its TD launch.  The forward is the same
+    arithmetic as the step-start forward, so heads, moments and every action must be IDENTICAL to
+    SFX_AHEAD=0 on the same index stream -- through dirty minibatches (a small ring: the newest
+    transition is sampled often), target syncs every 7 updates, and forced host rounds."""
+    from sfx.runner import NativeEnvLoop
+
+    spec = R.Spec(17, 64, 7, 8, ("relu", "relu"))
+    T, n = 5, 60
+    out = {}
+    for ahead in ("1", "0"):
+        monkeypatch.setenv("SFX_AHEAD", ahead)
+        eng, _ = make(spec, T, ev, max_batch=16)
+        if force >= 0:
+            eng.debug_force_rerun(force)
+        loop = NativeEnvLoop(eng, batch=16, capacity=48, gamma=0.9, epsilon=0.2, alpha_w=0.05, episode_len=13, seed=4)
+        loop.prefill(20)
+        loop.set_task(1)
+        loop.record(n)
+        loop.run(n // 2)
+        loop.run(n - n // 2)  # the chain continues across runs
+        recs = loop.records()
+        heads = torch.stack([eng.get_head(t, 0) for t in range(T)])
+        targets = torch.stack([eng.get_head(t, 1) for t in range(T)])
+        moms = [eng.get_adam(t) for t in range(T)]
+        ws = torch.stack([eng.get_w(t)[0] for t in range(T)])
+        out[ahead] = (heads, targets, moms, ws, [(r["c"], r["a_greedy"]) for r in recs], loop.action(), loop.stats())
+        loop.close()
+        eng.close()
+    h1, t1, m1, w1, a1, f1, s1 = out["1"]
+    h0, t0, m0, w0, a0, f0, s0 = out["0"]
+    assert a1 == a0 and f1 == f0
+    assert torch.equal(h1, h0) and torch.equal(t1, t0) and torch.equal(w1, w0)
+    for (ma, va, sa), (mb, vb, sb) in zip(m1, m0):
+        assert torch.equal(ma, mb) and torch.equal(va, vb) and sa == sb
+    assert s0["ahead_pre_steps"] == 0
+    assert s1["ahead_pre_steps"] > n // 2, s1
+    assert s1["ahead_own_forward_steps"] > 0, s1  # dirty minibatches (and syncs) ran their own forward
+
+
+def test_lookahead_runner_matches_oracle_c2():
+    """The C2 shape (T = 8, H = 256, B = 32) with look-ahead on (the bench's configuration),
+    replayed through the oracle from the runner's recorded inputs."""
+    from sfx.runner import NativeEnvLoop
+
+    spec = R.Spec(17, 256, 7, 8, ("relu", "relu"))
+    T, ev, alpha, n = 8, 1000, 1e-3, 24
+    eng, st = make(spec, T, ev, max_batch=32)
+    loop = NativeEnvLoop(eng, batch=32, capacity=400, gamma=0.9, epsilon=0.1, alpha_w=alpha, episode_len=500, seed=1)
+    loop.prefill(100)
+    loop.set_task(0)
+    loop.record(n)
+    loop.run(n)
+    recs = loop.records()
+    replay_with_oracle(st, spec, recs, alpha, ev, loop.action())
+    check_state(eng, st, T, n)
+    assert loop.stats()["ahead_pre_steps"] > n // 2
+    loop.close()
+    eng.close()
