@@ -152,6 +152,7 @@ struct sfx_handle {
   bool xcd = true;       // SFX_XCD=0: plain (tile, head) grids instead of XCD-aware ones
   int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
   int fwd_tpw = FWD_TPW; // column tiles per workgroup (layer-0+1 forward, oversubscribed launches); SFX_FWD_TPW=1: one
+  int ahead_tp = 4;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=2: two)
   int ncu = 256;         // compute units of the device
   bool fuse_l0 = true;   // SFX_FUSE_L0=0: layer 0 of a forward from the states as its own launch
   AdamHP hp_psi{1e-3, 0.0, 0.9, 0.999, 1e-8};
@@ -412,6 +413,25 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     F.ntN = cdiv(L.N, 16);
     F.ntM = cdiv(M, 32);
     F.tpw = 1;
+    // groups with their own rows on an XCD grid: per-group row tiles (FwdArgs::rowsplit)
+    long tiles = (long)F.ntN * F.ntM * ninst;
+    F.rowsplit = 0;
+    if (F.xcd) {
+      bool own = false;
+      for (const FwdGroup& g : groups) own = own || (g.m > 0 && g.m != M);
+      if (own) {
+        int* mt[4] = {&F.mt0, &F.mt1, &F.mt2, &F.mt3};
+        int gi = 0;
+        F.ntMs = 0;
+        tiles = 0;
+        for (const FwdGroup& g : groups) {
+          *mt[gi++] = cdiv(g.m > 0 ? g.m : M, 32);
+          F.ntMs += *mt[gi - 1];
+          tiles += (long)F.ntN * *mt[gi - 1] * g.n;
+        }
+        F.rowsplit = 1;
+      }
+    }
     const bool qa = ex.qa_role >= 0 && l == h->NL - 1;  // the maxima come from the ψ output layer
     if (qa) {
       F.qa_role = ex.qa_role;
@@ -434,12 +454,14 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     // plain launch's X operands loaded once) when the tiles would put two workgroups on at least
     // half the CUs and fit the chip when paired: C2's first forward of three roles (384 tiles ->
     // 192 workgroups, +1 %); Hopper TSF's 288 tiles stay unpaired (pairing measured 1 % slower)
-    const long tiles = (long)F.ntN * F.ntM * ninst;
+    // (the look-ahead's row-split launches pair above that too: 640 tiles of 32 x 16 measured 11.8 us
+    // unpaired, their workgroups dispatched over 5 us)
     if (!qa && h->fwd_tpw > 1 && h->fwd_waves == 8 && F.ntN > 1 && 2 * tiles >= 3L * h->ncu &&
-        tiles <= 2L * h->ncu && (l0 || ((L.K % 32) == 0 && aligned)))
-      F.tpw = h->fwd_tpw;
+        (tiles <= 2L * h->ncu || F.rowsplit) && (l0 || ((L.K % 32) == 0 && aligned)))
+      F.tpw = F.rowsplit && h->ahead_tp == 4 && F.ntN >= 4 ? 4 : h->fwd_tpw;
     const int ntNb = cdiv(F.ntN, F.tpw);
-    const dim3 grid = F.xcd ? dim3(8 * cdiv(h->T, 8) * ntNb * F.ntM * F.ngroups) : dim3(ntNb, ninst, F.ntM);
+    const dim3 grid = F.xcd ? dim3(8 * cdiv(h->T, 8) * ntNb * (F.rowsplit ? F.ntMs : F.ntM * F.ngroups))
+                            : dim3(ntNb, ninst, F.ntM);
     double by = 0.0;
     for (const FwdGroup& g : groups) {  // each group at its own rows
       const double m = g.m > 0 ? g.m : M;
@@ -457,6 +479,9 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
                tp2 ? (h->bf16 ? k_fwd<true, 8, true, true, 2> : k_fwd<true, 8, true, false, 2>)
                    : (h->bf16 ? k_fwd<true, 8, true, true> : k_fwd<true, 8, true>),
                grid, dim3(512), h->G, F);
+    } else if (h->fwd_waves == 8 && F.tpw == 4) {  // (the tpw rule above requires the vector path)
+      launch(h, K_FWD, by, h->bf16 ? k_fwd<true, 8, false, true, 4> : k_fwd<true, 8, false, false, 4>, grid, dim3(512),
+             h->G, F);
     } else if (h->fwd_waves == 8) {
       const bool vec = (L.K % 32) == 0 && aligned;
       launch(h, K_FWD, by,
@@ -986,6 +1011,28 @@ extern "C" {
 const char* sfx_version(void) { return "sfx 0.3 gfx950 fp32-mfma graphs speculative-gpi"; }
 const char* sfx_last_error(void) { return g_err.c_str(); }
 
+// Bounds-check builds (-DSFX_CHECK, libsfx_check.so): failed device bounds checks since the last
+// reset; -1 in the product build.  first_host: up to 8 records (line, a, b, c).
+int sfx_check_failures(long long* count, long long* first_host, int reset) {
+  if (!count) SFX_FAIL(SFX_E_ARG, "null argument");
+#ifdef SFX_CHECK
+  unsigned n = 0;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(&n, HIP_SYMBOL(sfx::g_chk_n), sizeof(n)));
+  if (first_host) HIPCHK(hipMemcpyFromSymbol(first_host, HIP_SYMBOL(sfx::g_chk_rec), sizeof(long long) * 32));
+  if (reset) {
+    const unsigned z = 0;
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(sfx::g_chk_n), &z, sizeof(z)));
+  }
+  *count = n;
+#else
+  (void)first_host;
+  (void)reset;
+  *count = -1;
+#endif
+  return SFX_OK;
+}
+
 #ifdef SFX_PROBE
 // Debug builds: copy out (and reset) the kernel timing probe records; returns the count.
 int sfx_probe_dump(void* out_host, int max_recs) {
@@ -1046,6 +1093,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   }
   const char* etp = std::getenv("SFX_FWD_TPW");
   h->fwd_tpw = etp && etp[0] == '1' ? 1 : FWD_TPW;
+  const char* eat = std::getenv("SFX_AHEAD_TP");
+  h->ahead_tp = eat && eat[0] == '2' ? 2 : 4;
   const char* el0 = std::getenv("SFX_FUSE_L0");
   h->fuse_l0 = !(el0 && el0[0] == '0');
   const char* esd = std::getenv("SFX_SPLIT_DX");
@@ -1167,6 +1216,9 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   G.cancel = h->dcancel;
   G.nonfin = h->dcancel + 8;  // sticky non-finite TD flag (sfx_nonfinite)
   G.lastOff = h->actOff[h->NL - 1];
+#ifdef SFX_CHECK
+  G.ext_dxpart = h->dxpart ? 512LL * T * h->dx_ntile * h->dxs_max : 0;
+#endif
   *out = h;
   return SFX_OK;
 }

@@ -175,6 +175,36 @@ __device__ __forceinline__ void load16u(float (&v)[16], const float* row, int kb
 // -------------------------------------------------------------------------------------
 // Handle geometry, passed by value to every kernel (all pointers derive from it).
 // -------------------------------------------------------------------------------------
+// Device bounds checks (SURVEY §5 "HIP debug mode with bounds asserts"; the `check` build,
+// -DSFX_CHECK, Makefile target `check` -> libsfx_check.so): SFX_CHK(cond, a, b, c) counts a failed
+// condition, records the first ones (file line, a, b, c) and prints them.  It does not trap:
+// a fault would take the shared GPU box down; the test harness reads the count after every test
+// (sfx_check_failures, tests/conftest.py) and fails the test.  Compiled out of the product build.
+#ifdef SFX_CHECK
+__device__ unsigned g_chk_n;
+__device__ long long g_chk_rec[8][4];
+__device__ __noinline__ void sfx_chk_fail(const char* file, int line, long long a, long long b, long long c) {
+  const unsigned i = atomicAdd(&g_chk_n, 1u);
+  if (i < 8) {
+    g_chk_rec[i][0] = line;
+    g_chk_rec[i][1] = a;
+    g_chk_rec[i][2] = b;
+    g_chk_rec[i][3] = c;
+  }
+  if (i < 4)
+    printf("SFX_CHECK %s:%d failed: %lld %lld %lld (block %u, %u thread %u)\n", file, line, a, b, c, blockIdx.x,
+           blockIdx.y, threadIdx.x);
+}
+#define SFX_CHK(cond, a, b, c)                                                                       \
+  do {                                                                                               \
+    if (!(cond)) sfx_chk_fail(__FILE__, __LINE__, (long long)(a), (long long)(b), (long long)(c)); \
+  } while (0)
+#else
+#define SFX_CHK(cond, a, b, c) \
+  do {                         \
+  } while (0)
+#endif
+
 struct LayerGeo {
   int N, K, wOff, bOff, actIn, actOut;  // actIn: activation that produced this layer's input
 };
@@ -206,16 +236,26 @@ struct Geo {
   __bf16* on16;
   __bf16* tg16;
   int mb, pad_mb;  // 0 or R_NS: the physical copy of the minibatch roles this launch calls R_S .. R_S1
+#ifdef SFX_CHECK
+  long long ext_dxpart;  // floats of the split-N dX partials
+#endif
 
   __device__ __forceinline__ int phys_role(int role) const {
     return role < R_G ? role + mb : role >= R_NS ? role - R_NS + (R_NS - mb) : role;
   }
   // off: per-layer offset inside a block (passed per launch as a scalar, never indexed)
   __device__ __forceinline__ float* actp(int role, int head, int off) const {
+    SFX_CHK(phys_role(role) >= 0 && phys_role(role) < NROLE && head >= 0 && head < T && off >= 0 && off < actSize,
+            role, head, off);
     return act + ((long long)phys_role(role) * T + head) * actSize + off;
   }
   __device__ __forceinline__ float* dzp(int head, int off) const {
+    SFX_CHK(head >= 0 && head < T && off >= 0 && off < actSize, head, off, actSize);
     return dz + (long long)head * actSize + off;
+  }
+  // element idx of the block at `off` (role, head) stays inside that (role, head) block
+  __device__ __forceinline__ void chk_act(int off, long long idx) const {
+    SFX_CHK(off + idx >= 0 && off + idx < actSize, off, idx, actSize);
   }
   __device__ __forceinline__ long long slot_off(int slot, int head) const {
     return ((long long)slot * T + head) * P;
@@ -379,6 +419,10 @@ struct FwdArgs {
   int M, N, K, act, wOff, bOff, xOff, yOff;  // xOff < 0: layer input is xa / xb
   int ngroups, lms_head, flag_value, xcd;  // xcd: 1-D XCD-aware grid (every group has heads 0..nh-1)
   int nh, ntN, ntM, tpw;  // tpw: column tiles per workgroup (L0 launches; else 1)
+  // rowsplit (XCD grids of groups with their own rows, FwdGroup::m): group g has mt_g row tiles
+  // and the grid holds ntMs = Σ mt_g of them per (head, column tile) -- no workgroups for rows a
+  // group does not have
+  int rowsplit, mt0, mt1, mt2, mt3, ntMs;
   int w0Off, b0Off, K0, y0Off;  // L0 launches: layer 0 (K0 -> K, identity) computed in-tile, stored at y0Off
   unsigned long long mask;
   FwdGroup g0, g1, g2, g3;
@@ -434,6 +478,7 @@ __device__ void q_accumulate(const Geo& G, const FwdArgs& F, int head, int tN, i
     float q = 0.f;
     for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], w[k], q);
     const int v = sortable(q);
+    SFX_CHK(i < Tg && m0 + bl < F.qa_M && head < G.T, i, m0 + bl, head);
     const size_t o = ((size_t)i * F.qa_M + m0 + bl) * Aa + a;
     if (all) atomicMax(F.qa_all + o, v);
     if (ge) atomicMax(F.qa_ge + o, v);
@@ -650,7 +695,10 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
             const int rr = (q >> 1) * 16 + g * 4 + i;
             const float v = __fadd_rn(c[i], bb);
             sA[rr * AS + cc] = v;
-            if (tN == 0 && m0 + rr < M) Y0[(size_t)(m0 + rr) * K + cc] = v;
+            if (tN == 0 && m0 + rr < M) {
+              G.chk_act(F.y0Off, (long long)(m0 + rr) * K + cc);
+              Y0[(size_t)(m0 + rr) * K + cc] = v;
+            }
           }
         }
       };
@@ -788,7 +836,10 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
       for (int i = 0; i < 4; ++i) {
         const int row = m0 + 16 * s + (Lx >> 4) * 4 + i;
         const float o = act_fwd(__fadd_rn(v[i], bias), F.act);
-        if (row < M) stc<C>(Y + (size_t)row * N + col, o);
+        if (row < M) {
+          G.chk_act(F.yOff, (long long)row * N + col);
+          stc<C>(Y + (size_t)row * N + col, o);
+        }
         if (sT) sT[(row - m0) * 16 + (col - n0)] = row < M ? o : 0.f;
       }
     }
@@ -807,9 +858,28 @@ __device__ __forceinline__ void fwd_body(const Geo& G, const FwdArgs& F, int bx,
   if (F.xcd) {  // head h's tiles on the XCD of slot h % 8 (see xcd_decode)
     const int b = bx, hp = (F.nh + 7) >> 3, k = b >> 3;
     const int r = hp == 1 ? k : k / fdiv(hp), hd = (b & 7) + 8 * (k - r * hp);
-    const int rN = r / fdiv(ntNb), gi = rN / fdiv(F.ntM);
+    const int rN = r / fdiv(ntNb);
+    int gi;
     tN = r - rN * ntNb;
-    tM = rN - gi * F.ntM;
+    if (F.rowsplit) {
+      tM = rN;
+      gi = 0;
+      if (tM >= F.mt0) {
+        tM -= F.mt0;
+        gi = 1;
+        if (tM >= F.mt1) {
+          tM -= F.mt1;
+          gi = 2;
+          if (tM >= F.mt2) {
+            tM -= F.mt2;
+            gi = 3;
+          }
+        }
+      }
+    } else {
+      gi = rN / fdiv(F.ntM);
+      tM = rN - gi * F.ntM;
+    }
     if (hd >= F.nh || gi >= F.ngroups) return;
     y = gi * F.nh + hd;
   }
@@ -986,6 +1056,7 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
         am = a;
       }
     s_next = am;
+    SFX_CHK(b < A.next_stride || !A.next, b, A.next_stride, 0);
     if (A.next) A.next[(size_t)blockIdx.y * A.next_stride + b] = am;
   }
   __syncthreads();
@@ -1014,6 +1085,7 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   if (tid == 0) {  // row Σ diff^2 in feature order
     float s = 0.f;
     for (int k = 0; k < d; ++k) s = __fadd_rn(s, s_sq[k]);
+    SFX_CHK(pol >= 0 && pol < G.T && b < MMAX, pol, b, 0);
     G.rowloss[(long long)pol * MMAX + b] = s;
   }
   PROBE_REC(17, pt0);
@@ -1220,6 +1292,8 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
       }
     sm.n[bl] = am;
     if (prev && (bl == tid ? prev_l : prev[bl]) != am) differs = 1;
+    SFX_CHK(!(pub && A.tdg_next) || (m0 + bl < A.tdg_next_stride && pol - A.head0 >= 0), pol, m0 + bl,
+            A.tdg_next_stride);
     if (pub && A.tdg_next) A.tdg_next[(size_t)(pol - A.head0) * A.tdg_next_stride + m0 + bl] = am;
   }
   const int same = !__syncthreads_or(differs);
@@ -1269,6 +1343,7 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
     for (int bl = tid; bl < nb; bl += 256) {  // row Σ diff^2 in feature order
       float sacc = 0.f;
       for (int k = 0; k < d; ++k) sacc = __fadd_rn(sacc, sq[bl * d + k]);
+      SFX_CHK(pol >= 0 && pol < G.T && m0 + bl < MMAX, pol, m0 + bl, 0);
       G.rowloss[(long long)pol * MMAX + m0 + bl] = sacc;
     }
   }
@@ -1276,7 +1351,7 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
 }
 
 template <bool TDG, int VMAX = 2, int U = 8, bool C = false, bool BF = false>
-__device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floatx4 (*red)[2][64]) {
+__device__ __forceinline__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floatx4 (*red)[2][64]) {
   static_assert(!(BF && (TDG || C)), "bf16 dX: the plain dX tiles only (the fused TD launch stays fp32)");
   const RoleGeo L = A.ra;
   const int N = L.N, K = L.K, M = A.M;
@@ -1391,6 +1466,9 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
       v += red[2][s][Lx];
       v += red[3][s][Lx];
       float* o = A.dxpart + ((pt + split) * 128 + threadIdx.x) * 4;
+#ifdef SFX_CHECK
+      SFX_CHK((long long)((pt + split) * 128 + threadIdx.x) * 4 + 3 < G.ext_dxpart, pt, split, G.ext_dxpart);
+#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i) stc<true>(o + i, v[i]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1414,7 +1492,10 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = m0 + 16 * s + (Lx >> 4) * 4 + i;
-        if (row < M) stc<C>(out + (size_t)row * K + col, act_bwd(v[i], xin[i], L.actIn));
+        if (row < M) {
+          G.chk_act(L.dzIn, (long long)row * K + col);
+          stc<C>(out + (size_t)row * K + col, act_bwd(v[i], xin[i], L.actIn));
+        }
       }
     }
     return;
@@ -1428,7 +1509,10 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = m0 + 16 * s + (Lx >> 4) * 4 + i;
-        if (row < M) stc<C>(out + (size_t)row * K + col, act_bwd(v[i], xin[i], L.actIn));
+        if (row < M) {
+          G.chk_act(L.dzIn, (long long)row * K + col);
+          stc<C>(out + (size_t)row * K + col, act_bwd(v[i], xin[i], L.actIn));
+        }
       }
     }
   }
@@ -1439,69 +1523,74 @@ __device__ void role_dx(const Geo& G, const BwdArgs& A, int head, int tile, floa
 // (sX[aoff + m * K + k], m < 2 aM) those rows into R_NS / R_NS1 and, with the target weights sWt,
 // NS1 into R_NS1T.  vrows = false: the look-ahead rows only (a skipped head).
 __device__ __forceinline__ int v0_aoff(const BwdArgs& A, int K) { return (A.vM * K + 3) & ~3; }
+constexpr int V0S = KFUSE + 4;  // LDS row stride of the tile's weights: lane (r, g) hits bank 4r + g
+
+// One 16-row x 16-column MFMA tile of the fused layer-0 forward: rows [m0, m0 + 16) of x (row
+// stride K, `rows` valid) times this lane's weight row w (K floats), bias bb, into Y (row stride
+// N).  Every LDS operand is read before the first MFMA (K <= KFUSE: at most 16 k-steps), in the
+// k-ordered accumulation of k_fwd's layer-0 path.
+template <bool C>
+__device__ __forceinline__ void v0_tile(const float* x, int K, int m0, int rows, const float* w, float bb, int act,
+                                        float* Y, int N, int n, long long lim) {
+  constexpr int KS = 8;  // k-steps whose operands are read together (K <= 32: one batch)
+  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4, ma = m0 + r;
+  floatx4 c = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += 4 * KS) {
+    float a[KS], b[KS];
+#pragma unroll
+    for (int q = 0; q < KS; ++q) {
+      const int k = k0 + 4 * q + g;
+      a[q] = (k < K && ma < rows) ? x[ma * K + k] : 0.f;
+      b[q] = k < K ? w[k] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < KS; ++q)
+      if (k0 + 4 * q < K) c = mfma4(a[q], b[q], c);
+  }
+  if (n < N) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + g * 4 + i;
+      if (m < rows) {
+        SFX_CHK((long long)m * N + n < lim, m, n, lim);
+        stc<C>(Y + (size_t)m * N + n, act_fwd(__fadd_rn(c[i], bb), act));
+      }
+    }
+  }
+}
 
 template <bool C>
-__device__ void fused_v0(const Geo& G, const BwdArgs& A, const RoleGeo& L, int head, int nbase, const float* sW,
+__device__ __forceinline__ void fused_v0(const Geo& G, const BwdArgs& A, const RoleGeo& L, int head, int nbase, const float* sW,
                          const float* sB, const float* sX, const float* sWt = nullptr, const float* sBt = nullptr,
                          bool vrows = true) {
   if (A.aM > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the look-ahead LDS-DMA has landed
   __syncthreads();
   PROBE_AT(3);
   const int K = L.K, N = L.N, VM = A.vM;
-  // MFMA from LDS (the same k-ordered accumulation as k_fwd's layer-0 path): wave w owns
-  // column half (w & 1) and row tiles (w >> 1), (w >> 1) + 2, ...
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  // wave w owns column half (w & 1) and row tiles (w >> 1), (w >> 1) + 2, ...
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15;
   const int nl = (wave & 1) * 16 + r, n = nbase + nl;
   const float bias = sB[nl];
   if (vrows) {
     float* Y = G.actp(A.vRole, head, A.vOff);
-    for (int mt = wave >> 1; mt * 16 < VM; mt += 2) {
-      floatx4 c = {0.f, 0.f, 0.f, 0.f};
-      const int ma = mt * 16 + r;
-      for (int k4 = 0; k4 < K; k4 += 4) {
-        const int k = k4 + g;
-        const float a = (k < K && ma < VM) ? sX[ma * K + k] : 0.f;
-        const float b = k < K ? sW[nl * KFUSE + k] : 0.f;
-        c = mfma4(a, b, c);
-      }
-      if (n < N) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = mt * 16 + g * 4 + i;
-          if (m < VM) stc<C>(Y + (size_t)m * N + n, act_fwd(__fadd_rn(c[i], bias), A.act0));
-        }
-      }
-    }
+    for (int mt = wave >> 1; mt * 16 < VM; mt += 2)
+      v0_tile<C>(sX, K, mt * 16, VM, sW + nl * V0S, bias, A.act0, Y, N, n, G.actSize - A.vOff);
   }
+  PROBE_AT(4);
   if (A.aM > 0) {
-    // 16-row tiles of three products, one per iteration: NS -> R_NS and NS1 -> R_NS1 with the
-    // post-update weights, NS1 -> R_NS1T with the target weights (row stride K in sWt)
+    // 16-row tiles of three products: NS -> R_NS and NS1 -> R_NS1 with the post-update weights,
+    // NS1 -> R_NS1T with the target weights (row stride K in sWt)
     const int aM = A.aM, nt = (aM + 15) >> 4;
     const float* xa = sX + v0_aoff(A, K);
     const float bt = sBt[nl];
     for (int it = wave >> 1; it < 3 * nt; it += 2) {
       const int which = it / nt, mt = it - which * nt;
-      const float* x = xa + (which ? aM * K : 0);
-      const float* w = which == 2 ? sWt + nl * K : sW + nl * KFUSE;
-      const float bb = which == 2 ? bt : bias;
-      float* Y = G.actp(which == 0 ? R_NS : which == 1 ? R_NS1 : R_NS1T, head, A.vOff);
-      floatx4 c = {0.f, 0.f, 0.f, 0.f};
-      const int ma = mt * 16 + r;
-      for (int k4 = 0; k4 < K; k4 += 4) {
-        const int k = k4 + g;
-        const float a = (k < K && ma < aM) ? x[ma * K + k] : 0.f;
-        const float b = k < K ? w[k] : 0.f;
-        c = mfma4(a, b, c);
-      }
-      if (n < N) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = mt * 16 + g * 4 + i;
-          if (m < aM) stc<C>(Y + (size_t)m * N + n, act_fwd(__fadd_rn(c[i], bb), A.act0));
-        }
-      }
+      v0_tile<C>(xa + (which ? aM * K : 0), K, mt * 16, aM, which == 2 ? sWt + nl * K : sW + nl * V0S,
+                 which == 2 ? bt : bias, A.act0, G.actp(which == 0 ? R_NS : which == 1 ? R_NS1 : R_NS1T, head, A.vOff),
+                 N, n, G.actSize - A.vOff);
     }
   }
+  PROBE_AT(5);
 }
 
 typedef __attribute__((address_space(3))) void* tsf_lds_t;
@@ -1529,7 +1618,7 @@ __device__ __forceinline__ void glds(float* dst, int n, F src, int w0 = 0, int n
 // (role_dw's layer-0 tiles and role_v0_only): the tile's weights and biases, the input rows, the
 // target weights and biases of the look-ahead rows.
 struct V0Smem {
-  float sW[32 * KFUSE];
+  float sW[32 * V0S];
   float sB[32];
   float sWt[32 * KFUSE];
   float sBt[32];
@@ -1560,7 +1649,7 @@ __device__ __forceinline__ void v0_stage_ahead(const Geo& G, const BwdArgs& A, c
 // forward of its 32 columns, from those weights (the bits role_dw would have staged): every row
 // (vrows), or the look-ahead rows alone (BwdArgs::a_noskip).
 // Fused layers have K <= KFUSE <= 64: one k-tile, so tile = column tile.
-__device__ void role_v0_only(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile, bool vrows) {
+__device__ __forceinline__ void role_v0_only(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile, bool vrows) {
   const int N = L.N, K = L.K, M = A.M, tid = threadIdx.x, nbase = tile * 32;
   const float* Pw = G.online + G.slot_off(rslot(A.mask, head) ^ 1, head);
   V0Smem& sm = v0_smem();
@@ -1571,7 +1660,7 @@ __device__ void role_v0_only(const Geo& G, const BwdArgs& A, int head, const Rol
   const FDiv fK = fdiv(K);
   for (int j = tid; j < 32 * K; j += 256) {
     const int nl = j / fK, k = j - nl * K;
-    sW[nl * KFUSE + k] = nbase + nl < N ? Pw[L.wOff + (size_t)(nbase + nl) * K + k] : 0.f;
+    sW[nl * V0S + k] = nbase + nl < N ? Pw[L.wOff + (size_t)(nbase + nl) * K + k] : 0.f;
   }
   if (tid < 32) sB[tid] = nbase + tid < N ? Pw[L.bOff + nbase + tid] : 0.f;
   if (vrows) {
@@ -1709,6 +1798,7 @@ __device__ __forceinline__ void role_dw(const Geo& G, const BwdArgs& A, int head
       if (ok[e]) {
         const int k = h ? kb1 : kb0;
         const size_t off = (size_t)L.wOff + (size_t)n * K + k;
+        SFX_CHK((long long)off < G.P, L.wOff, n, k);
         adam_apply(pp[e], pm[e], pv[e], h ? acc1[i] : acc0[i], c);
         if (!cx) {
           st_param<C>(Pw + off, pp[e]);
@@ -1716,7 +1806,7 @@ __device__ __forceinline__ void role_dw(const Geo& G, const BwdArgs& A, int head
           st_moment(Vw + off, pv[e]);
           if constexpr (BF) G.on16[wo + off] = (__bf16)pp[e];  // the bf16 copy of the write slot
         }
-        if (fuse) sW[(n - nbase) * KFUSE + k] = pp[e];
+        if (fuse) sW[(n - nbase) * V0S + k] = pp[e];
       }
     }
   }
@@ -1739,7 +1829,7 @@ __device__ __forceinline__ void role_dw(const Geo& G, const BwdArgs& A, int head
 // workgroups on 256 CUs at the C2 shape, and the co-resident pairs finish last).  Per column
 // the accumulation order is role_dw's, so the results are the same bits.  Layer 0 (with the
 // fused post-update forward) keeps role_dw.
-__device__ void role_dw_wide(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile) {
+__device__ __forceinline__ void role_dw_wide(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile) {
   constexpr int NW = 2;
   const int N = L.N, K = L.K, M = A.M;
   const int ntk = (K + 63) >> 6;
@@ -2208,6 +2298,7 @@ __device__ void ver_block(const Geo& G, const VerArgs& V) {
   PROBE_MARKA();
   const float* wrow = G.w + (long long)i * G.dpad;
   const int n = nb * TA;
+  SFX_CHK(!(tid < nb) || b0 + tid < V.spec_stride, i, b0 + tid, V.spec_stride);
   const int spec = tid < nb ? (int)V.spec_next[(size_t)i * V.spec_stride + b0 + tid] : 0;
   if (tid == 0) s_bad = 0;
   if (n <= 256 && (d & 3) == 0 && d <= 16) {

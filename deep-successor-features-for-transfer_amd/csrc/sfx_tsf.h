@@ -486,6 +486,8 @@ __device__ __forceinline__ void tsf_fwd_body(const TsfArgs& A, const float* __re
 template <int NP>
 __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A, const float* __restrict__ gfl) {
   __shared__ __attribute__((aligned(16))) float sm[TSF_FWD_SM];
+  SFX_CHK(threadIdx.x || tsf_fwd_lds(A.K, NP, A.G, A.d).total <= TSF_FWD_SM, tsf_fwd_lds(A.K, NP, A.G, A.d).total,
+          TSF_FWD_SM, 0);
   tsf_fwd_body<NP>(A, gfl, sm, blockIdx.x, gridDim.x);
 }
 
@@ -737,6 +739,8 @@ __global__ __launch_bounds__(256) void k_tsf_bwd(TsfArgs A, const float* __restr
   __shared__ __attribute__((aligned(16))) float sm[TSF_SM];
   __shared__ float s_dr[64], s_r[64], s_w[256], s_red[256];
   __shared__ int s_ab[64];
+  SFX_CHK(threadIdx.x || tsf_bwd_lds(A.K, NP, A.G, A.d, A.B).total <= TSF_SM, tsf_bwd_lds(A.K, NP, A.G, A.d, A.B).total,
+          TSF_SM, 1);
   tsf_bwd_block<NP>(A, sfl, sm, s_dr, s_r, s_w, s_red, s_ab, blockIdx.x);
 }
 
@@ -783,6 +787,8 @@ __device__ __forceinline__ void tsf_flow_block(const TsfArgs& A, float* sm, int 
 
 __global__ __launch_bounds__(256) void k_tsf_flow(TsfArgs A) {
   __shared__ __attribute__((aligned(16))) float sm[2 * 128 * TSF_NS + 256];  // 2B <= 128 rows
+  SFX_CHK(threadIdx.x || tsf_bwd_lds(A.K, A.np, A.G, A.d, A.B).fk_total <= 2 * 128 * TSF_NS + 256,
+          tsf_bwd_lds(A.K, A.np, A.G, A.d, A.B).fk_total, 2 * 128 * TSF_NS + 256, 2);
   tsf_flow_block(A, sm, blockIdx.x);
 }
 
@@ -801,6 +807,8 @@ __global__ __launch_bounds__(256) void k_bwd_tsf(Geo G, BwdArgs A, TsfArgs T, co
   __shared__ int s_ab[64];
   const int bx = blockIdx.x;
   if (bx < ntsf) {
+    SFX_CHK(threadIdx.x || (mode == 1 ? tsf_bwd_lds(T.K, NP, T.G, T.d, T.B).total : tsf_bwd_lds(T.K, T.np, T.G, T.d, T.B).fk_total) <= TSFX_SM,
+            mode, tsf_bwd_lds(T.K, NP, T.G, T.d, T.B).total, TSFX_SM);
     if (mode == 1)
       tsf_bwd_block<NP>(T, sfl, sm, s_dr, s_r, s_w, s_red, s_ab, bx);
     else
@@ -819,6 +827,8 @@ __global__ __launch_bounds__(512) void k_fwd_tsf(Geo G, FwdArgs F, TsfArgs T, co
   __shared__ __attribute__((aligned(16))) float sm[TSFXF_SM];
   const int b = blockIdx.x;
   if (b < ntsf) {
+    SFX_CHK(threadIdx.x || tsf_fwd_lds(T.K, NP, T.G, T.d).total <= TSFXF_SM, tsf_fwd_lds(T.K, NP, T.G, T.d).total,
+            TSFXF_SM, 3);
     tsf_fwd_body<NP>(T, gfl, sm, b, ntsf);
     return;
   }

@@ -85,6 +85,7 @@ SIGNATURES = {
     "sfx_comm_init": (_I, [_VP, _VP, _I, _I]),
     "sfx_set_comm": (_I, [_VP, _VP, _I, _I]),
     "sfx_set_comm_host": (_I, [_VP, _VP, _VP, _I, _I]),
+    "sfx_check_failures": (_I, [C.POINTER(C.c_longlong), _VP, _I]),
     "sfx_comm_state": (_I, [_VP, _VP]),
     "sfx_comm_size": (_I, [_VP, _VP, _VP, _VP, _VP]),
     "sfx_tsf_freeze_flows": (_I, [_VP, _I]),

@@ -10,7 +10,9 @@ unchanged on libsfx:
 * the user's single-file modules ``sfdqn``, ``tsfdqn``, ``tsfdqn_nf`` and
   ``agents.tsfdqn_sequential`` load as they are and are then bound (``sfx.dropin.bind``): their
   library classes become sfx's and the TSF agents' ``update_successor`` one libsfx call;
-* ``agents``, ``utils``, ``tasks`` and the scripts themselves are the user's, untouched.
+* ``agents.buffer`` is sfx's ``ReplayBuffer`` (the reference's API over a device-resident ring,
+  the same ``np.random`` index draws; ``sfx/dropin/agents/buffer.py``);
+* every other ``agents`` module, ``utils``, ``tasks`` and the scripts themselves are the user's, untouched.
 
 sfx ships no agent code: the agents are the reference's own.
 """
@@ -24,6 +26,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 FEATURES = os.path.join(ROOT, "features")
+AGENT_ALIASES = {"agents.buffer": os.path.join(ROOT, "agents", "buffer.py")}
 OURS = ("features.deep", "features.deep_sequential", "features.deep_sequential_tsf", "features.deep_phi",
         "features.successor")
 BOUND = ("sfdqn", "tsfdqn", "tsfdqn_nf", "agents.tsfdqn_sequential", "agents.sfdqn_phi")
@@ -54,6 +57,8 @@ class _Finder(importlib.abc.MetaPathFinder):
                 locs += [p for p in user.submodule_search_locations if os.path.abspath(p) != FEATURES]
             return importlib.util.spec_from_file_location("features", os.path.join(FEATURES, "__init__.py"),
                                                           submodule_search_locations=locs)
+        if fullname in AGENT_ALIASES:  # the user's agents package, sfx's module
+            return importlib.util.spec_from_file_location(fullname, AGENT_ALIASES[fullname])
         if fullname in BOUND:
             spec = importlib.machinery.PathFinder.find_spec(fullname, path)
             if spec is None or spec.loader is None:
@@ -68,6 +73,6 @@ def install() -> str:
     if not any(isinstance(f, _Finder) for f in sys.meta_path):
         sys.meta_path.insert(0, _Finder())
     for name in list(sys.modules):
-        if name == "features" or name.startswith("features.") or name in BOUND:
+        if name == "features" or name.startswith("features.") or name in BOUND or name in AGENT_ALIASES:
             del sys.modules[name]
     return ROOT

@@ -46,6 +46,10 @@ typedef struct sfx_handle* sfx_t;
 const char* sfx_version(void);
 /* Message describing the last failure on this thread. */
 const char* sfx_last_error(void);
+/* Device bounds checks of the check build (libsfx_check.so, -DSFX_CHECK): the number of
+ * failed checks since the last reset (count = -1 in the product build); first_host: up to 8
+ * records of (source line, a, b, c) or null; reset != 0 clears the count. */
+int sfx_check_failures(long long* count, long long* first_host, int reset);
 
 /*
  * Create the per-device library state for T ψ heads of geometry

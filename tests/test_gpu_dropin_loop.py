@@ -10,7 +10,7 @@ from tests.conftest import gpu_available
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("buffer", ["reference", "host"])
+@pytest.mark.parametrize("buffer", ["reference", "objring", "host"])
 def test_dropin_loop_fuses_every_env_step(buffer, monkeypatch):
     if not gpu_available():
         pytest.skip("no HIP device")

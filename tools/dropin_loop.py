@@ -11,11 +11,14 @@ next_sample + agents/sfdqn.py:39-60 get_Q_values / train_agent), restated as a b
   buffer.append(s_enc, a, φ, s1_enc, γ); batch = buffer.replay()
   for i in range(T): sf.update_successor(batch, i)       # fused by the drop-in into one step
 
-over ``sfx.dropin.features.deep.DeepSF`` (the ψ library every call above lands in).  Two replay
+over ``sfx.dropin.features.deep.DeepSF`` (the ψ library every call above lands in).  Replay
 buffers:
-  * ``reference``: agents/buffer.py's layout -- an object ring of per-transition device tensors,
-    ``torch.vstack`` on the device and ``torch.tensor`` of the per-transition action tensors
-    (one device read each) per replay, as the reference's program does;
+  * ``reference``: what main_sfdqn_torch.py's ``ReplayBuffer`` is under the drop-in --
+    ``agents.buffer`` resolves to ``sfx.dropin.agents.buffer`` (the reference's API and index
+    draws over a device-resident ring; the agent's calls unchanged);
+  * ``objring``: agents/buffer.py's own layout (without the alias) -- an object ring of
+    per-transition device tensors, ``torch.vstack`` on the device and ``torch.tensor`` of the
+    per-transition action tensors (one device read each) per replay;
   * ``host``: states and φ kept as numpy arrays, a numpy ring sampled on the host, one
     host->device copy per field per replay.
 The env, the buffer and the agent logic are the user's program, not the library; the numbers say
@@ -144,9 +147,16 @@ class DropinLoop:
         self.sf.reset()
         for t in self.tasks:
             self.sf.add_training_task(t)
-        self.buffer = (RefReplay(1_000_000, batch, self.device) if buffer == "reference" else
-                       HostReplay(1_000_000, batch, self.device, n_s, d))
-        self.ref_buffer = buffer == "reference"
+        if buffer == "reference":
+            from sfx.dropin.agents.buffer import ReplayBuffer
+
+            self.buffer = ReplayBuffer({}, n_batch=batch)
+            self.buffer.device = self.device
+        elif buffer == "objring":
+            self.buffer = RefReplay(1_000_000, batch, self.device)
+        else:
+            self.buffer = HostReplay(1_000_000, batch, self.device, n_s, d)
+        self.ref_buffer = buffer in ("reference", "objring")
         self.T, self.A, self.gamma, self.epsilon = T, A, gamma, epsilon
         self.task = 0
         self.s_enc = None
@@ -205,5 +215,5 @@ if __name__ == "__main__":
 
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                     "deep-successor-features-for-transfer_amd"))
-    for b in ("reference", "host"):
+    for b in ("reference", "objring", "host"):
         print(json.dumps({b: measure(b)}), flush=True)
