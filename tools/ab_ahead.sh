@@ -24,3 +24,9 @@ grep -E "^ +1[1-4] |sum" $O/probe_tp2.txt | cut -c1-110
 SFX_LIB=$PWD/deep-successor-features-for-transfer_amd/sfx/libsfx_check.so SFX_CHECK_RUN=1 timeout -k 10 600 \
   python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $O/check_suite.log 2>&1
 tail -3 $O/check_suite.log
+# the host-sanitizer drivers with every flag (the round-3 hang: ASan's default use-after-return
+# mode, UBSan's function / vptr checks); each bounded
+ASAN_OPTIONS=detect_leaks=0:verify_asan_link_order=0 timeout -k 10 300 tools/hostsan/runner_asan_full > $O/hostsan_asan_full.txt 2>&1
+echo "asan_full rc=$?"; tail -3 $O/hostsan_asan_full.txt
+UBSAN_OPTIONS=print_stacktrace=1 timeout -k 10 300 tools/hostsan/runner_ubsan_full > $O/hostsan_ubsan_full.txt 2>&1
+echo "ubsan_full rc=$?"; tail -3 $O/hostsan_ubsan_full.txt

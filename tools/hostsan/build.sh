@@ -4,6 +4,8 @@
 # csrc/Makefile).  Outputs (git-ignored) in tools/hostsan/:
 #   runner_asan   AddressSanitizer                       (default)
 #   runner_ubsan  UndefinedBehaviorSanitizer, no recover ("ubsan")
+#   runner_asan_full / runner_ubsan_full: the same with every flag ("asan_full": ASan's default
+#   use-after-return mode; "ubsan_full": UBSan's function and vptr checks too)
 # Run on the GPU box:
 #   ASAN_OPTIONS=detect_leaks=0:verify_asan_link_order=0 tools/hostsan/runner_asan
 #   UBSAN_OPTIONS=print_stacktrace=1 tools/hostsan/runner_ubsan
@@ -11,7 +13,14 @@ set -e
 cd "$(dirname "$0")"
 CSRC=../../deep-successor-features-for-transfer_amd/csrc
 F="--offload-arch=gfx950 -O3 -g -std=c++17 -ffp-contract=off -fno-omit-frame-pointer -I$CSRC"
-if [ "${1:-asan}" = ubsan ]; then
+if [ "${1:-asan}" = ubsan_full ]; then  # every UBSan check, function / vptr included (round-3 hang)
+  /opt/rocm/bin/hipcc $F -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined \
+    -o runner_ubsan_full runner_hostsan.cpp "$CSRC/sfx.hip" -ldl
+  echo built tools/hostsan/runner_ubsan_full
+elif [ "${1:-asan}" = asan_full ]; then  # ASan's default use-after-return mode (round-3 hang)
+  /opt/rocm/bin/hipcc $F -Xarch_host -fsanitize=address -o runner_asan_full runner_hostsan.cpp "$CSRC/sfx.hip" -ldl
+  echo built tools/hostsan/runner_asan_full
+elif [ "${1:-asan}" = ubsan ]; then
   /opt/rocm/bin/hipcc $F -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize=function,vptr \
     -Xarch_host -fno-sanitize-recover=undefined -o runner_ubsan runner_hostsan.cpp "$CSRC/sfx.hip" -ldl
   echo built tools/hostsan/runner_ubsan
