@@ -5,9 +5,11 @@ The reference keeps an object ring of per-transition device tensors and collates
 with ``torch.vstack`` and ``torch.tensor`` -- the latter reads each of the B action tensors back
 to the host (B synchronisations per replay).  Here every field lives in one preallocated device
 array (allocated at the first ``append`` from the shapes it sees), ``append`` writes its row with
-asynchronous device copies, and ``replay`` draws the SAME indices the reference draws
-(``np.random.randint(low=0, high=size, size=(n_batch,))``, one call on numpy's global state) and
-gathers the minibatch on the device with one index copy and one gather per field.  The returned
+asynchronous device copies (a discount factor given as a Python float -- what the reference's
+agents pass -- goes to a host array instead: no launch), and ``replay`` draws the SAME indices the
+reference draws (``np.random.randint(low=0, high=size, size=(n_batch,))``, one call on numpy's
+global state), hands the indices and the minibatch's discount factors to the device in ONE pinned
+copy, and gathers the other fields there, one gather each.  The returned
 tensors have the reference's shapes and dtypes: states / φ / next states ``[B, -1]`` float32,
 actions ``[B]`` int64, gammas ``[B]`` float32.
 """
@@ -50,8 +52,9 @@ class ReplayBuffer:
         n_s1 = int(torch.as_tensor(next_state).numel())
         cap = self.n_samples
         self._ring = (torch.zeros(cap, n_s, device=dev), torch.zeros(cap, dtype=torch.int64, device=dev),
-                      torch.zeros(cap, d, device=dev), torch.zeros(cap, n_s1, device=dev),
-                      torch.zeros(cap, device=dev))
+                      torch.zeros(cap, d, device=dev), torch.zeros(cap, n_s1, device=dev))
+        self._gam = np.zeros(cap, dtype=np.float32)  # γ per slot, float32 as torch.tensor(list) makes it
+        self._gdev = None  # set once a γ arrives as a device tensor: then γ is gathered on the device
 
     @staticmethod
     def _put(row, x):
@@ -64,7 +67,7 @@ class ReplayBuffer:
         """Adds the sample (agents/buffer.py:62-82); the oldest is overwritten once the ring is full."""
         if self._ring is None:
             self._alloc(state, reward, next_state)
-        rs, ra, rr, rs1, rg = self._ring
+        rs, ra, rr, rs1 = self._ring
         j = self.index
         self._put(rs[j], state)
         if torch.is_tensor(action):
@@ -74,9 +77,13 @@ class ReplayBuffer:
         self._put(rr[j], reward)
         self._put(rs1[j], next_state)
         if torch.is_tensor(gamma):
-            rg[j].copy_(gamma.reshape(()), non_blocking=True)
+            if self._gdev is None:
+                self._gdev = torch.as_tensor(self._gam, device=self.device).clone()
+            self._gdev[j].copy_(gamma.reshape(()), non_blocking=True)
         else:
-            rg[j] = float(gamma)
+            self._gam[j] = gamma
+            if self._gdev is not None:
+                self._gdev[j] = float(gamma)
         self.size = min(self.size + 1, self.n_samples)
         self.index = (self.index + 1) % self.n_samples
 
@@ -85,15 +92,20 @@ class ReplayBuffer:
         if self.size < self.n_batch:
             return None
         indices = np.random.randint(low=0, high=self.size, size=(self.n_batch,))
-        if self._pidx is None:
-            self._pidx = torch.empty(self.n_batch, dtype=torch.int64, pin_memory=self.device.type == "cuda")
+        B = self.n_batch
+        if self._pidx is None:  # one pinned slot: [B indices (int64) | B γ (float32 words)]
+            self._pidx = torch.empty(B + (B + 1) // 2, dtype=torch.int64, pin_memory=self.device.type == "cuda")
             self._pev = torch.cuda.Event() if self.device.type == "cuda" else None
         elif self._pev is not None:
-            self._pev.synchronize()  # the previous replay's index copy has left the pinned slot
-        self._pidx.numpy()[:] = indices
-        idx = self._pidx.to(self.device, non_blocking=True)
+            self._pev.synchronize()  # the previous replay's copy has left the pinned slot
+        host = self._pidx.numpy()
+        host[:B] = indices
+        host[B:].view(np.float32)[:B] = self._gam[indices]
+        dev = self._pidx.to(self.device, non_blocking=True, copy=True)  # never a view of the slot
         if self._pev is not None:
             self._pev.record()
-        rs, ra, rr, rs1, rg = self._ring
+        idx = dev[:B]
+        gam = dev[B:].view(torch.float32)[:B] if self._gdev is None else self._gdev.index_select(0, idx)
+        rs, ra, rr, rs1 = self._ring
         return (rs.index_select(0, idx), ra.index_select(0, idx), rr.index_select(0, idx),
-                rs1.index_select(0, idx), rg.index_select(0, idx))
+                rs1.index_select(0, idx), gam)

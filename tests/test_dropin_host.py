@@ -242,3 +242,33 @@ def test_replay_buffer_draws_and_collates_like_the_reference():
                 assert x.dtype == y.dtype and x.shape == y.shape and torch.equal(x, y)
     buf.reset()
     assert buf.replay() is None and buf.size == 0
+
+
+def test_replay_buffer_tensor_gammas_and_odd_batch():
+    """γ may arrive as tensors (then the ring keeps them on the device) or floats, mixed; an odd
+    n_batch exercises the packed index/γ slot; a returned minibatch is never overwritten by the
+    next replay."""
+    import numpy as np
+
+    from sfx.dropin.agents.buffer import ReplayBuffer
+
+    B, cap = 3, 5
+    buf = ReplayBuffer(n_samples=cap, n_batch=B)
+    gam = []
+    for k in range(8):
+        g = 0.5 + 0.01 * k
+        gam.append(np.float32(g))
+        buf.append(torch.full((1, 2), float(k)), torch.tensor(k % 3), torch.ones(1, 2), torch.zeros(1, 2),
+                   g if k < 4 else torch.tensor(g))
+        gam = gam[-cap:]
+    np.random.seed(3)
+    first = buf.replay()
+    keep = [x.clone() for x in first]
+    np.random.seed(3)
+    idx = np.random.randint(0, cap, size=(B,))
+    slot_gamma = {int(k) % cap: np.float32(0.5 + 0.01 * k) for k in range(8)}
+    assert torch.equal(first[4], torch.tensor([slot_gamma[int(i)] for i in idx]))
+    assert torch.equal(first[0][:, 0], torch.tensor([float(max(k for k in range(8) if k % cap == int(i))) for i in idx]))
+    buf.replay()
+    for x, y in zip(first, keep):
+        assert torch.equal(x, y)
