@@ -153,7 +153,8 @@ struct sfx_handle {
   int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
   int fwd_tpw = FWD_TPW; // column tiles per workgroup (layer-0+1 forward, oversubscribed launches); SFX_FWD_TPW=1: one
   int ahead_tp = 4;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=2: two)
-  bool ahead_early = true;  // the look-ahead rows ride in round 0's post-update forward (SFX_AHEAD_EARLY=0: the final round's)
+  bool ahead_early = true;
+  bool sel1 = true;  // one-state action selection by k_sel1 (SFX_SEL1=0: k_gpi + k_publish)  // the look-ahead rows ride in round 0's post-update forward (SFX_AHEAD_EARLY=0: the final round's)
   int ncu = 256;         // compute units of the device
   bool fuse_l0 = true;   // SFX_FUSE_L0=0: layer 0 of a forward from the states as its own launch
   AdamHP hp_psi{1e-3, 0.0, 0.9, 0.999, 1e-8};
@@ -944,10 +945,33 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
 // LMS + action selection when there is no minibatch yet).
 // SFDQN.get_Q_values + action choice for one state (sfdqn.py:577-596; agents/sfdqn.py:39-45):
 // forward of every head on s, GPI with w of `task`, selection into out[2] = (c, a).
-int select_body(sfx_handle* h, const float* s, int task, int use_gpi, float* q, int64_t* out) {
+// With `pub` (runner steps) the step's result is published after the selection: inside k_sel1, or
+// by k_publish after k_gpi.
+int select_body(sfx_handle* h, const float* s, int task, int use_gpi, float* q, int64_t* out,
+                const SelPub* pub = nullptr) {
   RC(run_fwd(h, {{R_A, P_ONLINE, 1, 0, h->T}}, 1, s, nullptr));
-  return run_gpi(h, gpi_args(R_A, 0, 0, h->w + (size_t)task * h->dpad, nullptr, q, nullptr, nullptr, out, task,
-                             use_gpi, 1));
+  const GpiArgs g = gpi_args(R_A, 0, 0, h->w + (size_t)task * h->dpad, nullptr, q, nullptr, nullptr, out, task, use_gpi, 1);
+  const int TA = h->T * h->A;
+  if (h->sel1 && TA <= SEL1_TA && h->A <= 256 && h->T <= 256) {
+    const SelPub P = pub ? *pub : SelPub{};
+    const dim3 grid(1), block((unsigned)(cdiv(TA, 64) * 64));
+    const double by = 4.0 * ((double)TA * h->d + h->d + (q ? TA : 0));
+    if (h->d % 4 == 0)
+      launch(h, K_GPI, by, k_sel1<4>, grid, block, h->G, g, P);
+    else if (h->d % 2 == 0)
+      launch(h, K_GPI, by, k_sel1<2>, grid, block, h->G, g, P);
+    else
+      launch(h, K_GPI, by, k_sel1<1>, grid, block, h->G, g, P);
+    LAUNCHCHK();
+    return SFX_OK;
+  }
+  RC(run_gpi(h, g));
+  if (pub && pub->res) {
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, h->stream, (const int64_t*)out, pub->flag, pub->res, pub->dctr,
+                       pub->cancel, pub->nonfin);
+    LAUNCHCHK();
+  }
+  return SFX_OK;
 }
 
 // DeepSF.update_successor of one head (sfdqn.py:303-371): forwards, GPI / own-ψ next actions,
@@ -1100,6 +1124,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->fwd_tpw = etp && etp[0] == '1' ? 1 : FWD_TPW;
   const char* eat = std::getenv("SFX_AHEAD_TP");
   h->ahead_tp = eat && eat[0] == '2' ? 2 : 4;
+  const char* es1 = std::getenv("SFX_SEL1");
+  h->sel1 = !(es1 && es1[0] == '0');
   const char* eae = std::getenv("SFX_AHEAD_EARLY");
   h->ahead_early = !(eae && eae[0] == '0');
   const char* el0 = std::getenv("SFX_FUSE_L0");

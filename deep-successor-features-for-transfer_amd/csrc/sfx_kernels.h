@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace sfx {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -2119,6 +2121,56 @@ __device__ __forceinline__ unsigned long long wave_max(unsigned long long k) {
   return k;
 }
 
+// The argmaxes of one row's q = ψ·w (s_q[t * A + a], in LDS, complete): head maxima and action
+// maxima by the nthr threads of the workgroup, then the first-index argmaxes by wave 0.  Returns
+// (in wave 0) the selection (c, a) packed as c * A + a, or -1 without a selection output.
+__device__ __forceinline__ int gpi_pick(const GpiArgs& A, const float* s_q, float* s_mt, float* s_ma, int T, int Aa,
+                                        long long ob, int64_t* so, int nthr) {
+  const int tid = threadIdx.x;
+  for (int t = tid; t < T; t += nthr) {  // max over actions per head (torch.max(q, axis=2))
+    float mx = s_q[t * Aa];
+    for (int a = 1; a < Aa; ++a) mx = fmaxf(mx, s_q[t * Aa + a]);
+    s_mt[t] = mx;
+  }
+  for (int a = tid; a < Aa; a += nthr) {  // max over heads per action (torch.max(q1, axis=1))
+    float mx = s_q[a];
+    for (int t = 1; t < T; ++t) mx = fmaxf(mx, s_q[t * Aa + a]);
+    s_ma[a] = mx;
+  }
+  __syncthreads();
+  int picked = -1;
+  if (tid < 64) {  // first-index argmaxes by one wave
+    unsigned long long kt = 0ull, ka = 0ull;
+    for (int t = tid; t < T; t += 64) {
+      const unsigned long long k = argmax_key(s_mt[t], t);
+      kt = k > kt ? k : kt;
+    }
+    for (int a = tid; a < Aa; a += 64) {
+      const unsigned long long k = argmax_key(s_ma[a], a);
+      ka = k > ka ? k : ka;
+    }
+    const int tb = argmax_idx(wave_max(kt)), ab = argmax_idx(wave_max(ka));
+    const int c = A.use_gpi ? tb : A.select_task;
+    unsigned long long kc = 0ull;
+    if (so)
+      for (int a = tid; a < Aa; a += 64) {
+        const unsigned long long k = argmax_key(s_q[c * Aa + a], a);
+        kc = k > kc ? k : kc;
+      }
+    const int act = so ? argmax_idx(wave_max(kc)) : 0;
+    if (so) picked = c * Aa + act;
+    if (tid == 0) {
+      if (A.task_out) A.task_out[ob] = tb;
+      if (A.next_out) A.next_out[ob] = ab;
+      if (so) {  // sc1 stores: k_ver's last workgroup may publish them in this launch
+        __hip_atomic_store(so, (int64_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(so + 1, (int64_t)act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  return picked;
+}
+
 __device__ void gpi_row(const Geo& G, const GpiArgs& A, int b) {
   const int tid = threadIdx.x;
   const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, TA = T * Aa;
@@ -2176,47 +2228,8 @@ __device__ void gpi_row(const Geo& G, const GpiArgs& A, int b) {
     }
   }
   __syncthreads();
-  for (int t = tid; t < T; t += 256) {  // max over actions per head (torch.max(q, axis=2))
-    float mx = s_q[t * Aa];
-    for (int a = 1; a < Aa; ++a) mx = fmaxf(mx, s_q[t * Aa + a]);
-    s_mt[t] = mx;
-  }
-  for (int a = tid; a < Aa; a += 256) {  // max over heads per action (torch.max(q1, axis=1))
-    float mx = s_q[a];
-    for (int t = 1; t < T; ++t) mx = fmaxf(mx, s_q[t * Aa + a]);
-    s_ma[a] = mx;
-  }
-  __syncthreads();
-  if (tid < 64) {  // first-index argmaxes by one wave
-    unsigned long long kt = 0ull, ka = 0ull;
-    for (int t = tid; t < T; t += 64) {
-      const unsigned long long k = argmax_key(s_mt[t], t);
-      kt = k > kt ? k : kt;
-    }
-    for (int a = tid; a < Aa; a += 64) {
-      const unsigned long long k = argmax_key(s_ma[a], a);
-      ka = k > ka ? k : ka;
-    }
-    const int tb = argmax_idx(wave_max(kt)), ab = argmax_idx(wave_max(ka));
-    const int c = A.use_gpi ? tb : A.select_task;
-    unsigned long long kc = 0ull;
-    if (so)
-      for (int a = tid; a < Aa; a += 64) {
-        const unsigned long long k = argmax_key(s_q[c * Aa + a], a);
-        kc = k > kc ? k : kc;
-      }
-    const int act = so ? argmax_idx(wave_max(kc)) : 0;
-    if (tid == 0) {
-      if (A.task_out) A.task_out[ob] = tb;
-      if (A.next_out) A.next_out[ob] = ab;
-      if (so) {  // sc1 stores: k_ver's last workgroup may publish them in this launch
-        __hip_atomic_store(so, (int64_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(so + 1, (int64_t)act, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
+  gpi_pick(A, s_q, s_mt, s_ma, T, Aa, ob, so, 256);
 }
-
 __global__ __launch_bounds__(256) void k_gpi(Geo G, GpiArgs A) {
   PROBE_T(pt0);
   gpi_row(G, A, blockIdx.x);
@@ -2646,6 +2659,71 @@ __global__ void k_publish(const int64_t* sel, const int* flag, HostResult* out, 
   PROBE_T(pt0);
   if (threadIdx.x == 0) publish_result(sel, flag, out, dctr, cancel, nonfin);
   PROBE_REC(18, pt0);
+}
+
+// -------------------------------------------------------------------------------------
+// K4s  The action for one state (select_body: SFDQN.get_Q_values + the choice, sfdqn.py:577-596,
+// tsfdqn.py's test/act path): gpi_row's arithmetic for M = 1 on ONE workgroup of up to 1024
+// threads, one (head, action) dot per thread with all of its d operands requested before the first
+// FMA (gpi_row's general path reads them 8 at a time: at d = 50 and T·A = 432, two dots per thread,
+// that is 14 dependent memory round trips).  Same k-order FMA chain, so q is bit-identical, and the
+// same argmaxes (gpi_pick).  The runner's publication (k_publish) is folded in: thread 0 publishes
+// right after its selection stores.
+// -------------------------------------------------------------------------------------
+struct SelPub {
+  HostResult* res;  // null: no publication
+  const long long* dctr;
+  const int* flag;
+  const int* cancel;
+  const int* nonfin;
+};
+constexpr int SEL1_TA = 1024;  // T·A up to which k_sel1 applies
+constexpr int SEL1_DC = 64;    // ψ operands per thread requested at once
+
+template <int VW>  // operand width: d % VW == 0 (rows of ψ are then VW-float aligned)
+__global__ __launch_bounds__(1024) void k_sel1(Geo G, GpiArgs A, SelPub P) {
+  PROBE_T(pt0);
+  __shared__ float s_q[SEL1_TA];
+  __shared__ float s_w[DMAX];
+  __shared__ float s_mt[256], s_ma[256];
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, TA = T * Aa;
+  const long long ob = A.row0;
+  const float* wr = A.w + ob * A.w_stride;
+  int64_t* so = A.sel_out ? A.sel_out + ob * A.sel_stride : nullptr;
+  const FDiv fA = fdiv(Aa);
+  const bool act = tid < TA;
+  const int t = act ? tid / fA : 0, a = act ? tid - t * Aa : 0;
+  const float* p = G.actp(A.role, t, NLm) + (size_t)A.rowoff * O + (size_t)a * d;
+  using vec = typename std::conditional<VW == 4, float4, typename std::conditional<VW == 2, float2, float>::type>::type;
+  for (int k = tid; k < d; k += nthr) s_w[k] = wr[k];
+  float q = 0.f;
+  for (int k0 = 0; k0 < d; k0 += SEL1_DC) {
+    vec v[SEL1_DC / VW];
+#pragma unroll
+    for (int j = 0; j < SEL1_DC / VW; ++j) {
+      const int k = k0 + j * VW;
+      v[j] = act && k < d ? *reinterpret_cast<const vec*>(p + k) : vec{};
+    }
+    if (k0 == 0) __syncthreads();  // s_w
+#pragma unroll
+    for (int j = 0; j < SEL1_DC / VW; ++j) {
+      const int k = k0 + j * VW;
+      if (k < d) {
+        const float* e = reinterpret_cast<const float*>(&v[j]);
+#pragma unroll
+        for (int u = 0; u < VW; ++u) q = __builtin_fmaf(e[u], s_w[k + u], q);
+      }
+    }
+  }
+  if (act) {
+    s_q[tid] = q;
+    if (A.q_out) A.q_out[(ob * T + t) * Aa + a] = q;
+  }
+  __syncthreads();
+  gpi_pick(A, s_q, s_mt, s_ma, T, Aa, ob, so, nthr);
+  if (tid == 0 && P.res) publish_result(so, P.flag, P.res, P.dctr, P.cancel, P.nonfin);
+  PROBE_REC(16, pt0);
 }
 
 }  // namespace sfx
