@@ -1575,6 +1575,18 @@ int sfx_set_precision(sfx_t h, int precision) {
 
 int sfx_get_precision(sfx_t h) { return h ? (h->bf16 ? SFX_PREC_BF16 : SFX_PREC_FP32) : SFX_E_ARG; }
 
+int sfx_set_huber(sfx_t h, float delta) {
+  RC(settle(h));
+  if (!h || !(delta >= 0.f) || !std::isfinite(delta)) SFX_FAIL(SFX_E_ARG, "huber delta must be finite and >= 0");
+  if (delta == h->G.huber) return SFX_OK;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  clear_graphs(h);  // Geo is baked into captured launches
+  h->G.huber = delta;
+  return SFX_OK;
+}
+
+float sfx_get_huber(sfx_t h) { return h ? h->G.huber : -1.f; }
+
 int sfx_set_spec_rounds(sfx_t h, int rounds) {
   RC(settle(h));
   if (!h || rounds < 1) SFX_FAIL(SFX_E_ARG, "bad args");

@@ -237,7 +237,8 @@ struct Geo {
   // updates).  Null in fp32 mode.
   __bf16* on16;
   __bf16* tg16;
-  int mb, pad_mb;  // 0 or R_NS: the physical copy of the minibatch roles this launch calls R_S .. R_S1
+  int mb;          // 0 or R_NS: the physical copy of the minibatch roles this launch calls R_S .. R_S1
+  float huber;     // ψ loss: 0 = MSELoss (the reference's), δ > 0 = HuberLoss(delta = δ) (opt-in, td_grad)
 #ifdef SFX_CHECK
   long long ext_dxpart;  // floats of the split-N dX partials
 #endif
@@ -975,6 +976,30 @@ __global__ __launch_bounds__(256) void k_fwd_gemv(Geo G, FwdArgs F) {
   PROBE_REC(19, pt0);
 }
 
+// The ψ loss of one element x = c - t of the merged-clone TD target.  MSELoss(mean) (the
+// reference's, sfdqn.py:341-342): gradient (2/N) x, loss x².  Opt-in HuberLoss(delta = δ, mean)
+// (north_star's wording): gradient (1/N) clamp(x, -δ, δ) as torch's
+// huber_loss_backward forms it (±(1/N)·δ outside), loss 0.5 x² for |x| < δ, else δ (|x| - 0.5 δ).
+// The loss tail divides Σ rowloss by N = M·O for both.
+__device__ __forceinline__ float td_norm(const Geo& G, int M, int O, const float* dz_scale) {
+  const float n = (float)((G.huber > 0.f ? 1.0 : 2.0) / ((double)M * (double)O));
+  return dz_scale ? __fmul_rn(n, *dz_scale) : n;
+}
+__device__ __forceinline__ float td_grad(float huber, float norm, float x) {
+  if (huber > 0.f) {
+    const float nd = __fmul_rn(norm, huber);
+    return x < -huber ? -nd : (x > huber ? nd : __fmul_rn(norm, x));
+  }
+  return __fmul_rn(norm, x);
+}
+__device__ __forceinline__ float td_loss(float huber, float x) {
+  if (huber > 0.f) {
+    const float z = fabsf(x);
+    return z < huber ? __fmul_rn(__fmul_rn(0.5f, z), z) : __fmul_rn(huber, __fsub_rn(z, __fmul_rn(0.5f, huber)));
+  }
+  return __fmul_rn(x, x);
+}
+
 // -------------------------------------------------------------------------------------
 // K2  TD target and output gradient, one workgroup per (policy, minibatch row b)
 // (sfdqn.py:313-341; features/deep.py:101-120):
@@ -1062,8 +1087,7 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
     if (A.next) A.next[(size_t)blockIdx.y * A.next_stride + b] = am;
   }
   __syncthreads();
-  const float norm = A.dz_scale ? __fmul_rn((float)(2.0 / ((double)M * (double)O)), *A.dz_scale)
-                                : (float)(2.0 / ((double)M * (double)O));
+  const float norm = td_norm(G, M, O, A.dz_scale);
   float* grow = G.dzp(pol, NLm) + (size_t)b * O;
   const float* crow = G.actp(R_S, pol, NLm) + (size_t)b * O;
   const int an = s_next;
@@ -1072,14 +1096,14 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
     if (aok && o >= ab * d && o < ab * d + d) {
       const int k = o - ab * d;
       const float tg = __fadd_rn(A.phi[(size_t)b * d + k], __fmul_rn(gam, s_t[an * d + k]));
-      gv = __fmul_rn(norm, __fsub_rn(crow[o], tg));
+      gv = td_grad(G.huber, norm, __fsub_rn(crow[o], tg));
     }
     grow[o] = gv;
   }
   float dsq = 0.f;
   if (tid < d && aok) {
     const float diff = __fsub_rn(cval, __fadd_rn(phik, __fmul_rn(gam, s_t[an * d + tid])));
-    dsq = __fmul_rn(diff, diff);
+    dsq = td_loss(G.huber, diff);
     if (!__builtin_isfinite(diff) && G.nonfin) atomicOr(G.nonfin, 1);
   }
   if (tid < d) s_sq[tid] = dsq;
@@ -1310,8 +1334,7 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
   PROBE_AT(4);
   // ---- stage E: output gradient rows -- nonzero only at the taken action: one thread per
   // (row, feature) of it -- and the rows' squared errors (into sm.q, free after stage C)
-  const float norm = A.dz_scale ? __fmul_rn((float)(2.0 / ((double)M * (double)O)), *A.dz_scale)
-                                : (float)(2.0 / ((double)M * (double)O));
+  const float norm = td_norm(G, M, O, A.dz_scale);
   const FDiv fd = fdiv(d);
   float* sq = sm.q;
   int nf = 0;
@@ -1321,8 +1344,8 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
     if (ab >= 0 && ab < Aa) {
       const float tg = __fadd_rn(sm.ph[bl * d + k], __fmul_rn(sm.gam[bl], sm.tt[bl * O + sm.n[bl] * d + k]));
       const float diff = __fsub_rn(sm.tc[bl * O + ab * d + k], tg);
-      sm.dz[bl * O + ab * d + k] = __fmul_rn(norm, diff);
-      e2 = __fmul_rn(diff, diff);
+      sm.dz[bl * O + ab * d + k] = td_grad(G.huber, norm, diff);
+      e2 = td_loss(G.huber, diff);
       nf |= !__builtin_isfinite(diff);
     }
     sq[i] = e2;

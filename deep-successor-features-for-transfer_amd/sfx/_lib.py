@@ -52,6 +52,8 @@ SIGNATURES = {
     "sfx_skip_stats": (_I, [_VP, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong), _I]),
     "sfx_set_precision": (_I, [_VP, _I]),
     "sfx_get_precision": (_I, [_VP]),
+    "sfx_set_huber": (_I, [_VP, _F]),
+    "sfx_get_huber": (_F, [_VP]),
     "sfx_set_target_update_ev": (_I, [_VP, _I]),
     "sfx_get_since_target": (_I, [_VP, _I, _IP]),
     "sfx_set_since_target": (_I, [_VP, _I, _I]),

@@ -87,6 +87,20 @@ class _FitW(list):
             sf._eng.load_w(i if i >= 0 else len(self) + i, v)
 
 
+
+def _huber_delta(loss) -> float:
+    """The ψ loss the user's model handle returns: MSELoss(mean) -- the reference's, 0 -- or the
+    opt-in HuberLoss(delta, mean) / SmoothL1Loss(beta=1, mean) (the same function at δ = 1):
+    δ for sfx_set_huber.  Anything else raises."""
+    if getattr(loss, "reduction", None) == "mean":
+        if isinstance(loss, torch.nn.MSELoss):
+            return 0.0
+        if isinstance(loss, torch.nn.HuberLoss) and loss.delta > 0:
+            return float(loss.delta)
+        if isinstance(loss, torch.nn.SmoothL1Loss) and loss.beta == 1.0:
+            return 1.0
+    raise NotImplementedError("sfx DeepSF trains with MSELoss, HuberLoss or SmoothL1Loss(beta=1), reduction='mean'")
+
 class DeepSF(SF):
     def __init__(self, pytorch_model_handle, *args, target_update_ev=1000, max_batch=256, **kwargs):
         super().__init__(*args, **kwargs)
@@ -169,8 +183,7 @@ class DeepSF(SF):
         n_s, H, acts, out = _geometry(model)
         if out != self.n_actions * self.n_features:
             raise ValueError("ψ output width != n_actions * n_features")
-        if not isinstance(loss, torch.nn.MSELoss) or loss.reduction != "mean":
-            raise NotImplementedError("sfx DeepSF trains with MSELoss(reduction='mean') only")
+        huber = _huber_delta(loss)
         g = optim.param_groups[0] if optim is not None else {"lr": 1e-3, "betas": (0.9, 0.999), "eps": 1e-8,
                                                              "weight_decay": 0.0}
         if optim is not None and (not isinstance(optim, torch.optim.Adam) or g.get("amsgrad") or g.get("maximize")):
@@ -180,6 +193,8 @@ class DeepSF(SF):
         (lr_sf, wd_sf), (lr_w, wd_w) = self._adam_groups(optim) if optim is not None else ((1e-3, 0.0), (1e-3, 0.0))
         eng.set_adam(lr_sf, wd_sf, lr_w, wd_w, betas=tuple(g["betas"]), eps=g["eps"])
         eng.set_target_update_ev(self.target_update_ev)
+        if huber:
+            eng.set_huber(huber)
         for t, ((m, _, _), (tm, _, _)) in enumerate(self._psi):
             eng.load_head(t, _flat(m), 0)
             eng.load_head(t, _flat(tm), 1)

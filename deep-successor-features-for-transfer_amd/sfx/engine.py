@@ -451,6 +451,15 @@ class SFEngine:
         p = lib.sfx_get_precision(self._h)
         return {v: k for k, v in self.PRECISIONS.items()}[p]
 
+    def set_huber(self, delta: float):
+        """The ψ loss: 0 (default) = MSELoss (the reference's); delta > 0 = opt-in
+        HuberLoss(delta) (sfx_set_huber)."""
+        check(lib.sfx_set_huber(self._h, float(delta)), "sfx_set_huber")
+
+    @property
+    def huber(self) -> float:
+        return float(lib.sfx_get_huber(self._h))
+
     def skip_stats(self, reset: bool = False):
         """Policies checked / skipped in speculative rounds r >= 1 (their next actions repeated
         round r-1's, so their update would have too)."""

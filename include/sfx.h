@@ -206,6 +206,14 @@ int sfx_set_spec_rounds(sfx_t h, int rounds);
  * wherever the top-2 gap exceeds the bf16 error).  Default SFX_PREC_FP32. */
 int sfx_set_precision(sfx_t h, int precision);
 int sfx_get_precision(sfx_t h);
+/* The ψ loss (sfdqn.py:341-342 and every update path that shares its TD kernels: the all-task
+ * step, sfx_update, TSF, learned φ, sharded heads).  delta == 0 (default): MSELoss(mean), the
+ * reference's.  delta > 0: opt-in HuberLoss(delta, mean) -- north_star names a "Huber backward",
+ * the reference has none, so this is an extra: gradient (1/N) clamp(c - t, -δ, δ) as
+ * torch's huber_loss_backward forms it, losses 0.5 x² / δ(|x| - 0.5δ) per element.
+ * delta < 0 or not finite: SFX_E_ARG.  sfx_get_huber returns the current delta. */
+int sfx_set_huber(sfx_t h, float delta);
+float sfx_get_huber(sfx_t h);
 /* Counters of fused steps: total, those that needed host-issued rounds, the policies
  * still unverified after the device rounds, and all rounds run. */
 int sfx_step_stats(sfx_t h, long long* steps, long long* fallbacks, long long* rerun_policies, long long* rounds);

@@ -228,15 +228,21 @@ class SFState:
                        list(self.step), list(self.since_target))
 
 
-def td_grad(c: torch.Tensor, actions: torch.Tensor, targets: torch.Tensor):
+def td_grad(c: torch.Tensor, actions: torch.Tensor, targets: torch.Tensor, huber: float = 0.0):
     """MSE(c, merged) with merged = clone(c); merged[b, a_b] = t_b (sfdqn.py:334-341).
 
     Returns (l1, dL1/dc).  Only the (b, a_b) rows differ, so the gradient is
-    2 (c - t)/(B*A*d) there and 0 elsewhere."""
+    2 (c - t)/(B*A*d) there and 0 elsewhere.  huber > 0: the opt-in HuberLoss(delta=huber)
+    instead (not in the reference) -- torch's own loss and autograd gradient."""
     B = c.shape[0]
     idx = torch.arange(B)
     merged = c.clone()
     merged[idx, actions, :] = targets
+    if huber > 0:
+        cc = c.detach().clone().requires_grad_(True)
+        l1 = F.huber_loss(cc, merged.detach(), delta=huber)
+        (g,) = torch.autograd.grad(l1, cc)
+        return l1.detach(), g
     l1 = F.mse_loss(c, merged)
     g = torch.zeros_like(c)
     g[idx, actions, :] = (2.0 / c.numel()) * (c[idx, actions, :] - targets)
@@ -245,7 +251,7 @@ def td_grad(c: torch.Tensor, actions: torch.Tensor, targets: torch.Tensor):
 
 def sf_update(st: SFState, batch, i: int, *, use_gpi: bool = True, lr_sf: float = 1e-3,
               lr_w: float = 1e-3, wd_sf: float = 0.0, wd_w: float = 0.0,
-              target_update_ev: int = 1000, train_w: bool = True):
+              target_update_ev: int = 1000, train_w: bool = True, huber: float = 0.0):
     """DeepSF.update_successor of sfdqn.py:303-371 (== features/deep_sequential.py:163-231).
 
     batch = (s [B,n_s], a [B] int64, r [B,1], phi [B,d], s1 [B,n_s], gamma [B]).
@@ -265,7 +271,7 @@ def sf_update(st: SFState, batch, i: int, *, use_gpi: bool = True, lr_sf: float 
     c, xs = forward(st.online[i], spec, s)
     tpsi, _ = forward(st.target[i], spec, s1)
     targets = phi + gamma * tpsi[idx, next_actions, :]
-    l1, gc = td_grad(c, a, targets)
+    l1, gc = td_grad(c, a, targets, huber)
     r_fit = F.linear(phi, w_i.reshape(1, -1))
     l2 = F.mse_loss(r_fit, r)
     g_psi = backward(st.online[i], spec, xs, gc)
@@ -281,7 +287,7 @@ def sf_update(st: SFState, batch, i: int, *, use_gpi: bool = True, lr_sf: float 
     return l1 + l2, l1, l2, next_actions
 
 
-def deep_update(st: SFState, batch, i: int, *, lr: float = 1e-3, target_update_ev: int = 1000):
+def deep_update(st: SFState, batch, i: int, *, lr: float = 1e-3, target_update_ev: int = 1000, huber: float = 0.0):
     """features/deep.py:93-131 (the main_sfdqn_torch.py path): GPI next actions always,
     loss = l1 only, Adam over ψ_i only (the lambda's optimizer), w_i = LMS w [d].
 
@@ -296,7 +302,7 @@ def deep_update(st: SFState, batch, i: int, *, lr: float = 1e-3, target_update_e
     c, xs = forward(st.online[i], spec, s)
     tpsi, _ = forward(st.target[i], spec, s1)
     targets = phi + gamma * tpsi[idx, next_actions, :]
-    l1, gc = td_grad(c, a, targets)
+    l1, gc = td_grad(c, a, targets, huber)
     g_psi = backward(st.online[i], spec, xs, gc)
     st.step[i] += 1
     adam_(st.online[i], g_psi, st.m[i], st.v[i], st.step[i], lr)
@@ -307,10 +313,10 @@ def deep_update(st: SFState, batch, i: int, *, lr: float = 1e-3, target_update_e
     return l1, next_actions
 
 
-def deep_all_task_step(st: SFState, batch, *, lr: float = 1e-3, target_update_ev: int = 1000):
+def deep_all_task_step(st: SFState, batch, *, lr: float = 1e-3, target_update_ev: int = 1000, huber: float = 0.0):
     """agents/sfdqn.py:57-60: every head updated on the same minibatch, in index order
     (each GPI sees the heads already updated earlier in the same step)."""
-    return [deep_update(st, batch, i, lr=lr, target_update_ev=target_update_ev) for i in range(st.T)]
+    return [deep_update(st, batch, i, lr=lr, target_update_ev=target_update_ev, huber=huber) for i in range(st.T)]
 
 
 # --------------------------------------------------------------------------------------

@@ -272,3 +272,18 @@ def test_replay_buffer_tensor_gammas_and_odd_batch():
     buf.replay()
     for x, y in zip(first, keep):
         assert torch.equal(x, y)
+
+
+def test_psi_loss_mapping():
+    """The drop-in maps the user's ψ loss: MSELoss -> the reference's MSE, HuberLoss(δ) and
+    SmoothL1Loss(beta=1) -> the opt-in Huber; other losses / reductions raise."""
+    import pytest
+
+    from sfx.dropin.features.deep import _huber_delta
+
+    assert _huber_delta(torch.nn.MSELoss()) == 0.0
+    assert _huber_delta(torch.nn.HuberLoss(delta=0.5)) == 0.5
+    assert _huber_delta(torch.nn.SmoothL1Loss()) == 1.0
+    for bad in (torch.nn.MSELoss(reduction="sum"), torch.nn.SmoothL1Loss(beta=0.5), torch.nn.L1Loss()):
+        with pytest.raises(NotImplementedError):
+            _huber_delta(bad)

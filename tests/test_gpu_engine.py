@@ -312,3 +312,50 @@ def test_ragged_shapes_update_vs_oracle(n_s, H, A, d, acts, B):
         eng.update_all(s, a, phi, s1, gamma)
     params_close(torch.stack([eng.get_head(t) for t in range(T)]), st.online, 5e-3)
     eng.close()
+
+
+@pytest.mark.parametrize("n_s,H,A,d,acts,B", [RAGGED[1], RAGGED[2], (17, 256, 7, 8, ("relu", "relu"), 32)])
+def test_huber_update_vs_oracle(n_s, H, A, d, acts, B):
+    """Opt-in HuberLoss (sfx_set_huber; not in the reference) through both TD paths --
+    the fused TD launch (A·d <= 128) and k_tdg (A·d = 1350) -- against torch's huber_loss and its
+    autograd gradient in the oracle: active-task updates (± GPI) and all-task steps, δ small enough
+    that part of the errors fall outside it.  Tolerances as for MSE."""
+    from sfx.init import reference_heads
+
+    T, delta = 3, 0.05
+    spec = R.Spec(n_s, H, A, d, acts)
+    online, w = reference_heads(T, n_s, H, A, d, acts, seed=6)
+    eng = engine_for(spec, T, max_batch=B)
+    eng.set_huber(delta)
+    assert abs(eng.huber - delta) < 1e-9
+    for t in range(T):
+        eng.load_head(t, online[t], 0)
+        eng.load_head(t, online[t], 1)
+        eng.load_w(t, w[t])
+    st = R.SFState(spec, online.clone(), online.clone(), w.clone())
+    gen = torch.Generator().manual_seed(12)
+
+    def batch():
+        return (torch.randn(B, n_s, generator=gen), torch.randint(0, A, (B,), generator=gen),
+                torch.rand(B, 1, generator=gen), torch.rand(B, d, generator=gen), torch.randn(B, n_s, generator=gen),
+                torch.full((B,), 0.9))
+
+    nxt = torch.empty(B, dtype=torch.long, device="cuda")
+    for i, use_gpi in ((1, True), (2, False)):
+        s, a, r, phi, s1, gamma = batch()
+        loss, l1, l2, na = R.sf_update(st, (s, a, r, phi, s1, gamma), i, use_gpi=use_gpi, huber=delta)
+        lo = eng.update(i, s, a, r, phi, s1, gamma, use_gpi=use_gpi, next_actions=nxt)
+        assert torch.equal(nxt.cpu(), na)
+        rel_close(lo, [float(loss), float(l1), float(l2)], rtol=1e-4, atol=1e-7)
+    params_close(torch.stack([eng.get_head(t) for t in range(T)]), st.online, 2e-3)
+    for _ in range(2):
+        s, a, r, phi, s1, gamma = batch()
+        R.deep_all_task_step(st, (s, a, phi, s1, gamma), huber=delta)
+        eng.update_all(s, a, phi, s1, gamma)
+    params_close(torch.stack([eng.get_head(t) for t in range(T)]), st.online, 4e-3)
+    eng.set_huber(0.0)  # back to the reference's MSE
+    s, a, r, phi, s1, gamma = batch()
+    loss, l1, l2, na = R.sf_update(st, (s, a, r, phi, s1, gamma), 0, use_gpi=True)
+    lo = eng.update(0, s, a, r, phi, s1, gamma, use_gpi=True, next_actions=nxt)
+    rel_close(lo, [float(loss), float(l1), float(l2)], rtol=1e-4, atol=1e-7)
+    eng.close()

@@ -202,3 +202,29 @@ def test_phi_update_matches_reference(golden, case):
     close(st.wb, g["wb"], rtol=1e-4, atol=1e-6)
     close(st.phi, g["phi"], rtol=1e-4, atol=1e-6)
     close(st.lam, g["lam"], rtol=1e-6)
+
+
+def test_huber_td_grad_closed_form():
+    """The oracle's opt-in Huber (td_grad(huber=δ); not in the reference, SURVEY F3 -- parity
+    unpinned by the reference, pinned here to the closed form the kernels implement): gradient
+    (1/N) clamp(c - t, -δ, δ) at the taken actions, 0 elsewhere; loss mean of 0.5 x² (|x| < δ) or
+    δ(|x| - 0.5 δ); and for δ past every error, half the MSE gradient."""
+    gen = torch.Generator().manual_seed(3)
+    B, A, d, delta = 16, 5, 4, 0.3
+    c = torch.randn(B, A, d, generator=gen)
+    a = torch.randint(0, A, (B,), generator=gen)
+    t = torch.randn(B, d, generator=gen)
+    l1, g = R.td_grad(c, a, t, huber=delta)
+    N = c.numel()
+    x = c[torch.arange(B), a] - t
+    assert (x.abs() > delta).any() and (x.abs() < delta).any()
+    want = torch.zeros_like(c)
+    want[torch.arange(B), a] = torch.where(x < -delta, -(1.0 / N) * delta,
+                                           torch.where(x > delta, (1.0 / N) * delta, (1.0 / N) * x))
+    torch.testing.assert_close(g, want, rtol=0, atol=1e-9)
+    z = x.abs()
+    lw = torch.where(z < delta, 0.5 * z * z, delta * (z - 0.5 * delta)).sum() / N
+    torch.testing.assert_close(l1, lw, rtol=1e-6, atol=0)
+    _, gm = R.td_grad(c, a, t)
+    _, gh = R.td_grad(c, a, t, huber=1e3)
+    torch.testing.assert_close(gh, 0.5 * gm, rtol=1e-6, atol=1e-9)
