@@ -153,8 +153,7 @@ struct sfx_handle {
   int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
   int fwd_tpw = FWD_TPW; // column tiles per workgroup (layer-0+1 forward, oversubscribed launches); SFX_FWD_TPW=1: one
   int ahead_tp = 4;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=2: two)
-  bool ahead_early = true;
-  bool sel1 = true;  // one-state action selection by k_sel1 (SFX_SEL1=0: k_gpi + k_publish)  // the look-ahead rows ride in round 0's post-update forward (SFX_AHEAD_EARLY=0: the final round's)
+  bool sel1 = true;      // one-state action selection by k_sel1 (SFX_SEL1=0: k_gpi + k_publish)
   int ncu = 256;         // compute units of the device
   bool fuse_l0 = true;   // SFX_FUSE_L0=0: layer 0 of a forward from the states as its own launch
   AdamHP hp_psi{1e-3, 0.0, 0.9, 0.999, 1e-8};
@@ -898,15 +897,13 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
   bx.v_x = p.S1;
   bx.v_xn = want_sel ? p.s_next : nullptr;
   const int vM = B + (want_sel ? 1 : 0);
-  // look-ahead: a round also forwards the next step's minibatch into the other copy of the
-  // minibatch roles.  Early (the default): round 0 computes them for every head and every later
-  // round (device or host) recomputes them only for the heads it does not skip -- a skipped head's
-  // parameters are those of the round that last computed its rows, so an all-skip round leaves
-  // its forwards empty.  Otherwise the final round (device or host) does; the first round that
-  // does (the last device round) computes them for every head, later host rounds skip them with
-  // the rest of a head.
-  const bool ahead = (final || h->ahead_early) && p.ax && p.aM > 0 && bx.fuse_v0 && can_fuse_ahead(h, vM, p.aM);
-  const int a_noskip = !ahead ? 0 : h->ahead_early ? (r == 0 ? 1 : 0) : (r <= h->spec_rounds - 1 ? 1 : 0);
+  // look-ahead: the final round (device or host) also forwards the next step's minibatch into the
+  // other copy of the minibatch roles; the first round that does (the last device round) computes
+  // them for every head, skipped or not -- later host rounds skip them with the rest of a head.
+  // (Forwarding them in round 0 instead, so that an all-skip round 1 leaves its forwards empty,
+  // measured 9 % slower: DESIGN.md §8.)
+  const bool ahead = final && p.ax && p.aM > 0 && bx.fuse_v0 && can_fuse_ahead(h, vM, p.aM);
+  const int a_noskip = ahead && r <= h->spec_rounds - 1 ? 1 : 0;
   if (ahead) {
     bx.ax = p.ax;
     bx.aM = p.aM;
@@ -1126,8 +1123,6 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->ahead_tp = eat && eat[0] == '2' ? 2 : 4;
   const char* es1 = std::getenv("SFX_SEL1");
   h->sel1 = !(es1 && es1[0] == '0');
-  const char* eae = std::getenv("SFX_AHEAD_EARLY");
-  h->ahead_early = !(eae && eae[0] == '0');
   const char* el0 = std::getenv("SFX_FUSE_L0");
   h->fuse_l0 = !(el0 && el0[0] == '0');
   const char* esd = std::getenv("SFX_SPLIT_DX");

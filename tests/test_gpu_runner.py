@@ -472,21 +472,19 @@ def test_round_skip_is_bit_exact(spec_rounds, force, monkeypatch):
     assert s1["policies_checked"] >= n * (spec_rounds - 1) * T // 2 and s1["policies_skipped"] > 0, s1
 
 
-@pytest.mark.parametrize("force,ev,early", [(-1, 7, "1"), (1, 1000, "1"), (2, 1000, "1"), (-1, 7, "0"), (1, 1000, "0")])
-def test_lookahead_is_bit_exact(force, ev, early, monkeypatch):
-    """Look-ahead: step E's rounds forward step E+1's minibatch into the other copy
-    of the minibatch roles and step E+1 starts at its TD launch -- round 0 for every head and later
-    rounds for the heads they do not skip (early, the default), or the final round (SFX_AHEAD_EARLY=0).
-    The forward is the same arithmetic as the step-start forward, so heads, moments and every action
-    must be IDENTICAL to SFX_AHEAD=0 on the same index stream -- through dirty minibatches (a small
-    ring: the newest transition is sampled often), target syncs every 7 updates, and forced host
-    rounds (which skip the heads whose actions repeat)."""
+@pytest.mark.parametrize("force,ev", [(-1, 7), (1, 1000), (2, 1000)])
+def test_lookahead_is_bit_exact(force, ev, monkeypatch):
+    """Look-ahead: step E's final round forwards step E+1's minibatch into the other
+    copy of the minibatch roles and step E+1 starts at its TD launch.  The forward is the same
+    arithmetic as the step-start forward, so heads, moments and every action must be IDENTICAL to
+    SFX_AHEAD=0 on the same index stream -- through dirty minibatches (a small ring: the newest
+    transition is sampled often), target syncs every 7 updates, and forced host rounds (which skip
+    the heads whose actions repeat)."""
     from sfx.runner import NativeEnvLoop
 
     spec = R.Spec(17, 64, 7, 8, ("relu", "relu"))
     T, n = 5, 60
     out = {}
-    monkeypatch.setenv("SFX_AHEAD_EARLY", early)
     for ahead in ("1", "0"):
         monkeypatch.setenv("SFX_AHEAD", ahead)
         eng, _ = make(spec, T, ev, max_batch=16)
