@@ -7,6 +7,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/${1:-r4g}
 mkdir -p $O
 ok() { local rc=$1; [ $rc -le 1 ] || { echo "rc=$rc: stopping"; exit $rc; }; }
+timeout -k 10 120 tools/fwdbench > $O/fwdbench.txt 2>&1; rc=$?; echo "fwdbench rc=$rc"; cat $O/fwdbench.txt; ok $rc
 timeout -k 10 60 tools/hostsan/fnptr_plain > $O/fnptr_plain.txt 2>&1; rc=$?; echo "fnptr_plain rc=$rc"; cat $O/fnptr_plain.txt; ok $rc
 timeout -k 10 60 tools/hostsan/fnptr_function > $O/fnptr_function.txt 2>&1; rc=$?; echo "fnptr_function rc=$rc"; cat $O/fnptr_function.txt; ok $rc
 UBSAN_OPTIONS=print_stacktrace=1 timeout -k 10 300 tools/hostsan/runner_ubsan_fn > $O/hostsan_ubsan_fn.txt 2>&1
