@@ -14,6 +14,10 @@ UBSAN_OPTIONS=print_stacktrace=1 timeout -k 10 300 tools/hostsan/runner_ubsan_fn
 rc=$?; echo "ubsan_fn rc=$rc"; tail -3 $O/hostsan_ubsan_fn.txt; ok $rc
 UBSAN_OPTIONS=print_stacktrace=1 timeout -k 10 300 tools/hostsan/runner_ubsan_vptr > $O/hostsan_ubsan_vptr.txt 2>&1
 rc=$?; echo "ubsan_vptr rc=$rc"; tail -3 $O/hostsan_ubsan_vptr.txt; ok $rc
+P=$PWD/deep-successor-features-for-transfer_amd/sfx/libsfx_probe.so
+SFX_LIB=$P timeout -k 10 150 python tools/probe_run.py 30 tsf-nf > $O/probe_tsfnf_sel1.txt 2>&1 || { tail -5 $O/probe_tsfnf_sel1.txt; exit 1; }
+SFX_SEL1=0 SFX_LIB=$P timeout -k 10 150 python tools/probe_run.py 30 tsf-nf > $O/probe_tsfnf_gpi.txt 2>&1 || { tail -5 $O/probe_tsfnf_gpi.txt; exit 1; }
+grep -E "gpi|publish|sum" $O/probe_tsfnf_sel1.txt $O/probe_tsfnf_gpi.txt | cut -c1-150
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 for v in 1 0; do
   SFX_SEL1=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_sel$v -o run -- \
