@@ -347,6 +347,8 @@ GraphKey make_key(int op, std::initializer_list<int> ints, unsigned long long ma
 
 struct FwdExtra {
   int l0 = 0;            // first layer to run
+  int lN = -1;           // layers [l0, lN) (-1: through the last)
+  const float* xc = nullptr;  // layer-0 input of groups with xsel 3
   int lms_head = -1;     // LMS in block 0 of layer 0
   const float* lms_phi = nullptr;
   const float* lms_r = nullptr;
@@ -371,6 +373,7 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
   F.M = M;
   F.xa = xa;
   F.xb = xb;
+  F.xc = ex.xc;
   F.mask = h->mask;
   F.lms_head = -1;
   F.qa_role = -1;
@@ -390,7 +393,9 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
   // layers 0 and 1 in one launch when layer 0 is small (its rows recomputed per tile in LDS)
   const bool fuse01 = h->fuse_l0 && ex.l0 == 0 && h->NL >= 3 && h->L[0].K <= L0_KMAX && h->L[0].N <= L0_NMAX &&
                       h->L[1].K % 32 == 0 && h->fwd_waves == 8;
-  for (int l = fuse01 ? 1 : ex.l0; l < h->NL; ++l) {
+  const int lend = ex.lN >= 0 ? ex.lN : h->NL;
+  if (fuse01 && lend < 2) SFX_FAIL(SFX_E_STATE, "run_fwd: the fused layer-0+1 launch needs layer 1");
+  for (int l = fuse01 ? 1 : ex.l0; l < lend; ++l) {
     const LayerGeo& L = h->L[l];
     const bool l0 = fuse01 && l == 1;
     F.N = L.N;
@@ -944,9 +949,15 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
 // forward of every head on s, GPI with w of `task`, selection into out[2] = (c, a).
 // With `pub` (runner steps) the step's result is published after the selection: inside k_sel1, or
 // by k_publish after k_gpi.
+int select_pick(sfx_handle* h, int task, int use_gpi, float* q, int64_t* out, const SelPub* pub);
 int select_body(sfx_handle* h, const float* s, int task, int use_gpi, float* q, int64_t* out,
                 const SelPub* pub = nullptr) {
   RC(run_fwd(h, {{R_A, P_ONLINE, 1, 0, h->T}}, 1, s, nullptr));
+  return select_pick(h, task, use_gpi, q, out, pub);
+}
+
+// the choice from role R_A row 0 (GPI with w of `task`, or `task`'s own q) and the publication
+int select_pick(sfx_handle* h, int task, int use_gpi, float* q, int64_t* out, const SelPub* pub) {
   const GpiArgs g = gpi_args(R_A, 0, 0, h->w + (size_t)task * h->dpad, nullptr, q, nullptr, nullptr, out, task, use_gpi, 1);
   const int TA = h->T * h->A;
   if (h->sel1 && TA <= SEL1_TA && h->A <= 256 && h->T <= 256) {
@@ -973,14 +984,19 @@ int select_body(sfx_handle* h, const float* s, int task, int use_gpi, float* q, 
 
 // DeepSF.update_successor of one head (sfdqn.py:303-371): forwards, GPI / own-ψ next actions,
 // TD target, backward + Adam (+ l2 and the w step when r is given).  Launches only.
+// pre: the previous runner step's look-ahead select (select_ahead_body) already forwarded this
+// minibatch with the current heads into the roles this step reads: start at the TD target.
 int update_body(sfx_handle* h, int policy, const float* S, const int64_t* a, const float* r, const float* phi,
-                const float* S1, const float* gamma, int B, int use_gpi, float* losses, int64_t* next) {
-  if (use_gpi)
+                const float* S1, const float* gamma, int B, int use_gpi, float* losses, int64_t* next,
+                bool pre = false) {
+  if (pre) {
+  } else if (use_gpi) {
     RC(run_fwd(h, {{R_S, P_ONLINE, 1, policy, 1}, {R_S1T, P_TARGET, 2, policy, 1}, {R_S1, P_ONLINE, 2, 0, h->T}}, B,
                S, S1));
-  else
+  } else {
     RC(run_fwd(h, {{R_S, P_ONLINE, 1, policy, 1}, {R_S1T, P_TARGET, 2, policy, 1}, {R_S1, P_ONLINE, 2, policy, 1}},
                B, S, S1));
+  }
   TdgSpec td;
   td.use_gpi = use_gpi;
   td.a = a;
@@ -993,7 +1009,43 @@ int update_body(sfx_handle* h, int policy, const float* S, const int64_t* a, con
 // TSFDQN.update_successor (sfx_tsf.inc)
 int tsf_body(sfx_handle* h, int policy, const float* S, const int64_t* a, const float* r, const float* phi,
              const float* S1, const float* gamma, int B, int use_gpi, float* losses, int64_t* next,
-             const int* xmax = nullptr);
+             const int* xmax = nullptr, bool pre = false);
+int tsf_fwd_with(sfx_handle* h, int policy, int B, const float* S, const float* S1, const float* phi,
+                 const std::function<int(const FwdExtra&)>& fwd, const float* xc);
+
+// The action for s_next (select_body) with the look-ahead of the active-task / TSF runner steps
+// (DESIGN.md §5): the next step's minibatch -- states ax[0, B), next states ax[B, 2B), TSF: its φ
+// rows axphi -- is forwarded with this step's post-update heads into the other copy of the
+// minibatch roles: ψ(S1) of every head (R_NS1; the next step's GPI), ψ(S) and ψ⁻(S1) of the active
+// head (R_NS, R_NS1T) and, for TSF, its φ̃ and flow states (the TSF forward riding in the first
+// launch) -- so the next step starts at its TD target.  Layers 0 .. NL-2 of the selection row
+// (R_A, its own group) and of the minibatch share launches; then the selection's last layer, the
+// choice and the publication; the minibatch's last layer comes after them, so it runs while the
+// host turns the published action into the next step's inputs.
+int select_ahead_body(sfx_handle* h, const float* s, const float* ax, const float* axphi, int B, int task,
+                      int use_gpi, int64_t* out, const SelPub* pub) {
+  const int T = h->T, n_s = h->n_s;
+  const float* S = ax;
+  const float* S1 = ax + (size_t)B * n_s;
+  const auto early = [&](const FwdExtra& fx0) -> int {
+    FwdExtra fx = fx0;
+    fx.lN = h->NL - 1;
+    fx.xc = s;
+    return run_fwd(h, {{R_A, P_ONLINE, 3, 0, T, 1, 0}, {R_NS1, P_ONLINE, 2, 0, T, B, 0}, {R_NS, P_ONLINE, 1, task, 1, B, 0},
+                       {R_NS1T, P_TARGET, 2, task, 1, B, 0}},
+                   B, S, S1, fx);
+  };
+  if (axphi)
+    RC(tsf_fwd_with(h, task, B, S, S1, axphi, early, s));
+  else
+    RC(early(FwdExtra()));
+  FwdExtra last;
+  last.l0 = h->NL - 1;
+  RC(run_fwd(h, {{R_A, P_ONLINE, 3, 0, T}}, 1, nullptr, nullptr, last));
+  RC(select_pick(h, task, use_gpi, nullptr, out, pub));
+  return run_fwd(h, {{R_NS1, P_ONLINE, 2, 0, T}, {R_NS, P_ONLINE, 1, task, 1}, {R_NS1T, P_TARGET, 2, task, 1}}, B,
+                 nullptr, nullptr, last);
+}
 
 
 int launch_step_all(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, const float* lms_phi, const float* lms_r,

@@ -413,7 +413,7 @@ __device__ __forceinline__ void adam_el(float* p, float* m, float* v, float g, c
 // (features/successor.py:164-167) and reset the speculation flag.
 // -------------------------------------------------------------------------------------
 struct FwdGroup {
-  int role, which, xsel, head0, n;  // which: P_*; xsel: 1 -> xa, 2 -> xb
+  int role, which, xsel, head0, n;  // which: P_*; xsel: 1 -> xa, 2 -> xb, 3 -> xc
   int m;       // rows of this group (0: FwdArgs::M); tiles past them exit
   int noskip;  // FwdArgs::skip does not apply (look-ahead groups of the final device round)
 };
@@ -431,6 +431,7 @@ struct FwdArgs {
   FwdGroup g0, g1, g2, g3;
   const float* xa;
   const float* xb;
+  const float* xc;       // a third layer-0 input (the look-ahead select: s_next beside the next minibatch)
   const float* lms_phi;  // LMS (lms_head >= 0): w[lms_head] += α (r - φ·w) φ
   const float* lms_r;
   float lms_alpha;
@@ -595,7 +596,7 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
   if (tM * 32 >= M) return;  // a group with fewer rows than the launch (block-uniform, before any barrier)
   const float* P = grp.which == P_TARGET ? G.target + (long long)head * G.P
                                          : G.online + G.slot_off(rslot(F.mask, head) ^ (grp.which == P_NEW), head);
-  const float* X = F.xOff < 0 ? (grp.xsel == 1 ? F.xa : F.xb) : G.actp(grp.role, head, F.xOff);
+  const float* X = F.xOff < 0 ? (grp.xsel == 1 ? F.xa : grp.xsel == 2 ? F.xb : F.xc) : G.actp(grp.role, head, F.xOff);
   float* Y = G.actp(grp.role, head, F.yOff);
   const int m0 = tM * 32;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
@@ -932,7 +933,7 @@ __global__ __launch_bounds__(256) void k_fwd_gemv(Geo G, FwdArgs F) {
   const int M = F.M, N = F.N, K = F.K;
   const float* P = grp.which == P_TARGET ? G.target + (long long)head * G.P
                                          : G.online + G.slot_off(rslot(F.mask, head) ^ (grp.which == P_NEW), head);
-  const float* X = F.xOff < 0 ? (grp.xsel == 1 ? F.xa : F.xb) : G.actp(grp.role, head, F.xOff);
+  const float* X = F.xOff < 0 ? (grp.xsel == 1 ? F.xa : grp.xsel == 2 ? F.xb : F.xc) : G.actp(grp.role, head, F.xOff);
   float* Y = G.actp(grp.role, head, F.yOff);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane & 3;
   const int n = blockIdx.x * 64 + wave * 16 + (lane >> 2);

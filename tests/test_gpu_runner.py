@@ -515,6 +515,60 @@ def test_lookahead_is_bit_exact(force, ev, monkeypatch):
     assert s1["ahead_own_forward_steps"] > 0, s1  # dirty minibatches (and syncs) ran their own forward
 
 
+@pytest.mark.parametrize("schedule,upd_use_gpi,ev", [("active", True, 7), ("active", False, 1000), ("tsf", True, 7),
+                                                     ("tsf", False, 1000)])
+def test_active_lookahead_is_bit_exact(schedule, upd_use_gpi, ev, monkeypatch):
+    """Look-ahead of the active-task / TSF schedules (select_ahead_body): step E's
+    select also forwards step E+1's minibatch (ψ(S1) of every head, ψ(S) and ψ⁻(S1) of the active
+    head; TSF: its φ̃ and flow states) and step E+1 starts at its TD target.  Same arithmetic as the
+    step-start forward, so heads, targets, moments, w (TSF: g_i, h) and every action must be
+    IDENTICAL to SFX_AHEAD=0 on the same index stream -- through dirty minibatches (a small ring),
+    target syncs every 7 updates and episode ends."""
+    from sfx.runner import NativeEnvLoop
+
+    spec = R.Spec(11, 48, 5, 6, ("relu", "relu"))
+    T, n, task = 3, 50, 1
+    out = {}
+    for ahead in ("1", "0"):
+        monkeypatch.setenv("SFX_AHEAD", ahead)
+        eng, _ = make(spec, T, ev)
+        if schedule == "tsf":
+            K, G = 3, 12
+            gs = R.GSpec(spec.n_s, G, K)
+            gen = torch.Generator().manual_seed(4)
+            g = torch.empty(T, gs.P).uniform_(-0.3, 0.3, generator=gen)
+            h = torch.empty(spec.d * G + spec.d).uniform_(-0.2, 0.2, generator=gen)
+            eng.tsf_setup(G, K, 1.0, 1e-3, 0.0, 1e-3, 0.0)
+            for t in range(T):
+                eng.tsf_load_g(t, g[t])
+            eng.tsf_load_h(h)
+        loop = NativeEnvLoop(eng, batch=16, capacity=40, gamma=0.9, epsilon=0.3, episode_len=11, seed=5,
+                             schedule=schedule, upd_use_gpi=upd_use_gpi, p_end=0.1)
+        loop.prefill(20)
+        loop.set_task(task)
+        loop.record(n)
+        loop.run(n // 2)
+        loop.run(n - n // 2)
+        recs = loop.records()
+        res = [torch.stack([eng.get_head(t, 0) for t in range(T)]), torch.stack([eng.get_head(t, 1) for t in range(T)]),
+               torch.stack([eng.get_w(t)[0] for t in range(T)])]
+        for t in range(T):
+            m, v, st = eng.get_adam(t)
+            res += [m, v, torch.tensor(st)]
+        if schedule == "tsf":
+            res += [torch.stack([eng.tsf_get_g(t)[0] for t in range(T)]), eng.tsf_get_h()]
+        out[ahead] = (res, [(r["c"], r["a_greedy"]) for r in recs], loop.action(), loop.stats())
+        loop.close()
+        eng.close()
+    (r1, a1, f1, s1), (r0, a0, f0, s0) = out["1"], out["0"]
+    assert a1 == a0 and f1 == f0
+    for x, y in zip(r1, r0):
+        assert torch.equal(x, y)
+    assert s0["ahead_pre_steps"] == 0
+    assert s1["ahead_pre_steps"] > n // 2, s1
+    assert s1["ahead_own_forward_steps"] > 0, s1
+
+
 def test_lookahead_runner_matches_oracle_c2():
     """The C2 shape (T = 8, H = 256, B = 32) with look-ahead on (the bench's configuration),
     replayed through the oracle from the runner's recorded inputs."""
