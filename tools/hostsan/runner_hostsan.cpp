@@ -14,6 +14,8 @@
 #include <cstring>
 #include <vector>
 
+#include <hip/hip_runtime.h>
+
 #include "../../include/sfx.h"
 
 #define CK(x)                                                                         \
@@ -165,9 +167,71 @@ void scenario(const char* name, int schedule, int T, bool callbacks) {
   CK(sfx_destroy(h));
 }
 
+// the engine's all-task update (sfx_update_all: graph-captured speculative rounds, settled by the
+// next call) without the runner: device inputs, five steps, finite and moved parameters
+void engine_scenario() {
+  std::printf("engine update_all (T=3)\n");
+  std::fflush(stdout);
+  const int T = 3, B = 32;
+  sfx_t h = make_handle(T);
+  std::vector<float> s(B * NS), s1(B * NS), phi(B * D), g(B, 0.9f), p0((size_t)sfx_head_numel(h)), p1(p0.size());
+  std::vector<int64_t> a(B);
+  float *dS, *dS1, *dphi, *dg;
+  int64_t* da;
+  if (hipMalloc(&dS, 4 * s.size()) || hipMalloc(&dS1, 4 * s1.size()) || hipMalloc(&dphi, 4 * phi.size()) ||
+      hipMalloc(&dg, 4 * g.size()) || hipMalloc(&da, 8 * a.size())) {
+    std::fprintf(stderr, "FAIL engine: hipMalloc\n");
+    std::exit(1);
+  }
+  CK(sfx_get_head(h, 1, 0, p0.data()));
+  for (int it = 0; it < 5; ++it) {
+    for (float& x : s) x = urand() - 0.5f;
+    for (float& x : s1) x = urand() - 0.5f;
+    for (float& x : phi) x = urand();
+    for (int64_t& x : a) x = (int64_t)(urand() * A) % A;
+    if (hipMemcpy(dS, s.data(), 4 * s.size(), hipMemcpyHostToDevice) ||
+        hipMemcpy(dS1, s1.data(), 4 * s1.size(), hipMemcpyHostToDevice) ||
+        hipMemcpy(dphi, phi.data(), 4 * phi.size(), hipMemcpyHostToDevice) ||
+        hipMemcpy(dg, g.data(), 4 * g.size(), hipMemcpyHostToDevice) ||
+        hipMemcpy(da, a.data(), 8 * a.size(), hipMemcpyHostToDevice)) {
+      std::fprintf(stderr, "FAIL engine: hipMemcpy\n");
+      std::exit(1);
+    }
+    CK(sfx_update_all(h, dS, da, dphi, dS1, dg, B, nullptr));
+  }
+  CK(sfx_get_head(h, 1, 0, p1.data()));  // settles the last step
+  bool moved = false;
+  for (size_t i = 0; i < p1.size(); ++i) {
+    if (!std::isfinite(p1[i])) {
+      std::fprintf(stderr, "FAIL engine: non-finite parameter\n");
+      std::exit(1);
+    }
+    moved = moved || p1[i] != p0[i];
+  }
+  std::printf("  5 steps, parameters %s\n", moved ? "moved" : "UNCHANGED");
+  std::fflush(stdout);
+  (void)hipFree(dS);
+  (void)hipFree(dS1);
+  (void)hipFree(dphi);
+  (void)hipFree(dg);
+  (void)hipFree(da);
+  CK(sfx_destroy(h));
+}
+
 }  // namespace
 
 int main() {
+  // HOSTSAN_BISECT=1: the engine path first, then the all-task runner eager (no graphs), then
+  // without pre-launched graphs -- the first one that stops narrows a hang down
+  if (const char* b = std::getenv("HOSTSAN_BISECT"); b && b[0] == '1') {
+    engine_scenario();
+    setenv("SFX_GRAPHS", "0", 1);
+    scenario("all-task, eager launches", 0, 3, false);
+    unsetenv("SFX_GRAPHS");
+    setenv("SFX_RUNNER_PIPELINE", "0", 1);
+    scenario("all-task, graphs, no pre-launch", 0, 3, false);
+    unsetenv("SFX_RUNNER_PIPELINE");
+  }
   scenario("all-task", 0, 3, false);
   scenario("all-task", 0, 4, true);
   scenario("active-task", 1, 3, true);
