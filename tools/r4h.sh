@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-4 checks on one box: the runner / TSF / engine GPU tests (look-ahead of the active and TSF
-# schedules), A/B of that look-ahead (2000-step windows), the TSF-NF probe timeline, then the
-# diagnostics of tools/r4g.sh.  Every GPU step time-limited; stops at a time-out or crash.
+# Round-4 checks on one box: the runner / TSF / engine GPU tests, A/B of the all-task look-ahead
+# placements (final round vs after the publication; 2000-step windows), the probe timeline of the
+# post-publish placement, then the UBSan function-check bisection.  Every GPU step time-limited; stops at a time-out or crash.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/${1:-r4h}
 mkdir -p $O
@@ -16,19 +16,10 @@ run() {  # tag, env VAR=value..., then bench flags
     --repeats 2 "$@" > $O/bench_$tag.json 2>/dev/null || return 1
   python -c "import json,sys;d=json.loads(open(sys.argv[1]).read().splitlines()[-1]);print(sys.argv[2], d['value'], d['repeats']['values'], d['speculation'].get('ahead_pre_steps'))" $O/bench_$tag.json $tag
 }
-run nf_on SFX_AHEAD=1 --workload hopper-tsf-nf && run nf_off SFX_AHEAD=0 --workload hopper-tsf-nf && \
-  run tsf_on SFX_AHEAD=1 --workload hopper-tsf && run tsf_off SFX_AHEAD=0 --workload hopper-tsf && \
-  run act_on SFX_AHEAD=1 --schedule active && run act_off SFX_AHEAD=0 --schedule active && \
-  run nf_on2 SFX_AHEAD=1 --workload hopper-tsf-nf && run nf_off2 SFX_AHEAD=0 --workload hopper-tsf-nf && \
-  run c2 || exit 1
+run post_a SFX_AHEAD_POST=1 && run round_a SFX_AHEAD_POST=0 && run post_b SFX_AHEAD_POST=1 && \
+  run round_b SFX_AHEAD_POST=0 && run off_a SFX_AHEAD=0 || exit 1
 P=$PWD/deep-successor-features-for-transfer_amd/sfx/libsfx_probe.so
-SFX_LIB=$P timeout -k 10 150 python tools/probe_run.py 30 tsf-nf > $O/probe_tsfnf_ahead.txt 2>&1 || { tail -5 $O/probe_tsfnf_ahead.txt; exit 1; }
-SFX_AHEAD=0 SFX_LIB=$P timeout -k 10 150 python tools/probe_run.py 30 tsf-nf > $O/probe_tsfnf_noahead.txt 2>&1 || exit 1
-grep -E "sum" $O/probe_tsfnf_ahead.txt $O/probe_tsfnf_noahead.txt
-timeout -k 10 120 tools/fwdbench > $O/fwdbench.txt 2>&1; rc=$?; echo "fwdbench rc=$rc"; cat $O/fwdbench.txt; ok $rc
-timeout -k 10 60 tools/hostsan/fnptr_plain > $O/fnptr_plain.txt 2>&1; rc=$?; echo "fnptr_plain rc=$rc"; cat $O/fnptr_plain.txt; ok $rc
-timeout -k 10 60 tools/hostsan/fnptr_function > $O/fnptr_function.txt 2>&1; rc=$?; echo "fnptr_function rc=$rc"; cat $O/fnptr_function.txt; ok $rc
-UBSAN_OPTIONS=print_stacktrace=1 timeout -k 10 300 tools/hostsan/runner_ubsan_fn > $O/hostsan_ubsan_fn.txt 2>&1
-rc=$?; echo "ubsan_fn rc=$rc"; tail -3 $O/hostsan_ubsan_fn.txt; ok $rc
-UBSAN_OPTIONS=print_stacktrace=1 timeout -k 10 300 tools/hostsan/runner_ubsan_vptr > $O/hostsan_ubsan_vptr.txt 2>&1
-rc=$?; echo "ubsan_vptr rc=$rc"; tail -3 $O/hostsan_ubsan_vptr.txt; ok $rc
+SFX_AHEAD_POST=1 SFX_LIB=$P timeout -k 10 150 python tools/probe_run.py 30 > $O/probe_post.txt 2>&1 || { tail -5 $O/probe_post.txt; exit 1; }
+grep -E "sum" $O/probe_post.txt
+HOSTSAN_BISECT=1 UBSAN_OPTIONS=print_stacktrace=1 timeout -k 10 300 tools/hostsan/runner_ubsan_fn > $O/hostsan_ubsan_fn_bisect.txt 2>&1
+rc=$?; echo "ubsan_fn bisect rc=$rc"; cat $O/hostsan_ubsan_fn_bisect.txt | head -30; ok $rc
