@@ -154,9 +154,6 @@ struct sfx_handle {
   int fwd_tpw = FWD_TPW; // column tiles per workgroup (layer-0+1 forward, oversubscribed launches); SFX_FWD_TPW=1: one
   int ahead_tp = 4;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=2: two)
   bool sel1 = true;      // one-state action selection by k_sel1 (SFX_SEL1=0: k_gpi + k_publish)
-  // all-task look-ahead placement: after the step's published result (SFX_AHEAD_POST=1), beside the
-  // host's turnaround, instead of as extra groups of the final round's post-update forward
-  bool ahead_post = false;
   int ncu = 256;         // compute units of the device
   bool fuse_l0 = true;   // SFX_FUSE_L0=0: layer 0 of a forward from the states as its own launch
   AdamHP hp_psi{1e-3, 0.0, 0.9, 0.999, 1e-8};
@@ -910,7 +907,7 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
   // them for every head, skipped or not -- later host rounds skip them with the rest of a head.
   // (Forwarding them in round 0 instead, so that an all-skip round 1 leaves its forwards empty,
   // measured 9 % slower: DESIGN.md §8.)
-  const bool ahead = final && !h->ahead_post && p.ax && p.aM > 0 && bx.fuse_v0 && can_fuse_ahead(h, vM, p.aM);
+  const bool ahead = final && p.ax && p.aM > 0 && bx.fuse_v0 && can_fuse_ahead(h, vM, p.aM);
   const int a_noskip = ahead && r <= h->spec_rounds - 1 ? 1 : 0;
   if (ahead) {
     bx.ax = p.ax;
@@ -1051,16 +1048,6 @@ int select_ahead_body(sfx_handle* h, const float* s, const float* ax, const floa
 }
 
 
-// Post-publish look-ahead (SFX_AHEAD_POST=1): the next step's minibatch forwarded with the step's
-// final parameters (the write slot) into the other copy of the minibatch roles, after the final
-// k_ver has published -- the step-start forward's three launches, run while the host turns the
-// action into the next step's inputs.  Host rounds recompute it after their last round.
-int run_ahead_post(sfx_handle* h, const sfx_handle::Pending& p) {
-  const int T = h->T;
-  return run_fwd(h, {{R_NS, P_NEW, 1, 0, T}, {R_NS1T, P_TARGET, 2, 0, T}, {R_NS1, P_NEW, 2, 0, T}}, p.aM, p.ax,
-                 p.ax + (size_t)p.aM * h->n_s);
-}
-
 int launch_step_all(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, const float* lms_phi, const float* lms_r,
                     float lms_alpha, int rounds) {
   const int T = h->T, B = p.B;
@@ -1082,7 +1069,6 @@ int launch_step_all(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, c
   if (!p.pre)
     RC(run_fwd(h, {{R_S, P_ONLINE, 1, 0, T}, {R_S1T, P_TARGET, 2, 0, T}, {R_S1, P_ONLINE, 2, 0, T}}, B, p.S, p.S1, ex));
   for (int r = 0; r < rounds; ++r) RC(launch_round(h, p, r, r == rounds - 1));
-  if (p.ax && p.aM > 0 && h->ahead_post) RC(run_ahead_post(h, p));
   return SFX_OK;
 }
 
@@ -1187,8 +1173,6 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->fwd_tpw = etp && etp[0] == '1' ? 1 : FWD_TPW;
   const char* eat = std::getenv("SFX_AHEAD_TP");
   h->ahead_tp = eat && eat[0] == '2' ? 2 : 4;
-  const char* eap = std::getenv("SFX_AHEAD_POST");
-  h->ahead_post = eap && eap[0] == '1';
   const char* es1 = std::getenv("SFX_SEL1");
   h->sel1 = !(es1 && es1[0] == '0');
   const char* el0 = std::getenv("SFX_FUSE_L0");

@@ -2500,9 +2500,6 @@ struct GateArgs {
   const float* lms_phi;  // in the staging the gate copies from
   const float* lms_r;
   float lms_alpha, pad3_;
-  // host-coherent: the step number of the last gate that ENTERED (post-publish look-ahead: the
-  // host knows from it that the step before has run its tail); null: not written
-  long long* entered;
 };
 
 // Wait for the host's go of this step (bounded); 1 if the step may run, 0 if it is cancelled.
@@ -2518,7 +2515,6 @@ struct GateArgs {
 __device__ __forceinline__ int gate_wait(const GateArgs& g) {
   int ok = 1;
   const long long want = *g.dctr + 1;
-  if (g.entered) __hip_atomic_store(g.entered, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const long long t0 = wall_clock64();
   unsigned it = 0;
   bool held = false;

@@ -472,22 +472,19 @@ def test_round_skip_is_bit_exact(spec_rounds, force, monkeypatch):
     assert s1["policies_checked"] >= n * (spec_rounds - 1) * T // 2 and s1["policies_skipped"] > 0, s1
 
 
-@pytest.mark.parametrize("force,ev,post", [(-1, 7, "0"), (1, 1000, "0"), (2, 1000, "0"), (-1, 7, "1"), (1, 1000, "1"),
-                                           (2, 7, "1")])
-def test_lookahead_is_bit_exact(force, ev, post, monkeypatch):
-    """Look-ahead: step E's final round (SFX_AHEAD_POST=1: its tail, after the
-    published result) forwards step E+1's minibatch into the other copy of the minibatch roles and
-    step E+1 starts at its TD launch.  The forward is the same arithmetic as the step-start
-    forward, so heads, moments and every action must be IDENTICAL to SFX_AHEAD=0 on the same index
-    stream -- through dirty minibatches (a small ring: the newest transition is sampled often),
-    target syncs every 7 updates, and forced host rounds (which skip the heads whose actions
-    repeat; with the post-publish placement they wait for the step's tail and redo its rows)."""
+@pytest.mark.parametrize("force,ev", [(-1, 7), (1, 1000), (2, 1000)])
+def test_lookahead_is_bit_exact(force, ev, monkeypatch):
+    """Look-ahead: step E's final round forwards step E+1's minibatch into the other
+    copy of the minibatch roles and step E+1 starts at its TD launch.  The forward is the same
+    arithmetic as the step-start forward, so heads, moments and every action must be IDENTICAL to
+    SFX_AHEAD=0 on the same index stream -- through dirty minibatches (a small ring: the newest
+    transition is sampled often), target syncs every 7 updates, and forced host rounds (which skip
+    the heads whose actions repeat)."""
     from sfx.runner import NativeEnvLoop
 
     spec = R.Spec(17, 64, 7, 8, ("relu", "relu"))
     T, n = 5, 60
     out = {}
-    monkeypatch.setenv("SFX_AHEAD_POST", post)
     for ahead in ("1", "0"):
         monkeypatch.setenv("SFX_AHEAD", ahead)
         eng, _ = make(spec, T, ev, max_batch=16)
@@ -572,13 +569,10 @@ def test_active_lookahead_is_bit_exact(schedule, upd_use_gpi, ev, monkeypatch):
     assert s1["ahead_own_forward_steps"] > 0, s1
 
 
-@pytest.mark.parametrize("post", ["0", "1"])
-def test_lookahead_runner_matches_oracle_c2(post, monkeypatch):
-    """The C2 shape (T = 8, H = 256, B = 32) with look-ahead on (the bench's configuration; both
-    placements), replayed through the oracle from the runner's recorded inputs."""
+def test_lookahead_runner_matches_oracle_c2():
+    """The C2 shape (T = 8, H = 256, B = 32) with look-ahead on (the bench's configuration),
+    replayed through the oracle from the runner's recorded inputs."""
     from sfx.runner import NativeEnvLoop
-
-    monkeypatch.setenv("SFX_AHEAD_POST", post)
 
     spec = R.Spec(17, 256, 7, 8, ("relu", "relu"))
     T, ev, alpha, n = 8, 1000, 1e-3, 24
