@@ -2,7 +2,7 @@
 ranks, GPI maxima and the selection key all-reduced (MAX).  Against the unsharded oracle
 (agents/sfdqn.py:47-60 over features/deep.py in index order): same env actions, same heads."""
 import os
-import socket
+import tempfile
 
 import pytest
 import torch
@@ -37,8 +37,8 @@ def _heads():
 
 
 def _worker(rank, port, q, rounds):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    # a file rendezvous: no TCP port to race other processes for
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=WORLD)
     from sfx.shard import ShardedAllTask, all_reduce_max_fn
     from tests.shard_oracle import OracleShardBackend
 
@@ -59,11 +59,11 @@ def _worker(rank, port, q, rounds):
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A fresh rendezvous file for the ranks' FileStore (the name kept from the TCP version)."""
+    fd, path = tempfile.mkstemp(prefix="sfx_gloo_")
+    os.close(fd)
+    os.unlink(path)  # the store creates it; a leftover file would carry an old run's keys
+    return path
 
 
 @pytest.mark.parametrize("rounds", [1, 2])
@@ -126,8 +126,8 @@ def _tsf_stream(seed):
 
 
 def _tsf_worker(rank, port, q, use_gpi):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    # a file rendezvous: no TCP port to race other processes for
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=WORLD)
     from sfx.shard import ShardedTSF, all_reduce_max_fn, broadcast_fn
     from tests.shard_oracle import OracleTSFShardBackend
 
