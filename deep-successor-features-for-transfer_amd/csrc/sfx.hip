@@ -964,12 +964,13 @@ int select_pick(sfx_handle* h, int task, int use_gpi, float* q, int64_t* out, co
     const SelPub P = pub ? *pub : SelPub{};
     const dim3 grid(1), block((unsigned)(cdiv(TA, 64) * 64));
     const double by = 4.0 * ((double)TA * h->d + h->d + (q ? TA : 0));
+    const bool st = (long)h->T * h->O <= SEL1_STAGE;  // rows 16-B aligned: actSize, O*rowoff multiples of VW
     if (h->d % 4 == 0)
-      launch(h, K_GPI, by, k_sel1<4>, grid, block, h->G, g, P);
+      launch(h, K_GPI, by, st ? k_sel1<4, true> : k_sel1<4, false>, grid, block, h->G, g, P);
     else if (h->d % 2 == 0)
-      launch(h, K_GPI, by, k_sel1<2>, grid, block, h->G, g, P);
+      launch(h, K_GPI, by, st ? k_sel1<2, true> : k_sel1<2, false>, grid, block, h->G, g, P);
     else
-      launch(h, K_GPI, by, k_sel1<1>, grid, block, h->G, g, P);
+      launch(h, K_GPI, by, st ? k_sel1<1, true> : k_sel1<1, false>, grid, block, h->G, g, P);
     LAUNCHCHK();
     return SFX_OK;
   }

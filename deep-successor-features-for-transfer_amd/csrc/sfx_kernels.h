@@ -2702,14 +2702,16 @@ struct SelPub {
   const int* nonfin;
 };
 constexpr int SEL1_TA = 1024;  // T·A up to which k_sel1 applies
-constexpr int SEL1_DC = 64;    // ψ operands per thread requested at once
+constexpr int SEL1_DC = 64;    // ψ operands per thread requested at once (unstaged path)
+constexpr int SEL1_STAGE = 24576;  // floats of the T selection rows staged in LDS (96 KB)
 
-template <int VW>  // operand width: d % VW == 0 (rows of ψ are then VW-float aligned)
+template <int VW, bool STAGE>  // VW: operand width, d % VW == 0; STAGE: the T rows of ψ fit SEL1_STAGE floats
 __global__ __launch_bounds__(1024) void k_sel1(Geo G, GpiArgs A, SelPub P) {
   PROBE_T(pt0);
   __shared__ float s_q[SEL1_TA];
   __shared__ float s_w[DMAX];
   __shared__ float s_mt[256], s_ma[256];
+  __shared__ __attribute__((aligned(16))) float s_psi[STAGE ? SEL1_STAGE : 4];
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, TA = T * Aa;
   const long long ob = A.row0;
@@ -2718,25 +2720,41 @@ __global__ __launch_bounds__(1024) void k_sel1(Geo G, GpiArgs A, SelPub P) {
   const FDiv fA = fdiv(Aa);
   const bool act = tid < TA;
   const int t = act ? tid / fA : 0, a = act ? tid - t * Aa : 0;
-  const float* p = G.actp(A.role, t, NLm) + (size_t)A.rowoff * O + (size_t)a * d;
   using vec = typename std::conditional<VW == 4, float4, typename std::conditional<VW == 2, float2, float>::type>::type;
   for (int k = tid; k < d; k += nthr) s_w[k] = wr[k];
   float q = 0.f;
-  for (int k0 = 0; k0 < d; k0 += SEL1_DC) {
-    vec v[SEL1_DC / VW];
-#pragma unroll
-    for (int j = 0; j < SEL1_DC / VW; ++j) {
-      const int k = k0 + j * VW;
-      v[j] = act && k < d ? *reinterpret_cast<const vec*>(p + k) : vec{};
+  if constexpr (STAGE) {
+    // the selection row of every head into LDS, VW floats per load, consecutive threads on
+    // consecutive words (a thread-per-dot read of d contiguous floats spreads one wave's load over
+    // 64 rows of d floats: at d = 50 it cost ~12 µs on one workgroup)
+    const int ov = O / VW;
+    const FDiv fo = fdiv(ov);
+    for (int i = tid; i < T * ov; i += nthr) {
+      const int tt = i / fo, j = i - tt * ov;
+      reinterpret_cast<vec*>(s_psi + (size_t)tt * O)[j] =
+          reinterpret_cast<const vec*>(G.actp(A.role, tt, NLm) + (size_t)A.rowoff * O)[j];
     }
-    if (k0 == 0) __syncthreads();  // s_w
+    __syncthreads();
+    const float* p = s_psi + (size_t)t * O + (size_t)a * d;
+    for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);  // the k-order chain of gpi_row
+  } else {
+    const float* p = G.actp(A.role, t, NLm) + (size_t)A.rowoff * O + (size_t)a * d;
+    for (int k0 = 0; k0 < d; k0 += SEL1_DC) {
+      vec v[SEL1_DC / VW];
 #pragma unroll
-    for (int j = 0; j < SEL1_DC / VW; ++j) {
-      const int k = k0 + j * VW;
-      if (k < d) {
-        const float* e = reinterpret_cast<const float*>(&v[j]);
+      for (int j = 0; j < SEL1_DC / VW; ++j) {
+        const int k = k0 + j * VW;
+        v[j] = act && k < d ? *reinterpret_cast<const vec*>(p + k) : vec{};
+      }
+      if (k0 == 0) __syncthreads();  // s_w
 #pragma unroll
-        for (int u = 0; u < VW; ++u) q = __builtin_fmaf(e[u], s_w[k + u], q);
+      for (int j = 0; j < SEL1_DC / VW; ++j) {
+        const int k = k0 + j * VW;
+        if (k < d) {
+          const float* e = reinterpret_cast<const float*>(&v[j]);
+#pragma unroll
+          for (int u = 0; u < VW; ++u) q = __builtin_fmaf(e[u], s_w[k + u], q);
+        }
       }
     }
   }
