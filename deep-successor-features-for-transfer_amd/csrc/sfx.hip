@@ -525,8 +525,16 @@ int run_tdg(sfx_handle* h, int pol0, int npol, int guess, int M, int use_gpi, co
   A.gamma = gamma;
   A.next = next;
   const double nt = use_gpi ? h->T : 1;
-  launch(h, K_TDG, 4.0 * npol * M * (nt * h->O + 2.0 * h->O + 2.0 * h->d + 4), k_tdg, dim3(M, npol), dim3(256),
-         h->G, A);
+  const double by = 4.0 * npol * M * (nt * h->O + 2.0 * h->O + 2.0 * h->d + 4);
+  const bool st = !xmax && nt * h->O <= TDG_STAGE;  // rows VW-aligned: actSize, b·O multiples of VW
+  if (st && h->O % 4 == 0)
+    launch(h, K_TDG, by, k_tdg<4, true>, dim3(M, npol), dim3(256), h->G, A);
+  else if (st && h->O % 2 == 0)
+    launch(h, K_TDG, by, k_tdg<2, true>, dim3(M, npol), dim3(256), h->G, A);
+  else if (st)
+    launch(h, K_TDG, by, k_tdg<1, true>, dim3(M, npol), dim3(256), h->G, A);
+  else
+    launch(h, K_TDG, by, k_tdg<1, false>, dim3(M, npol), dim3(256), h->G, A);
   LAUNCHCHK();
   return SFX_OK;
 }

@@ -1029,6 +1029,13 @@ struct TdgArgs {
   const float* dz_scale;  // learned φ: the output gradient is scaled by the loss coefficient λ (device)
 };
 
+// STAGE (GPI over nt heads with nt·O <= TDG_STAGE floats): the row b of every head's ψ(s1) is
+// first copied into LDS, VW floats per load with consecutive threads on consecutive words, and the
+// dots read it from there -- a thread-per-dot read of d contiguous floats from global memory spreads
+// each wave load over 64 rows of d floats (at Hopper width, 27 actions x 50 features x 16 heads, the
+// per-row TD launch took ~10 µs).  Same k-order FMA chains either way.
+constexpr int TDG_STAGE = 22528;  // floats (88 KB)
+template <int VW, bool STAGE>
 __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   PROBE_T(pt0);
   const int b = blockIdx.x, pol = A.pol0 + blockIdx.y, tid = threadIdx.x;
@@ -1039,6 +1046,7 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   __shared__ float s_m[256];
   __shared__ float s_sq[DMAX];
   __shared__ int s_next;
+  __shared__ __attribute__((aligned(16))) float s_psi[STAGE ? TDG_STAGE : 4];
   const float* wrow = G.w + (long long)pol * G.dpad;
   for (int k = tid; k < d; k += 256) s_w[k] = wrow[k];
   if (A.flag && b == 0 && blockIdx.y == 0 && tid == 0) *A.flag = A.flag_value;
@@ -1059,9 +1067,20 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   } else {
     const int t0 = A.use_gpi ? 0 : pol, nt = A.use_gpi ? T : 1;
     const FDiv fA = fdiv(Aa);
+    if constexpr (STAGE) {
+      using vec = typename std::conditional<VW == 4, float4, typename std::conditional<VW == 2, float2, float>::type>::type;
+      const int ov = O / VW;
+      const FDiv fo = fdiv(ov);
+      for (int i = tid; i < nt * ov; i += 256) {
+        const int tq = i / fo, j = i - tq * ov, t = t0 + tq;
+        reinterpret_cast<vec*>(s_psi + (size_t)tq * O)[j] =
+            reinterpret_cast<const vec*>(G.actp(t < pol ? A.guess : R_S1, t, NLm) + (size_t)b * O)[j];
+      }
+      __syncthreads();
+    }
     for (int idx = tid; idx < nt * Aa; idx += 256) {
       const int tq = idx / fA, t = t0 + tq, a = idx - tq * Aa;
-      const float* p = G.actp(t < pol ? A.guess : R_S1, t, NLm) + (size_t)b * O + a * d;
+      const float* p = STAGE ? s_psi + (size_t)tq * O + a * d : G.actp(t < pol ? A.guess : R_S1, t, NLm) + (size_t)b * O + a * d;
       float q = 0.f;
 #pragma unroll 8
       for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);

@@ -1,5 +1,5 @@
 #!/bin/bash
-# k_sel1 with the selection rows staged in LDS: the selection / runner / TSF GPU tests, the TSF-NF
+# k_sel1 and k_tdg with their rows staged in LDS: the selection / runner / TSF GPU tests, the TSF-NF
 # and active-task rates with k_sel1 and with k_gpi + k_publish, the TSF-NF probe timeline.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/${1:-r4j}
@@ -19,4 +19,4 @@ run nf_sel1 SFX_SEL1=1 --workload hopper-tsf-nf && run nf_gpi SFX_SEL1=0 --workl
   run act_sel1 SFX_SEL1=1 --schedule active && run act_gpi SFX_SEL1=0 --schedule active || exit 1
 P=$PWD/deep-successor-features-for-transfer_amd/sfx/libsfx_probe.so
 SFX_LIB=$P timeout -k 10 150 python tools/probe_run.py 30 tsf-nf > $O/probe_tsfnf.txt 2>&1 || { tail -5 $O/probe_tsfnf.txt; exit 1; }
-grep -E " gpi |fwd_gemv|sum" $O/probe_tsfnf.txt | cut -c1-120
+grep -E " gpi | tdg |fwd_gemv|sum" $O/probe_tsfnf.txt | cut -c1-120
