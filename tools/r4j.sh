@@ -20,3 +20,6 @@ run nf_sel1 SFX_SEL1=1 --workload hopper-tsf-nf && run nf_gpi SFX_SEL1=0 --workl
 P=$PWD/deep-successor-features-for-transfer_amd/sfx/libsfx_probe.so
 SFX_LIB=$P timeout -k 10 150 python tools/probe_run.py 30 tsf-nf > $O/probe_tsfnf.txt 2>&1 || { tail -5 $O/probe_tsfnf.txt; exit 1; }
 grep -E " gpi | tdg |fwd_gemv|sum" $O/probe_tsfnf.txt | cut -c1-120
+# the drop-in's rates under the reference user's Python loop (the agents.buffer alias leg: >= 2,500?)
+timeout -k 10 300 python tools/dropin_loop.py > $O/dropin.json 2> $O/dropin.err || { tail -5 $O/dropin.err; exit 1; }
+cat $O/dropin.json
