@@ -1035,6 +1035,27 @@ struct TdgArgs {
 // each wave load over 64 rows of d floats (at Hopper width, 27 actions x 50 features x 16 heads, the
 // per-row TD launch took ~10 µs).  Same k-order FMA chains either way.
 constexpr int TDG_STAGE = 22528;  // floats (88 KB)
+
+// dst[i] = *src(i) for the n VW-float words i < n, by the nthr threads of the workgroup: U loads
+// per thread in flight before their LDS stores (a load-then-store loop waits once per word).
+// Completes at the caller's next __syncthreads().
+template <int VW, int U, class Src>
+__device__ __forceinline__ void stage_words(float* dst, int n, int nthr, Src src) {
+  using vec = typename std::conditional<VW == 4, float4, typename std::conditional<VW == 2, float2, float>::type>::type;
+  for (int i0 = 0; i0 < n; i0 += U * nthr) {
+    vec v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * nthr + (int)threadIdx.x;
+      v[u] = i < n ? *src(i) : vec{};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * nthr + (int)threadIdx.x;
+      if (i < n) reinterpret_cast<vec*>(dst)[i] = v[u];
+    }
+  }
+}
 template <int VW, bool STAGE>
 __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   PROBE_T(pt0);
@@ -1067,15 +1088,14 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   } else {
     const int t0 = A.use_gpi ? 0 : pol, nt = A.use_gpi ? T : 1;
     const FDiv fA = fdiv(Aa);
-    if constexpr (STAGE) {
+    if constexpr (STAGE) {  // rows of nt heads, O = ov words each, contiguous in s_psi
       using vec = typename std::conditional<VW == 4, float4, typename std::conditional<VW == 2, float2, float>::type>::type;
       const int ov = O / VW;
       const FDiv fo = fdiv(ov);
-      for (int i = tid; i < nt * ov; i += 256) {
+      stage_words<VW, 48 / VW>(s_psi, nt * ov, 256, [&](int i) {
         const int tq = i / fo, j = i - tq * ov, t = t0 + tq;
-        reinterpret_cast<vec*>(s_psi + (size_t)tq * O)[j] =
-            reinterpret_cast<const vec*>(G.actp(t < pol ? A.guess : R_S1, t, NLm) + (size_t)b * O)[j];
-      }
+        return reinterpret_cast<const vec*>(G.actp(t < pol ? A.guess : R_S1, t, NLm) + (size_t)b * O) + j;
+      });
       __syncthreads();
     }
     for (int idx = tid; idx < nt * Aa; idx += 256) {
@@ -2748,11 +2768,10 @@ __global__ __launch_bounds__(1024) void k_sel1(Geo G, GpiArgs A, SelPub P) {
     // 64 rows of d floats: at d = 50 it cost ~12 µs on one workgroup)
     const int ov = O / VW;
     const FDiv fo = fdiv(ov);
-    for (int i = tid; i < T * ov; i += nthr) {
+    stage_words<VW, 48 / VW>(s_psi, T * ov, nthr, [&](int i) {
       const int tt = i / fo, j = i - tt * ov;
-      reinterpret_cast<vec*>(s_psi + (size_t)tt * O)[j] =
-          reinterpret_cast<const vec*>(G.actp(A.role, tt, NLm) + (size_t)A.rowoff * O)[j];
-    }
+      return reinterpret_cast<const vec*>(G.actp(A.role, tt, NLm) + (size_t)A.rowoff * O) + j;
+    });
     __syncthreads();
     const float* p = s_psi + (size_t)t * O + (size_t)a * d;
     for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);  // the k-order chain of gpi_row
