@@ -153,7 +153,8 @@ struct sfx_handle {
   int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
   int fwd_tpw = FWD_TPW; // column tiles per workgroup (layer-0+1 forward, oversubscribed launches); SFX_FWD_TPW=1: one
   int ahead_tp = 4;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=2: two)
-  bool sel1 = true;      // one-state action selection by k_sel1 (SFX_SEL1=0: k_gpi + k_publish)
+  int sel1 = 2;          // one-state action selection: 2 k_sel1m (one workgroup per head), 1 k_sel1, 0 k_gpi + k_publish (SFX_SEL1)
+  SelScratch* selk = nullptr;  // k_sel1m's per-head keys and arrival counter
   int ncu = 256;         // compute units of the device
   bool fuse_l0 = true;   // SFX_FUSE_L0=0: layer 0 of a forward from the states as its own launch
   AdamHP hp_psi{1e-3, 0.0, 0.9, 0.999, 1e-8};
@@ -525,16 +526,8 @@ int run_tdg(sfx_handle* h, int pol0, int npol, int guess, int M, int use_gpi, co
   A.gamma = gamma;
   A.next = next;
   const double nt = use_gpi ? h->T : 1;
-  const double by = 4.0 * npol * M * (nt * h->O + 2.0 * h->O + 2.0 * h->d + 4);
-  const bool st = !xmax && nt * h->O <= TDG_STAGE;  // rows VW-aligned: actSize, b·O multiples of VW
-  if (st && h->O % 4 == 0)
-    launch(h, K_TDG, by, k_tdg<4, true>, dim3(M, npol), dim3(256), h->G, A);
-  else if (st && h->O % 2 == 0)
-    launch(h, K_TDG, by, k_tdg<2, true>, dim3(M, npol), dim3(256), h->G, A);
-  else if (st)
-    launch(h, K_TDG, by, k_tdg<1, true>, dim3(M, npol), dim3(256), h->G, A);
-  else
-    launch(h, K_TDG, by, k_tdg<1, false>, dim3(M, npol), dim3(256), h->G, A);
+  launch(h, K_TDG, 4.0 * npol * M * (nt * h->O + 2.0 * h->O + 2.0 * h->d + 4), k_tdg, dim3(M, npol), dim3(256),
+         h->G, A);
   LAUNCHCHK();
   return SFX_OK;
 }
@@ -857,7 +850,7 @@ void free_all(sfx_handle* h) {
   for (hipEvent_t e : h->prof_pool) (void)hipEventDestroy(e);
   for (void* p : {(void*)h->online, (void*)h->target, (void*)h->am, (void*)h->av, (void*)h->w, (void*)h->wm,
                   (void*)h->wv, (void*)h->step, (void*)h->dcancel, (void*)h->adamc, (void*)h->act, (void*)h->dz, (void*)h->rowloss, (void*)h->spec_next, (void*)h->skip, (void*)h->skipc,
-                  (void*)h->dout, (void*)h->dxpart, (void*)h->dxctr, (void*)h->qh})
+                  (void*)h->dout, (void*)h->dxpart, (void*)h->dxctr, (void*)h->qh, (void*)h->selk})
     if (p) (void)hipFree(p);
   if (h->hout) (void)hipHostFree(h->hout);
   if (h->on16) (void)hipFree(h->on16);
@@ -968,6 +961,19 @@ int select_body(sfx_handle* h, const float* s, int task, int use_gpi, float* q, 
 int select_pick(sfx_handle* h, int task, int use_gpi, float* q, int64_t* out, const SelPub* pub) {
   const GpiArgs g = gpi_args(R_A, 0, 0, h->w + (size_t)task * h->dpad, nullptr, q, nullptr, nullptr, out, task, use_gpi, 1);
   const int TA = h->T * h->A;
+  if (h->sel1 == 2 && h->T <= 64 && h->A <= 256) {  // one workgroup per head, the last one picks
+    const SelPub P = pub ? *pub : SelPub{};
+    const dim3 grid(h->T), block((unsigned)(cdiv(h->A, 64) * 64));
+    const double by = 4.0 * ((double)TA * h->d + h->d + (q ? TA : 0));
+    if (h->d % 4 == 0)
+      launch(h, K_GPI, by, k_sel1m<4>, grid, block, h->G, g, P, h->selk);
+    else if (h->d % 2 == 0)
+      launch(h, K_GPI, by, k_sel1m<2>, grid, block, h->G, g, P, h->selk);
+    else
+      launch(h, K_GPI, by, k_sel1m<1>, grid, block, h->G, g, P, h->selk);
+    LAUNCHCHK();
+    return SFX_OK;
+  }
   if (h->sel1 && TA <= SEL1_TA && h->A <= 256 && h->T <= 256) {
     const SelPub P = pub ? *pub : SelPub{};
     const dim3 grid(1), block((unsigned)(cdiv(TA, 64) * 64));
@@ -1183,7 +1189,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   const char* eat = std::getenv("SFX_AHEAD_TP");
   h->ahead_tp = eat && eat[0] == '2' ? 2 : 4;
   const char* es1 = std::getenv("SFX_SEL1");
-  h->sel1 = !(es1 && es1[0] == '0');
+  h->sel1 = es1 && (es1[0] == '0' || es1[0] == '1') ? es1[0] - '0' : 2;
   const char* el0 = std::getenv("SFX_FUSE_L0");
   h->fuse_l0 = !(el0 && el0[0] == '0');
   const char* esd = std::getenv("SFX_SPLIT_DX");
@@ -1268,6 +1274,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   alloc((void**)&h->skip, sizeof(int) * (size_t)T);
   alloc((void**)&h->skipc, 64);
   alloc((void**)&h->dout, sizeof(StepOut));
+  alloc((void**)&h->selk, sizeof(SelScratch));
   if (rc == SFX_OK && hipHostMalloc((void**)&h->hout, sizeof(StepOut), hipHostMallocDefault) != hipSuccess) {
     g_err = "hipHostMalloc failed";
     rc = SFX_E_HIP;

@@ -1029,13 +1029,6 @@ struct TdgArgs {
   const float* dz_scale;  // learned φ: the output gradient is scaled by the loss coefficient λ (device)
 };
 
-// STAGE (GPI over nt heads with nt·O <= TDG_STAGE floats): the row b of every head's ψ(s1) is
-// first copied into LDS, VW floats per load with consecutive threads on consecutive words, and the
-// dots read it from there -- a thread-per-dot read of d contiguous floats from global memory spreads
-// each wave load over 64 rows of d floats (at Hopper width, 27 actions x 50 features x 16 heads, the
-// per-row TD launch took ~10 µs).  Same k-order FMA chains either way.
-constexpr int TDG_STAGE = 22528;  // floats (88 KB)
-
 // dst[i] = *src(i) for the n VW-float words i < n, by the nthr threads of the workgroup: U loads
 // per thread in flight before their LDS stores (a load-then-store loop waits once per word).
 // Completes at the caller's next __syncthreads().
@@ -1056,7 +1049,6 @@ __device__ __forceinline__ void stage_words(float* dst, int n, int nthr, Src src
     }
   }
 }
-template <int VW, bool STAGE>
 __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   PROBE_T(pt0);
   const int b = blockIdx.x, pol = A.pol0 + blockIdx.y, tid = threadIdx.x;
@@ -1067,7 +1059,6 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   __shared__ float s_m[256];
   __shared__ float s_sq[DMAX];
   __shared__ int s_next;
-  __shared__ __attribute__((aligned(16))) float s_psi[STAGE ? TDG_STAGE : 4];
   const float* wrow = G.w + (long long)pol * G.dpad;
   for (int k = tid; k < d; k += 256) s_w[k] = wrow[k];
   if (A.flag && b == 0 && blockIdx.y == 0 && tid == 0) *A.flag = A.flag_value;
@@ -1088,19 +1079,9 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   } else {
     const int t0 = A.use_gpi ? 0 : pol, nt = A.use_gpi ? T : 1;
     const FDiv fA = fdiv(Aa);
-    if constexpr (STAGE) {  // rows of nt heads, O = ov words each, contiguous in s_psi
-      using vec = typename std::conditional<VW == 4, float4, typename std::conditional<VW == 2, float2, float>::type>::type;
-      const int ov = O / VW;
-      const FDiv fo = fdiv(ov);
-      stage_words<VW, 48 / VW>(s_psi, nt * ov, 256, [&](int i) {
-        const int tq = i / fo, j = i - tq * ov, t = t0 + tq;
-        return reinterpret_cast<const vec*>(G.actp(t < pol ? A.guess : R_S1, t, NLm) + (size_t)b * O) + j;
-      });
-      __syncthreads();
-    }
     for (int idx = tid; idx < nt * Aa; idx += 256) {
       const int tq = idx / fA, t = t0 + tq, a = idx - tq * Aa;
-      const float* p = STAGE ? s_psi + (size_t)tq * O + a * d : G.actp(t < pol ? A.guess : R_S1, t, NLm) + (size_t)b * O + a * d;
+      const float* p = G.actp(t < pol ? A.guess : R_S1, t, NLm) + (size_t)b * O + a * d;
       float q = 0.f;
 #pragma unroll 8
       for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
@@ -2743,6 +2724,96 @@ struct SelPub {
 constexpr int SEL1_TA = 1024;  // T·A up to which k_sel1 applies
 constexpr int SEL1_DC = 64;    // ψ operands per thread requested at once (unstaged path)
 constexpr int SEL1_STAGE = 24576;  // floats of the T selection rows staged in LDS (96 KB)
+
+// K4m  The same selection over T workgroups, one head each (a row of A dots of d: a few KB per
+// workgroup instead of the T·A·d floats one workgroup reads at a memory latency per ~8 KB in
+// flight), the heads combined by the last workgroup to arrive (k_ver's hand-off: each workgroup's
+// lane 0 stores its head's (max_a q key, argmax_a) write-through, waits for the store, then adds to
+// the arrival counter; the add's return tells the last one, which reads the keys write-through,
+// picks, publishes and re-arms the counter).  Per head: q in gpi_row's k order; the head maximum as
+// gpi_pick's head maxima; the task as its first-index argmax over heads (argmax_key(max_a q_t, t));
+// the action as the first-index argmax over a of q[c][a].  Launch: grid T, 64·⌈A/64⌉ threads; only
+// for selections (no task_out / next_out).
+struct SelScratch {
+  unsigned long long key[64];  // per head: argmax_key(max_a q_t, t)
+  int act[64];                 // per head: first argmax_a q_t[a]
+  unsigned done;               // arrivals (re-armed to 0 by the last)
+};
+
+template <int VW>  // d % VW == 0
+__global__ __launch_bounds__(256) void k_sel1m(Geo G, GpiArgs A, SelPub P, SelScratch* S) {
+  PROBE_T(pt0);
+  __shared__ float s_w[DMAX];
+  __shared__ float s_q[256];
+  const int t = blockIdx.x, tid = threadIdx.x;
+  const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff;
+  const long long ob = A.row0;
+  const float* wr = A.w + ob * A.w_stride;
+  int64_t* so = A.sel_out ? A.sel_out + ob * A.sel_stride : nullptr;
+  const bool act = tid < Aa;
+  const float* p = G.actp(A.role, t, NLm) + (size_t)A.rowoff * O + (size_t)(act ? tid : 0) * d;
+  using vec = typename std::conditional<VW == 4, float4, typename std::conditional<VW == 2, float2, float>::type>::type;
+  for (int k = tid; k < d; k += blockDim.x) s_w[k] = wr[k];
+  float q = 0.f;
+  for (int k0 = 0; k0 < d; k0 += SEL1_DC) {
+    vec v[SEL1_DC / VW];
+#pragma unroll
+    for (int j = 0; j < SEL1_DC / VW; ++j) {
+      const int k = k0 + j * VW;
+      v[j] = act && k < d ? *reinterpret_cast<const vec*>(p + k) : vec{};
+    }
+    if (k0 == 0) __syncthreads();  // s_w
+#pragma unroll
+    for (int j = 0; j < SEL1_DC / VW; ++j) {
+      const int k = k0 + j * VW;
+      if (k < d) {
+        const float* e = reinterpret_cast<const float*>(&v[j]);
+#pragma unroll
+        for (int u = 0; u < VW; ++u) q = __builtin_fmaf(e[u], s_w[k + u], q);
+      }
+    }
+  }
+  if (act) {
+    s_q[tid] = q;
+    if (A.q_out) A.q_out[(ob * T + t) * Aa + tid] = q;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    // head maximum as gpi_pick forms it (sequential fmaxf over a), first-index argmax over a
+    float mx = s_q[0];
+    for (int a = 1; a < Aa; ++a) mx = fmaxf(mx, s_q[a]);
+    unsigned long long ka = 0ull;
+    for (int a = tid; a < Aa; a += 64) {
+      const unsigned long long k = argmax_key(s_q[a], a);
+      ka = k > ka ? k : ka;
+    }
+    const int am = argmax_idx(wave_max(ka));
+    if (tid == 0) {
+      __hip_atomic_store(S->key + t, argmax_key(mx, t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(S->act + t, am, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_waitcnt(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned prev = __hip_atomic_fetch_add(&S->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("" ::: "memory");
+      if (prev == (unsigned)T - 1) {
+        unsigned long long best = 0ull;
+        for (int u = 0; u < T; ++u) {
+          const unsigned long long k = __hip_atomic_load(S->key + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          best = k > best ? k : best;
+        }
+        const int c = A.use_gpi ? argmax_idx(best) : A.select_task;
+        const int a = __hip_atomic_load(S->act + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (so) {
+          __hip_atomic_store(so, (int64_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(so + 1, (int64_t)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (P.res) publish_result(so, P.flag, P.res, P.dctr, P.cancel, P.nonfin);
+        }
+        __hip_atomic_store(&S->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  PROBE_REC(16, pt0);
+}
 
 template <int VW, bool STAGE>  // VW: operand width, d % VW == 0; STAGE: the T rows of ψ fit SEL1_STAGE floats
 __global__ __launch_bounds__(1024) void k_sel1(Geo G, GpiArgs A, SelPub P) {
