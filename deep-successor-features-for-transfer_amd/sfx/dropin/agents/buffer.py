@@ -69,17 +69,13 @@ class ReplayBuffer:
             self._alloc(state, reward, next_state)
         rs, ra, rr, rs1 = self._ring
         j = self.index
-        rows, srcs = (rs[j], rr[j], rs1[j]), (state, reward, next_state)
-        if all(torch.is_tensor(x) and x.device == self.device and x.dtype == torch.float32 for x in srcs):
-            # the three float rows in one multi-tensor copy (one launch instead of three)
-            torch._foreach_copy_(list(rows), [x.reshape(r.shape) for x, r in zip(srcs, rows)], non_blocking=True)
-        else:
-            for r, x in zip(rows, srcs):
-                self._put(r, x)
+        self._put(rs[j], state)
         if torch.is_tensor(action):
             ra[j].copy_(action.reshape(()), non_blocking=True)
         else:
             ra[j] = int(action)
+        self._put(rr[j], reward)
+        self._put(rs1[j], next_state)
         if torch.is_tensor(gamma):
             if self._gdev is None:
                 self._gdev = torch.as_tensor(self._gam, device=self.device).clone()
