@@ -153,7 +153,7 @@ struct sfx_handle {
   int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
   int fwd_tpw = FWD_TPW; // column tiles per workgroup (layer-0+1 forward, oversubscribed launches); SFX_FWD_TPW=1: one
   int ahead_tp = 4;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=2: two)
-  int sel1 = 2;          // one-state action selection: 2 k_sel1m (one workgroup per head), 1 k_sel1, 0 k_gpi + k_publish (SFX_SEL1)
+  bool sel1 = true;      // one-state action selection by k_sel1m (SFX_SEL1=0: k_gpi + k_publish)
   SelScratch* selk = nullptr;  // k_sel1m's per-head keys and arrival counter
   int ncu = 256;         // compute units of the device
   bool fuse_l0 = true;   // SFX_FUSE_L0=0: layer 0 of a forward from the states as its own launch
@@ -948,7 +948,7 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
 // LMS + action selection when there is no minibatch yet).
 // SFDQN.get_Q_values + action choice for one state (sfdqn.py:577-596; agents/sfdqn.py:39-45):
 // forward of every head on s, GPI with w of `task`, selection into out[2] = (c, a).
-// With `pub` (runner steps) the step's result is published after the selection: inside k_sel1, or
+// With `pub` (runner steps) the step's result is published after the selection: inside k_sel1m, or
 // by k_publish after k_gpi.
 int select_pick(sfx_handle* h, int task, int use_gpi, float* q, int64_t* out, const SelPub* pub);
 int select_body(sfx_handle* h, const float* s, int task, int use_gpi, float* q, int64_t* out,
@@ -961,7 +961,7 @@ int select_body(sfx_handle* h, const float* s, int task, int use_gpi, float* q, 
 int select_pick(sfx_handle* h, int task, int use_gpi, float* q, int64_t* out, const SelPub* pub) {
   const GpiArgs g = gpi_args(R_A, 0, 0, h->w + (size_t)task * h->dpad, nullptr, q, nullptr, nullptr, out, task, use_gpi, 1);
   const int TA = h->T * h->A;
-  if (h->sel1 == 2 && h->T <= 64 && h->A <= 256) {  // one workgroup per head, the last one picks
+  if (h->sel1 && h->T <= 64 && h->A <= 256) {  // one workgroup per head, the last one picks
     const SelPub P = pub ? *pub : SelPub{};
     const dim3 grid(h->T), block((unsigned)(cdiv(h->A, 64) * 64));
     const double by = 4.0 * ((double)TA * h->d + h->d + (q ? TA : 0));
@@ -971,20 +971,6 @@ int select_pick(sfx_handle* h, int task, int use_gpi, float* q, int64_t* out, co
       launch(h, K_GPI, by, k_sel1m<2>, grid, block, h->G, g, P, h->selk);
     else
       launch(h, K_GPI, by, k_sel1m<1>, grid, block, h->G, g, P, h->selk);
-    LAUNCHCHK();
-    return SFX_OK;
-  }
-  if (h->sel1 && TA <= SEL1_TA && h->A <= 256 && h->T <= 256) {
-    const SelPub P = pub ? *pub : SelPub{};
-    const dim3 grid(1), block((unsigned)(cdiv(TA, 64) * 64));
-    const double by = 4.0 * ((double)TA * h->d + h->d + (q ? TA : 0));
-    const bool st = (long)h->T * h->O <= SEL1_STAGE;  // rows 16-B aligned: actSize, O*rowoff multiples of VW
-    if (h->d % 4 == 0)
-      launch(h, K_GPI, by, st ? k_sel1<4, true> : k_sel1<4, false>, grid, block, h->G, g, P);
-    else if (h->d % 2 == 0)
-      launch(h, K_GPI, by, st ? k_sel1<2, true> : k_sel1<2, false>, grid, block, h->G, g, P);
-    else
-      launch(h, K_GPI, by, st ? k_sel1<1, true> : k_sel1<1, false>, grid, block, h->G, g, P);
     LAUNCHCHK();
     return SFX_OK;
   }
@@ -1189,7 +1175,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   const char* eat = std::getenv("SFX_AHEAD_TP");
   h->ahead_tp = eat && eat[0] == '2' ? 2 : 4;
   const char* es1 = std::getenv("SFX_SEL1");
-  h->sel1 = es1 && (es1[0] == '0' || es1[0] == '1') ? es1[0] - '0' : 2;
+  h->sel1 = !(es1 && es1[0] == '0');
   const char* el0 = std::getenv("SFX_FUSE_L0");
   h->fuse_l0 = !(el0 && el0[0] == '0');
   const char* esd = std::getenv("SFX_SPLIT_DX");

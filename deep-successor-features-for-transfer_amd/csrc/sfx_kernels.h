@@ -1029,26 +1029,6 @@ struct TdgArgs {
   const float* dz_scale;  // learned φ: the output gradient is scaled by the loss coefficient λ (device)
 };
 
-// dst[i] = *src(i) for the n VW-float words i < n, by the nthr threads of the workgroup: U loads
-// per thread in flight before their LDS stores (a load-then-store loop waits once per word).
-// Completes at the caller's next __syncthreads().
-template <int VW, int U, class Src>
-__device__ __forceinline__ void stage_words(float* dst, int n, int nthr, Src src) {
-  using vec = typename std::conditional<VW == 4, float4, typename std::conditional<VW == 2, float2, float>::type>::type;
-  for (int i0 = 0; i0 < n; i0 += U * nthr) {
-    vec v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = i0 + u * nthr + (int)threadIdx.x;
-      v[u] = i < n ? *src(i) : vec{};
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = i0 + u * nthr + (int)threadIdx.x;
-      if (i < n) reinterpret_cast<vec*>(dst)[i] = v[u];
-    }
-  }
-}
 __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   PROBE_T(pt0);
   const int b = blockIdx.x, pol = A.pol0 + blockIdx.y, tid = threadIdx.x;
@@ -2706,13 +2686,17 @@ __global__ void k_publish(const int64_t* sel, const int* flag, HostResult* out, 
 }
 
 // -------------------------------------------------------------------------------------
-// K4s  The action for one state (select_body: SFDQN.get_Q_values + the choice, sfdqn.py:577-596,
-// tsfdqn.py's test/act path): gpi_row's arithmetic for M = 1 on ONE workgroup of up to 1024
-// threads, one (head, action) dot per thread with all of its d operands requested before the first
-// FMA (gpi_row's general path reads them 8 at a time: at d = 50 and T·A = 432, two dots per thread,
-// that is 14 dependent memory round trips).  Same k-order FMA chain, so q is bit-identical, and the
-// same argmaxes (gpi_pick).  The runner's publication (k_publish) is folded in: thread 0 publishes
-// right after its selection stores.
+// K4m  The action for one state (select_body: SFDQN.get_Q_values + the choice, sfdqn.py:577-596)
+// over T workgroups, one head each: a row of A dots of d (a few KB per workgroup -- one workgroup
+// reading all T·A·d floats, at a memory latency per ~8 KB in flight, took 10-12 µs at Hopper width,
+// k_gpi 8-9 µs), the heads combined by the last workgroup to arrive (k_ver's hand-off: each
+// workgroup's lane 0 stores its head's (max_a q key, argmax_a) write-through, waits for the store,
+// then adds to the arrival counter; the add's return tells the last one, which reads the keys
+// write-through, picks, publishes and re-arms the counter).  Per head: q in gpi_row's k order
+// (bit-identical); the head maximum as gpi_pick forms it; the task as its first-index argmax over
+// heads (argmax_key(max_a q_t, t)); the action as the first-index argmax over a of q[c][a].  The
+// runner's publication (k_publish) is folded into the last workgroup.  Launch: grid T, 64·⌈A/64⌉
+// threads; selections only (no task_out / next_out).
 // -------------------------------------------------------------------------------------
 struct SelPub {
   HostResult* res;  // null: no publication
@@ -2721,19 +2705,8 @@ struct SelPub {
   const int* cancel;
   const int* nonfin;
 };
-constexpr int SEL1_TA = 1024;  // T·A up to which k_sel1 applies
-constexpr int SEL1_DC = 64;    // ψ operands per thread requested at once (unstaged path)
-constexpr int SEL1_STAGE = 24576;  // floats of the T selection rows staged in LDS (96 KB)
+constexpr int SEL1_DC = 64;  // ψ operands per thread requested at once
 
-// K4m  The same selection over T workgroups, one head each (a row of A dots of d: a few KB per
-// workgroup instead of the T·A·d floats one workgroup reads at a memory latency per ~8 KB in
-// flight), the heads combined by the last workgroup to arrive (k_ver's hand-off: each workgroup's
-// lane 0 stores its head's (max_a q key, argmax_a) write-through, waits for the store, then adds to
-// the arrival counter; the add's return tells the last one, which reads the keys write-through,
-// picks, publishes and re-arms the counter).  Per head: q in gpi_row's k order; the head maximum as
-// gpi_pick's head maxima; the task as its first-index argmax over heads (argmax_key(max_a q_t, t));
-// the action as the first-index argmax over a of q[c][a].  Launch: grid T, 64·⌈A/64⌉ threads; only
-// for selections (no task_out / next_out).
 struct SelScratch {
   unsigned long long key[64];  // per head: argmax_key(max_a q_t, t)
   int act[64];                 // per head: first argmax_a q_t[a]
@@ -2812,68 +2785,6 @@ __global__ __launch_bounds__(256) void k_sel1m(Geo G, GpiArgs A, SelPub P, SelSc
       }
     }
   }
-  PROBE_REC(16, pt0);
-}
-
-template <int VW, bool STAGE>  // VW: operand width, d % VW == 0; STAGE: the T rows of ψ fit SEL1_STAGE floats
-__global__ __launch_bounds__(1024) void k_sel1(Geo G, GpiArgs A, SelPub P) {
-  PROBE_T(pt0);
-  __shared__ float s_q[SEL1_TA];
-  __shared__ float s_w[DMAX];
-  __shared__ float s_mt[256], s_ma[256];
-  __shared__ __attribute__((aligned(16))) float s_psi[STAGE ? SEL1_STAGE : 4];
-  const int tid = threadIdx.x, nthr = blockDim.x;
-  const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, TA = T * Aa;
-  const long long ob = A.row0;
-  const float* wr = A.w + ob * A.w_stride;
-  int64_t* so = A.sel_out ? A.sel_out + ob * A.sel_stride : nullptr;
-  const FDiv fA = fdiv(Aa);
-  const bool act = tid < TA;
-  const int t = act ? tid / fA : 0, a = act ? tid - t * Aa : 0;
-  using vec = typename std::conditional<VW == 4, float4, typename std::conditional<VW == 2, float2, float>::type>::type;
-  for (int k = tid; k < d; k += nthr) s_w[k] = wr[k];
-  float q = 0.f;
-  if constexpr (STAGE) {
-    // the selection row of every head into LDS, VW floats per load, consecutive threads on
-    // consecutive words (a thread-per-dot read of d contiguous floats spreads one wave's load over
-    // 64 rows of d floats: at d = 50 it cost ~12 µs on one workgroup)
-    const int ov = O / VW;
-    const FDiv fo = fdiv(ov);
-    stage_words<VW, 48 / VW>(s_psi, T * ov, nthr, [&](int i) {
-      const int tt = i / fo, j = i - tt * ov;
-      return reinterpret_cast<const vec*>(G.actp(A.role, tt, NLm) + (size_t)A.rowoff * O) + j;
-    });
-    __syncthreads();
-    const float* p = s_psi + (size_t)t * O + (size_t)a * d;
-    for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);  // the k-order chain of gpi_row
-  } else {
-    const float* p = G.actp(A.role, t, NLm) + (size_t)A.rowoff * O + (size_t)a * d;
-    for (int k0 = 0; k0 < d; k0 += SEL1_DC) {
-      vec v[SEL1_DC / VW];
-#pragma unroll
-      for (int j = 0; j < SEL1_DC / VW; ++j) {
-        const int k = k0 + j * VW;
-        v[j] = act && k < d ? *reinterpret_cast<const vec*>(p + k) : vec{};
-      }
-      if (k0 == 0) __syncthreads();  // s_w
-#pragma unroll
-      for (int j = 0; j < SEL1_DC / VW; ++j) {
-        const int k = k0 + j * VW;
-        if (k < d) {
-          const float* e = reinterpret_cast<const float*>(&v[j]);
-#pragma unroll
-          for (int u = 0; u < VW; ++u) q = __builtin_fmaf(e[u], s_w[k + u], q);
-        }
-      }
-    }
-  }
-  if (act) {
-    s_q[tid] = q;
-    if (A.q_out) A.q_out[(ob * T + t) * Aa + a] = q;
-  }
-  __syncthreads();
-  gpi_pick(A, s_q, s_mt, s_ma, T, Aa, ob, so, nthr);
-  if (tid == 0 && P.res) publish_result(so, P.flag, P.res, P.dctr, P.cancel, P.nonfin);
   PROBE_REC(16, pt0);
 }
 
