@@ -154,9 +154,6 @@ struct sfx_handle {
   int fwd_tpw = FWD_TPW; // column tiles per workgroup (layer-0+1 forward, oversubscribed launches); SFX_FWD_TPW=1: one
   int ahead_tp = 4;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=2: two)
   bool sel1 = true;      // one-state action selection by k_sel1m (SFX_SEL1=0: k_gpi + k_publish)
-  bool tdg_split = true;  // k_tdg of wide rows over (row, policy, head) workgroups (SFX_TDG_SPLIT=0: one per row)
-  float* tdq = nullptr;       // its q hand-off [T][Mmax][T][A]
-  unsigned* tdq_ctr = nullptr;  // its arrival counters [T][Mmax]
   SelScratch* selk = nullptr;  // k_sel1m's per-head keys and arrival counter
   int ncu = 256;         // compute units of the device
   bool fuse_l0 = true;   // SFX_FUSE_L0=0: layer 0 of a forward from the states as its own launch
@@ -529,14 +526,8 @@ int run_tdg(sfx_handle* h, int pol0, int npol, int guess, int M, int use_gpi, co
   A.gamma = gamma;
   A.next = next;
   const double nt = use_gpi ? h->T : 1;
-  // wide rows: split the GPI over (row, policy, head) workgroups (TdgArgs::qs)
-  const bool split = h->tdg_split && !xmax && nt * h->O > 4096 && M <= h->Mmax && pol0 + npol <= h->T;
-  if (split) {
-    A.qs = h->tdq;
-    A.ctr = h->tdq_ctr;
-  }
-  launch(h, K_TDG, 4.0 * npol * M * (nt * h->O + 2.0 * h->O + 2.0 * h->d + 4), k_tdg,
-         dim3(M, npol * (split ? (int)nt : 1)), dim3(256), h->G, A);
+  launch(h, K_TDG, 4.0 * npol * M * (nt * h->O + 2.0 * h->O + 2.0 * h->d + 4), k_tdg, dim3(M, npol), dim3(256),
+         h->G, A);
   LAUNCHCHK();
   return SFX_OK;
 }
@@ -859,7 +850,7 @@ void free_all(sfx_handle* h) {
   for (hipEvent_t e : h->prof_pool) (void)hipEventDestroy(e);
   for (void* p : {(void*)h->online, (void*)h->target, (void*)h->am, (void*)h->av, (void*)h->w, (void*)h->wm,
                   (void*)h->wv, (void*)h->step, (void*)h->dcancel, (void*)h->adamc, (void*)h->act, (void*)h->dz, (void*)h->rowloss, (void*)h->spec_next, (void*)h->skip, (void*)h->skipc,
-                  (void*)h->dout, (void*)h->dxpart, (void*)h->dxctr, (void*)h->qh, (void*)h->selk, (void*)h->tdq, (void*)h->tdq_ctr})
+                  (void*)h->dout, (void*)h->dxpart, (void*)h->dxctr, (void*)h->qh, (void*)h->selk})
     if (p) (void)hipFree(p);
   if (h->hout) (void)hipHostFree(h->hout);
   if (h->on16) (void)hipFree(h->on16);
@@ -1185,8 +1176,6 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->ahead_tp = eat && eat[0] == '2' ? 2 : 4;
   const char* es1 = std::getenv("SFX_SEL1");
   h->sel1 = !(es1 && es1[0] == '0');
-  const char* ets = std::getenv("SFX_TDG_SPLIT");
-  h->tdg_split = !(ets && ets[0] == '0');
   const char* el0 = std::getenv("SFX_FUSE_L0");
   h->fuse_l0 = !(el0 && el0[0] == '0');
   const char* esd = std::getenv("SFX_SPLIT_DX");
@@ -1272,8 +1261,6 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   alloc((void**)&h->skipc, 64);
   alloc((void**)&h->dout, sizeof(StepOut));
   alloc((void**)&h->selk, sizeof(SelScratch));
-  alloc((void**)&h->tdq, sizeof(float) * (size_t)T * max_batch * T * A);
-  alloc((void**)&h->tdq_ctr, sizeof(unsigned) * (size_t)T * max_batch);
   if (rc == SFX_OK && hipHostMalloc((void**)&h->hout, sizeof(StepOut), hipHostMallocDefault) != hipSuccess) {
     g_err = "hipHostMalloc failed";
     rc = SFX_E_HIP;

@@ -1027,21 +1027,12 @@ struct TdgArgs {
   const int* xmax;
   int poloff, pad2_;
   const float* dz_scale;  // learned φ: the output gradient is scaled by the loss coefficient λ (device)
-  // split GPI (wide rows, no xmax): grid (M, npol·nt), workgroup (b, policy, head) forms that head's
-  // A dots of row b and hands them write-through to qs[policy][b][head][a]; the last of a row's nt
-  // workgroups to arrive on ctr[policy][b] (k_ver's hand-off) reads them back and finishes the row.
-  // One workgroup reading all nt·A·d floats of a row is bound by its own memory parallelism (at
-  // Hopper width ~10 µs); null: one workgroup per row.
-  float* qs;
-  unsigned* ctr;
 };
 
 __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   PROBE_T(pt0);
+  const int b = blockIdx.x, pol = A.pol0 + blockIdx.y, tid = threadIdx.x;
   const int T = G.T, Aa = G.A, d = G.d, O = G.O, M = A.M, NLm = G.lastOff;
-  const int ntq = A.use_gpi ? T : 1;                               // heads in a policy's GPI
-  const int pl = A.qs ? (int)blockIdx.y / ntq : (int)blockIdx.y;  // policy (local), split: its head
-  const int b = blockIdx.x, pol = A.pol0 + pl, tid = threadIdx.x;
   __shared__ float s_w[DMAX];
   __shared__ float s_q[QMAX];
   __shared__ float s_t[OMAX];  // ψ⁻_i(s1_b) row
@@ -1051,7 +1042,6 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   const float* wrow = G.w + (long long)pol * G.dpad;
   for (int k = tid; k < d; k += 256) s_w[k] = wrow[k];
   if (A.flag && b == 0 && blockIdx.y == 0 && tid == 0) *A.flag = A.flag_value;
-  __shared__ int s_last;
   const float* trow = G.actp(R_S1T, pol, NLm) + (size_t)b * O;
   for (int o = tid; o < O; o += 256) s_t[o] = trow[o];
   const int ab = (int)A.a[b];
@@ -1066,33 +1056,6 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
   if (A.xmax) {
     const int* xr = A.xmax + ((size_t)(A.poloff + pol) * M + b) * Aa;
     for (int a = tid; a < Aa; a += 256) s_m[a] = unsortable(xr[a]);
-  } else if (A.qs) {
-    const int t0 = A.use_gpi ? 0 : pol, tq = (int)blockIdx.y - pl * ntq, t = t0 + tq;
-    float* qrow = A.qs + ((size_t)pl * M + b) * ntq * Aa;
-    for (int a = tid; a < Aa; a += 256) {  // this head's dots, k order as below
-      const float* p = G.actp(t < pol ? A.guess : R_S1, t, NLm) + (size_t)b * O + a * d;
-      float q = 0.f;
-#pragma unroll 8
-      for (int k = 0; k < d; ++k) q = __builtin_fmaf(p[k], s_w[k], q);
-      __hip_atomic_store(qrow + tq * Aa + a, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned prev = __hip_atomic_fetch_add(A.ctr + (size_t)pl * M + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = prev == (unsigned)ntq - 1;
-      if (s_last) __hip_atomic_store(A.ctr + (size_t)pl * M + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (!s_last) return;  // block-uniform
-    for (int idx = tid; idx < ntq * Aa; idx += 256)
-      s_q[idx] = __hip_atomic_load(qrow + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    for (int a = tid; a < Aa; a += 256) {  // max over heads for each action, as below
-      float mx = s_q[a];
-      for (int u = 1; u < ntq; ++u) mx = fmaxf(mx, s_q[u * Aa + a]);
-      s_m[a] = mx;
-    }
   } else {
     const int t0 = A.use_gpi ? 0 : pol, nt = A.use_gpi ? T : 1;
     const FDiv fA = fdiv(Aa);
@@ -1122,7 +1085,7 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
       }
     s_next = am;
     SFX_CHK(b < A.next_stride || !A.next, b, A.next_stride, 0);
-    if (A.next) A.next[(size_t)pl * A.next_stride + b] = am;
+    if (A.next) A.next[(size_t)blockIdx.y * A.next_stride + b] = am;
   }
   __syncthreads();
   const float norm = td_norm(G, M, O, A.dz_scale);

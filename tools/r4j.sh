@@ -1,5 +1,5 @@
 #!/bin/bash
-# the wide TD over (row, head) workgroups (k_tdg split): engine / runner / TSF GPU tests, the TSF-NF
+# the one-state selection over one workgroup per head (k_sel1m): selection / runner / TSF GPU tests, the TSF-NF
 # and active-task rates with k_sel1 and with k_gpi + k_publish, the TSF-NF probe timeline.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/${1:-r4j}
@@ -14,9 +14,10 @@ run() {  # tag, env VAR=value..., then bench flags
     --repeats 2 "$@" > $O/bench_$tag.json 2>/dev/null || return 1
   python -c "import json,sys;d=json.loads(open(sys.argv[1]).read().splitlines()[-1]);print(sys.argv[2], d['value'], d['repeats']['values'])" $O/bench_$tag.json $tag
 }
-run nf_split SFX_TDG_SPLIT=1 --workload hopper-tsf-nf && run nf_row SFX_TDG_SPLIT=0 --workload hopper-tsf-nf && \
-  run tsf_split SFX_TDG_SPLIT=1 --workload hopper-tsf && run tsf_row SFX_TDG_SPLIT=0 --workload hopper-tsf && \
-  run nf_split2 SFX_TDG_SPLIT=1 --workload hopper-tsf-nf && run nf_row2 SFX_TDG_SPLIT=0 --workload hopper-tsf-nf || exit 1
+run nf_m SFX_SEL1=2 --workload hopper-tsf-nf && run nf_one SFX_SEL1=1 --workload hopper-tsf-nf && \
+  run nf_gpi SFX_SEL1=0 --workload hopper-tsf-nf && run tsf_m SFX_SEL1=2 --workload hopper-tsf && \
+  run tsf_gpi SFX_SEL1=0 --workload hopper-tsf && run act_m SFX_SEL1=2 --schedule active && \
+  run act_gpi SFX_SEL1=0 --schedule active && run nf_m2 SFX_SEL1=2 --workload hopper-tsf-nf || exit 1
 P=$PWD/deep-successor-features-for-transfer_amd/sfx/libsfx_probe.so
 SFX_LIB=$P timeout -k 10 150 python tools/probe_run.py 30 tsf-nf > $O/probe_tsfnf.txt 2>&1 || { tail -5 $O/probe_tsfnf.txt; exit 1; }
 grep -E " gpi | tdg |fwd_gemv|sum" $O/probe_tsfnf.txt | cut -c1-120
