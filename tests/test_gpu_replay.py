@@ -49,6 +49,26 @@ def test_device_replay_all_task(capacity):
     eng.close()
 
 
+def test_device_replay_at_the_bench_batch():
+    """B = 32 at the C2 state width (the bench's device-replay leg): the staging's look-ahead block
+    (2 B n_s floats, host replay only) must not count against the device-replay gate's tail."""
+    from sfx.runner import NativeEnvLoop
+
+    spec = R.Spec(17, 32, 7, 8, ("relu", "relu"))
+    T, ev, alpha, n = 3, 1000, 0.05, 12
+    eng, st = make(spec, T, ev, max_batch=32)
+    loop = NativeEnvLoop(eng, batch=32, capacity=100, gamma=0.9, epsilon=0.3, alpha_w=alpha, episode_len=9,
+                         seed=6, device_replay=True)
+    loop.prefill(40)
+    loop.set_task(0)
+    loop.record(n)
+    loop.run(n)
+    replay_with_oracle(st, spec, loop.records(), alpha, ev, loop.action())
+    check_state(eng, st, T, n)
+    loop.close()
+    eng.close()
+
+
 def test_device_replay_switch_between_runs():
     """Host-replay steps, then device-replay steps on the same ring (uploaded at the switch),
     then host again: one continuous oracle replay."""
