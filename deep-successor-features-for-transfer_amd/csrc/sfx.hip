@@ -1075,6 +1075,41 @@ int launch_step_all(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, c
 
 }  // namespace
 
+// The drop-in's agents.buffer ring (sfx/dropin/agents/buffer.py; agents/buffer.py:34-82): one
+// launch appends a transition's row to every field, one launch gathers a minibatch -- in place of
+// a framework copy per field and an index_select per field.
+__global__ void k_replay_put(float* __restrict__ rs, float* __restrict__ rphi, float* __restrict__ rs1,
+                             int64_t* __restrict__ ra, long long j, const float* __restrict__ s,
+                             const float* __restrict__ phi, const float* __restrict__ s1, const int64_t* __restrict__ a,
+                             int n_s, int d) {
+  for (int k = threadIdx.x; k < n_s; k += blockDim.x) {
+    rs[j * n_s + k] = s[k];
+    rs1[j * n_s + k] = s1[k];
+  }
+  for (int k = threadIdx.x; k < d; k += blockDim.x) rphi[j * d + k] = phi[k];
+  if (threadIdx.x == 0) ra[j] = *a;
+}
+
+// workgroup b: row idx[b] of each field; γ from the packed copy (gam) or from the ring (rg)
+__global__ void k_replay_gather(const float* __restrict__ rs, const float* __restrict__ rphi,
+                                const float* __restrict__ rs1, const int64_t* __restrict__ ra,
+                                const float* __restrict__ rg, const int64_t* __restrict__ idx,
+                                const float* __restrict__ gam, float* __restrict__ S, float* __restrict__ PHI,
+                                float* __restrict__ S1, int64_t* __restrict__ Aout, float* __restrict__ G, int n_s,
+                                int d) {
+  const int b = blockIdx.x;
+  const long long i = idx[b];
+  for (int k = threadIdx.x; k < n_s; k += blockDim.x) {
+    S[(size_t)b * n_s + k] = rs[i * n_s + k];
+    S1[(size_t)b * n_s + k] = rs1[i * n_s + k];
+  }
+  for (int k = threadIdx.x; k < d; k += blockDim.x) PHI[(size_t)b * d + k] = rphi[i * d + k];
+  if (threadIdx.x == 0) {
+    Aout[b] = ra[i];
+    G[b] = rg ? rg[i] : gam[b];
+  }
+}
+
 // sfx_update_all returns once its step is enqueued; the speculation verdict -- and host rounds,
 // should the device rounds leave a policy unverified -- is collected by the next API call on the
 // handle (every entry point settles first), so the host never waits on a step it has not asked
@@ -1088,6 +1123,28 @@ static int settle(sfx_handle* h) {
 extern "C" {
 
 const char* sfx_version(void) { return "sfx 0.3 gfx950 fp32-mfma graphs speculative-gpi"; }
+
+int sfx_replay_put(void* stream, float* rs, float* rphi, float* rs1, int64_t* ra, long long j, const float* s,
+                   const float* phi, const float* s1, const int64_t* a, int n_s, int d) {
+  if (!rs || !rphi || !rs1 || !ra || !s || !phi || !s1 || !a || j < 0 || n_s < 1 || d < 1)
+    SFX_FAIL(SFX_E_ARG, "sfx_replay_put: bad arguments");
+  hipLaunchKernelGGL(k_replay_put, dim3(1), dim3(64), 0, (hipStream_t)stream, rs, rphi, rs1, ra, j, s, phi, s1, a, n_s,
+                     d);
+  LAUNCHCHK();
+  return SFX_OK;
+}
+
+int sfx_replay_gather(void* stream, const float* rs, const float* rphi, const float* rs1, const int64_t* ra,
+                      const float* rg, const int64_t* idx, const float* gam, int B, float* S, float* PHI, float* S1,
+                      int64_t* A, float* G, int n_s, int d) {
+  if (!rs || !rphi || !rs1 || !ra || !idx || (!rg && !gam) || B < 1 || !S || !PHI || !S1 || !A || !G || n_s < 1 ||
+      d < 1)
+    SFX_FAIL(SFX_E_ARG, "sfx_replay_gather: bad arguments");
+  hipLaunchKernelGGL(k_replay_gather, dim3(B), dim3(64), 0, (hipStream_t)stream, rs, rphi, rs1, ra, rg, idx, gam, S,
+                     PHI, S1, A, G, n_s, d);
+  LAUNCHCHK();
+  return SFX_OK;
+}
 const char* sfx_last_error(void) { return g_err.c_str(); }
 
 // Bounds-check builds (-DSFX_CHECK, libsfx_check.so): failed device bounds checks since the last

@@ -53,6 +53,8 @@ SIGNATURES = {
     "sfx_set_precision": (_I, [_VP, _I]),
     "sfx_get_precision": (_I, [_VP]),
     "sfx_set_huber": (_I, [_VP, _F]),
+    "sfx_replay_put": (_I, [_VP] * 5 + [C.c_longlong] + [_VP] * 4 + [_I, _I]),
+    "sfx_replay_gather": (_I, [_VP] * 8 + [_I] + [_VP] * 5 + [_I, _I]),
     "sfx_get_huber": (_F, [_VP]),
     "sfx_set_target_update_ev": (_I, [_VP, _I]),
     "sfx_get_since_target": (_I, [_VP, _I, _IP]),

@@ -63,12 +63,29 @@ class ReplayBuffer:
         else:
             row.copy_(torch.as_tensor(np.asarray(x, dtype=np.float32)).reshape(row.shape))
 
+    def _native(self, *xs) -> bool:
+        """Device tensors of the ring's dtypes, contiguous: libsfx's one-launch row copy applies."""
+        return self.device.type == "cuda" and all(
+            torch.is_tensor(x) and x.device == self.device and x.is_contiguous() and
+            x.dtype == (torch.int64 if i == 1 else torch.float32) for i, x in enumerate(xs))
+
     def append(self, state, action, reward, next_state, gamma) -> None:
         """Adds the sample (agents/buffer.py:62-82); the oldest is overwritten once the ring is full."""
         if self._ring is None:
             self._alloc(state, reward, next_state)
         rs, ra, rr, rs1 = self._ring
         j = self.index
+        if self._native(state, action, reward, next_state) and action.numel() == 1:
+            from sfx import _lib
+
+            _lib.check(_lib.lib.sfx_replay_put(torch.cuda.current_stream(self.device).cuda_stream, rs.data_ptr(),
+                                               rr.data_ptr(), rs1.data_ptr(), ra.data_ptr(), j, state.data_ptr(),
+                                               reward.data_ptr(), next_state.data_ptr(), action.data_ptr(),
+                                               rs.shape[1], rr.shape[1]), "sfx_replay_put")
+            self._put_gamma(j, gamma)
+            self.size = min(self.size + 1, self.n_samples)
+            self.index = (self.index + 1) % self.n_samples
+            return
         self._put(rs[j], state)
         if torch.is_tensor(action):
             ra[j].copy_(action.reshape(()), non_blocking=True)
@@ -76,6 +93,11 @@ class ReplayBuffer:
             ra[j] = int(action)
         self._put(rr[j], reward)
         self._put(rs1[j], next_state)
+        self._put_gamma(j, gamma)
+        self.size = min(self.size + 1, self.n_samples)
+        self.index = (self.index + 1) % self.n_samples
+
+    def _put_gamma(self, j, gamma):
         if torch.is_tensor(gamma):
             if self._gdev is None:
                 self._gdev = torch.as_tensor(self._gam, device=self.device).clone()
@@ -84,8 +106,6 @@ class ReplayBuffer:
             self._gam[j] = gamma
             if self._gdev is not None:
                 self._gdev[j] = float(gamma)
-        self.size = min(self.size + 1, self.n_samples)
-        self.index = (self.index + 1) % self.n_samples
 
     def replay(self):
         """A uniform minibatch (agents/buffer.py:34-60) or None while fewer than n_batch samples."""
@@ -105,7 +125,22 @@ class ReplayBuffer:
         if self._pev is not None:
             self._pev.record()
         idx = dev[:B]
-        gam = dev[B:].view(torch.float32)[:B] if self._gdev is None else self._gdev.index_select(0, idx)
         rs, ra, rr, rs1 = self._ring
+        if self.device.type == "cuda":  # every field in one gather launch
+            from sfx import _lib
+
+            n_s, d = rs.shape[1], rr.shape[1]
+            flat = torch.empty(B * (2 * n_s + d + 1), device=self.device)  # S | PHI | S1 | G, each contiguous
+            S, PHI = flat[:B * n_s].view(B, n_s), flat[B * n_s:B * (n_s + d)].view(B, d)
+            S1, G = flat[B * (n_s + d):B * (2 * n_s + d)].view(B, n_s), flat[B * (2 * n_s + d):]
+            A = torch.empty(B, dtype=torch.int64, device=self.device)
+            gsrc = dev[B:].view(torch.float32)
+            _lib.check(_lib.lib.sfx_replay_gather(
+                torch.cuda.current_stream(self.device).cuda_stream, rs.data_ptr(), rr.data_ptr(), rs1.data_ptr(),
+                ra.data_ptr(), self._gdev.data_ptr() if self._gdev is not None else None, idx.data_ptr(),
+                gsrc.data_ptr(), B, S.data_ptr(), PHI.data_ptr(), S1.data_ptr(), A.data_ptr(), G.data_ptr(),
+                n_s, d), "sfx_replay_gather")
+            return S, A, PHI, S1, G
+        gam = dev[B:].view(torch.float32)[:B] if self._gdev is None else self._gdev.index_select(0, idx)
         return (rs.index_select(0, idx), ra.index_select(0, idx), rr.index_select(0, idx),
                 rs1.index_select(0, idx), gam)

@@ -231,6 +231,20 @@ int sfx_skip_stats(sfx_t h, long long* checked, long long* skipped, int reset);
  */
 int sfx_nonfinite(sfx_t h, int* flag_host, int reset);
 
+/*
+ * The drop-in's agents.buffer ring (replaces agents/buffer.py:62-82 append and :34-60 replay's
+ * collation): device arrays rs [cap][n_s], rphi [cap][d], rs1 [cap][n_s], ra [cap] (int64).
+ * sfx_replay_put writes row j from device vectors s, phi, s1 and the int64 scalar *a in one
+ * launch; sfx_replay_gather writes the minibatch rows idx[0, B) (device int64) into S, PHI, S1, A
+ * and the discount factors into G -- from rg [cap] when non-null, else gam [B] -- in one launch.
+ * Both enqueue on `stream` (a hipStream_t; NULL = the legacy default stream) and need no handle.
+ */
+int sfx_replay_put(void* stream, float* rs, float* rphi, float* rs1, int64_t* ra, long long j, const float* s,
+                   const float* phi, const float* s1, const int64_t* a, int n_s, int d);
+int sfx_replay_gather(void* stream, const float* rs, const float* rphi, const float* rs1, const int64_t* ra,
+                      const float* rg, const int64_t* idx, const float* gam, int B, float* S, float* PHI, float* S1,
+                      int64_t* A, float* G, int n_s, int d);
+
 /* LMS reward fit SF.update_reward (features/successor.py:164-167) on w_t:
  * w <- w + alpha (r - φ·w) φ ;  phi_dev [d], r_dev [1]. */
 int sfx_lms(sfx_t h, int t, const float* phi_dev, const float* r_dev, float alpha);
