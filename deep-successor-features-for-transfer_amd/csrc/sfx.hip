@@ -154,6 +154,7 @@ struct sfx_handle {
   int fwd_tpw = FWD_TPW; // column tiles per workgroup (layer-0+1 forward, oversubscribed launches); SFX_FWD_TPW=1: one
   int ahead_tp = 4;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=2: two)
   bool sel1 = true;      // one-state action selection by k_sel1m (SFX_SEL1=0: k_gpi + k_publish)
+  bool debug_ver = false;  // SFX_DEBUG_VER=1: print each k_ver launch's publication setup
   SelScratch* selk = nullptr;  // k_sel1m's per-head keys and arrival counter
   int ncu = 256;         // compute units of the device
   bool fuse_l0 = true;   // SFX_FUSE_L0=0: layer 0 of a forward from the states as its own launch
@@ -781,6 +782,10 @@ int run_ver(sfx_handle* h, int M, int npol, bool sel, int post, const GpiArgs& g
     V.nblocks = (int)(grid.x * grid.y);
     h->pub_folded = true;
   }
+  if (h->debug_ver)  // SFX_DEBUG_VER=1 (sanitizer investigations): the folded publication's setup
+    std::fprintf(stderr, "k_ver M %d npol %d sel %d post %d rows %d grid %ux%u pub %p dctr %p done %p nblocks %d\n",
+                 V.M, V.npol, V.sel, V.post, V.rows, grid.x, grid.y, (void*)V.pub, (const void*)V.pub_dctr,
+                 (void*)V.done, V.nblocks);
   launch(h, K_VER, 4.0 * (double)M * npol * h->T * h->O + 4.0 * h->T * h->O, k_ver, grid, dim3(256), h->G, V);
   LAUNCHCHK();
   return SFX_OK;
@@ -1231,6 +1236,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->fwd_tpw = etp && etp[0] == '1' ? 1 : FWD_TPW;
   const char* eat = std::getenv("SFX_AHEAD_TP");
   h->ahead_tp = eat && eat[0] == '2' ? 2 : 4;
+  const char* edv = std::getenv("SFX_DEBUG_VER");
+  h->debug_ver = edv && edv[0] == '1';
   const char* es1 = std::getenv("SFX_SEL1");
   h->sel1 = !(es1 && es1[0] == '0');
   const char* el0 = std::getenv("SFX_FUSE_L0");

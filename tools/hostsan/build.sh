@@ -16,7 +16,10 @@ set -e
 cd "$(dirname "$0")"
 CSRC=../../deep-successor-features-for-transfer_amd/csrc
 F="--offload-arch=gfx950 -O3 -g -std=c++17 -ffp-contract=off -fno-omit-frame-pointer -I$CSRC"
-if [ "${1:-asan}" = ubsan_fn ] || [ "${1:-asan}" = ubsan_vptr ]; then  # one of the two suspects alone
+if [ "${1:-asan}" = plain ]; then  # no sanitizer (the reference run for a diff)
+  /opt/rocm/bin/hipcc $F -o runner_plain runner_hostsan.cpp "$CSRC/sfx.hip" -ldl
+  echo built tools/hostsan/runner_plain
+elif [ "${1:-asan}" = ubsan_fn ] || [ "${1:-asan}" = ubsan_vptr ]; then  # one of the two suspects alone
   chk=${1#ubsan_}; [ $chk = fn ] && chk=function
   /opt/rocm/bin/hipcc $F -Xarch_host -fsanitize=$chk -Xarch_host -fno-sanitize-recover=$chk \
     -o runner_$1 runner_hostsan.cpp "$CSRC/sfx.hip" -ldl

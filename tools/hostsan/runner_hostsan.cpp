@@ -225,6 +225,12 @@ int main() {
   // without pre-launched graphs -- the first one that stops narrows a hang down
   // HOSTSAN_BISECT=2: the all-task runner with the result published by its own k_publish (no
   // k_ver fold); =3: with the inputs pulled across PCIe instead of pushed through the BAR
+  // HOSTSAN_BISECT=4: the plain all-task scenario alone (with SFX_DEBUG_VER=1: a diff of k_ver's setup)
+  if (const char* b = std::getenv("HOSTSAN_BISECT"); b && b[0] == '4') {
+    scenario("all-task", 0, 3, false);
+    std::printf("hostsan: bisect scenario clean\n");
+    return 0;
+  }
   if (const char* b = std::getenv("HOSTSAN_BISECT"); b && (b[0] == '2' || b[0] == '3')) {
     setenv(b[0] == '2' ? "SFX_FOLD_PUBLISH" : "SFX_RUNNER_PUSH", "0", 1);
     scenario(b[0] == '2' ? "all-task, separate k_publish" : "all-task, pulled inputs", 0, 3, false);
