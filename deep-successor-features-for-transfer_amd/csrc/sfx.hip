@@ -152,7 +152,7 @@ struct sfx_handle {
   bool xcd = true;       // SFX_XCD=0: plain (tile, head) grids instead of XCD-aware ones
   int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
   int fwd_tpw = FWD_TPW; // column tiles per workgroup (layer-0+1 forward, oversubscribed launches); SFX_FWD_TPW=1: one
-  int ahead_tp = 4;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=2: two)
+  int ahead_tp = 4;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=2 / 3)
   bool sel1 = true;      // one-state action selection by k_sel1m (SFX_SEL1=0: k_gpi + k_publish)
   bool debug_ver = false;  // SFX_DEBUG_VER=1: print each k_ver launch's publication setup
   SelScratch* selk = nullptr;  // k_sel1m's per-head keys and arrival counter
@@ -466,7 +466,7 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     // unpaired, their workgroups dispatched over 5 us)
     if (!qa && h->fwd_tpw > 1 && h->fwd_waves == 8 && F.ntN > 1 && 2 * tiles >= 3L * h->ncu &&
         (tiles <= 2L * h->ncu || F.rowsplit) && (l0 || ((L.K % 32) == 0 && aligned)))
-      F.tpw = F.rowsplit && h->ahead_tp == 4 && F.ntN >= 4 ? 4 : h->fwd_tpw;
+      F.tpw = F.rowsplit && h->ahead_tp >= 3 && F.ntN >= h->ahead_tp ? h->ahead_tp : h->fwd_tpw;
     const int ntNb = cdiv(F.ntN, F.tpw);
     const dim3 grid = F.xcd ? dim3(8 * cdiv(h->T, 8) * ntNb * (F.rowsplit ? F.ntMs : F.ntM * F.ngroups))
                             : dim3(ntNb, ninst, F.ntM);
@@ -489,6 +489,9 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
                grid, dim3(512), h->G, F);
     } else if (h->fwd_waves == 8 && F.tpw == 4) {  // (the tpw rule above requires the vector path)
       launch(h, K_FWD, by, h->bf16 ? k_fwd<true, 8, false, true, 4> : k_fwd<true, 8, false, false, 4>, grid, dim3(512),
+             h->G, F);
+    } else if (h->fwd_waves == 8 && F.tpw == 3) {
+      launch(h, K_FWD, by, h->bf16 ? k_fwd<true, 8, false, true, 3> : k_fwd<true, 8, false, false, 3>, grid, dim3(512),
              h->G, F);
     } else if (h->fwd_waves == 8) {
       const bool vec = (L.K % 32) == 0 && aligned;
@@ -1235,7 +1238,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   const char* etp = std::getenv("SFX_FWD_TPW");
   h->fwd_tpw = etp && etp[0] == '1' ? 1 : FWD_TPW;
   const char* eat = std::getenv("SFX_AHEAD_TP");
-  h->ahead_tp = eat && eat[0] == '2' ? 2 : 4;
+  h->ahead_tp = eat && (eat[0] == '2' || eat[0] == '3') ? eat[0] - '0' : 4;
   const char* edv = std::getenv("SFX_DEBUG_VER");
   h->debug_ver = edv && edv[0] == '1';
   const char* es1 = std::getenv("SFX_SEL1");

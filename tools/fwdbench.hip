@@ -80,6 +80,7 @@ int main() {
       {"plain R_V 33 rows (round-0 post-update)", {gv}, 33, 4, false},
       {"look-ahead 4 groups, TP 4 (default)", {gv, gns, gn1, gnt}, 33, 4, false},
       {"look-ahead 4 groups, TP 2", {gv, gns, gn1, gnt}, 33, 2, false},
+      {"look-ahead 4 groups, TP 3", {gv, gns, gn1, gnt}, 33, 3, false},
       {"4 groups, target group on online heads", {gv, gns, gn1, gno}, 33, 4, false},
       {"3 look-ahead groups only (no R_V)", {gns, gn1, gnt}, 32, 4, false},
       {"plain R_V 33 rows, L2 flushed", {gv}, 33, 4, true},
