@@ -152,7 +152,7 @@ struct sfx_handle {
   bool xcd = true;       // SFX_XCD=0: plain (tile, head) grids instead of XCD-aware ones
   int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
   int fwd_tpw = FWD_TPW; // column tiles per workgroup (layer-0+1 forward, oversubscribed launches); SFX_FWD_TPW=1: one
-  int ahead_tp = 4;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=2 / 3)
+  int ahead_tp = 3;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=2 / 4)
   bool sel1 = true;      // one-state action selection by k_sel1m (SFX_SEL1=0: k_gpi + k_publish)
   bool debug_ver = false;  // SFX_DEBUG_VER=1: print each k_ver launch's publication setup
   SelScratch* selk = nullptr;  // k_sel1m's per-head keys and arrival counter
@@ -1238,7 +1238,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   const char* etp = std::getenv("SFX_FWD_TPW");
   h->fwd_tpw = etp && etp[0] == '1' ? 1 : FWD_TPW;
   const char* eat = std::getenv("SFX_AHEAD_TP");
-  h->ahead_tp = eat && (eat[0] == '2' || eat[0] == '3') ? eat[0] - '0' : 4;
+  h->ahead_tp = eat && (eat[0] == '2' || eat[0] == '4') ? eat[0] - '0' : 3;
   const char* edv = std::getenv("SFX_DEBUG_VER");
   h->debug_ver = edv && edv[0] == '1';
   const char* es1 = std::getenv("SFX_SEL1");
