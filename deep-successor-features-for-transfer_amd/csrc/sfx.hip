@@ -153,6 +153,7 @@ struct sfx_handle {
   int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
   int fwd_tpw = FWD_TPW; // column tiles per workgroup (layer-0+1 forward, oversubscribed launches); SFX_FWD_TPW=1: one
   int ahead_tp = 3;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=2 / 4)
+  int fwd_tail = 0;      // FwdArgs::tail: SFX_FWD_TAIL=1 on row-split launches, 2 on every plain vector launch
   bool sel1 = true;      // one-state action selection by k_sel1m (SFX_SEL1=0: k_gpi + k_publish)
   bool debug_ver = false;  // SFX_DEBUG_VER=1: print each k_ver launch's publication setup
   SelScratch* selk = nullptr;  // k_sel1m's per-head keys and arrival counter
@@ -418,29 +419,34 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     F.lms_alpha = ex.lms_alpha;
     F.flag = first ? ex.flag : nullptr;
     F.flag_value = ex.flag_value;
+    const bool qa = ex.qa_role >= 0 && l == h->NL - 1;  // the maxima come from the ψ output layer
+    // the vector path needs K % (256/NW) == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
+    const bool aligned = l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0);
+    bool own = false;  // groups with their own rows on an XCD grid: per-group row tiles (FwdArgs::rowsplit)
+    if (F.xcd)
+      for (const FwdGroup& g : groups) own = own || (g.m > 0 && g.m != M);
+    // a group's last row tile takes up to 16 more rows (FwdArgs::tail; plain 8-wave vector launches)
+    F.tail = !l0 && !qa && h->fwd_waves == 8 && (L.K % 32) == 0 && aligned &&
+                     (h->fwd_tail == 2 || (h->fwd_tail == 1 && own))
+                 ? 1
+                 : 0;
     F.ntN = cdiv(L.N, 16);
-    F.ntM = cdiv(M, 32);
+    F.ntM = fwd_row_tiles(M, F.tail);
     F.tpw = 1;
-    // groups with their own rows on an XCD grid: per-group row tiles (FwdArgs::rowsplit)
     long tiles = (long)F.ntN * F.ntM * ninst;
     F.rowsplit = 0;
-    if (F.xcd) {
-      bool own = false;
-      for (const FwdGroup& g : groups) own = own || (g.m > 0 && g.m != M);
-      if (own) {
-        int* mt[4] = {&F.mt0, &F.mt1, &F.mt2, &F.mt3};
-        int gi = 0;
-        F.ntMs = 0;
-        tiles = 0;
-        for (const FwdGroup& g : groups) {
-          *mt[gi++] = cdiv(g.m > 0 ? g.m : M, 32);
-          F.ntMs += *mt[gi - 1];
-          tiles += (long)F.ntN * *mt[gi - 1] * g.n;
-        }
-        F.rowsplit = 1;
+    if (own) {
+      int* mt[4] = {&F.mt0, &F.mt1, &F.mt2, &F.mt3};
+      int gi = 0;
+      F.ntMs = 0;
+      tiles = 0;
+      for (const FwdGroup& g : groups) {
+        *mt[gi++] = fwd_row_tiles(g.m > 0 ? g.m : M, F.tail);
+        F.ntMs += *mt[gi - 1];
+        tiles += (long)F.ntN * *mt[gi - 1] * g.n;
       }
+      F.rowsplit = 1;
     }
-    const bool qa = ex.qa_role >= 0 && l == h->NL - 1;  // the maxima come from the ψ output layer
     if (qa) {
       F.qa_role = ex.qa_role;
       F.qa_Tg = h->Tg;
@@ -456,8 +462,6 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
       F.qh = ex.qh;
       F.qhs = ex.qhs;
     }
-    // the vector path needs K % (256/NW) == 0 and 16-B aligned rows of X (layer 0 reads the caller's S)
-    const bool aligned = l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0);
     // two column tiles per workgroup (an L0 launch's in-tile layer 0 computed once for them, a
     // plain launch's X operands loaded once) when the tiles would put two workgroups on at least
     // half the CUs and fit the chip when paired: C2's first forward of three roles (384 tiles ->
@@ -1239,6 +1243,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->fwd_tpw = etp && etp[0] == '1' ? 1 : FWD_TPW;
   const char* eat = std::getenv("SFX_AHEAD_TP");
   h->ahead_tp = eat && (eat[0] == '2' || eat[0] == '4') ? eat[0] - '0' : 3;
+  const char* eft = std::getenv("SFX_FWD_TAIL");
+  h->fwd_tail = eft && (eft[0] == '1' || eft[0] == '2') ? eft[0] - '0' : 0;
   const char* edv = std::getenv("SFX_DEBUG_VER");
   h->debug_ver = edv && edv[0] == '1';
   const char* es1 = std::getenv("SFX_SEL1");

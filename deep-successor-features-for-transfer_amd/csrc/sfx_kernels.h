@@ -426,6 +426,9 @@ struct FwdArgs {
   // and the grid holds ntMs = Σ mt_g of them per (head, column tile) -- no workgroups for rows a
   // group does not have
   int rowsplit, mt0, mt1, mt2, mt3, ntMs;
+  // tail: a group's last row tile also takes up to 16 rows past its 32 (a third 16-row MFMA block;
+  // plain vector launches only): the 33-row post-update roles in one row tile, not two
+  int tail, pad_t;
   int w0Off, b0Off, K0, y0Off;  // L0 launches: layer 0 (K0 -> K, identity) computed in-tile, stored at y0Off
   unsigned long long mask;
   FwdGroup g0, g1, g2, g3;
@@ -576,6 +579,11 @@ __device__ __forceinline__ FwdGroup fwd_group(const FwdArgs& F, int& y) {
 
 constexpr int FWD_TPW = 2;  // column tiles per workgroup (FwdArgs::tpw <= TP)
 
+// row tiles of an m-row group (FwdArgs::tail: the last one covers up to 48 rows)
+__host__ __device__ __forceinline__ int fwd_row_tiles(int m, int tail) {
+  return tail && m > 32 ? (m + 15) >> 5 : (m + 31) >> 5;
+}
+
 // TP > 1: the workgroup computes column tiles tN .. tN + tpw - 1 of its rows -- an L0 launch's
 // layer-0 rows computed once for them, a plain launch's X operands loaded once for them (launches
 // that would otherwise put more workgroups than CUs on the chip)
@@ -593,15 +601,19 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
   const FwdGroup grp = fwd_group(F, y);
   const int head = grp.head0 + y;
   const int M = grp.m > 0 ? grp.m : F.M, N = F.N, K = F.K;
-  if (tM * 32 >= M) return;  // a group with fewer rows than the launch (block-uniform, before any barrier)
+  if (tM >= fwd_row_tiles(M, F.tail)) return;  // a group with fewer rows than the launch (block-uniform)
   const float* P = grp.which == P_TARGET ? G.target + (long long)head * G.P
                                          : G.online + G.slot_off(rslot(F.mask, head) ^ (grp.which == P_NEW), head);
   const float* X = F.xOff < 0 ? (grp.xsel == 1 ? F.xa : grp.xsel == 2 ? F.xb : F.xc) : G.actp(grp.role, head, F.xOff);
   float* Y = G.actp(grp.role, head, F.yOff);
   const int m0 = tM * 32;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
-  const int ma = m0 + r, mb = m0 + 16 + r;
+  const int ma = m0 + r, mb = m0 + 16 + r, mc = m0 + 32 + r;
   const bool oka = ma < M, okb = mb < M;
+  // FwdArgs::tail: rows m0 + 32 .. m0 + 47 as a third MFMA block (block-uniform)
+  constexpr bool EXT = VEC && !L0 && !C;
+  const bool ext = EXT && F.tail && M - m0 > 32;
+  const bool okc = ext && mc < M;
   const float* Pw = P + F.wOff;
   // bf16 mode: the W operand from the bf16 copy (same packing, 16-B aligned rows: wOff % 8 == 0)
   const __bf16* Pw16 = nullptr;
@@ -615,7 +627,7 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
     const int col = (tN + j) * 16 + (Lx & 15);
-    biasv[j] = (j < ntile && threadIdx.x < 128 && col < N) ? ldc<C>(P + F.bOff + col) : 0.f;
+    biasv[j] = (j < ntile && threadIdx.x < (ext ? 192 : 128) && col < N) ? ldc<C>(P + F.bOff + col) : 0.f;
   }
   constexpr int AS = L0 ? L0_NMAX + 4 : 4;  // LDS row stride of a0 (padded against bank conflicts)
   __shared__ __align__(16) float sA[L0 ? 32 * AS : 4];
@@ -717,10 +729,13 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
   }
   const float* xra = L0 ? sA + r * AS : X + (size_t)ma * K;
   const float* xrb = L0 ? sA + (16 + r) * AS : X + (size_t)mb * K;
-  __shared__ floatx4 red[NW][2][64];
-  floatx4 acc0[TPW], acc1[TPW];
+  const float* xrc = X + (size_t)(okc ? mc : 0) * K;
+  __shared__ floatx4 red[NW][EXT ? 3 : 2][64];
+  floatx4 acc0[TPW], acc1[TPW], acc2[EXT ? TPW : 1];
 #pragma unroll
   for (int j = 0; j < TPW; ++j) acc0[j] = acc1[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < (EXT ? TPW : 1); ++j) acc2[j] = floatx4{0.f, 0.f, 0.f, 0.f};
   const float* wrj[TPW];
   const __bf16* wr16j[TPW];
   bool oknj[TPW];
@@ -735,7 +750,7 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
     // bf16 operands: per lane KL consecutive k as KL / 8 MFMA steps of 8 (the fp32 path's k
     // assignment, regrouped), X rounded to bf16 in registers, W from the bf16 copy
     const int kb = kc + g * KL;
-    float a0[KL], a1[KL];
+    float a0[KL], a1[KL], a2[EXT ? KL : 1];
 #pragma unroll
     for (int q = 0; q < KL / 4; ++q) {
       float4 ta, tb;
@@ -748,6 +763,10 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
       }
       a0[4 * q] = ta.x; a0[4 * q + 1] = ta.y; a0[4 * q + 2] = ta.z; a0[4 * q + 3] = ta.w;
       a1[4 * q] = tb.x; a1[4 * q + 1] = tb.y; a1[4 * q + 2] = tb.z; a1[4 * q + 3] = tb.w;
+      if constexpr (EXT) {
+        const float4 tc = okc ? *reinterpret_cast<const float4*>(xrc + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+        a2[4 * q] = tc.x; a2[4 * q + 1] = tc.y; a2[4 * q + 2] = tc.z; a2[4 * q + 3] = tc.w;
+      }
     }
     bf16x8 w16[TPW][KL / 8];
 #pragma unroll
@@ -768,10 +787,18 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
         acc1[j] = mfma_bf16(x1, w16[j][q], acc1[j]);
       }
     }
+    if constexpr (EXT)
+      if (ext)
+#pragma unroll
+        for (int q = 0; q < KL / 8; ++q) {
+          const bf16x8 x2 = to_bf16x8(a2 + 8 * q);
+#pragma unroll
+          for (int j = 0; j < TPW; ++j) acc2[j] = mfma_bf16(x2, w16[j][q], acc2[j]);
+        }
   }
   for (int kc = wave * KW; kc < K && !BF; kc += 256) {
     const int kb = kc + g * KL;
-    float a0[KL], a1[KL], bw[TPW][KL];
+    float a0[KL], a1[KL], bw[TPW][KL], a2[EXT ? KL : 1];
     if constexpr (VEC) {  // K % KW == 0, rows 16-B aligned: KL/4 float4 per operand row
 #pragma unroll
       for (int q = 0; q < KL / 4; ++q) {
@@ -796,6 +823,10 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
         }
         a0[4 * q] = ta.x; a0[4 * q + 1] = ta.y; a0[4 * q + 2] = ta.z; a0[4 * q + 3] = ta.w;
         a1[4 * q] = tb.x; a1[4 * q + 1] = tb.y; a1[4 * q + 2] = tb.z; a1[4 * q + 3] = tb.w;
+        if constexpr (EXT) {
+          const float4 tc = okc ? ldc4<C>(xrc + kb + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+          a2[4 * q] = tc.x; a2[4 * q + 1] = tc.y; a2[4 * q + 2] = tc.z; a2[4 * q + 3] = tc.w;
+        }
       }
     } else {
 #pragma unroll
@@ -819,6 +850,12 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
         acc0[j] = mfma4(a0[i], bw[j][i], acc0[j]);
         acc1[j] = mfma4(a1[i], bw[j][i], acc1[j]);
       }
+    if constexpr (EXT)
+      if (ext)
+#pragma unroll
+        for (int i = 0; i < KL; ++i)
+#pragma unroll
+          for (int j = 0; j < TPW; ++j) acc2[j] = mfma4(a2[i], bw[j][i], acc2[j]);
   }
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
@@ -829,8 +866,10 @@ __device__ __forceinline__ void fwd_tile(const Geo& G, const FwdArgs& F, int y, 
   if (j > 0) __syncthreads();  // the previous tile's reduction has read red
   red[wave][0][lane] = acc0[j];
   red[wave][1][lane] = acc1[j];
+  if constexpr (EXT)
+    if (ext) red[wave][EXT ? 2 : 1][lane] = acc2[EXT ? j : 0];
   __syncthreads();
-  if (threadIdx.x < 128) {
+  if (threadIdx.x < (ext ? 192 : 128)) {
     const int s = threadIdx.x >> 6;
     floatx4 v = red[0][s][Lx];
 #pragma unroll

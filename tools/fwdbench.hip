@@ -1,7 +1,7 @@
 // Microbenchmark of the post-update forward launches (layers 1..3 of the C2 shape, T = 8, H = 256)
 // in the group layouts the all-task step uses: the plain post-update forward (one group, 33 rows)
 // and the look-ahead's four-group row-split launch, plus variants that isolate one
-// factor each (target heads vs online, row-split groups alone, 2 vs 4 column tiles, L2 flushed
+// factor each (target heads vs online, 2 / 3 / 4 column tiles, the 33-row groups in one 48-row tile or two, L2 flushed
 // before each repetition).  It compiles libsfx's translation unit in (#include) to call run_fwd
 // directly and reads the per-launch packet timestamps the bench instrumentation records.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -o tools/fwdbench tools/fwdbench.hip -ldl
@@ -18,10 +18,12 @@ struct Variant {
   int M;
   int tp;      // SFX_AHEAD_TP
   bool flush;  // stream 256 MB through the L2s before each repetition
+  int tail = 1;  // SFX_FWD_TAIL
 };
 
 int run_variant(sfx_handle* h, const Variant& v, float* junk, size_t junk_n, int reps, double* per_layer) {
   h->ahead_tp = v.tp;
+  h->fwd_tail = v.tail;
   FwdExtra vx;
   vx.l0 = 1;
   for (int l = 0; l < 3; ++l) per_layer[l] = 0.0;
@@ -77,23 +79,25 @@ int main() {
   const FwdGroup gv{R_V, P_NEW, 0, 0, T, 33, 0}, gns{R_NS, P_NEW, 0, 0, T, 32, 1},
       gn1{R_NS1, P_NEW, 0, 0, T, 32, 1}, gnt{R_NS1T, P_TARGET, 0, 0, T, 32, 1}, gno{R_NS1T, P_NEW, 0, 0, T, 32, 1};
   const std::vector<Variant> vs = {
-      {"plain R_V 33 rows (round-0 post-update)", {gv}, 33, 4, false},
-      {"look-ahead 4 groups, TP 4 (default)", {gv, gns, gn1, gnt}, 33, 4, false},
-      {"look-ahead 4 groups, TP 2", {gv, gns, gn1, gnt}, 33, 2, false},
-      {"look-ahead 4 groups, TP 3", {gv, gns, gn1, gnt}, 33, 3, false},
-      {"4 groups, target group on online heads", {gv, gns, gn1, gno}, 33, 4, false},
-      {"3 look-ahead groups only (no R_V)", {gns, gn1, gnt}, 32, 4, false},
-      {"plain R_V 33 rows, L2 flushed", {gv}, 33, 4, true},
-      {"look-ahead 4 groups TP 4, L2 flushed", {gv, gns, gn1, gnt}, 33, 4, true},
+      {"plain R_V 33 rows (round-0 post-update)", {gv}, 33, 4, false, 0},
+      {"plain R_V 33 rows, one 48-row tile", {gv}, 33, 4, false, 2},
+      {"look-ahead 4 groups, TP 4, 33 rows in 2 tiles", {gv, gns, gn1, gnt}, 33, 4, false, 0},
+      {"look-ahead 4 groups, TP 3, 33 rows in 2 tiles", {gv, gns, gn1, gnt}, 33, 3, false, 0},
+      {"look-ahead 4 groups, TP 2, 33 rows in 2 tiles", {gv, gns, gn1, gnt}, 33, 2, false, 0},
+      {"look-ahead 4 groups, TP 4, 48-row tail tile", {gv, gns, gn1, gnt}, 33, 4, false, 1},
+      {"look-ahead 4 groups, TP 3, 48-row tail tile", {gv, gns, gn1, gnt}, 33, 3, false, 1},
+      {"look-ahead 4 groups, TP 2, 48-row tail tile", {gv, gns, gn1, gnt}, 33, 2, false, 1},
+      {"4 groups TP 3 tail, target group on online", {gv, gns, gn1, gno}, 33, 3, false, 1},
+      {"look-ahead 4 groups TP 3 tail, L2 flushed", {gv, gns, gn1, gnt}, 33, 3, true, 1},
   };
-  std::printf("%-44s %9s %9s %9s  (us per launch, mean of 200; layers 1 / 2 / 3)\n", "variant", "L1", "L2", "L3");
+  std::printf("%-48s %9s %9s %9s  (us per launch, mean of 200; layers 1 / 2 / 3)\n", "variant", "L1", "L2", "L3");
   for (const Variant& v : vs) {
     double us[3];
     if (run_variant(h, v, junk, junk_n, 200, us) != SFX_OK) {
       std::fprintf(stderr, "%s: %s\n", v.name, sfx_last_error());
       return 1;
     }
-    std::printf("%-44s %9.2f %9.2f %9.2f\n", v.name, us[0], us[1], us[2]);
+    std::printf("%-48s %9.2f %9.2f %9.2f\n", v.name, us[0], us[1], us[2]);
   }
   (void)hipFree(junk);
   sfx_destroy(hh);
