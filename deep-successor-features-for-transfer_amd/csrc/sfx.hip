@@ -152,8 +152,8 @@ struct sfx_handle {
   bool xcd = true;       // SFX_XCD=0: plain (tile, head) grids instead of XCD-aware ones
   int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
   int fwd_tpw = FWD_TPW; // column tiles per workgroup (layer-0+1 forward, oversubscribed launches); SFX_FWD_TPW=1: one
-  int ahead_tp = 3;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=2 / 4)
-  int fwd_tail = 0;      // FwdArgs::tail: SFX_FWD_TAIL=1 on row-split launches, 2 on every plain vector launch
+  int ahead_tp = 2;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=3 / 4)
+  int fwd_tail = 1;      // FwdArgs::tail on oversubscribed row-split launches (SFX_FWD_TAIL=0: off, 2: every plain vector launch)
   bool sel1 = true;      // one-state action selection by k_sel1m (SFX_SEL1=0: k_gpi + k_publish)
   bool debug_ver = false;  // SFX_DEBUG_VER=1: print each k_ver launch's publication setup
   SelScratch* selk = nullptr;  // k_sel1m's per-head keys and arrival counter
@@ -425,12 +425,17 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     bool own = false;  // groups with their own rows on an XCD grid: per-group row tiles (FwdArgs::rowsplit)
     if (F.xcd)
       for (const FwdGroup& g : groups) own = own || (g.m > 0 && g.m != M);
-    // a group's last row tile takes up to 16 more rows (FwdArgs::tail; plain 8-wave vector launches)
+    F.ntN = cdiv(L.N, 16);
+    // a group's last row tile takes up to 16 more rows (FwdArgs::tail; plain 8-wave vector launches):
+    // on row-split launches with more 32-row tiles than CUs (the look-ahead's hidden layers: 640 ->
+    // 512 tiles, paired into 256 workgroups; tools/fwdbench 6.8 / 6.4 us against 7.8 / 7.5 for 240
+    // workgroups of 3 tiles without it -- it is slower where the tiles already fit the chip)
+    long tiles32 = 0;
+    for (const FwdGroup& g : groups) tiles32 += (long)F.ntN * cdiv(own && g.m > 0 ? g.m : M, 32) * g.n;
     F.tail = !l0 && !qa && h->fwd_waves == 8 && (L.K % 32) == 0 && aligned &&
-                     (h->fwd_tail == 2 || (h->fwd_tail == 1 && own))
+                     (h->fwd_tail == 2 || (h->fwd_tail == 1 && own && tiles32 > h->ncu))
                  ? 1
                  : 0;
-    F.ntN = cdiv(L.N, 16);
     F.ntM = fwd_row_tiles(M, F.tail);
     F.tpw = 1;
     long tiles = (long)F.ntN * F.ntM * ninst;
@@ -1242,9 +1247,9 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   const char* etp = std::getenv("SFX_FWD_TPW");
   h->fwd_tpw = etp && etp[0] == '1' ? 1 : FWD_TPW;
   const char* eat = std::getenv("SFX_AHEAD_TP");
-  h->ahead_tp = eat && (eat[0] == '2' || eat[0] == '4') ? eat[0] - '0' : 3;
+  h->ahead_tp = eat && (eat[0] == '3' || eat[0] == '4') ? eat[0] - '0' : 2;
   const char* eft = std::getenv("SFX_FWD_TAIL");
-  h->fwd_tail = eft && (eft[0] == '1' || eft[0] == '2') ? eft[0] - '0' : 0;
+  h->fwd_tail = eft && (eft[0] == '0' || eft[0] == '2') ? eft[0] - '0' : 1;
   const char* edv = std::getenv("SFX_DEBUG_VER");
   h->debug_ver = edv && edv[0] == '1';
   const char* es1 = std::getenv("SFX_SEL1");

@@ -209,6 +209,8 @@ def _worker(rank, port, q, cfg):
         if rank == 0:
             q.put((recs, final, np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]),
                    ws.numpy(), stats, [p[2] for p in parts]))
+            q.close()
+            q.join_thread()  # flushed into the pipe before the teardown
     finally:
         dist.destroy_process_group()
 

@@ -123,6 +123,8 @@ def _worker(rank, port, q, cfg=SMALL):
         if rank == 0:
             q.put((actions, torch.cat([p[0] for p in parts]).numpy(), torch.cat([p[1] for p in parts]).numpy(),
                    ws.numpy(), stats))
+            q.close()
+            q.join_thread()  # flushed into the pipe before the teardown
     finally:
         dist.destroy_process_group()
 
@@ -268,6 +270,8 @@ def _tsf_worker(rank, port, q, cfg=TSF_SMALL):
         if rank == 0:
             q.put((actions, torch.cat([p[0] for p in parts]).numpy(), torch.cat([p[1] for p in parts]).numpy(),
                    h.numpy(), w.numpy()))
+            q.close()
+            q.join_thread()  # flushed into the pipe before the teardown
     finally:
         dist.destroy_process_group()
 

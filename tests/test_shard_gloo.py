@@ -55,6 +55,8 @@ def _worker(rank, port, q, rounds):
     dist.all_gather_object(heads, be.st.online)
     if rank == 0:
         q.put((actions, torch.cat(heads), be.w, step.stats))
+        q.close()
+        q.join_thread()  # the result is in the pipe before the teardown (a crash there reset the pipe once)
     dist.destroy_process_group()
 
 
@@ -145,6 +147,8 @@ def _tsf_worker(rank, port, q, use_gpi):
     dist.all_gather_object(parts, (be.st.online, be.st.g))
     if rank == 0:
         q.put((actions, torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts]), be.st.h, be.w))
+        q.close()
+        q.join_thread()
     dist.destroy_process_group()
 
 
