@@ -149,7 +149,6 @@ struct sfx_handle {
   bool use_graphs = true;
   bool fuse_tdg = true;  // SFX_FUSE_TDG=0: K2 as its own launch
   bool fuse_v0 = true;   // SFX_FUSE_V0=0: post-update layer-0 forward as its own launch
-  bool v0_pair = false;  // SFX_V0_PAIR=1: the fused layer-0 tiles two at a time (BwdArgs::v0_pair)
   bool xcd = true;       // SFX_XCD=0: plain (tile, head) grids instead of XCD-aware ones
   int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
   int fwd_tpw = FWD_TPW; // column tiles per workgroup (layer-0+1 forward, oversubscribed launches); SFX_FWD_TPW=1: one
@@ -741,7 +740,6 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.ax = ex.fuse_v0 ? ex.ax : nullptr;
   A.aM = ex.fuse_v0 && ex.ax ? ex.aM : 0;
   A.a_noskip = ex.a_noskip;
-  A.v0_pair = h->v0_pair ? 1 : 0;
   const int ntile = A.nb + A.nc + A.tail;
   if (!(ex.ride && nhead == 1 && !A.xcd && ex.ride(h->NL - 1, tail_at, A, ntile, nhead * (dw_bytes(1) + dw_bytes(0)))))
     launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), h->bf16 ? k_bwd<true> : k_bwd<false>,
@@ -1234,8 +1232,6 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->fuse_tdg = !(ef && ef[0] == '0');
   const char* ev0 = std::getenv("SFX_FUSE_V0");
   h->fuse_v0 = !(ev0 && ev0[0] == '0');
-  const char* evp = std::getenv("SFX_V0_PAIR");
-  h->v0_pair = evp && evp[0] == '1';
   const char* efp = std::getenv("SFX_FOLD_PUBLISH");
   h->fold_publish = !(efp && efp[0] == '0');
   const char* ex = std::getenv("SFX_XCD");

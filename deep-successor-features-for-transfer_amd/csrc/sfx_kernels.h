@@ -1211,7 +1211,6 @@ struct BwdArgs {
   // layer-0 tiles of a head that skips this round still compute them (first round that has them)
   const float* ax;
   int aM, a_noskip;
-  int v0_pair, pad_v0;  // fused_v0 runs its tiles two at a time (v0_tile2)
   // sharded step: the fused-TD launch re-initialises the next round's maxima buffer (xi_dst[j] =
   // xi_src[j] for j < xi_copy, SORT_EMPTY up to xi_n) -- its last reader was an earlier launch
   const int* xi_src;
@@ -1625,57 +1624,6 @@ __device__ __forceinline__ void v0_tile(const float* x, int K, int m0, int rows,
   }
 }
 
-// Two tiles of v0_tile at once (BwdArgs::v0_pair): both tiles' LDS operands read before either
-// MFMA chain, the chains interleaved -- each chain is v0_tile's, so the bits are.
-struct V0T {
-  const float* x;
-  int m0, rows;
-  const float* w;
-  float bb;
-  float* Y;
-};
-template <bool C>
-__device__ __forceinline__ void v0_tile2(const V0T& t0, const V0T& t1, int K, int act, int N, int n, long long lim) {
-  constexpr int KS = 8;
-  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4, ma0 = t0.m0 + r, ma1 = t1.m0 + r;
-  floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
-  for (int k0 = 0; k0 < K; k0 += 4 * KS) {
-    float a0[KS], b0[KS], a1[KS], b1[KS];
-#pragma unroll
-    for (int q = 0; q < KS; ++q) {
-      const int k = k0 + 4 * q + g;
-      a0[q] = (k < K && ma0 < t0.rows) ? t0.x[ma0 * K + k] : 0.f;
-      b0[q] = k < K ? t0.w[k] : 0.f;
-      a1[q] = (k < K && ma1 < t1.rows) ? t1.x[ma1 * K + k] : 0.f;
-      b1[q] = k < K ? t1.w[k] : 0.f;
-    }
-#pragma unroll
-    for (int q = 0; q < KS; ++q)
-      if (k0 + 4 * q < K) {
-        c0 = mfma4(a0[q], b0[q], c0);
-        c1 = mfma4(a1[q], b1[q], c1);
-      }
-  }
-  if (n < N) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = t0.m0 + g * 4 + i;
-      if (m < t0.rows) {
-        SFX_CHK((long long)m * N + n < lim, m, n, lim);
-        stc<C>(t0.Y + (size_t)m * N + n, act_fwd(__fadd_rn(c0[i], t0.bb), act));
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = t1.m0 + g * 4 + i;
-      if (m < t1.rows) {
-        SFX_CHK((long long)m * N + n < lim, m, n, lim);
-        stc<C>(t1.Y + (size_t)m * N + n, act_fwd(__fadd_rn(c1[i], t1.bb), act));
-      }
-    }
-  }
-}
-
 template <bool C>
 __device__ __forceinline__ void fused_v0(const Geo& G, const BwdArgs& A, const RoleGeo& L, int head, int nbase, const float* sW,
                          const float* sB, const float* sX, const float* sWt = nullptr, const float* sBt = nullptr,
@@ -1688,31 +1636,6 @@ __device__ __forceinline__ void fused_v0(const Geo& G, const BwdArgs& A, const R
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15;
   const int nl = (wave & 1) * 16 + r, n = nbase + nl;
   const float bias = sB[nl];
-  if (A.v0_pair) {
-    // one index space over the post-update rows' tiles and the look-ahead's three products, this
-    // wave's tiles two at a time
-    const int nv = vrows ? (VM + 15) >> 4 : 0, aM = A.aM, nt = aM > 0 ? (aM + 15) >> 4 : 0;
-    const float* xa = sX + v0_aoff(A, K);
-    const float bt = aM > 0 ? sBt[nl] : 0.f;
-    auto tile = [&](int u) -> V0T {
-      if (u < nv) return V0T{sX, u * 16, VM, sW + nl * V0S, bias, G.actp(A.vRole, head, A.vOff)};
-      u -= nv;
-      const int which = u / nt, mt = u - which * nt;
-      return V0T{xa + (which ? aM * K : 0), mt * 16, aM, which == 2 ? sWt + nl * K : sW + nl * V0S,
-                 which == 2 ? bt : bias, G.actp(which == 0 ? R_NS : which == 1 ? R_NS1 : R_NS1T, head, A.vOff)};
-    };
-    const int nall = nv + 3 * nt;
-    const long long lim = G.actSize - A.vOff;
-    int u = wave >> 1;
-    for (; u + 2 < nall; u += 4) v0_tile2<C>(tile(u), tile(u + 2), K, A.act0, N, n, lim);
-    if (u < nall) {
-      const V0T t = tile(u);
-      v0_tile<C>(t.x, K, t.m0, t.rows, t.w, t.bb, A.act0, t.Y, N, n, lim);
-    }
-    PROBE_AT(4);
-    PROBE_AT(5);
-    return;
-  }
   if (vrows) {
     float* Y = G.actp(A.vRole, head, A.vOff);
     for (int mt = wave >> 1; mt * 16 < VM; mt += 2)
