@@ -28,6 +28,8 @@
 #include <random>
 #include <string>
 #include <functional>
+#include <tuple>
+#include <utility>
 #include <vector>
 
 #include "sfx_kernels.h"
@@ -147,18 +149,9 @@ struct sfx_handle {
   hipStream_t stream = nullptr;  // caller's stream: everything is ordered on it
   hipStream_t cap = nullptr;     // private stream used only to capture graphs
   bool use_graphs = true;
-  bool fuse_tdg = true;  // SFX_FUSE_TDG=0: K2 as its own launch
-  bool fuse_v0 = true;   // SFX_FUSE_V0=0: post-update layer-0 forward as its own launch
-  bool xcd = true;       // SFX_XCD=0: plain (tile, head) grids instead of XCD-aware ones
-  int fwd_waves = 8;     // forward tiles split K over 8 waves (512 threads); SFX_FWD_WAVES=4: 4 waves
   int fwd_tpw = FWD_TPW; // column tiles per workgroup (layer-0+1 forward, oversubscribed launches); SFX_FWD_TPW=1: one
-  int ahead_tp = 2;      // column tiles per workgroup of the look-ahead's row-split forwards (SFX_AHEAD_TP=3 / 4)
-  int fwd_tail = 1;      // FwdArgs::tail on oversubscribed row-split launches (SFX_FWD_TAIL=0: off, 2: every plain vector launch)
-  bool sel1 = true;      // one-state action selection by k_sel1m (SFX_SEL1=0: k_gpi + k_publish)
-  bool debug_ver = false;  // SFX_DEBUG_VER=1: print each k_ver launch's publication setup
   SelScratch* selk = nullptr;  // k_sel1m's per-head keys and arrival counter
   int ncu = 256;         // compute units of the device
-  bool fuse_l0 = true;   // SFX_FUSE_L0=0: layer 0 of a forward from the states as its own launch
   AdamHP hp_psi{1e-3, 0.0, 0.9, 0.999, 1e-8};
   AdamHP hp_w{1e-3, 0.0, 0.9, 0.999, 1e-8};
   int target_update_ev = 1000;
@@ -239,7 +232,6 @@ struct sfx_handle {
   int* skip = nullptr;            // [T]: the policy repeats the previous round (BwdArgs::skip)
   unsigned long long* skipc = nullptr;  // [0] policies checked, [1] skipped (rounds >= 1)
   bool skip_rounds = true;        // SFX_SKIP=0: every round recomputes every policy
-  bool shard_skip_fwd = true;     // SFX_SHARD_SKIPF=0: sharded rounds skip backward work only
   StepOut* dout = nullptr;  // device
   // set by the runner while it captures a step: the final k_ver (with action selection)
   // publishes to pub_res instead of a separate k_publish; pub_folded reports that it did
@@ -256,10 +248,13 @@ struct sfx_handle {
   int dxs_max = 1, dx_ntile = 1;
   float* dxpart = nullptr;
   unsigned* dxctr = nullptr;
-  bool split_dx = true;  // SFX_SPLIT_DX=0: one workgroup reduces all of N
-  bool gemv_fwd = true;  // SFX_GEMV_FWD=0: wide layers of a <= 4-row forward through the MFMA tiles
-  bool dw_wide = false;  // SFX_DW_WIDE=1: 64 x 64 dW tiles for wide hidden layers (measured: no gain)
   StepOut* hout = nullptr;  // pinned host
+  // generation of the handle's device state: bumped by every launch and every parameter / moment /
+  // role write made outside the native runner (touch()); a runner whose look-ahead chain was
+  // recorded at another generation drops it (the minibatch roles or the weights it forwarded with
+  // may have been overwritten in between: ADVICE r4)
+  unsigned long long gen = 0;
+  int in_runner = 0;  // > 0 while a sfx_runner_* call drives the handle
 
   int slot(int head) const { return (int)((mask >> head) & 1ull); }
   unsigned long long all_bits() const { return T >= 64 ? ~0ull : ((1ull << T) - 1ull); }
@@ -272,6 +267,10 @@ struct sfx_handle {
 };
 
 namespace {
+
+inline void touch(sfx_handle* h) {
+  if (!h->in_runner) ++h->gen;
+}
 
 void clear_graphs(sfx_handle* h) {
   for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
@@ -293,21 +292,38 @@ hipEvent_t prof_event(sfx_handle* h) {
 
 // Launch a kernel; when instrumentation is on, the dispatch packet itself records start and
 // stop timestamps into an event pair (hipExtLaunchKernelGGL: the timestamps rocprofv3 reads).
-template <typename... KArgs, typename... Args>
-void launch(sfx_handle* h, int kind, double bytes, void (*kern)(KArgs...), dim3 grid, dim3 block, Args... args) {
+//
+// The kernel is launched through the runtime entry point with an explicit argument array, not with
+// `kern<<<...>>>` on the pointer: a triple-chevron call through a pointer to a kernel is an indirect
+// call to its host handle, and a host build with clang's -fsanitize=function compiled that call
+// away -- the call configuration was pushed and no kernel launched, so the runner's first update
+// step never published (profiles/r05_ubsan_fn_disasm.txt).
+template <typename... KArgs, std::size_t... I>
+void launch_argv(sfx_handle* h, int kind, double bytes, const void* kern, dim3 grid, dim3 block,
+                 std::tuple<KArgs...>& t, std::index_sequence<I...>) {
+  void* argv[sizeof...(KArgs) > 0 ? sizeof...(KArgs) : 1] = {static_cast<void*>(&std::get<I>(t))...};
   if (!h->prof) {
-    hipLaunchKernelGGL(kern, grid, block, 0, h->stream, args...);
+    (void)hipLaunchKernel(kern, grid, block, argv, 0, h->stream);  // errors: LAUNCHCHK / hipGetLastError
     return;
   }
   hipEvent_t a = prof_event(h), b = prof_event(h);
-  hipExtLaunchKernelGGL(kern, grid, block, 0, h->stream, a, b, 0, args...);
+  (void)hipExtLaunchKernel(kern, grid, block, argv, 0, h->stream, a, b, 0);
   h->prof_recs.push_back({kind, bytes, a, b});
+}
+
+template <typename... KArgs, typename... Args>
+void launch(sfx_handle* h, int kind, double bytes, void (*kern)(KArgs...), dim3 grid, dim3 block, Args... args) {
+  static_assert(sizeof...(KArgs) == sizeof...(Args), "launch: argument count");
+  touch(h);
+  std::tuple<KArgs...> t(args...);  // each argument converted to the kernel's parameter type
+  launch_argv(h, kind, bytes, reinterpret_cast<const void*>(kern), grid, block, t, std::index_sequence_for<KArgs...>{});
 }
 
 // Capture `body` (which launches on h->stream) into a graph keyed by `key`, then replay
 // (launch = false: instantiate only -- sfx_runner_warm).
 template <class F>
 int run_graph(sfx_handle* h, const GraphKey& key, F body, bool launch_it = true) {
+  touch(h);
   if (!h->use_graphs || h->prof) return launch_it ? body() : SFX_OK;
   auto it = h->graphs.find(key);
   if (it == h->graphs.end()) {
@@ -391,11 +407,10 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     ninst += g.n;
     uniform = uniform && g.head0 == 0 && g.n == h->T;
   }
-  F.xcd = h->xcd && uniform && h->T > 1 ? 1 : 0;
+  F.xcd = uniform && h->T > 1 ? 1 : 0;
   F.nh = h->T;
   // layers 0 and 1 in one launch when layer 0 is small (its rows recomputed per tile in LDS)
-  const bool fuse01 = h->fuse_l0 && ex.l0 == 0 && h->NL >= 3 && h->L[0].K <= L0_KMAX && h->L[0].N <= L0_NMAX &&
-                      h->L[1].K % 32 == 0 && h->fwd_waves == 8;
+  const bool fuse01 = ex.l0 == 0 && h->NL >= 3 && h->L[0].K <= L0_KMAX && h->L[0].N <= L0_NMAX && h->L[1].K % 32 == 0;
   const int lend = ex.lN >= 0 ? ex.lN : h->NL;
   if (fuse01 && lend < 2) SFX_FAIL(SFX_E_STATE, "run_fwd: the fused layer-0+1 launch needs layer 1");
   for (int l = fuse01 ? 1 : ex.l0; l < lend; ++l) {
@@ -432,10 +447,7 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     // workgroups of 3 tiles without it -- it is slower where the tiles already fit the chip)
     long tiles32 = 0;
     for (const FwdGroup& g : groups) tiles32 += (long)F.ntN * cdiv(own && g.m > 0 ? g.m : M, 32) * g.n;
-    F.tail = !l0 && !qa && h->fwd_waves == 8 && (L.K % 32) == 0 && aligned &&
-                     (h->fwd_tail == 2 || (h->fwd_tail == 1 && own && tiles32 > h->ncu))
-                 ? 1
-                 : 0;
+    F.tail = !l0 && !qa && (L.K % 32) == 0 && aligned && own && tiles32 > h->ncu ? 1 : 0;
     F.ntM = fwd_row_tiles(M, F.tail);
     F.tpw = 1;
     long tiles = (long)F.ntN * F.ntM * ninst;
@@ -473,9 +485,9 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     // 192 workgroups, +1 %); Hopper TSF's 288 tiles stay unpaired (pairing measured 1 % slower)
     // (the look-ahead's row-split launches pair above that too: 640 tiles of 32 x 16 measured 11.8 us
     // unpaired, their workgroups dispatched over 5 us)
-    if (!qa && h->fwd_tpw > 1 && h->fwd_waves == 8 && F.ntN > 1 && 2 * tiles >= 3L * h->ncu &&
-        (tiles <= 2L * h->ncu || F.rowsplit) && (l0 || ((L.K % 32) == 0 && aligned)))
-      F.tpw = F.rowsplit && h->ahead_tp >= 3 && F.ntN >= h->ahead_tp ? h->ahead_tp : h->fwd_tpw;
+    if (!qa && h->fwd_tpw > 1 && F.ntN > 1 && 2 * tiles >= 3L * h->ncu && (tiles <= 2L * h->ncu || F.rowsplit) &&
+        (l0 || ((L.K % 32) == 0 && aligned)))
+      F.tpw = h->fwd_tpw;
     const int ntNb = cdiv(F.ntN, F.tpw);
     const dim3 grid = F.xcd ? dim3(8 * cdiv(h->T, 8) * ntNb * (F.rowsplit ? F.ntMs : F.ntM * F.ngroups))
                             : dim3(ntNb, ninst, F.ntM);
@@ -486,7 +498,7 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
       if (l0) by += 4.0 * g.n * ((double)h->L[0].N * h->L[0].K + h->L[0].N + m * h->L[0].K);
     }
     const bool tp2 = F.tpw > 1;
-    const bool gemv = !l0 && !qa && h->gemv_fwd && M <= GEMV_M && L.N >= GEMV_N && L.K % 16 == 0 &&
+    const bool gemv = !l0 && !qa && M <= GEMV_M && L.N >= GEMV_N && L.K % 16 == 0 &&
                       (l > 0 || ((uintptr_t)xa % 16 == 0 && (uintptr_t)xb % 16 == 0));
     if (gemv) {
       launch(h, K_FWD, by, k_fwd_gemv, dim3(cdiv(L.N, 64), ninst), dim3(256), h->G, F);
@@ -496,23 +508,13 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
                tp2 ? (h->bf16 ? k_fwd<true, 8, true, true, 2> : k_fwd<true, 8, true, false, 2>)
                    : (h->bf16 ? k_fwd<true, 8, true, true> : k_fwd<true, 8, true>),
                grid, dim3(512), h->G, F);
-    } else if (h->fwd_waves == 8 && F.tpw == 4) {  // (the tpw rule above requires the vector path)
-      launch(h, K_FWD, by, h->bf16 ? k_fwd<true, 8, false, true, 4> : k_fwd<true, 8, false, false, 4>, grid, dim3(512),
-             h->G, F);
-    } else if (h->fwd_waves == 8 && F.tpw == 3) {
-      launch(h, K_FWD, by, h->bf16 ? k_fwd<true, 8, false, true, 3> : k_fwd<true, 8, false, false, 3>, grid, dim3(512),
-             h->G, F);
-    } else if (h->fwd_waves == 8) {
+    } else {  // (the tpw rule above requires the vector path)
       const bool vec = (L.K % 32) == 0 && aligned;
       launch(h, K_FWD, by,
              !vec ? k_fwd<false, 8, false>
                   : tp2 ? (h->bf16 ? k_fwd<true, 8, false, true, 2> : k_fwd<true, 8, false, false, 2>)
                         : (h->bf16 ? k_fwd<true, 8, false, true> : k_fwd<true, 8, false>),
              grid, dim3(512), h->G, F);
-    } else {
-      const bool vec = (L.K % 64) == 0 && aligned;
-      launch(h, K_FWD, by, vec ? (h->bf16 ? k_fwd<true, 4, false, true> : k_fwd<true, 4, false>) : k_fwd<false, 4, false>,
-             grid, dim3(256), h->G, F);
     }
   }
   LAUNCHCHK();
@@ -568,7 +570,7 @@ struct TdgSpec {
 
 // 0: K2 as its own launch; 1: fused, d <= 8; 2: fused, d <= 16 (see tdg_rows)
 int tdg_variant(const sfx_handle* h) {
-  if (!h->fuse_tdg || (h->d & 3) != 0 || h->O > TDG_ROWS_O || h->A > 128) return 0;
+  if ((h->d & 3) != 0 || h->O > TDG_ROWS_O || h->A > 128) return 0;
   const long ta = (long)h->T * h->A;
   if (h->d <= 8 && 32 * ta <= 256 * 8) return 1;
   if (h->d <= 16 && 32 * ta <= 256 * 4) return 2;
@@ -578,10 +580,6 @@ int tdg_variant(const sfx_handle* h) {
 bool can_fuse_tdg(const sfx_handle* h) { return tdg_variant(h) != 0; }
 
 struct BwdExtra {
-  // called right after backward launch `hook_after` (0 = the first, fused-TD launch); TSF forks
-  // its own backward onto a side stream there (the ψ loss tail and output gradient are final)
-  std::function<int()> hook;
-  int hook_after = -1;
   int inc_step = 1;
   bool fuse_v0 = false;  // post-update forward of layer 0 into vRole (rows S1 ++ s_next)
   int vRole = R_V;
@@ -597,7 +595,7 @@ struct BwdExtra {
   std::function<bool(int li, int tail_at, const BwdArgs& A, int ntile, double bytes)> ride;
 };
 
-bool can_fuse_v0(const sfx_handle* h, int vM) { return h->fuse_v0 && h->L[0].K <= KFUSE && vM * h->L[0].K <= VFUSE; }
+bool can_fuse_v0(const sfx_handle* h, int vM) { return h->L[0].K <= KFUSE && vM * h->L[0].K <= VFUSE; }
 // the fused forward with the look-ahead rows as well (2 aM rows after vM, 16-B aligned, whole float4s)
 bool can_fuse_ahead(const sfx_handle* h, int vM, int aM) {
   const int K = h->L[0].K;
@@ -613,7 +611,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     RC(run_tdg(h, head0, nhead, td.guess, M, td.use_gpi, td.a, phi, td.gamma, td.next, td.next_stride, td.flag,
                td.xmax, td.poloff, td.dz_scale));
   BwdArgs A{};
-  A.xcd = h->xcd && nhead > 1 ? 1 : 0;
+  A.xcd = nhead > 1 ? 1 : 0;
   A.nhead = nhead;
   A.step_in_tail = fuse ? 0 : 1;
   A.tdg_use_gpi = td.use_gpi;
@@ -649,15 +647,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.train_w = r != nullptr;
   A.losses = losses;
   A.inc_step = ex.inc_step;
-  // opt-in 64 x 64 dW tiles (role_dw_wide) for wide hidden layers when several heads share a
-  // launch, which then stays within about one workgroup per CU (measured: no gain)
-  auto dw_nw = [&](int l) {
-    return l >= 1 && h->dw_wide && !h->bf16 && nhead >= 4 && h->L[l].N >= 128 &&
-                   h->L[l].K >= 64
-               ? 2
-               : 1;
-  };
-  auto dw_tiles = [&](int l) { return cdiv(h->L[l].N, 32 * dw_nw(l)) * cdiv(h->L[l].K, 64); };
+  auto dw_tiles = [&](int l) { return cdiv(h->L[l].N, 32) * cdiv(h->L[l].K, 64); };
   auto geo = [&](int l) {
     const LayerGeo& L = h->L[l];
     RoleGeo r{};
@@ -669,7 +659,6 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     r.xOff = l == 0 ? -1 : h->actOff[l - 1];
     r.dzOff = h->actOff[l];
     r.dzIn = l == 0 ? 0 : h->actOff[l - 1];
-    r.nw = dw_nw(l);
     return r;
   };
   // algorithmic bytes: dX reads W, dZ, X and writes dZ_{l-1}; dW reads dZ, X and does Adam's
@@ -695,7 +684,7 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     // wide layers: the dX tiles split N in <= 256-wide chunks over workgroups (not in a fused
     // TD launch)
     A.dxs = 1;
-    if (!A.tdg && h->split_dx && h->dxpart && h->L[l].N > DX_SPLIT_N && M <= 32 * cdiv(h->Mmax, 32) &&
+    if (!A.tdg && h->dxpart && h->L[l].N > DX_SPLIT_N && M <= 32 * cdiv(h->Mmax, 32) &&
         nhead <= h->T) {
       A.dxs = cdiv(h->L[l].N, DX_SPLIT_N);
       A.dxpart = h->dxpart;
@@ -718,7 +707,6 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
       launch(h, K_BWD, by, k_bwd_tdg<4, 4>, grid, dim3(256), h->G, A);
     else if (!(ex.ride && nhead == 1 && !A.xcd && ex.ride(li, tail_at, A, ntile, by)))
       launch(h, K_BWD, by, h->bf16 ? k_bwd<true> : k_bwd<false>, grid, dim3(256), h->G, A);
-    if (ex.hook && li == ex.hook_after) RC(ex.hook());
   }
   A.na = 0;
   A.dxs = 1;
@@ -745,7 +733,6 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
     launch(h, K_BWD, nhead * (dw_bytes(1) + dw_bytes(0)), h->bf16 ? k_bwd<true> : k_bwd<false>,
            A.xcd ? dim3(8 * cdiv(nhead, 8) * ntile) : dim3(ntile, nhead), dim3(256), h->G, A);
   LAUNCHCHK();
-  if (ex.hook && ex.hook_after >= h->NL - 1) RC(ex.hook());  // fewer launches than hook_after + 1
   return SFX_OK;
 }
 
@@ -794,10 +781,6 @@ int run_ver(sfx_handle* h, int M, int npol, bool sel, int post, const GpiArgs& g
     V.nblocks = (int)(grid.x * grid.y);
     h->pub_folded = true;
   }
-  if (h->debug_ver)  // SFX_DEBUG_VER=1 (sanitizer investigations): the folded publication's setup
-    std::fprintf(stderr, "k_ver M %d npol %d sel %d post %d rows %d grid %ux%u pub %p dctr %p done %p nblocks %d\n",
-                 V.M, V.npol, V.sel, V.post, V.rows, grid.x, grid.y, (void*)V.pub, (const void*)V.pub_dctr,
-                 (void*)V.done, V.nblocks);
   launch(h, K_VER, 4.0 * (double)M * npol * h->T * h->O + 4.0 * h->T * h->O, k_ver, grid, dim3(256), h->G, V);
   LAUNCHCHK();
   return SFX_OK;
@@ -810,6 +793,7 @@ void after_update(sfx_handle* h, int t) {
 
 int maybe_sync_target(sfx_handle* h, int t) {
   if (h->since_target[t] >= h->target_update_ev) {
+    touch(h);
     HIPCHK(hipMemcpyAsync(h->target_of(t), h->online_cur(t), sizeof(float) * h->P, hipMemcpyDeviceToDevice,
                           h->stream));
     if (h->bf16)
@@ -852,6 +836,7 @@ __global__ void k_to_bf16(const float* __restrict__ src, __bf16* __restrict__ ds
 }
 
 int refresh_bf16(sfx_handle* h, const float* src, __bf16* dst, long long n) {
+  touch(h);
   hipLaunchKernelGGL(k_to_bf16, dim3((unsigned)std::min<long long>(1024, (n + 255) / 256)), dim3(256), 0, h->stream, src,
                      dst, n);
   LAUNCHCHK();
@@ -978,7 +963,7 @@ int select_body(sfx_handle* h, const float* s, int task, int use_gpi, float* q, 
 int select_pick(sfx_handle* h, int task, int use_gpi, float* q, int64_t* out, const SelPub* pub) {
   const GpiArgs g = gpi_args(R_A, 0, 0, h->w + (size_t)task * h->dpad, nullptr, q, nullptr, nullptr, out, task, use_gpi, 1);
   const int TA = h->T * h->A;
-  if (h->sel1 && h->T <= 64 && h->A <= 256) {  // one workgroup per head, the last one picks
+  if (h->T <= 64 && h->A <= 256) {  // one workgroup per head, the last one picks
     const SelPub P = pub ? *pub : SelPub{};
     const dim3 grid(h->T), block((unsigned)(cdiv(h->A, 64) * 64));
     const double by = 4.0 * ((double)TA * h->d + h->d + (q ? TA : 0));
@@ -1228,16 +1213,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   h->dpad = align4(d);
   const char* eg = std::getenv("SFX_GRAPHS");
   h->use_graphs = !(eg && eg[0] == '0');
-  const char* ef = std::getenv("SFX_FUSE_TDG");
-  h->fuse_tdg = !(ef && ef[0] == '0');
-  const char* ev0 = std::getenv("SFX_FUSE_V0");
-  h->fuse_v0 = !(ev0 && ev0[0] == '0');
   const char* efp = std::getenv("SFX_FOLD_PUBLISH");
   h->fold_publish = !(efp && efp[0] == '0');
-  const char* ex = std::getenv("SFX_XCD");
-  h->xcd = !(ex && ex[0] == '0');
-  const char* efw = std::getenv("SFX_FWD_WAVES");
-  h->fwd_waves = efw && std::atoi(efw) == 4 ? 4 : 8;
   {
     int dev = 0, ncu = 0;
     if (hipGetDevice(&dev) == hipSuccess &&
@@ -1246,26 +1223,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   }
   const char* etp = std::getenv("SFX_FWD_TPW");
   h->fwd_tpw = etp && etp[0] == '1' ? 1 : FWD_TPW;
-  const char* eat = std::getenv("SFX_AHEAD_TP");
-  h->ahead_tp = eat && (eat[0] == '3' || eat[0] == '4') ? eat[0] - '0' : 2;
-  const char* eft = std::getenv("SFX_FWD_TAIL");
-  h->fwd_tail = eft && (eft[0] == '0' || eft[0] == '2') ? eft[0] - '0' : 1;
-  const char* edv = std::getenv("SFX_DEBUG_VER");
-  h->debug_ver = edv && edv[0] == '1';
-  const char* es1 = std::getenv("SFX_SEL1");
-  h->sel1 = !(es1 && es1[0] == '0');
-  const char* el0 = std::getenv("SFX_FUSE_L0");
-  h->fuse_l0 = !(el0 && el0[0] == '0');
-  const char* esd = std::getenv("SFX_SPLIT_DX");
-  h->split_dx = !(esd && esd[0] == '0');
-  const char* egv = std::getenv("SFX_GEMV_FWD");
-  h->gemv_fwd = !(egv && egv[0] == '0');
   const char* eqa = std::getenv("SFX_SHARD_QA");
   h->shard_qa = !(eqa && eqa[0] == '0');
-  const char* edw = std::getenv("SFX_DW_WIDE");
-  h->dw_wide = edw && edw[0] == '1';  // opt-in
-  const char* essf = std::getenv("SFX_SHARD_SKIPF");
-  h->shard_skip_fwd = !(essf && essf[0] == '0');
   const char* esk = std::getenv("SFX_SKIP");
   h->skip_rounds = !(esk && esk[0] == '0');
   int off = 0, ptorch = 0;
@@ -1430,6 +1389,7 @@ int sfx_load_head(sfx_t h, int t, int which, const float* params_host) {
   std::vector<float> buf(h->P);
   pack_head(h, params_host, buf.data());
   HIPCHK(hipStreamSynchronize(h->stream));
+  touch(h);
   HIPCHK(hipMemcpyAsync(which ? h->target_of(t) : h->online_cur(t), buf.data(), sizeof(float) * h->P,
                         hipMemcpyHostToDevice, h->stream));
   if (h->bf16) RC(refresh_bf16(h, which ? h->target_of(t) : h->online_cur(t), which ? h->tg16_of(t) : h->on16_cur(t), h->P));
@@ -1455,6 +1415,7 @@ int sfx_load_adam(sfx_t h, int t, const float* m_host, const float* v_host, int 
   pack_head(h, m_host, bm.data());
   pack_head(h, v_host, bv.data());
   HIPCHK(hipStreamSynchronize(h->stream));
+  touch(h);
   HIPCHK(hipMemcpyAsync(h->am_cur(t), bm.data(), sizeof(float) * h->P, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->av_cur(t), bv.data(), sizeof(float) * h->P, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->step + t, &step, sizeof(int), hipMemcpyHostToDevice, h->stream));
@@ -1482,6 +1443,7 @@ int sfx_load_w(sfx_t h, int t, const float* w_host) {
   RC(settle(h));
   if (!valid_w(h, t) || !w_host) SFX_FAIL(SFX_E_ARG, "bad args");
   HIPCHK(hipStreamSynchronize(h->stream));
+  touch(h);
   HIPCHK(hipMemcpyAsync(h->w + (size_t)t * h->dpad, w_host, sizeof(float) * h->d, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   return SFX_OK;
@@ -1493,6 +1455,7 @@ int sfx_load_w_state(sfx_t h, int t, const float* w_host, const float* wm_host, 
   if (!valid_w(h, t) || !w_host || !wm_host || !wv_host) SFX_FAIL(SFX_E_ARG, "bad args");
   HIPCHK(hipStreamSynchronize(h->stream));
   const size_t o = (size_t)t * h->dpad, n = sizeof(float) * h->d;
+  touch(h);
   HIPCHK(hipMemcpyAsync(h->w + o, w_host, n, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->wm + o, wm_host, n, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->wv + o, wv_host, n, hipMemcpyHostToDevice, h->stream));
@@ -1680,6 +1643,7 @@ int sfx_set_precision(sfx_t h, int precision) {
   RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   if (precision != SFX_PREC_FP32 && precision != SFX_PREC_BF16) SFX_FAIL(SFX_E_ARG, "unknown precision");
+  touch(h);
   const bool want = precision == SFX_PREC_BF16;
   if (want == h->bf16) return SFX_OK;
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -1806,6 +1770,7 @@ int sfx_set_since_target(sfx_t h, int t, int count) {
 int sfx_sync_target(sfx_t h, int t) {
   RC(settle(h));
   if (!valid_head(h, t)) SFX_FAIL(SFX_E_ARG, "bad head");
+  touch(h);
   HIPCHK(hipMemcpyAsync(h->target_of(t), h->online_cur(t), sizeof(float) * h->P, hipMemcpyDeviceToDevice, h->stream));
   return SFX_OK;
 }

@@ -1175,7 +1175,6 @@ struct RoleGeo {
   int xOff;   // input activation offset (R_S block); < 0: the minibatch states x0
   int dzOff;  // this layer's output-gradient offset (dz block)
   int dzIn;   // dX role: offset of the gradient it writes (layer l-1)
-  int nw;     // dW role: 16-column groups per wave (1: 32 x 64 tiles, role_dw; 2: 64 x 64, role_dw_wide)
 };
 
 struct BwdArgs {
@@ -1888,132 +1887,6 @@ __device__ __forceinline__ void role_dw(const Geo& G, const BwdArgs& A, int head
   if (fuse) fused_v0<C>(G, A, L, head, nbase, sW, sB, sX, sm.sWt, sm.sBt);
 }
 
-// dW + Adam of a 64 (output columns) x 64 (inputs) tile of a wide hidden layer (RoleGeo::nw == 2,
-// several heads per launch): role_dw with two 16-column groups per wave, so the launch needs
-// half the workgroups and stays within about one per CU (the 32-column tiles put 384 / 320
-// workgroups on 256 CUs at the C2 shape, and the co-resident pairs finish last).  Per column
-// the accumulation order is role_dw's, so the results are the same bits.  Layer 0 (with the
-// fused post-update forward) keeps role_dw.
-__device__ __forceinline__ void role_dw_wide(const Geo& G, const BwdArgs& A, int head, const RoleGeo& L, int tile) {
-  constexpr int NW = 2;
-  const int N = L.N, K = L.K, M = A.M;
-  const int ntk = (K + 63) >> 6;
-  const int kt = tile % ntk, nt = tile / ntk;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
-  const int n0 = nt * 32 * NW + (wave & 1) * 16 * NW, k0 = kt * 64 + (wave >> 1) * 32;
-  const float* dZ = G.dzp(head, L.dzOff);
-  const float* X = layer_input(G, A, head, L.xOff);
-  const int rs = rslot(A.mask, head);
-  const long long ro = G.slot_off(rs, head), wo = G.slot_off(rs ^ 1, head);
-  const float* Pr = G.online + ro;
-  const float* Mr = G.am + ro;
-  const float* Vr = G.av + ro;
-  float* Pw = G.online + wo;
-  float* Mw = G.am + wo;
-  float* Vw = G.av + wo;
-  const AdamC c = load_adamc<false>(G.adamc + head);
-  const int cx = step_cancelled(G.cancel);
-  const int kb0 = k0 + r, kb1 = k0 + 16 + r;
-  // optimizer state of the 8·NW weights this lane updates, requested first
-  float pp[8 * NW], pm[8 * NW], pv[8 * NW];
-  bool ok[8 * NW];
-#pragma unroll
-  for (int s = 0; s < NW; ++s)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = n0 + 16 * s + g * 4 + i;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int k = h ? kb1 : kb0;
-        const int e = (s * 4 + i) * 2 + h;
-        ok[e] = n < N && k < K;
-        const size_t off = (size_t)L.wOff + (size_t)n * K + k;
-        pp[e] = ok[e] ? Pr[off] : 0.f;
-        pm[e] = ok[e] ? Mr[off] : 0.f;
-        pv[e] = ok[e] ? Vr[off] : 0.f;
-      }
-    }
-  // biases of columns n0 + 16 s + r (lanes r of the k-half-0 waves of the kt == 0 tiles),
-  // gradients from the dZ operands in registers
-  bool dob[NW];
-  float bp[NW], bm[NW], bv[NW];
-#pragma unroll
-  for (int s = 0; s < NW; ++s) {
-    const int nb = n0 + 16 * s + r;
-    dob[s] = kt == 0 && wave < 2 && g == 0 && nb < N;
-    bp[s] = dob[s] ? Pr[L.bOff + nb] : 0.f;
-    bm[s] = dob[s] ? Mr[L.bOff + nb] : 0.f;
-    bv[s] = dob[s] ? Vr[L.bOff + nb] : 0.f;
-  }
-  __builtin_amdgcn_sched_barrier(0);  // keep those loads ahead of the MFMA operands
-  floatx4 acc[NW][2];
-  float bsum[NW];
-#pragma unroll
-  for (int s = 0; s < NW; ++s) {
-    acc[s][0] = floatx4{0.f, 0.f, 0.f, 0.f};
-    acc[s][1] = floatx4{0.f, 0.f, 0.f, 0.f};
-    bsum[s] = 0.f;
-  }
-  for (int mc = 0; mc < M; mc += MT) {
-    float av[NW][MT / 4], bv0[MT / 4], bv1[MT / 4];
-#pragma unroll
-    for (int j = 0; j < MT / 4; ++j) {
-      const int m = mc + 4 * j + g;
-      const bool okm = m < M;
-#pragma unroll
-      for (int s = 0; s < NW; ++s) {
-        const int nn = n0 + 16 * s + r;
-        av[s][j] = (okm && nn < N) ? ldc<false>(dZ + (size_t)m * N + nn) : 0.f;
-      }
-      bv0[j] = (okm && kb0 < K) ? X[(size_t)m * K + kb0] : 0.f;
-      bv1[j] = (okm && kb1 < K) ? X[(size_t)m * K + kb1] : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < MT / 4; ++j)
-#pragma unroll
-      for (int s = 0; s < NW; ++s) {
-        acc[s][0] = mfma4(av[s][j], bv0[j], acc[s][0]);
-        acc[s][1] = mfma4(av[s][j], bv1[j], acc[s][1]);
-      }
-#pragma unroll
-    for (int j = 0; j < MT / 4; ++j)
-#pragma unroll
-      for (int s = 0; s < NW; ++s) bsum[s] = __fadd_rn(bsum[s], av[s][j]);  // rows mc + 4j + g
-  }
-#pragma unroll
-  for (int s = 0; s < NW; ++s) {  // + the other three row classes, fixed order
-    bsum[s] = __fadd_rn(bsum[s], __shfl_xor(bsum[s], 16));
-    bsum[s] = __fadd_rn(bsum[s], __shfl_xor(bsum[s], 32));
-  }
-  PROBE_MARK();
-#pragma unroll
-  for (int s = 0; s < NW; ++s)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = n0 + 16 * s + g * 4 + i;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int e = (s * 4 + i) * 2 + h;
-        if (ok[e] && !cx) {
-          const size_t off = (size_t)L.wOff + (size_t)n * K + (h ? kb1 : kb0);
-          adam_apply(pp[e], pm[e], pv[e], acc[s][h][i], c);
-          st_param<false>(Pw + off, pp[e]);
-          st_moment(Mw + off, pm[e]);
-          st_moment(Vw + off, pv[e]);
-        }
-      }
-    }
-#pragma unroll
-  for (int s = 0; s < NW; ++s)
-    if (dob[s] && !cx) {
-      const int nb = n0 + 16 * s + r;
-      adam_apply(bp[s], bm[s], bv[s], bsum[s], c);
-      stc<false>(Pw + L.bOff + nb, bp[s]);
-      st_moment(Mw + L.bOff + nb, bm[s]);
-      st_moment(Vw + L.bOff + nb, bv[s]);
-    }
-}
-
 // loss finalisation, optional w step, Adam step counter (one workgroup per head)
 // Deterministic block sum (fixed pairwise tree over 256 partials) -- result in every thread.
 __device__ __forceinline__ float block_sum(float v, float* red) {
@@ -2105,10 +1978,7 @@ __device__ __forceinline__ void bwd_body(const Geo& G, const BwdArgs& A, int hea
   bx -= A.nc;
   if (bx < A.nb) {
     if (skip) return;
-    if (A.rb.nw == 2 && !BF)  // bf16 mode never builds wide tiles (run_bwd)
-      role_dw_wide(G, A, head, A.rb, bx);
-    else
-      role_dw<false, BF>(G, A, head, A.rb, bx, false);
+    role_dw<false, BF>(G, A, head, A.rb, bx, false);
     PROBE_REC(5, pt0);
     return;
   }
@@ -2329,7 +2199,7 @@ __device__ __forceinline__ void publish_result(const int64_t* sel, const int* fl
   const long long s1 = __hip_atomic_load(sel + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int cx = __hip_atomic_load(cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const long long seq = *dctr;
+  const long long seq = __hip_atomic_load(dctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   HostResult* out = ring + (seq & (RES_RING - 1));
   out->sel0 = s0;
   out->sel1 = s1;
@@ -2443,14 +2313,13 @@ __global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
   PROBE_T(pt0);
   ver_block(G, V);
   if (V.pub) {
-    // this workgroup's sel stores / flag atomic are sc1 (coherent) and issued by wave 0:
-    // wait for them, then arrive; the last arrival publishes
+    // every wave's stores (the selection, the flag) are ordered before the arrival by the barrier
+    // and the arrival's agent-scope release; the last arrival acquires them all before it reads
+    // the selection and the flag and publishes (the counter is re-armed by the last arrival and by
+    // every runner gate: GateArgs::rearm)
     __syncthreads();
     if (threadIdx.x == 0) {
-      __builtin_amdgcn_s_waitcnt(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned prev = __hip_atomic_fetch_add(V.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("" ::: "memory");
+      const unsigned prev = __hip_atomic_fetch_add(V.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       if (prev == (unsigned)V.nblocks - 1) {
         publish_result(V.g.sel_out, V.flag, V.pub, V.pub_dctr, G.cancel, G.nonfin);
         __hip_atomic_store(V.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2539,6 +2408,7 @@ struct GateArgs {
   const float* lms_phi;  // in the staging the gate copies from
   const float* lms_r;
   float lms_alpha, pad3_;
+  unsigned *rearm0, *rearm1;  // arrival counters of the step's folded publications (k_ver, k_sel1m)
 };
 
 // Wait for the host's go of this step (bounded); 1 if the step may run, 0 if it is cancelled.
@@ -2553,7 +2423,7 @@ struct GateArgs {
 // its err back and keeps waiting (up to `hard`).
 __device__ __forceinline__ int gate_wait(const GateArgs& g) {
   int ok = 1;
-  const long long want = *g.dctr + 1;
+  const long long want = __hip_atomic_load(g.dctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   const long long t0 = wall_clock64();
   unsigned it = 0;
   bool held = false;
@@ -2575,8 +2445,11 @@ __device__ __forceinline__ int gate_wait(const GateArgs& g) {
     }
     __builtin_amdgcn_s_sleep(8);
   }
-  *g.dctr = want;
+  __hip_atomic_store(g.dctr, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   *g.cancel = ok ? 0 : 1;
+  // the step's folded publications count their arrivals from zero whatever an earlier launch left
+  if (g.rearm0) __hip_atomic_store(g.rearm0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (g.rearm1) __hip_atomic_store(g.rearm1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return ok;
 }
 
@@ -2803,10 +2676,8 @@ __global__ __launch_bounds__(256) void k_sel1m(Geo G, GpiArgs A, SelPub P, SelSc
     if (tid == 0) {
       __hip_atomic_store(S->key + t, argmax_key(mx, t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(S->act + t, am, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_s_waitcnt(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned prev = __hip_atomic_fetch_add(&S->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("" ::: "memory");
+      // release this head's key, acquire every earlier arrival's (the last arrival reads them all)
+      const unsigned prev = __hip_atomic_fetch_add(&S->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       if (prev == (unsigned)T - 1) {
         unsigned long long best = 0ull;
         for (int u = 0; u < T; ++u) {

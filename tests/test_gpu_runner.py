@@ -92,12 +92,11 @@ def test_runner_matches_oracle(pipeline, monkeypatch):
     eng.close()
 
 
-def test_runner_wide_dw_tiles(monkeypatch):
-    """Opt-in 64 x 64 dW tiles (SFX_DW_WIDE=1, role_dw_wide): used for the 128-wide hidden
-    layers here (4 heads share each backward launch) -- same results as the oracle."""
+def test_runner_four_heads_wide_backward():
+    """4 heads sharing each backward launch at 128-wide hidden layers (the geometry the removed
+    64 x 64 dW tiles were built for): the 32 x 64 tiles give the oracle's results."""
     from sfx.runner import NativeEnvLoop
 
-    monkeypatch.setenv("SFX_DW_WIDE", "1")
     spec = R.Spec(17, 128, 7, 8, ("relu", "relu"))
     T, ev, alpha, n = 4, 5, 0.05, 16
     eng, st = make(spec, T, ev)
@@ -513,6 +512,56 @@ def test_lookahead_is_bit_exact(force, ev, monkeypatch):
     assert s0["ahead_pre_steps"] == 0
     assert s1["ahead_pre_steps"] > n // 2, s1
     assert s1["ahead_own_forward_steps"] > 0, s1  # dirty minibatches (and syncs) ran their own forward
+
+
+@pytest.mark.parametrize("between", ["load_head", "sync_target", "update_all", "gpi"])
+def test_lookahead_chain_dropped_by_calls_between_runs(between, monkeypatch):
+    """The look-ahead chain (the last step of a run forwarded the next step's minibatch) must not
+    survive a call on the handle between two runs that writes parameters or the minibatch roles
+    (ADVICE r4: sfx_handle::gen).  Each call here changes what the next step's forward would see;
+    heads, moments and every action must stay IDENTICAL to SFX_AHEAD=0 with the same calls."""
+    from sfx.runner import NativeEnvLoop
+
+    spec = R.Spec(17, 64, 7, 8, ("relu", "relu"))
+    T, n = 4, 24
+    out = {}
+    for ahead in ("1", "0"):
+        monkeypatch.setenv("SFX_AHEAD", ahead)
+        eng, _ = make(spec, T, 1000, max_batch=16)
+        loop = NativeEnvLoop(eng, batch=16, capacity=400, gamma=0.9, epsilon=0.2, alpha_w=0.05, episode_len=50, seed=4)
+        loop.prefill(200)
+        loop.set_task(1)
+        loop.record(2 * n)
+        loop.run(n)
+        gen = torch.Generator().manual_seed(11)
+        if between == "load_head":
+            h = eng.get_head(2, 0)
+            eng.load_head(2, h + 1e-2 * torch.randn(h.shape, generator=gen), 0)
+        elif between == "sync_target":
+            eng.sync_target(1)
+        elif between == "update_all":
+            B = 16
+            s, s1 = torch.randn(B, spec.n_s, generator=gen), torch.randn(B, spec.n_s, generator=gen)
+            a = torch.randint(0, spec.A, (B,), generator=gen)
+            phi = torch.rand(B, spec.d, generator=gen)
+            eng.update_all(s.cuda(), a.cuda(), phi.cuda(), s1.cuda(), torch.full((B,), 0.9).cuda())
+        else:  # a GPI over other states (forwards into the handle's activation roles)
+            eng.gpi(torch.randn(16, spec.n_s, generator=gen).cuda())
+        eng.synchronize()
+        loop.run(n)
+        recs = loop.records()
+        heads = torch.stack([eng.get_head(t, 0) for t in range(T)])
+        moms = [eng.get_adam(t) for t in range(T)]
+        out[ahead] = (heads, moms, [(r["c"], r["a_greedy"]) for r in recs], loop.action(), loop.stats())
+        loop.close()
+        eng.close()
+    h1, m1, a1, f1, s1 = out["1"]
+    h0, m0, a0, f0, s0 = out["0"]
+    assert a1 == a0 and f1 == f0
+    assert torch.equal(h1, h0)
+    for (ma, va, sa), (mb, vb, sb) in zip(m1, m0):
+        assert torch.equal(ma, mb) and torch.equal(va, vb) and sa == sb
+    assert s1["ahead_pre_steps"] > n, s1
 
 
 @pytest.mark.parametrize("schedule,upd_use_gpi,ev", [("active", True, 7), ("active", False, 1000), ("tsf", True, 7),

@@ -105,15 +105,14 @@ def test_tsf_full_c3_vs_oracle(K):
     eng.close()
 
 
-@pytest.mark.parametrize("n_s,B,K,G,d,fork", [(20, 13, 5, 24, 7, "1"), (9, 7, 9, 33, 5, "0"), (30, 64, 2, 16, 12, "1")])
-def test_tsf_ragged_shapes_vs_oracle(n_s, B, K, G, d, fork, monkeypatch):
+@pytest.mark.parametrize("n_s,B,K,G,d", [(20, 13, 5, 24, 7), (9, 7, 9, 33, 5), (30, 64, 2, 16, 12)])
+def test_tsf_ragged_shapes_vs_oracle(n_s, B, K, G, d):
     """Shapes that exercise the kernels' edges: n_s > 16 (32 lanes per flow row), batches that
     leave partial row groups, d not a multiple of 4, G not a multiple of the g-Linear column
-    block, the largest batch (64), with and without the side-stream fork (SFX_TSF_FORK)."""
+    block, the largest batch (64)."""
     from sfx.engine import SFEngine
     from sfx.init import reference_heads
 
-    monkeypatch.setenv("SFX_TSF_FORK", fork)
     T = 3
     spec = R.Spec(n_s, 24, 5, d, ("relu", "relu"))
     gs = R.GSpec(n_s, G, K)
