@@ -50,6 +50,8 @@ class ReplayBuffer:
         n_s = int(torch.as_tensor(state).numel())
         d = int(torch.as_tensor(reward).numel())
         n_s1 = int(torch.as_tensor(next_state).numel())
+        if n_s1 != n_s:  # one state width: the gather reads both state rows with it
+            raise ValueError(f"ReplayBuffer: next_state has {n_s1} entries, state {n_s}")
         cap = self.n_samples
         self._ring = (torch.zeros(cap, n_s, device=dev), torch.zeros(cap, dtype=torch.int64, device=dev),
                       torch.zeros(cap, d, device=dev), torch.zeros(cap, n_s1, device=dev))
@@ -76,6 +78,10 @@ class ReplayBuffer:
         rs, ra, rr, rs1 = self._ring
         j = self.index
         if self._native(state, action, reward, next_state) and action.numel() == 1:
+            # the kernel reads the ring's widths from each tensor: a shorter one would be read past its end
+            for name, x, row in (("state", state, rs), ("reward", reward, rr), ("next_state", next_state, rs1)):
+                if x.numel() != row.shape[1]:
+                    raise ValueError(f"ReplayBuffer.append: {name} has {x.numel()} entries, the ring {row.shape[1]}")
             from sfx import _lib
 
             _lib.check(_lib.lib.sfx_replay_put(torch.cuda.current_stream(self.device).cuda_stream, rs.data_ptr(),
