@@ -88,8 +88,40 @@ class SF:
             self._count(task_index, task)
         return q, task
 
+    # The GPI counters (features/successor.py:266-272 increments them inside GPI).  A device task
+    # tensor is not read back at every call -- that would be a device synchronisation per env step
+    # beside the agent's own (its greedy action) -- but kept, and the counts are settled on the host
+    # whenever ``gpi_counters`` is read (GPI_usage_percent, the agents' logs) or every _GPI_SETTLE
+    # calls: one transfer for all of them.  The counts read are the reference's.
+    _GPI_SETTLE = 4096
+
+    @property
+    def gpi_counters(self):
+        pend = self.__dict__.get("_gpi_pending")
+        if pend:
+            self._gpi_pending = []
+            counts = self.__dict__["_gpi_counts"]
+            flat = [p[1].reshape(-1) for p in pend]
+            idx = torch.cat([t.to(flat[0].device) for t in flat]).cpu().numpy()
+            off = 0
+            for (ti, _), t in zip(pend, flat):  # per call, as the reference's counts[ti][idx] += 1
+                counts[ti][idx[off:off + t.numel()]] += 1
+                off += t.numel()
+        return self.__dict__.get("_gpi_counts")
+
+    @gpi_counters.setter
+    def gpi_counters(self, value):
+        self.__dict__["_gpi_pending"] = []
+        self.__dict__["_gpi_counts"] = value
+
     def _count(self, task_index, task):
-        idx = task.detach().cpu().numpy() if torch.is_tensor(task) else np.asarray(task)
+        if torch.is_tensor(task) and task.device.type != "cpu":
+            pend = self.__dict__.setdefault("_gpi_pending", [])
+            pend.append((task_index, task.detach()))
+            if len(pend) >= self._GPI_SETTLE:
+                self.gpi_counters
+            return
+        idx = task.detach().numpy() if torch.is_tensor(task) else np.asarray(task)
         self.gpi_counters[task_index][idx] += 1
 
     def GPI_usage_percent(self, task_index):

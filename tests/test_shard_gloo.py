@@ -4,6 +4,7 @@ ranks, GPI maxima and the selection key all-reduced (MAX).  Against the unsharde
 import os
 import tempfile
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -54,7 +55,9 @@ def _worker(rank, port, q, rounds):
     heads = [None] * WORLD
     dist.all_gather_object(heads, be.st.online)
     if rank == 0:
-        q.put((actions, torch.cat(heads), be.w, step.stats))
+        # numpy, pickled by value: a torch tensor goes through a shared-memory fd that the parent
+        # fetches from this process while unpickling -- refused once this process has exited
+        q.put((actions, torch.cat(heads).numpy(), np.asarray(be.w), step.stats))
         q.close()
         q.join_thread()  # the result is in the pipe before the teardown (a crash there reset the pipe once)
     dist.destroy_process_group()
@@ -77,6 +80,7 @@ def test_sharded_step_matches_unsharded_oracle(rounds):
     for p in procs:
         p.start()
     actions, heads, w, stats = q.get(timeout=300)
+    heads, w = torch.from_numpy(heads), torch.from_numpy(w)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -146,7 +150,8 @@ def _tsf_worker(rank, port, q, use_gpi):
     parts = [None] * WORLD
     dist.all_gather_object(parts, (be.st.online, be.st.g))
     if rank == 0:
-        q.put((actions, torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts]), be.st.h, be.w))
+        q.put((actions, torch.cat([p[0] for p in parts]).numpy(), torch.cat([p[1] for p in parts]).numpy(),
+               np.asarray(be.st.h), np.asarray(be.w)))  # by value (see _worker)
         q.close()
         q.join_thread()
     dist.destroy_process_group()
@@ -164,6 +169,7 @@ def test_sharded_tsf_matches_unsharded_oracle(use_gpi):
     for p in procs:
         p.start()
     actions, heads, gg, h, w = q.get(timeout=300)
+    heads, gg, h, w = (torch.from_numpy(x) for x in (heads, gg, h, w))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
