@@ -380,9 +380,9 @@ struct FwdExtra {
   const int* skip = nullptr;  // post-update forward of rounds r >= 1 (FwdArgs::skip; one group)
   int* qh = nullptr;          // sharded rounds: the local heads' maxima terms (FwdArgs::qh)
   int* qhs = nullptr;
-  // the first launch when it is the fused layer-0+1 one (k_fwd<true, 8, true, BF>, one column
-  // tile per workgroup): issued by the caller instead, with workgroups of its own riding along
-  // (TSF: k_fwd_tsf); returns true when it launched
+  // the first launch when it is the fused layer-0+1 one (k_fwd<true, 8, true, BF, TP>): issued by
+  // the caller instead, with workgroups of its own riding along (TSF: k_fwd_tsf); returns true when
+  // it launched
   std::function<bool(const FwdArgs& F, dim3 grid, double bytes)> ride_l0;
 };
 
@@ -481,11 +481,13 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     }
     // two column tiles per workgroup (an L0 launch's in-tile layer 0 computed once for them, a
     // plain launch's X operands loaded once) when the tiles would put two workgroups on at least
-    // half the CUs and fit the chip when paired: C2's first forward of three roles (384 tiles ->
-    // 192 workgroups, +1 %); Hopper TSF's 288 tiles stay unpaired (pairing measured 1 % slower)
-    // (the look-ahead's row-split launches pair above that too: 640 tiles of 32 x 16 measured 11.8 us
-    // unpaired, their workgroups dispatched over 5 us)
-    if (!qa && h->fwd_tpw > 1 && F.ntN > 1 && 2 * tiles >= 3L * h->ncu && (tiles <= 2L * h->ncu || F.rowsplit) &&
+    // half the CUs and, paired, fit the two workgroups a CU holds: C2's first forward of three roles
+    // (384 tiles -> 192 workgroups, +1 %); the TSF look-ahead select's layer-0+1 and layer-2
+    // launches (544 tiles: unpaired, the last 32 waited a whole workgroup body for a slot);
+    // Hopper TSF's 288 tiles stay unpaired (pairing measured 1 % slower) (the look-ahead's
+    // row-split launches pair above that too: 640 tiles of 32 x 16 measured 11.8 us unpaired, their
+    // workgroups dispatched over 5 us)
+    if (!qa && h->fwd_tpw > 1 && F.ntN > 1 && 2 * tiles >= 3L * h->ncu && (tiles <= 4L * h->ncu || F.rowsplit) &&
         (l0 || ((L.K % 32) == 0 && aligned)))
       F.tpw = h->fwd_tpw;
     const int ntNb = cdiv(F.ntN, F.tpw);
@@ -503,7 +505,7 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     if (gemv) {
       launch(h, K_FWD, by, k_fwd_gemv, dim3(cdiv(L.N, 64), ninst), dim3(256), h->G, F);
     } else if (l0) {
-      if (!(ex.ride_l0 && !tp2 && !F.xcd && ex.ride_l0(F, grid, by)))
+      if (!(ex.ride_l0 && !F.xcd && ex.ride_l0(F, grid, by)))
         launch(h, K_FWD, by,
                tp2 ? (h->bf16 ? k_fwd<true, 8, true, true, 2> : k_fwd<true, 8, true, false, 2>)
                    : (h->bf16 ? k_fwd<true, 8, true, true> : k_fwd<true, 8, true>),
@@ -1136,6 +1138,20 @@ int sfx_replay_put(void* stream, float* rs, float* rphi, float* rs1, int64_t* ra
   return SFX_OK;
 }
 
+int sfx_host_alloc(size_t bytes, void** out) {
+  if (!out || bytes == 0) SFX_FAIL(SFX_E_ARG, "sfx_host_alloc: bad arguments");
+  *out = nullptr;
+  if (hipHostMalloc(out, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+    SFX_FAIL(SFX_E_HIP, "sfx_host_alloc: hipHostMalloc failed");
+  std::memset(*out, 0, bytes);
+  return SFX_OK;
+}
+
+int sfx_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+  return SFX_OK;
+}
+
 int sfx_replay_gather(void* stream, const float* rs, const float* rphi, const float* rs1, const int64_t* ra,
                       const float* rg, const int64_t* idx, const float* gam, int B, float* S, float* PHI, float* S1,
                       int64_t* A, float* G, int n_s, int d) {
@@ -1482,17 +1498,36 @@ int sfx_w_ptr(sfx_t h, int t, float** w_dev) {
 }
 
 int sfx_gpi(sfx_t h, const float* S, int B, const float* w, float* psi, float* q, int64_t* task, int64_t* next) {
-  RC(settle(h));
   if (!h || !S || !w || B < 1) SFX_FAIL(SFX_E_ARG, "bad args");
-  const GraphKey key = make_key(1, {B}, h->mask, {S, w, psi, q, task, next});
-  return run_graph(h, key, [&]() -> int {
-    for (int row0 = 0; row0 < B; row0 += h->Mmax) {
-      const int m = B - row0 < h->Mmax ? B - row0 : h->Mmax;
-      RC(run_fwd(h, {{R_G, P_ONLINE, 1, 0, h->T}}, m, S + (size_t)row0 * h->n_s, nullptr));
-      RC(run_gpi(h, gpi_args(R_G, 0, row0, w, psi, q, task, next, nullptr, 0, 0, m)));
-    }
-    return SFX_OK;
-  });
+  auto gpi = [&]() -> int {
+    const GraphKey key = make_key(1, {B}, h->mask, {S, w, psi, q, task, next});
+    return run_graph(h, key, [&]() -> int {
+      for (int row0 = 0; row0 < B; row0 += h->Mmax) {
+        const int m = B - row0 < h->Mmax ? B - row0 : h->Mmax;
+        RC(run_fwd(h, {{R_G, P_ONLINE, 1, 0, h->T}}, m, S + (size_t)row0 * h->n_s, nullptr));
+        RC(run_gpi(h, gpi_args(R_G, 0, row0, w, psi, q, task, next, nullptr, 0, 0, m)));
+      }
+      return SFX_OK;
+    });
+  };
+  if (h->lazy_finish && h->pend.active && h->pend.update) {
+    // An all-task update (sfx_update_all) is pending its verdict.  Queue this GPI behind it first,
+    // on the slots that update writes (h->mask flips to them when the verdict is collected), so it
+    // runs while the host waits for the verdict; only when the verdict needs host rounds -- which
+    // rewrite those slots -- is it queued again behind them.  (The drop-in's agent loop calls GPI
+    // right after the update: the wait then ends with the GPI done, not before it is launched.)
+    const unsigned long long m0 = h->mask;
+    h->mask = m0 ^ h->all_bits();
+    const int rc = gpi();
+    h->mask = m0;
+    RC(rc);
+    const long long fb = h->steps_fallback;
+    RC(settle(h));
+    if (h->steps_fallback == fb) return SFX_OK;
+    return gpi();
+  }
+  RC(settle(h));
+  return gpi();
 }
 
 int sfx_successors(sfx_t h, const float* S, int B, int which, float* psi) {
@@ -1741,7 +1776,16 @@ int sfx_lms(sfx_t h, int t, const float* phi, const float* r, float alpha) {
   RC(settle(h));
   if (!valid_w(h, t) || !phi || !r) SFX_FAIL(SFX_E_ARG, "bad args");
   launch(h, K_LMS, 4.0 * (3.0 * h->d + 1), k_lms, dim3(1), dim3(256), h->w + (size_t)t * h->dpad, phi, r, alpha,
-         h->d);
+         h->d, 0.f);
+  LAUNCHCHK();
+  return SFX_OK;
+}
+
+int sfx_lms_value(sfx_t h, int t, const float* phi, float r, float alpha) {
+  RC(settle(h));
+  if (!valid_w(h, t) || !phi) SFX_FAIL(SFX_E_ARG, "bad args");
+  launch(h, K_LMS, 4.0 * (3.0 * h->d), k_lms, dim3(1), dim3(256), h->w + (size_t)t * h->dpad, phi,
+         static_cast<const float*>(nullptr), alpha, h->d, r);
   LAUNCHCHK();
   return SFX_OK;
 }

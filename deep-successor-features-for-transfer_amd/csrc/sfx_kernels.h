@@ -1335,6 +1335,7 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
     if (idx < n) sm.q[idx] = q;
   }
   __syncthreads();
+  PROBE_AT(5);
   // ---- stage C: max over heads per (row, action)   (torch.max(q1, axis=1))
   for (int i = tid; i < (xm ? 0 : nb * Aa); i += 256) {
     const int bl = i / fA, a = i - bl * Aa;
@@ -1344,6 +1345,7 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
     sm.m[i] = mx;
   }
   __syncthreads();
+  PROBE_AT(6);
   // ---- stage D: first argmax over actions
   int differs = prev == nullptr || m0 != 0 || nb != M;  // skipping needs every row of the policy
   for (int bl = tid; bl < nb; bl += 256) {
@@ -1390,6 +1392,7 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
     sq[i] = e2;
   }
   if (__syncthreads_or(nf) && tid == 0 && G.nonfin) atomicOr(G.nonfin, 1);
+  PROBE_AT(7);
   if (pub) {
     float4* gout4 = reinterpret_cast<float4*>(G.dzp(pol, NLm) + (size_t)m0 * O);
     for (int i = tid; i < n4; i += 256) {
@@ -1411,6 +1414,7 @@ __device__ int tdg_rows(const Geo& G, const BwdArgs& A, int pol, int m0, bool pu
       G.rowloss[(long long)pol * MMAX + m0 + bl] = sacc;
     }
   }
+  PROBE_AT(8);
   return 0;
 }
 
@@ -2318,10 +2322,13 @@ __global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
     // the selection and the flag and publishes (the counter is re-armed by the last arrival and by
     // every runner gate: GateArgs::rearm)
     __syncthreads();
+    PROBE_AT(3);
     if (threadIdx.x == 0) {
       const unsigned prev = __hip_atomic_fetch_add(V.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      PROBE_AT(4);
       if (prev == (unsigned)V.nblocks - 1) {
         publish_result(V.g.sel_out, V.flag, V.pub, V.pub_dctr, G.cancel, G.nonfin);
+        PROBE_AT(5);
         __hip_atomic_store(V.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -2330,8 +2337,9 @@ __global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
 }
 
 // LMS reward fit (features/successor.py:164-167): w += α (r - Σ φ⊙w) φ
+// rv: the reward as a value (sfx_lms_value) when r is null
 __global__ void k_lms(float* __restrict__ w, const float* __restrict__ phi, const float* __restrict__ r,
-                      float alpha, int d) {
+                      float alpha, int d, float rv) {
   __shared__ float s_p[DMAX];
   const int tid = threadIdx.x;
   const float wk = tid < d ? w[tid] : 0.f, pk = tid < d ? phi[tid] : 0.f;
@@ -2341,7 +2349,7 @@ __global__ void k_lms(float* __restrict__ w, const float* __restrict__ phi, cons
   if (tid == 0) {
     float rf = 0.f;
     for (int k = 0; k < d; ++k) rf = __fadd_rn(rf, s_p[k]);
-    s_e = __fmul_rn(alpha, __fsub_rn(r[0], rf));
+    s_e = __fmul_rn(alpha, __fsub_rn(r ? r[0] : rv, rf));
   }
   __syncthreads();
   if (tid < d) w[tid] = __fadd_rn(wk, __fmul_rn(s_e, pk));
@@ -2625,12 +2633,13 @@ struct SelScratch {
   unsigned done;               // arrivals (re-armed to 0 by the last)
 };
 
+// head t's workgroup of k_sel1m
 template <int VW>  // d % VW == 0
-__global__ __launch_bounds__(256) void k_sel1m(Geo G, GpiArgs A, SelPub P, SelScratch* S) {
+__device__ __forceinline__ void sel1m_body(const Geo& G, const GpiArgs& A, const SelPub& P, SelScratch* S, int t) {
   PROBE_T(pt0);
   __shared__ float s_w[DMAX];
   __shared__ float s_q[256];
-  const int t = blockIdx.x, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff;
   const long long ob = A.row0;
   const float* wr = A.w + ob * A.w_stride;
@@ -2696,6 +2705,11 @@ __global__ __launch_bounds__(256) void k_sel1m(Geo G, GpiArgs A, SelPub P, SelSc
     }
   }
   PROBE_REC(16, pt0);
+}
+
+template <int VW>
+__global__ __launch_bounds__(256) void k_sel1m(Geo G, GpiArgs A, SelPub P, SelScratch* S) {
+  sel1m_body<VW>(G, A, P, S, blockIdx.x);
 }
 
 }  // namespace sfx

@@ -64,17 +64,24 @@ struct TsfArgs {
   const float* r;
   const int64_t* a;
   float* g;  // [T][Pg]: flow k at k*(2n_s+1) (w[n_s], b, u[n_s]); Linear W[G][n_s] at K*(2n_s+1), then b[G]
+  // [T][K][tsf_fst(NP)]: the same flows in the chain layout (zeros in the padding), kept by every
+  // writer of g's flows (the flows' Adam in tsf_flow_block, the host loads): the forward and the
+  // backward's flow rows stage it with one contiguous 16-byte LDS-DMA.  The c slots hold the
+  // look-ahead coefficients of the last forward (which the backward after it uses as they are)
+  float* gch;
   float* gm;
   float* gv;
   float* hp;  // [Ph]: W_h[d][G] then b_h[d]
   float* hm;  // [T][Ph] (each task's optimizer keeps its own moments of the shared h)
   float* hv;
   float* zs;     // [K+1][2B][NP] flow states (rows 0..B-1: s, B..2B-1: s1)
-  float* ts;     // [K][2B] tanh outputs
+  float* ts;     // tanh outputs [2B / TSF_FR groups][K][TSF_FR]: a backward flow-row workgroup's block is contiguous (tsf_ts_at)
   float* gfeat;  // [2B][G]
   float* tphi;   // [B][d]
   float* part;   // [K][2B][tsf_pst(NP)] per-row flow gradients (dz_{k+1}, da_k)
   float* scratch;  // [TSF_SCR]: stores of flow-chain lanes past the batch (never read)
+  float* bimg;   // [NP][G4] W_l transposed, then [G][D4] W_h transposed: the pre-step values, written by the
+                 // forward for the backward's flow rows (one contiguous LDS-DMA there)
   float* snap;   // [Pg + Ph + d]: g_i, h, w_i before this step (written by k_tsf_fwd)
   float* losses; // [3]: [1] = l1 (written by the ψ tail); [0], [2] written here
   const float* dzlast;  // output gradient of the policy's ψ head [B][O] (written by K2)
@@ -88,6 +95,10 @@ struct TsfArgs {
 };
 
 __device__ __forceinline__ int tsf_flow_stride(int n_s) { return 2 * n_s + 1; }
+// tanh output t_k of flow row `row` in TsfArgs::ts
+__host__ __device__ __forceinline__ long long tsf_ts_at(int row, int k, int K) {
+  return ((long long)(row / TSF_FR) * K + k) * TSF_FR + row % TSF_FR;
+}
 
 // LDS carve of the backward roles (float offsets, 16-byte aligned), from the geometry: the
 // flow-row role, the h / g-Linear / w roles and k_tsf_flow's flows each start at 0 of the same
@@ -261,22 +272,15 @@ __device__ __forceinline__ float tsf_dot4(const float* a, const float* b, int n4
   return __fadd_rn(__fadd_rn(acc.x, acc.y), __fadd_rn(acc.z, acc.w));
 }
 
-// glds / tsf_lds_t (LDS-DMA staging): sfx_kernels.h
-
-// The K flows of g (packed: flow k at k(2 n_s + 1): w[n_s], b, u[n_s]) -> LDS in the chain layout
-// (tsf_fst): w at [0, NP), u at [NP, 2NP), b at 2NP, c (filled by the caller) at 2NP + 1, zeros
-// elsewhere.  Completes at the caller's next __syncthreads().
-template <int NP>
-__device__ __forceinline__ void tsf_stage_flows(float* dst, const float* src, int K, int n_s) {
-  constexpr int FA = tsf_fst(NP);
-  const int fs = tsf_flow_stride(n_s);
-  glds(dst, K * FA, [&](int j) -> const float* {
-    const int k = j / FA, e = j - k * FA;
-    const float* f = src + k * fs;
-    if (e < NP) return e < n_s ? f + e : nullptr;
-    if (e < 2 * NP) return e - NP < n_s ? f + n_s + 1 + (e - NP) : nullptr;
-    return e == 2 * NP ? f + n_s : nullptr;
-  });
+// glds / tsf_lds_t (LDS-DMA staging): sfx_kernels.h.  glds16: a contiguous copy of n4 16-byte
+// groups (16-byte aligned source and destination) by global_load_lds_dwordx4, one KB per wave
+// instruction, by waves [w0, w0 + nw); completes at the caller's next __syncthreads()
+__device__ __forceinline__ void glds16(float* dst, const float* src, int n4, int w0 = 0, int nw = 4) {
+  const int lane = threadIdx.x & 63, wv = (threadIdx.x >> 6) - w0;
+  if (wv < 0 || wv >= nw) return;
+  for (int c = wv; c * 64 < n4; c += nw)
+    if (c * 64 + lane < n4)
+      __builtin_amdgcn_global_load_lds((const void*)(src + 4 * (c * 64 + lane)), (tsf_lds_t)(dst + c * 256), 16, 0, 0);
 }
 
 // Rows [0, n) of the minibatch (row rl is batch index bmap(rl)), staged for the backward roles:
@@ -307,6 +311,7 @@ __device__ float tsf_stage_daff(const TsfArgs& A, int n, BMap bmap, float* s_tp,
     s_ab[tid] = av;
   }
   __syncthreads();
+  PROBE_AT(5);
   glds(s_gc, n * d, [&](int j) {
     const int rl = j / fd, ab = s_ab[rl];
     return (ab >= 0 && ab * d < O) ? A.dzlast + (size_t)bmap(rl) * O + ab * d + (j - rl * d) : A.dzlast;
@@ -321,6 +326,7 @@ __device__ float tsf_stage_daff(const TsfArgs& A, int n, BMap bmap, float* s_tp,
     s_dr[tid] = __fmul_rn(bnorm, e);
   }
   __syncthreads();
+  PROBE_AT(6);
   for (int j = tid; j < n * d; j += 256) {
     const int rl = j / fd, c = j - rl * d, ab = s_ab[rl];
     const float gc = (ab >= 0 && ab * d < O) ? s_gc[j] : 0.f;
@@ -352,8 +358,10 @@ __device__ __forceinline__ void tsf_fwd_body(const TsfArgs& A, const float* __re
   float *s_fa = sm + L.fa, *s_wl = sm + L.wl, *s_wh = sm + L.wh, *s_gf = sm + L.gf, *s_z = sm + L.z;
   float *s_ph = sm + L.ph, *s_bl = sm + L.bl, *s_bh = sm + L.bh;
   const int b0 = blk * PB, nb = min(PB, B - b0);
+  __shared__ int s_sync;  // waves 1-3 meet on it before writing the backward's image
+  if (tid == 0) s_sync = 0;
   PROBE_T(t0_);
-  tsf_stage_flows<NP>(s_fa, gfl, K, n_s);
+  glds16(s_fa, A.gch + (size_t)A.pol * K * FA, K * FA / 4);  // the flows, chain layout
   // flow row rl = tid / LPR on lanes [LPR rl, LPR rl + LPR) (components [hf NL, hf NL + NL) each):
   // rows 0..PB-1 the s rows of batch indices b0.., PB.. the s1 rows
   constexpr int LPR = tsf_lpr(NP), NL = NP / LPR;
@@ -371,15 +379,22 @@ __device__ __forceinline__ void tsf_fwd_body(const TsfArgs& A, const float* __re
       z[p] = (tsf_f2){valid && i < n_s ? src[i] : 0.f, valid && i + 1 < n_s ? src[i + 1] : 0.f};
     }
   }
+  PROBE_AT(4);
   __syncthreads();
+  PROBE_AT(5);
   if (tid < 64) {
     tsf_lookahead<NP>(s_fa, K);
+    // the coefficients into the chain-layout copy too: the backward's flow rows read these flows
+    // (its own launch comes before their Adam step) with c already in place
+    if (blk == 0)
+      for (int k = tid; k < K; k += 64)
+        A.gch[((size_t)A.pol * K + k) * FA + 2 * NP + 1] = s_fa[k * FA + 2 * NP + 1];
     if (rl < RPW) {
       // rows past the batch write their (unused) states to a scratch row, so the loop body is one
       // basic block: the LDS reads for step k + 2 issue at its top
       float* zrow = valid ? A.zs + (size_t)row * NP + hf * NL : A.scratch + rl * TSF_NS + hf * NL;
-      float* trow = valid ? A.ts + row : A.scratch + rl * TSF_NS + NP;  // both lanes: the same t
-      const size_t zstep = valid ? (size_t)R2 * NP : 0, tstep = valid ? (size_t)R2 : 0;
+      float* trow = valid ? A.ts + tsf_ts_at(row, 0, K) : A.scratch + rl * TSF_NS + NP;  // both lanes: the same t
+      const size_t zstep = valid ? (size_t)R2 * NP : 0, tstep = valid ? (size_t)TSF_FR : 0;
       PROBE_AT(1);
       // flows k (F0) and k + 1 (F1) in registers; flow k + 2's LDS reads are issued a full step
       // before their use
@@ -393,9 +408,11 @@ __device__ __forceinline__ void tsf_fwd_body(const TsfArgs& A, const float* __re
       // one flow step: Fa = flow k, Fb = flow k + 1, Fc <- flow k + 2; the loop rotates the three
       // register sets by name (unrolled by 3), so no step copies parameters
       auto step = [&](const TsfFlow<NL>& Fa, const TsfFlow<NL>& Fb, TsfFlow<NL>& Fc, int k) {
-        tsf_flow_ld<NL, NP>(Fc, s_fa + min(k + 2, K - 1) * FA, hf);
         // w_{k+1}·z_k + b_{k+1}: off the critical path
         const float q = __fadd_rn(tsf_row_sum<LPR>(tsf_dot<NL>(z, Fb.w)), Fb.b);
+        // flow k + 2's reads go out after the dot has read flow k + 1, so the wait for flow k + 1's
+        // reads (issued a step ago) does not also wait for these
+        tsf_flow_ld<NL, NP>(Fc, s_fa + min(k + 2, K - 1) * FA, hf);
         const float t = tsf_tanh(a);
         tsf_store<NL>(zrow, z);
         *trow = t;
@@ -453,6 +470,27 @@ __device__ __forceinline__ void tsf_fwd_body(const TsfArgs& A, const float* __re
     const int lo = blk * per, hi = min(S, lo + per);
     for (int j = lo + tid - 64; j < hi; j += 192)
       A.snap[j] = j < A.Pg ? gfl[j] : (j < A.Pg + A.Ph ? A.hp[j - A.Pg] : A.w[j - A.Pg - A.Ph]);
+    // this workgroup's slice of the backward flow rows' staging image (TsfArgs::bimg): W_l and W_h
+    // transposed, from the LDS copies once every one of waves 1-3 has landed its part of them (a
+    // wave's own LDS-DMA is complete at its vmcnt(0); the waves meet on an LDS counter -- wave 0 is
+    // in the flow chain)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if ((tid & 63) == 0) __hip_atomic_fetch_add(&s_sync, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(&s_sync, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 3) __builtin_amdgcn_s_sleep(1);
+    const int D4 = (d + 3) & ~3, nwl = NP * GP, nimg = nwl + G * D4;
+    const int ip = (nimg + nblk - 1) / nblk, ilo = blk * ip, ihi = min(nimg, ilo + ip);
+    const FDiv fd4 = fdiv(D4);
+    for (int j = ilo + tid - 64; j < ihi; j += 192) {
+      float v;
+      if (j < nwl) {
+        const int i = j / fgp, q = j - i * GP;
+        v = q < G ? s_wl[q * NP + i] : 0.f;
+      } else {
+        const int jj = j - nwl, q = jj / fd4, c = jj - q * D4;
+        v = c < d ? s_wh[c * GP + q] : 0.f;
+      }
+      A.bimg[j] = v;
+    }
   }
   __syncthreads();
   if (tid < 256) {  // Linear(n_s, G) of g for this workgroup's rows (columns past G: zero)
@@ -492,7 +530,8 @@ __global__ __launch_bounds__(256) void k_tsf_fwd(TsfArgs A, const float* __restr
 }
 
 // flow-row role: rows [f FR, (f+1) FR) of the 2B rows; lanes 0..FR-1 of wave 0 run the reverse
-// flow chains (one row each).  sfl = A.snap (the pre-step g_i first).  With r_k = dz_{k+1}·u_{k-1}
+// flow chains (one row each).  The pre-step flows come from TsfArgs::gch (their Adam step runs in a
+// later launch), W_l / W_h transposed from TsfArgs::bimg (the forward's image).  With r_k = dz_{k+1}·u_{k-1}
 // (known before da_k) the next chain value is su_{k-1} = dz_k·u_{k-1} = r_k + da_k c_{k-1}, so a
 // step's critical path is two operations (da_k = su_k (1 - t_k^2), then that FMA); the update
 // dz_k = dz_{k+1} + da_k w_k and the stores of dz_{k+1}, da_k run beside it.
@@ -501,7 +540,6 @@ __device__ __forceinline__ void tsf_bwd_flows(const TsfArgs& A, const float* __r
                               float* s_r, int* s_ab, int f) {
   constexpr int FR = TSF_FR, PST = tsf_pst(NP), FA = tsf_fst(NP);
   const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
-  const int fs = tsf_flow_stride(n_s), nfl = K * fs;
   const int D4 = (d + 3) & ~3, G4 = (G + 3) & ~3;   // rows padded to 16 bytes (zeros)
   const TsfBwdLds L = tsf_bwd_lds(K, NP, G, d, B);
   float* s_t = sm + L.t;                            // [K][FR]
@@ -514,23 +552,13 @@ __device__ __forceinline__ void tsf_bwd_flows(const TsfArgs& A, const float* __r
   PROBE_T(t0_);
   const int r0 = f * FR;
   const int nr = min(FR, R2 - r0);
-  // stage everything up front (LDS-DMA, all in flight together)
-  glds(s_t, K * FR, [&](int j) {
-    const int k = j / FR, e = j - k * FR;
-    return A.ts + (size_t)k * R2 + r0 + (e < nr ? e : 0);
-  });
-  {
-    const FDiv fg4 = fdiv(G4), fd4 = fdiv(D4);
-    glds(s_wlT, NP * G4, [&](int j) -> const float* {
-      const int i = j / fg4, q = j - i * G4;
-      return i < n_s && q < G ? sfl + nfl + q * n_s + i : nullptr;
-    });
-    glds(s_whT, G * D4, [&](int j) -> const float* {
-      const int q = j / fd4, c = j - q * D4;
-      return c < d ? sfl + A.Pg + c * G + q : nullptr;
-    });
-  }
-  tsf_stage_flows<NP>(s_fa, sfl, K, n_s);
+  // stage everything up front (LDS-DMA, all in flight together): the flows from the chain-layout
+  // copy (the flows' Adam runs in a later launch, so it still holds the pre-step values), W_l and
+  // W_h transposed, this workgroup's tanh outputs
+  glds16(s_fa, A.gch + (size_t)A.pol * K * FA, K * FA / 4);
+  glds16(s_wlT, A.bimg, (NP * G4 + G * D4) / 4);  // W_l, W_h transposed (adjacent in the carve and the image)
+  glds16(s_t, A.ts + tsf_ts_at(r0, 0, K), K * FR / 4);  // this workgroup's [K][FR] block (rows past nr unused)
+  PROBE_AT(4);
   (void)tsf_stage_daff(A, nr, [&](int rl) { const int row = r0 + rl; return row < B ? row : row - B; }, s_dg, s_da,
                        s_gc, s_dr, s_w, s_r, s_ab);
   PROBE_AT(1);
@@ -560,7 +588,7 @@ __device__ __forceinline__ void tsf_bwd_flows(const TsfArgs& A, const float* __r
   PROBE_AT(2);
   constexpr int LPR = tsf_lpr(NP), NL = NP / LPR;
   if (tid >= 64 || K == 0) return;
-  tsf_lookahead<NP>(s_fa, K);  // all 64 lanes of wave 0 (a lane per flow)
+  // c_k = w_{k+1}·u_k came with the flows: the forward that staged these flows stored them
   if (tid >= LPR * FR) return;
   // row rl on lanes [LPR rl, LPR rl + LPR) (components [hf NL, hf NL + NL) each)
   const int rl = tid / LPR, hf = tid % LPR, row = r0 + rl;
@@ -583,9 +611,10 @@ __device__ __forceinline__ void tsf_bwd_flows(const TsfArgs& A, const float* __r
   // k_tsf_fwd); tb = t_{k-1}, tc <- t_{k-2}
   float t1 = s_t[max(K - 2, 0) * FR + rl], t2 = 0.f;
   auto step = [&](const TsfFlow<NL>& Fa, const TsfFlow<NL>& Fb, TsfFlow<NL>& Fc, float ta, float& tc, int k) {
+    const float rn = tsf_row_sum<LPR>(tsf_dot<NL>(dz, Fb.u));  // dz_{k+1}·u_{k-1}: off the critical path
+    // flow k - 2's reads after the dot has read flow k - 1 (as in k_tsf_fwd)
     tsf_flow_ld<NL, NP>(Fc, s_fa + max(k - 2, 0) * FA, hf);
     tc = s_t[max(k - 2, 0) * FR + rl];
-    const float rn = tsf_row_sum<LPR>(tsf_dot<NL>(dz, Fb.u));  // dz_{k+1}·u_{k-1}: off the critical path
     const float da = __fmul_rn(su, __fsub_rn(1.f, __fmul_rn(ta, ta)));
     tsf_store<NL>(pk, dz);
     *pda = da;  // both lanes: the same value
@@ -763,7 +792,7 @@ __device__ __forceinline__ void tsf_flow_block(const TsfArgs& A, float* sm, int 
     return A.part + ((size_t)k * R2 + r) * PST + (j - r * NP);
   });
   glds(s_da, R2, [&](int j) { return A.part + ((size_t)k * R2 + j) * PST + NP; });
-  glds(s_t, R2, [&](int j) { return A.ts + (size_t)k * R2 + j; });
+  glds(s_t, R2, [&](int j) { return A.ts + tsf_ts_at(j, k, A.K); });
   __syncthreads();
   if (tid >= fs) return;
   const int e = tid;
@@ -781,8 +810,30 @@ __device__ __forceinline__ void tsf_flow_block(const TsfArgs& A, float* sm, int 
   }
   const float g = __fadd_rn(g0, g1);
   const long long go = (long long)A.pol * A.Pg + (long long)k * fs + e;
-  if (!step_cancelled(A.cancel)) adam_el(A.g + go, A.gm + go, A.gv + go, g, adam_consts(A.hpf, *A.step));
+  if (!step_cancelled(A.cancel)) {
+    adam_el(A.g + go, A.gm + go, A.gv + go, g, adam_consts(A.hpf, *A.step));
+    // the chain-layout copy (TsfArgs::gch): w at e, b at 2NP, u at NP + (e - n_s - 1)
+    const int slot = e < n_s ? e : e == n_s ? 2 * NP : NP + (e - n_s - 1);
+    A.gch[((long long)A.pol * A.K + k) * tsf_fst(NP) + slot] = A.g[go];
+  }
   PROBE_REC(15, t0_);
+}
+
+// TsfArgs::gch of one head from its packed flows (after a host load of g): workgroup k writes
+// flow k's chain-layout row, zeros in the padding and c slots
+__global__ __launch_bounds__(64) void k_tsf_gch(const float* __restrict__ g, float* __restrict__ gch, int n_s, int np) {
+  const int k = blockIdx.x, FA = tsf_fst(np), fs = tsf_flow_stride(n_s);
+  const float* f = g + (long long)k * fs;
+  for (int e = threadIdx.x; e < FA; e += blockDim.x) {
+    float v = 0.f;
+    if (e < n_s)
+      v = f[e];
+    else if (e >= np && e < np + n_s)
+      v = f[n_s + 1 + (e - np)];
+    else if (e == 2 * np)
+      v = f[n_s];
+    gch[(long long)k * FA + e] = v;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_tsf_flow(TsfArgs A) {
@@ -821,7 +872,7 @@ __global__ __launch_bounds__(256) void k_bwd_tsf(Geo G, BwdArgs A, TsfArgs T, co
 // The ψ forward's first launch (layers 0 + 1 from the states, k_fwd<true, 8, true, BF>) with
 // k_tsf_fwd's workgroups riding along first in the same grid: the flow chains run beside the ψ
 // tiles.  (gx, gy) = the ψ launch's own grid; its workgroup r is (r % gx, r / gx % gy, r / gx gy).
-template <int NP, bool BF>
+template <int NP, bool BF, int TP>
 __global__ __launch_bounds__(512) void k_fwd_tsf(Geo G, FwdArgs F, TsfArgs T, const float* __restrict__ gfl,
                                                   int ntsf, int gx, int gy) {
   __shared__ __attribute__((aligned(16))) float sm[TSFXF_SM];
@@ -833,7 +884,7 @@ __global__ __launch_bounds__(512) void k_fwd_tsf(Geo G, FwdArgs F, TsfArgs T, co
     return;
   }
   const int r = b - ntsf;
-  fwd_body<true, 8, true, BF, 1>(G, F, r % gx, (r / gx) % gy, r / (gx * gy));
+  fwd_body<true, 8, true, BF, TP>(G, F, r % gx, (r / gx) % gy, r / (gx * gy));
 }
 
 // -------------------------------------------------------------------------------------

@@ -44,6 +44,9 @@ SIGNATURES = {
     "sfx_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP]),
     "sfx_update_all": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _VP]),
     "sfx_lms": (_I, [_VP, _I, _VP, _VP, _F]),
+    "sfx_lms_value": (_I, [_VP, _I, _VP, _F, _F]),
+    "sfx_host_alloc": (_I, [C.c_size_t, C.POINTER(_VP)]),
+    "sfx_host_free": (_I, [_VP]),
     "sfx_step_all": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _I, _VP, _VP, _F, _VP, _I, _I, _VP]),
     "sfx_step_finish": (_I, [_VP, C.POINTER(C.c_int64)]),
     "sfx_debug_force_rerun": (_I, [_VP, _I]),
@@ -175,3 +178,36 @@ def fptr(arr) -> "C.POINTER(C.c_float)":
 def dptr(t) -> int:
     """Device tensor (or None) -> raw device pointer for *_dev arguments."""
     return None if t is None else t.data_ptr()
+
+
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def stream_ptr(device_index: int) -> int:
+    """The hipStream_t of torch's current stream on a device (per call: a `with torch.cuda.stream`
+    block changes it).  torch.cuda.current_stream(dev).cuda_stream costs ≈7 µs of device-argument
+    parsing per call on the drop-in's per-step path; the raw accessor returns the same pointer."""
+    if _raw_stream is not None:
+        return _raw_stream(device_index)
+    return torch.cuda.current_stream(device_index).cuda_stream
+
+
+class HostBuffer:
+    """Coherent, device-mapped host memory (sfx_host_alloc): kernels read it directly.  `.np` is a
+    numpy int64 view of `n` words; `.ptr` the address (the same on host and device)."""
+
+    def __init__(self, n: int):
+        import numpy as np
+
+        p = C.c_void_p()
+        check(lib.sfx_host_alloc(8 * int(n), C.byref(p)), "sfx_host_alloc")
+        self.ptr = p.value
+        self.np = np.ctypeslib.as_array((C.c_int64 * int(n)).from_address(self.ptr))
+
+    def __del__(self):
+        p, self.ptr = getattr(self, "ptr", None), None
+        if p:
+            try:
+                lib.sfx_host_free(p)
+            except Exception:
+                pass

@@ -65,6 +65,10 @@ class ReplayBuffer:
         else:
             row.copy_(torch.as_tensor(np.asarray(x, dtype=np.float32)).reshape(row.shape))
 
+    def _dev_index(self) -> int:
+        i = self.device.index
+        return torch.cuda.current_device() if i is None else i
+
     def _native(self, *xs) -> bool:
         """Device tensors of the ring's dtypes, contiguous: libsfx's one-launch row copy applies."""
         return self.device.type == "cuda" and all(
@@ -84,7 +88,7 @@ class ReplayBuffer:
                     raise ValueError(f"ReplayBuffer.append: {name} has {x.numel()} entries, the ring {row.shape[1]}")
             from sfx import _lib
 
-            _lib.check(_lib.lib.sfx_replay_put(torch.cuda.current_stream(self.device).cuda_stream, rs.data_ptr(),
+            _lib.check(_lib.lib.sfx_replay_put(_lib.stream_ptr(self._dev_index()), rs.data_ptr(),
                                                rr.data_ptr(), rs1.data_ptr(), ra.data_ptr(), j, state.data_ptr(),
                                                reward.data_ptr(), next_state.data_ptr(), action.data_ptr(),
                                                rs.shape[1], rr.shape[1]), "sfx_replay_put")
@@ -113,40 +117,54 @@ class ReplayBuffer:
             if self._gdev is not None:
                 self._gdev[j] = float(gamma)
 
+    _RING = 4  # pinned index slots: a slot is rewritten 4 replays after its gather was queued
+
     def replay(self):
         """A uniform minibatch (agents/buffer.py:34-60) or None while fewer than n_batch samples."""
         if self.size < self.n_batch:
             return None
         indices = np.random.randint(low=0, high=self.size, size=(self.n_batch,))
         B = self.n_batch
-        if self._pidx is None:  # one pinned slot: [B indices (int64) | B γ (float32 words)]
-            self._pidx = torch.empty(B + (B + 1) // 2, dtype=torch.int64, pin_memory=self.device.type == "cuda")
-            self._pev = torch.cuda.Event() if self.device.type == "cuda" else None
-        elif self._pev is not None:
-            self._pev.synchronize()  # the previous replay's copy has left the pinned slot
-        host = self._pidx.numpy()
-        host[:B] = indices
-        host[B:].view(np.float32)[:B] = self._gam[indices]
-        dev = self._pidx.to(self.device, non_blocking=True, copy=True)  # never a view of the slot
-        if self._pev is not None:
-            self._pev.record()
-        idx = dev[:B]
         rs, ra, rr, rs1 = self._ring
-        if self.device.type == "cuda":  # every field in one gather launch
-            from sfx import _lib
-
-            n_s, d = rs.shape[1], rr.shape[1]
-            flat = torch.empty(B * (2 * n_s + d + 1), device=self.device)  # S | PHI | S1 | G, each contiguous
-            S, PHI = flat[:B * n_s].view(B, n_s), flat[B * n_s:B * (n_s + d)].view(B, d)
-            S1, G = flat[B * (n_s + d):B * (2 * n_s + d)].view(B, n_s), flat[B * (2 * n_s + d):]
-            A = torch.empty(B, dtype=torch.int64, device=self.device)
-            gsrc = dev[B:].view(torch.float32)
-            _lib.check(_lib.lib.sfx_replay_gather(
-                torch.cuda.current_stream(self.device).cuda_stream, rs.data_ptr(), rr.data_ptr(), rs1.data_ptr(),
-                ra.data_ptr(), self._gdev.data_ptr() if self._gdev is not None else None, idx.data_ptr(),
-                gsrc.data_ptr(), B, S.data_ptr(), PHI.data_ptr(), S1.data_ptr(), A.data_ptr(), G.data_ptr(),
-                n_s, d), "sfx_replay_gather")
-            return S, A, PHI, S1, G
-        gam = dev[B:].view(torch.float32)[:B] if self._gdev is None else self._gdev.index_select(0, idx)
+        if self.device.type == "cuda":
+            return self._replay_dev(indices, B, rs, ra, rr, rs1)
+        idx = torch.as_tensor(indices, dtype=torch.int64)
+        gam = torch.as_tensor(self._gam[indices]) if self._gdev is None else self._gdev.index_select(0, idx)
         return (rs.index_select(0, idx), ra.index_select(0, idx), rr.index_select(0, idx),
                 rs1.index_select(0, idx), gam)
+
+    def _replay_dev(self, indices, B, rs, ra, rr, rs1):
+        """Every field in one gather launch.  The indices and the minibatch's γ go to the kernel in a
+        slot of coherent host memory it reads directly (no host->device copy); the slot is reused
+        only after the gather that read it has completed (its event)."""
+        from sfx import _lib
+
+        if self._pidx is None:  # slots of [B indices (int64) | B γ (float32 words)], coherent host memory
+            w = B + (B + 1) // 2
+            self._pidx = _lib.HostBuffer(self._RING * w)
+            self._pnp = self._pidx.np.reshape(self._RING, w)
+            self._pptr = [self._pidx.ptr + 8 * w * i for i in range(self._RING)]
+            self._pev = [None] * self._RING
+            self._pi = 0
+        i = self._pi
+        self._pi = (i + 1) % self._RING
+        ev = self._pev[i]
+        if ev is not None:
+            ev.synchronize()
+        host = self._pnp[i]
+        host[:B] = indices
+        host[B:].view(np.float32)[:B] = self._gam[indices]
+        n_s, d = rs.shape[1], rr.shape[1]
+        # A (int64, as 2B float words) | S | PHI | S1 | G, each contiguous, one allocation
+        a2, S, PHI, S1, G = torch.empty(B * (2 * n_s + d + 3), device=self.device).split(
+            (2 * B, B * n_s, B * d, B * n_s, B))
+        A = a2.view(torch.int64)
+        S, PHI, S1 = S.view(B, n_s), PHI.view(B, d), S1.view(B, n_s)
+        p = self._pptr[i]
+        _lib.check(_lib.lib.sfx_replay_gather(
+            _lib.stream_ptr(self._dev_index()), rs.data_ptr(), rr.data_ptr(), rs1.data_ptr(), ra.data_ptr(),
+            self._gdev.data_ptr() if self._gdev is not None else None, p, p + 8 * B, B, S.data_ptr(),
+            PHI.data_ptr(), S1.data_ptr(), A.data_ptr(), G.data_ptr(), n_s, d), "sfx_replay_gather")
+        ev = self._pev[i] = ev or torch.cuda.Event()
+        ev.record()
+        return S, A, PHI, S1, G

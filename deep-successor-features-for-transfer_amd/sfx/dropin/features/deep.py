@@ -250,7 +250,10 @@ class DeepSF(SF):
         same = all(p[0] is pend[0][0] for p in pend)
         if same and [p[1] for p in pend] == list(range(T)):
             s, a, phi, s1, g = pend[0][2]
-            eng.update_all(s, a, phi, s1, g)
+            lb = getattr(eng, "_dropin_losses", None)  # the losses nobody reads: one buffer per engine
+            if lb is None:
+                lb = eng._dropin_losses = torch.empty(T, 3, device=eng.device)
+            eng.update_all(s, a, phi, s1, g, losses=lb)
         else:
             for _, i, (s, a, phi, s1, g) in pend:
                 eng.update(i, s, a, None, phi, s1, g, use_gpi=True)
@@ -284,7 +287,9 @@ class DeepSF(SF):
         self._flush()
         _, q, task, _ = eng.gpi(s, w_index=task_index)
         dev = self._out_device()
-        q, task = q.to(dev), torch.squeeze(task).to(dev)
+        if q.device != dev:
+            q, task = q.to(dev), task.to(dev)
+        task = torch.squeeze(task)
         if update_counters:
             self._count(task_index, task)
         return q, task
@@ -293,8 +298,12 @@ class DeepSF(SF):
     def update_reward(self, phi, r, task_index, exact=False):
         eng = self._engine()
         self._flush()
-        eng.lms(task_index, torch.as_tensor(phi).reshape(-1), torch.as_tensor(r, dtype=torch.float32).reshape(1),
-                float(self.alpha_w))
+        if isinstance(r, (float, int, np.floating, np.integer)) or (torch.is_tensor(r) and r.device.type == "cpu"
+                                                                  and r.numel() == 1):
+            rr = float(r)  # a host reward goes to the kernel as a value (rounded to float32 there)
+        else:
+            rr = torch.as_tensor(r, dtype=torch.float32).reshape(1)
+        eng.lms(task_index, torch.as_tensor(phi).reshape(-1), rr, float(self.alpha_w))
         if exact:
             w_true = torch.as_tensor(self.true_w[task_index]).reshape(-1).cpu()
             r_true = torch.sum(torch.as_tensor(phi).reshape(-1).cpu() * w_true)
@@ -303,6 +312,13 @@ class DeepSF(SF):
 
     def update_successor(self, transitions, policy_index):
         if transitions is None:
+            return
+        pend = self._pending
+        if pend and pend[0][0] is transitions and pend[-1][1] + 1 == policy_index:
+            # the all-task loop's next policy on the same minibatch (checked when policy 0 came)
+            pend.append((transitions, policy_index, pend[0][2]))
+            if len(pend) == self._eng_T:
+                self._flush()
             return
         states, actions, phis, next_states, gammas = transitions
         eng = self._engine(len(gammas))

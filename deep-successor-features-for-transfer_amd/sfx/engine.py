@@ -13,7 +13,7 @@ from typing import Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ._lib import check, dptr, fptr, lib
+from ._lib import check, dptr, fptr, lib, stream_ptr
 
 ACT_CODES = {"none": 0, "relu": 1, "tanh": 2}
 
@@ -118,7 +118,7 @@ class SFEngine:
         caching allocator then reuses a freed block only in that stream's order)."""
         import contextlib
 
-        if self.stream == torch.cuda.current_stream(self.device).cuda_stream:
+        if self.stream == stream_ptr(self.device.index):
             return contextlib.nullcontext()
         st = getattr(self, "_xstream", None)
         if st is None:
@@ -175,7 +175,15 @@ class SFEngine:
                 out.append(dev[o:o + a.nbytes].view(dt).view(a.shape))
         return out
 
+    def _on_dev(self, x, dt) -> bool:
+        """x is already what a kernel reads: a contiguous `dt` tensor on the engine's device (the
+        drop-in's agents pass device tensors: no conversion, no copy, no framework call)."""
+        return (type(x) is torch.Tensor and x.is_cuda and x.dtype is dt and x.get_device() == self.device.index
+                and x.is_contiguous())
+
     def _f(self, x, shape=None) -> torch.Tensor:
+        if self._on_dev(x, torch.float32):
+            return x if shape is None else x.view(shape)
         t = self._h2d(x, torch.float32)
         if shape is not None:
             t = t.reshape(shape)
@@ -187,6 +195,14 @@ class SFEngine:
     def _batch_in(self, s, s1, a, phi, gamma, r=None):
         """A minibatch's device inputs (s, s1 [B, n_s], a [B] int64, φ [B, d], γ [B], r [B] or None),
         one staged copy for all of them."""
+        f32 = torch.float32
+        if (self._on_dev(s, f32) and self._on_dev(s1, f32) and self._on_dev(a, torch.long)
+                and self._on_dev(phi, f32) and self._on_dev(gamma, f32) and s.dim() == 2
+                and (r is None or self._on_dev(r, f32))):
+            B = s.shape[0]  # device tensors as the kernels read them: only their sizes are checked
+            if (s.shape[1] == self.n_s and s1.shape == s.shape and a.numel() == B and phi.numel() == B * self.d
+                    and gamma.numel() == B and (r is None or r.numel() == B)):
+                return [s, s1, a, phi, gamma, r]
         items = [(s, torch.float32), (s1, torch.float32), (a, torch.long), (phi, torch.float32),
                  (gamma, torch.float32)] + ([] if r is None else [(r, torch.float32)])
         t = self._h2d_many(items)
@@ -468,6 +484,10 @@ class SFEngine:
         return {"policies_checked": c.value, "policies_skipped": s.value}
 
     def lms(self, t: int, phi, r, alpha: float):
+        if self._on_dev(phi, torch.float32) and phi.numel() == self.d and isinstance(r, (float, int)):
+            # a device φ and a host reward (the reference agents' call): r as a kernel argument
+            check(lib.sfx_lms_value(self._h, int(t), phi.data_ptr(), float(r), float(alpha)), "sfx_lms_value")
+            return
         phi, r = self._h2d_many([(phi, torch.float32), (r, torch.float32)])  # host values: one copy
         phi, r = phi.reshape(-1).contiguous(), r.reshape(1).contiguous()
         check(lib.sfx_lms(self._h, int(t), phi.data_ptr(), r.data_ptr(), float(alpha)), "sfx_lms")

@@ -22,6 +22,7 @@
 #ifndef SFX_H
 #define SFX_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -244,10 +245,17 @@ int sfx_replay_put(void* stream, float* rs, float* rphi, float* rs1, int64_t* ra
 int sfx_replay_gather(void* stream, const float* rs, const float* rphi, const float* rs1, const int64_t* ra,
                       const float* rg, const int64_t* idx, const float* gam, int B, float* S, float* PHI, float* S1,
                       int64_t* A, float* G, int n_s, int d);
+/* Host memory the kernels read directly, coherently (hipHostMalloc coherent + mapped): the drop-in
+ * replay hands the minibatch's indices and γ to sfx_replay_gather in it instead of copying them. */
+int sfx_host_alloc(size_t bytes, void** out);
+int sfx_host_free(void* p);
 
 /* LMS reward fit SF.update_reward (features/successor.py:164-167) on w_t:
  * w <- w + alpha (r - φ·w) φ ;  phi_dev [d], r_dev [1]. */
 int sfx_lms(sfx_t h, int t, const float* phi_dev, const float* r_dev, float alpha);
+/* The same with the reward as a value (the reference's agents pass a host float; features/
+ * successor.py:164-167): no host->device copy of r, one launch. */
+int sfx_lms_value(sfx_t h, int t, const float* phi_dev, float r, float alpha);
 
 /* Target bookkeeping (sfdqn.py:366-369; utils/torch.py:31-33). */
 int sfx_set_target_update_ev(sfx_t h, int target_update_ev);

@@ -246,7 +246,10 @@ def test_full_size_update_vs_oracle():
     eng.close()
 
 
-def test_lms_vs_oracle():
+@pytest.mark.parametrize("form", ["host", "device_phi_float_r"])
+def test_lms_vs_oracle(form):
+    """LMS reward fit; device_phi_float_r: the drop-in agents' call (φ on the device, r a host
+    float) -- sfx_lms_value, r as a kernel argument -- bit-identical to the pointer form."""
     spec = R.Spec(17, 32, 7, 8)
     eng = engine_for(spec, 2)
     gen = torch.Generator().manual_seed(1)
@@ -257,7 +260,10 @@ def test_lms_vs_oracle():
         phi = torch.rand(8, generator=gen)
         r = torch.rand((), generator=gen)
         wr = R.lms_update(wr, phi, r, 0.05)
-        eng.lms(1, phi, r.reshape(1), 0.05)
+        if form == "host":
+            eng.lms(1, phi, r.reshape(1), 0.05)
+        else:
+            eng.lms(1, phi.cuda(), float(r), 0.05)
     rel_close(eng.get_w(1)[0], wr.reshape(-1), rtol=1e-5, atol=1e-7)
     eng.close()
 

@@ -618,6 +618,46 @@ def test_active_lookahead_is_bit_exact(schedule, upd_use_gpi, ev, monkeypatch):
     assert s1["ahead_own_forward_steps"] > 0, s1
 
 
+def test_tsf_lookahead_full_shape_is_bit_exact(monkeypatch):
+    """The TSF look-ahead at the Hopper shape (T = 16, H = 256, A = 27, d = 50, G = 100, B = 32): the
+    select's first forward then has 544 column tiles and the TSF forward riding along, so it runs
+    with three column tiles per workgroup (one workgroup per CU there) -- heads, g_i, h, w and every
+    action identical to SFX_AHEAD=0, whose step-start forward runs one tile per workgroup."""
+    from sfx.runner import NativeEnvLoop
+
+    spec = R.Spec(11, 256, 27, 50, ("relu", "relu"))
+    T, n, task, K, G = 16, 8, 3, 4, 100
+    out = {}
+    for ahead in ("1", "0"):
+        monkeypatch.setenv("SFX_AHEAD", ahead)
+        eng, _ = make(spec, T, 1000, max_batch=32)
+        gs = R.GSpec(spec.n_s, G, K)
+        gen = torch.Generator().manual_seed(6)
+        g = torch.empty(T, gs.P).uniform_(-0.1, 0.1, generator=gen)
+        h = torch.empty(spec.d * G + spec.d).uniform_(-0.05, 0.05, generator=gen)
+        eng.tsf_setup(G, K, 1.0, 1e-3, 0.0, 1e-3, 0.0)
+        for t in range(T):
+            eng.tsf_load_g(t, g[t])
+        eng.tsf_load_h(h)
+        loop = NativeEnvLoop(eng, batch=32, capacity=200, gamma=0.9, epsilon=0.3, episode_len=50, seed=7,
+                             schedule="tsf", upd_use_gpi=True)
+        loop.prefill(40)
+        loop.set_task(task)
+        loop.record(n)
+        loop.run(n)
+        recs = loop.records()
+        res = [torch.stack([eng.get_head(t, 0) for t in range(T)]), torch.stack([eng.get_w(t)[0] for t in range(T)]),
+               torch.stack([eng.tsf_get_g(t)[0] for t in range(T)]), eng.tsf_get_h()]
+        out[ahead] = (res, [(r["c"], r["a_greedy"]) for r in recs], loop.stats())
+        loop.close()
+        eng.close()
+    (r1, a1, s1), (r0, a0, s0) = out["1"], out["0"]
+    assert a1 == a0
+    for x, y in zip(r1, r0):
+        assert torch.equal(x, y)
+    assert s1["ahead_pre_steps"] > 0 and s0["ahead_pre_steps"] == 0
+
+
 def test_lookahead_runner_matches_oracle_c2():
     """The C2 shape (T = 8, H = 256, B = 32) with look-ahead on (the bench's configuration),
     replayed through the oracle from the runner's recorded inputs."""

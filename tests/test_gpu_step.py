@@ -166,3 +166,17 @@ def test_paired_forward_tiles_are_bit_exact(monkeypatch):
     assert torch.equal(h1, h2) and torch.equal(w1, w2)
     for (p, q, s_), (p2, q2, s2) in zip(m1, m2):
         assert torch.equal(p, p2) and torch.equal(q, q2) and s_ == s2
+
+
+@pytest.mark.parametrize("force", [-1, 2])
+def test_step_all_many_heads(force):
+    """40 heads: past the fused TD launch's bound (32·T·A <= 2048), so every round's TD target runs
+    in k_tdg, and the final round's post-update ψ output layer spans more workgroups than CUs --
+    the same results as the oracle's in-order loop, with and without forced host rounds."""
+    spec = R.Spec(17, 32, 7, 8, ("relu", "relu"))
+    T = 40
+    eng, st = setup(spec, T, seed=4)
+    eng.debug_force_rerun(force)
+    run_steps(eng, st, spec, T, k=3, seed=8)
+    assert eng.step_stats()["steps"] == 3
+    eng.close()
