@@ -154,7 +154,7 @@ __host__ __device__ inline TsfFwdLds tsf_fwd_lds(int K, int np, int G, int d) {
   const int GP = tsf_r4(G), RPW = 2 * TSF_PB;
   int o = 0;
   L.fa = o; o += K * tsf_fst(np);  // flows, chain layout
-  L.wl = o; o += G * np;           // Linear of g: [G][NP]
+  L.wl = o; o += G * (np + 4);     // Linear of g: [G][NP + 4] (the padded stride: conflict-free b128 reads)
   L.wh = o; o += d * GP;           // W_h: [d][GP]
   L.gf = o; o += RPW * GP;         // g features [RPW][GP]
   L.z = o;  o += RPW * np;         // z_K rows [RPW][NP]
@@ -351,7 +351,7 @@ __device__ float tsf_stage_daff(const TsfArgs& A, int n, BMap bmap, float* s_tp,
 template <int NP>
 __device__ __forceinline__ void tsf_fwd_body(const TsfArgs& A, const float* __restrict__ gfl, float* sm, int blk,
                                              int nblk) {
-  constexpr int PB = TSF_PB, RPW = 2 * PB, FA = tsf_fst(NP);
+  constexpr int PB = TSF_PB, RPW = 2 * PB, FA = tsf_fst(NP), WLS = NP + 4;  // WLS: s_wl's row stride
   const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
   const int fs = tsf_flow_stride(n_s), nfl = K * fs, GP = (G + 3) & ~3;
   const TsfFwdLds L = tsf_fwd_lds(K, NP, G, d);
@@ -452,10 +452,10 @@ __device__ __forceinline__ void tsf_fwd_body(const TsfArgs& A, const float* __re
       PROBE_AT(2);
     }
   } else if (tid < 256) {
-    const FDiv fnp = fdiv(NP), fgp = fdiv(GP);
+    const FDiv fws = fdiv(WLS), fgp = fdiv(GP);
     const float* Wl = gfl + nfl;
-    glds(s_wl, G * NP, [&](int j) -> const float* {
-      const int c = j / fnp, i = j - c * NP;
+    glds(s_wl, G * WLS, [&](int j) -> const float* {
+      const int c = j / fws, i = j - c * WLS;
       return i < n_s ? Wl + c * n_s + i : nullptr;
     }, 1, 3);
     glds(s_bl, G, [&](int j) { return Wl + G * n_s + j; }, 1, 3);
@@ -484,7 +484,7 @@ __device__ __forceinline__ void tsf_fwd_body(const TsfArgs& A, const float* __re
       float v;
       if (j < nwl) {
         const int i = j / fgp, q = j - i * GP;
-        v = q < G ? s_wl[q * NP + i] : 0.f;
+        v = q < G ? s_wl[q * WLS + i] : 0.f;
       } else {
         const int jj = j - nwl, q = jj / fd4, c = jj - q * D4;
         v = c < d ? s_wh[c * GP + q] : 0.f;
@@ -499,7 +499,7 @@ __device__ __forceinline__ void tsf_fwd_body(const TsfArgs& A, const float* __re
       const int r = j / fgp, c = j - r * GP;
       float v = 0.f;
       if (c < G) {
-        v = __fadd_rn(tsf_dot4(s_z + r * NP, s_wl + c * NP, NP / 4), s_bl[c]);
+        v = __fadd_rn(tsf_dot4(s_z + r * NP, s_wl + c * WLS, NP / 4), s_bl[c]);
         const int bb = b0 + (r >= PB ? r - PB : r);
         if (bb < B) A.gfeat[(size_t)(r >= PB ? B + bb : bb) * G + c] = v;
       }
