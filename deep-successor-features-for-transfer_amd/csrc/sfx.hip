@@ -954,7 +954,15 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
 // forward of every head on s, GPI with w of `task`, selection into out[2] = (c, a).
 // With `pub` (runner steps) the step's result is published after the selection: inside k_sel1m, or
 // by k_publish after k_gpi.
-int select_pick(sfx_handle* h, int task, int use_gpi, float* q, int64_t* out, const SelPub* pub);
+// the look-ahead TSF forward's tail riding along in the selection launch (k_sel1m_tsft)
+struct TsfTail {
+  TsfArgs A;  // fwd_mode 2
+  const float* gfl;
+  int nblk;
+  double bytes;
+};
+int select_pick(sfx_handle* h, int task, int use_gpi, float* q, int64_t* out, const SelPub* pub,
+                const TsfTail* tail = nullptr);
 int select_body(sfx_handle* h, const float* s, int task, int use_gpi, float* q, int64_t* out,
                 const SelPub* pub = nullptr) {
   RC(run_fwd(h, {{R_A, P_ONLINE, 1, 0, h->T}}, 1, s, nullptr));
@@ -962,13 +970,32 @@ int select_body(sfx_handle* h, const float* s, int task, int use_gpi, float* q, 
 }
 
 // the choice from role R_A row 0 (GPI with w of `task`, or `task`'s own q) and the publication
-int select_pick(sfx_handle* h, int task, int use_gpi, float* q, int64_t* out, const SelPub* pub) {
+int select_pick(sfx_handle* h, int task, int use_gpi, float* q, int64_t* out, const SelPub* pub,
+                const TsfTail* tail) {
   const GpiArgs g = gpi_args(R_A, 0, 0, h->w + (size_t)task * h->dpad, nullptr, q, nullptr, nullptr, out, task, use_gpi, 1);
   const int TA = h->T * h->A;
   if (h->T <= 64 && h->A <= 256) {  // one workgroup per head, the last one picks
     const SelPub P = pub ? *pub : SelPub{};
     const dim3 grid(h->T), block((unsigned)(cdiv(h->A, 64) * 64));
     const double by = 4.0 * ((double)TA * h->d + h->d + (q ? TA : 0));
+    if (tail) {  // the TSF tail's workgroups first, 256-thread workgroups
+      void (*k)(Geo, GpiArgs, SelPub, SelScratch*, TsfArgs, const float*, int) = nullptr;
+      const int vw = h->d % 4 == 0 ? 4 : h->d % 2 == 0 ? 2 : 1;
+      const int np = tail->A.np;
+#define SFX_SEL_TAIL(V) \
+  k = np == 4 ? k_sel1m_tsft<V, 4> : np == 8 ? k_sel1m_tsft<V, 8> : np == 16 ? k_sel1m_tsft<V, 16> : k_sel1m_tsft<V, 32>
+      if (vw == 4)
+        SFX_SEL_TAIL(4);
+      else if (vw == 2)
+        SFX_SEL_TAIL(2);
+      else
+        SFX_SEL_TAIL(1);
+#undef SFX_SEL_TAIL
+      launch(h, K_GPI, by + tail->bytes, k, dim3(tail->nblk + h->T), dim3(256), h->G, g, P, h->selk, tail->A,
+             tail->gfl, tail->nblk);
+      LAUNCHCHK();
+      return SFX_OK;
+    }
     if (h->d % 4 == 0)
       launch(h, K_GPI, by, k_sel1m<4>, grid, block, h->G, g, P, h->selk);
     else if (h->d % 2 == 0)
@@ -1016,7 +1043,8 @@ int tsf_body(sfx_handle* h, int policy, const float* S, const int64_t* a, const 
              const float* S1, const float* gamma, int B, int use_gpi, float* losses, int64_t* next,
              const int* xmax = nullptr, bool pre = false);
 int tsf_fwd_with(sfx_handle* h, int policy, int B, const float* S, const float* S1, const float* phi,
-                 const std::function<int(const FwdExtra&)>& fwd, const float* xc);
+                 const std::function<int(const FwdExtra&)>& fwd, const float* xc, int mode = 0);
+bool tsf_tail_rider(sfx_handle* h, int policy, int B, const float* S, const float* S1, const float* phi, TsfTail* out);
 
 // The action for s_next (select_body) with the look-ahead of the active-task / TSF runner steps
 // (DESIGN.md §5): the next step's minibatch -- states ax[0, B), next states ax[B, 2B), TSF: its φ
@@ -1040,14 +1068,18 @@ int select_ahead_body(sfx_handle* h, const float* s, const float* ax, const floa
                        {R_NS1T, P_TARGET, 2, task, 1, B, 0}},
                    B, S, S1, fx);
   };
+  // TSF: the chains in the first launch, the Linear of g and φ̃ (the tail) in the selection
+  // launch when it can take them, so they run beside the selection instead of after the chains
+  TsfTail tail;
+  const bool split = axphi && T <= 64 && h->A <= 256 && tsf_tail_rider(h, task, B, S, S1, axphi, &tail);
   if (axphi)
-    RC(tsf_fwd_with(h, task, B, S, S1, axphi, early, s));
+    RC(tsf_fwd_with(h, task, B, S, S1, axphi, early, s, split ? 1 : 0));
   else
     RC(early(FwdExtra()));
   FwdExtra last;
   last.l0 = h->NL - 1;
   RC(run_fwd(h, {{R_A, P_ONLINE, 3, 0, T}}, 1, nullptr, nullptr, last));
-  RC(select_pick(h, task, use_gpi, nullptr, out, pub));
+  RC(select_pick(h, task, use_gpi, nullptr, out, pub, split ? &tail : nullptr));
   return run_fwd(h, {{R_NS1, P_ONLINE, 2, 0, T}, {R_NS, P_ONLINE, 1, task, 1}, {R_NS1T, P_TARGET, 2, task, 1}}, B,
                  nullptr, nullptr, last);
 }

@@ -58,6 +58,8 @@ struct TsfArgs {
   float beta;
   int nflow, nh, nlin;  // k_tsf_bwd roles: flow-row / h / g-Linear workgroups, then one w workgroup
   int np;               // tsf_np(n_s)
+  int fwd_mode;         // the forward: 0 whole, 1 staging + chains + images (no Linear / φ̃), 2 Linear + φ̃ only
+  int pad_m_;
   const float* S;
   const float* S1;
   const float* phi;
@@ -161,6 +163,25 @@ __host__ __device__ inline TsfFwdLds tsf_fwd_lds(int K, int np, int G, int d) {
   L.ph = o; o += tsf_r4(TSF_PB * d);  // φ rows [PB][d]
   L.bl = o; o += tsf_r4(G);
   L.bh = o; o += tsf_r4(d);
+  L.total = o;
+  return L;
+}
+// LDS carve of the forward's tail alone (tsf_fwd_tail): W_l transposed [NP][GP], W_h [d][GP], g
+// features [RPW][GP], the z_K rows, φ rows, b_l, b_h
+struct TsfTailLds {
+  int wlT, wh, gf, z, ph, bl, bh, total;
+};
+__host__ __device__ inline TsfTailLds tsf_tail_lds(int np, int G, int d) {
+  TsfTailLds L{};
+  const int GP = tsf_r4(G), RPW = 2 * TSF_PB;
+  int o = 0;
+  L.wlT = o; o += np * GP;
+  L.wh = o;  o += d * GP;
+  L.gf = o;  o += RPW * GP;
+  L.z = o;   o += RPW * np;
+  L.ph = o;  o += tsf_r4(TSF_PB * d);
+  L.bl = o;  o += tsf_r4(G);
+  L.bh = o;  o += tsf_r4(d);
   L.total = o;
   return L;
 }
@@ -349,8 +370,15 @@ __device__ float tsf_stage_daff(const TsfArgs& A, int n, BMap bmap, float* s_tp,
 // workgroup blk of nblk (threads past 256 of a wider workgroup -- k_fwd_tsf's -- only join the
 // barriers); sm holds tsf_fwd_lds(...).total floats
 template <int NP>
+__device__ __forceinline__ void tsf_fwd_tail(const TsfArgs& A, const float* __restrict__ gfl, float* sm, int blk);
+
+template <int NP>
 __device__ __forceinline__ void tsf_fwd_body(const TsfArgs& A, const float* __restrict__ gfl, float* sm, int blk,
                                              int nblk) {
+  if (A.fwd_mode == 2) {
+    tsf_fwd_tail<NP>(A, gfl, sm, blk);
+    return;
+  }
   constexpr int PB = TSF_PB, RPW = 2 * PB, FA = tsf_fst(NP), WLS = NP + 4;  // WLS: s_wl's row stride
   const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
   const int fs = tsf_flow_stride(n_s), nfl = K * fs, GP = (G + 3) & ~3;
@@ -493,6 +521,10 @@ __device__ __forceinline__ void tsf_fwd_body(const TsfArgs& A, const float* __re
     }
   }
   __syncthreads();
+  if (A.fwd_mode == 1) {  // the Linear and φ̃ run later, in the selection launch (tsf_fwd_tail)
+    PROBE_REC(10, t0_);
+    return;
+  }
   if (tid < 256) {  // Linear(n_s, G) of g for this workgroup's rows (columns past G: zero)
     const FDiv fgp = fdiv(GP);
     for (int j = tid; j < RPW * GP; j += 256) {
@@ -508,6 +540,75 @@ __device__ __forceinline__ void tsf_fwd_body(const TsfArgs& A, const float* __re
   }
   __syncthreads();
   PROBE_AT(3);
+  // φ̃ = (h(g(s)) + h(g(s1))) ⊙ φ
+  const FDiv fd = fdiv(d);
+  for (int j = tid; j < (tid < 256 ? nb * d : 0); j += 256) {
+    const int r = j / fd, c = j - r * d, bb = b0 + r;
+    const float h0 = tsf_dot4(s_gf + r * GP, s_wh + c * GP, GP / 4);
+    const float h1 = tsf_dot4(s_gf + (PB + r) * GP, s_wh + c * GP, GP / 4);
+    const float hb = s_bh[c];
+    const float aff = __fadd_rn(__fadd_rn(h0, hb), __fadd_rn(h1, hb));
+    A.tphi[(size_t)bb * d + c] = __fmul_rn(aff, s_ph[j]);
+  }
+  PROBE_REC(10, t0_);
+}
+
+// The forward's Linear of g and φ̃ for workgroup blk's rows (TsfArgs::fwd_mode 2: the chains ran
+// in an earlier launch with mode 1).  Operands: the chain's final states z_K (TsfArgs::zs), W_l
+// transposed from the backward's image (TsfArgs::bimg, written by that launch), W_h as stored, the
+// biases and φ -- the same values and the same arithmetic as the whole forward's tail.
+template <int NP>
+__device__ __forceinline__ void tsf_fwd_tail(const TsfArgs& A, const float* __restrict__ gfl, float* sm, int blk) {
+  constexpr int PB = TSF_PB, RPW = 2 * PB;
+  const int tid = threadIdx.x, n_s = A.n_s, G = A.G, K = A.K, d = A.d, B = A.B, R2 = 2 * B;
+  const int nfl = K * tsf_flow_stride(n_s), GP = (G + 3) & ~3;
+  const TsfTailLds L = tsf_tail_lds(NP, G, d);
+  float *s_wlT = sm + L.wlT, *s_wh = sm + L.wh, *s_gf = sm + L.gf, *s_z = sm + L.z;
+  float *s_ph = sm + L.ph, *s_bl = sm + L.bl, *s_bh = sm + L.bh;
+  const int b0 = blk * PB, nb = min(PB, B - b0);
+  PROBE_T(t0_);
+  if (tid < 256) {
+    glds16(s_wlT, A.bimg, NP * GP / 4);
+    if (GP == G && (((uintptr_t)A.hp) & 15) == 0) {
+      glds16(s_wh, A.hp, d * GP / 4);
+    } else {
+      const FDiv fgp = fdiv(GP);
+      glds(s_wh, d * GP, [&](int j) -> const float* {
+        const int c = j / fgp, q = j - c * GP;
+        return q < G ? A.hp + c * G + q : nullptr;
+      });
+    }
+    glds(s_z, RPW * NP, [&](int j) -> const float* {
+      const int r = j / NP, i = j - r * NP, bb = b0 + (r >= PB ? r - PB : r);
+      return bb < B ? A.zs + ((size_t)K * R2 + (r >= PB ? B + bb : bb)) * NP + i : nullptr;
+    });
+    glds(s_bl, G, [&](int j) { return gfl + nfl + G * n_s + j; });
+    glds(s_bh, d, [&](int j) { return A.hp + d * G + j; });
+    glds(s_ph, nb * d, [&](int j) { return A.phi + (size_t)b0 * d + j; });
+  }
+  __syncthreads();
+  if (tid < 256) {  // Linear(n_s, G): tsf_dot4's four accumulators over i mod 4, W_l read transposed
+    const FDiv fgp = fdiv(GP);
+    for (int j = tid; j < RPW * GP; j += 256) {
+      const int r = j / fgp, c = j - r * GP;
+      float v = 0.f;
+      if (c < G) {
+        const float* zr = s_z + r * NP;
+        tsf_f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < NP / 4; ++q) {
+          const tsf_f4 wv = {s_wlT[(4 * q) * GP + c], s_wlT[(4 * q + 1) * GP + c], s_wlT[(4 * q + 2) * GP + c],
+                             s_wlT[(4 * q + 3) * GP + c]};
+          acc = __builtin_elementwise_fma(*(const tsf_f4*)(zr + 4 * q), wv, acc);
+        }
+        v = __fadd_rn(__fadd_rn(__fadd_rn(acc.x, acc.y), __fadd_rn(acc.z, acc.w)), s_bl[c]);
+        const int bb = b0 + (r >= PB ? r - PB : r);
+        if (bb < B) A.gfeat[(size_t)(r >= PB ? B + bb : bb) * G + c] = v;
+      }
+      s_gf[j] = v;
+    }
+  }
+  __syncthreads();
   // φ̃ = (h(g(s)) + h(g(s1))) ⊙ φ
   const FDiv fd = fdiv(d);
   for (int j = tid; j < (tid < 256 ? nb * d : 0); j += 256) {
@@ -885,6 +986,23 @@ __global__ __launch_bounds__(512) void k_fwd_tsf(Geo G, FwdArgs F, TsfArgs T, co
   }
   const int r = b - ntsf;
   fwd_body<true, 8, true, BF, TP>(G, F, r % gx, (r / gx) % gy, r / (gx * gy));
+}
+
+// The one-state selection (k_sel1m: a workgroup per head, the last to arrive picks and publishes)
+// with the look-ahead TSF forward's tail (Linear of g, φ̃: TsfArgs::fwd_mode 2) riding along first
+// in its grid (select_ahead_body): its chains ran in the select's first launch (mode 1), and the
+// tail runs beside the selection instead of after the chains there.  256-thread workgroups.
+template <int VW, int NP>
+__global__ __launch_bounds__(256) void k_sel1m_tsft(Geo G, GpiArgs A, SelPub P, SelScratch* S, TsfArgs T,
+                                                     const float* __restrict__ gfl, int ntsf) {
+  __shared__ __attribute__((aligned(16))) float sm[TSFXF_SM];
+  const int b = blockIdx.x;
+  if (b < ntsf) {
+    SFX_CHK(threadIdx.x || tsf_tail_lds(NP, T.G, T.d).total <= TSFXF_SM, tsf_tail_lds(NP, T.G, T.d).total, TSFXF_SM, 5);
+    tsf_fwd_tail<NP>(T, gfl, sm, b);
+    return;
+  }
+  sel1m_body<VW>(G, A, P, S, b - ntsf);
 }
 
 // -------------------------------------------------------------------------------------
