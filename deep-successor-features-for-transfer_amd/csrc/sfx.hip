@@ -249,6 +249,9 @@ struct sfx_handle {
   float* dxpart = nullptr;
   unsigned* dxctr = nullptr;
   StepOut* hout = nullptr;  // pinned host
+  // recorded after a fused step's graph (which ends with the StepOut copy): sfx_step_finish waits
+  // for the step itself, not for work queued behind it (the drop-in's speculative GPI graph)
+  hipEvent_t ev_step = nullptr;
   // generation of the handle's device state: bumped by every launch and every parameter / moment /
   // role write made outside the native runner (touch()); a runner whose look-ahead chain was
   // recorded at another generation drops it (the minibatch roles or the weights it forwarded with
@@ -857,6 +860,7 @@ void free_all(sfx_handle* h) {
                   (void*)h->dout, (void*)h->dxpart, (void*)h->dxctr, (void*)h->qh, (void*)h->selk})
     if (p) (void)hipFree(p);
   if (h->hout) (void)hipHostFree(h->hout);
+  if (h->ev_step) (void)hipEventDestroy(h->ev_step);
   if (h->on16) (void)hipFree(h->on16);
   if (h->tg16) (void)hipFree(h->tg16);
   if (h->host_ar_buf) (void)hipHostFree(h->host_ar_buf);
@@ -1350,6 +1354,10 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
     g_err = "hipHostMalloc failed";
     rc = SFX_E_HIP;
   }
+  if (rc == SFX_OK && hipEventCreateWithFlags(&h->ev_step, hipEventDisableTiming) != hipSuccess) {
+    g_err = "hipEventCreate failed";
+    rc = SFX_E_HIP;
+  }
   if (rc == SFX_OK && hipStreamCreateWithFlags(&h->cap, hipStreamNonBlocking) != hipSuccess) {
     g_err = "hipStreamCreate failed";
     rc = SFX_E_HIP;
@@ -1655,8 +1663,12 @@ int sfx_step_all(sfx_t h, const float* S, const int64_t* a, const float* phi, co
   const GraphKey key = make_key(5, {p.B, p.use_gpi, lms_task, p.task, p.sel_use_gpi, (int)alpha_bits, h->spec_rounds}, h->mask,
                                 {S, a, phi, S1, gamma, lms_phi, lms_r, s_next, losses});
   const int rounds = p.use_gpi ? h->spec_rounds : 1;
-  RC(run_graph(h, key, [&]() -> int { return launch_step_all(h, p, lms_task, lms_phi, lms_r, lms_alpha, rounds); }));
-  HIPCHK(hipMemcpyAsync(h->hout, h->dout, sizeof(StepOut), hipMemcpyDeviceToHost, h->stream));
+  RC(run_graph(h, key, [&]() -> int {
+    RC(launch_step_all(h, p, lms_task, lms_phi, lms_r, lms_alpha, rounds));
+    HIPCHK(hipMemcpyAsync(h->hout, h->dout, sizeof(StepOut), hipMemcpyDeviceToHost, h->stream));
+    return SFX_OK;
+  }));
+  HIPCHK(hipEventRecord(h->ev_step, h->stream));
   h->pend = p;
   return SFX_OK;
 }
@@ -1667,7 +1679,7 @@ int sfx_step_finish(sfx_t h, int64_t* out_host) {
   if (!h->pend.active) SFX_FAIL(SFX_E_STATE, "sfx_step_finish without sfx_step_all");
   sfx_handle::Pending p = h->pend;
   h->pend.active = false;
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipEventSynchronize(h->ev_step));
   int first = h->T, dev_flag = h->T;
   if (p.update) {
     first = p.use_gpi ? h->hout->flag : h->T;

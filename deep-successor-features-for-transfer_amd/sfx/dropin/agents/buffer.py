@@ -15,6 +15,8 @@ actions ``[B]`` int64, gammas ``[B]`` float32.
 """
 from __future__ import annotations
 
+import sys
+
 import numpy as np
 import torch
 
@@ -36,6 +38,7 @@ class ReplayBuffer:
         self.device = _device()
         self._ring = None
         self._pidx = None
+        self._pB = 0
         self._pev = None
         self.index = 0
         self.size = 0
@@ -57,6 +60,8 @@ class ReplayBuffer:
                       torch.zeros(cap, d, device=dev), torch.zeros(cap, n_s1, device=dev))
         self._gam = np.zeros(cap, dtype=np.float32)  # γ per slot, float32 as torch.tensor(list) makes it
         self._gdev = None  # set once a γ arrives as a device tensor: then γ is gathered on the device
+        self._ring_dev = self._ring[0].get_device() if self._ring[0].is_cuda else -2
+        self._widths = (n_s, d, n_s1)
 
     @staticmethod
     def _put(row, x):
@@ -69,11 +74,16 @@ class ReplayBuffer:
         i = self.device.index
         return torch.cuda.current_device() if i is None else i
 
-    def _native(self, *xs) -> bool:
-        """Device tensors of the ring's dtypes, contiguous: libsfx's one-launch row copy applies."""
-        return self.device.type == "cuda" and all(
-            torch.is_tensor(x) and x.device == self.device and x.is_contiguous() and
-            x.dtype == (torch.int64 if i == 1 else torch.float32) for i, x in enumerate(xs))
+    def _native(self, state, action, reward, next_state) -> bool:
+        """Device tensors of the ring's dtypes, on the ring's device, contiguous: libsfx's one-launch
+        row copy applies."""
+        dev = self._ring_dev
+        f32 = torch.float32
+        for x, dt in ((state, f32), (action, torch.int64), (reward, f32), (next_state, f32)):
+            if not (type(x) is torch.Tensor and x.is_cuda and x.get_device() == dev and x.dtype is dt
+                    and x.is_contiguous()):
+                return False
+        return True
 
     def append(self, state, action, reward, next_state, gamma) -> None:
         """Adds the sample (agents/buffer.py:62-82); the oldest is overwritten once the ring is full."""
@@ -83,15 +93,17 @@ class ReplayBuffer:
         j = self.index
         if self._native(state, action, reward, next_state) and action.numel() == 1:
             # the kernel reads the ring's widths from each tensor: a shorter one would be read past its end
-            for name, x, row in (("state", state, rs), ("reward", reward, rr), ("next_state", next_state, rs1)):
-                if x.numel() != row.shape[1]:
-                    raise ValueError(f"ReplayBuffer.append: {name} has {x.numel()} entries, the ring {row.shape[1]}")
+            n_s, d, _ = self._widths
+            if (state.numel(), reward.numel(), next_state.numel()) != self._widths:
+                for name, x, w in (("state", state, n_s), ("reward", reward, d), ("next_state", next_state, n_s)):
+                    if x.numel() != w:
+                        raise ValueError(f"ReplayBuffer.append: {name} has {x.numel()} entries, the ring {w}")
             from sfx import _lib
 
-            _lib.check(_lib.lib.sfx_replay_put(_lib.stream_ptr(self._dev_index()), rs.data_ptr(),
+            _lib.check(_lib.lib.sfx_replay_put(_lib.stream_ptr(self._ring_dev), rs.data_ptr(),
                                                rr.data_ptr(), rs1.data_ptr(), ra.data_ptr(), j, state.data_ptr(),
                                                reward.data_ptr(), next_state.data_ptr(), action.data_ptr(),
-                                               rs.shape[1], rr.shape[1]), "sfx_replay_put")
+                                               n_s, d), "sfx_replay_put")
             self._put_gamma(j, gamma)
             self.size = min(self.size + 1, self.n_samples)
             self.index = (self.index + 1) % self.n_samples
@@ -117,7 +129,10 @@ class ReplayBuffer:
             if self._gdev is not None:
                 self._gdev[j] = float(gamma)
 
-    _RING = 4  # pinned index slots: a slot is rewritten 4 replays after its gather was queued
+    # pinned index slots: a ring of _RING, guarded per block of _BLOCK slots by one event (recorded
+    # after the block's last gather, waited for before the block is rewritten a ring later)
+    _RING, _BLOCK = 256, 64
+    _OUT = 3  # minibatch output slots reused once nothing outside the buffer holds them
 
     def replay(self):
         """A uniform minibatch (agents/buffer.py:34-60) or None while fewer than n_batch samples."""
@@ -133,38 +148,67 @@ class ReplayBuffer:
         return (rs.index_select(0, idx), ra.index_select(0, idx), rr.index_select(0, idx),
                 rs1.index_select(0, idx), gam)
 
+    def _out_slot(self, B, n_s, d):
+        """Output tensors for one minibatch: a slot of the buffer's own whose tensors nobody else
+        holds any more (the storage's use count and each returned tensor's reference count are back
+        to what the slot itself holds), else a new allocation.  Reuse is in stream order: the
+        gather that refills a slot runs after every queued kernel that read it."""
+        from torch._C import _storage_Use_Count as use_count
+
+        for k, sl in enumerate(self._outs):
+            if sl is not None and use_count(sl[0]) == sl[1] and all(
+                    sys.getrefcount(x) == 3 for x in sl[2]):  # the slot's tuple, the loop name, the argument
+                return sl[2]
+        # A (int64, as 2B float words) | S | PHI | S1 | G, each contiguous, one allocation
+        base = torch.empty(B * (2 * n_s + d + 3), device=self.device)
+        a2, S, PHI, S1, G = base.split((2 * B, B * n_s, B * d, B * n_s, B))
+        views = (S.view(B, n_s), a2.view(torch.int64), PHI.view(B, d), S1.view(B, n_s), G)
+        for k, sl in enumerate(self._outs):
+            if sl is None:  # keep it as a slot (holding the storage object keeps its handle valid)
+                st = base.untyped_storage()
+                self._outs[k] = (st._cdata, use_count(st._cdata), views, (st, base, a2, S, PHI, S1))
+                break
+        return views
+
     def _replay_dev(self, indices, B, rs, ra, rr, rs1):
         """Every field in one gather launch.  The indices and the minibatch's γ go to the kernel in a
-        slot of coherent host memory it reads directly (no host->device copy); the slot is reused
-        only after the gather that read it has completed (its event)."""
+        slot of coherent host memory it reads directly (no host->device copy); a block of slots is
+        rewritten only after the gathers that read it have completed (its event)."""
         from sfx import _lib
 
-        if self._pidx is None:  # slots of [B indices (int64) | B γ (float32 words)], coherent host memory
+        stream = _lib.stream_ptr(self._dev_index())
+        if self._pidx is None or self._pB != B:  # slots of [B indices (int64) | B γ (float32 words)]
+            if self._pidx is not None:  # a new batch size: no queued gather may still read the old slots
+                torch.cuda.synchronize(self.device)
             w = B + (B + 1) // 2
             self._pidx = _lib.HostBuffer(self._RING * w)
+            self._pB = B
             self._pnp = self._pidx.np.reshape(self._RING, w)
             self._pptr = [self._pidx.ptr + 8 * w * i for i in range(self._RING)]
-            self._pev = [None] * self._RING
+            self._pev = [None] * (self._RING // self._BLOCK)
             self._pi = 0
+            self._pstream = stream
+            self._outs = [None] * self._OUT
+        if stream != self._pstream:  # gathers on another stream: the events no longer order them
+            torch.cuda.synchronize(self.device)
+            self._pev = [None] * len(self._pev)
+            self._pstream = stream
         i = self._pi
         self._pi = (i + 1) % self._RING
-        ev = self._pev[i]
-        if ev is not None:
-            ev.synchronize()
+        blk, last = divmod(i, self._BLOCK)
+        if last == 0 and self._pev[blk] is not None:
+            self._pev[blk].synchronize()
         host = self._pnp[i]
         host[:B] = indices
         host[B:].view(np.float32)[:B] = self._gam[indices]
         n_s, d = rs.shape[1], rr.shape[1]
-        # A (int64, as 2B float words) | S | PHI | S1 | G, each contiguous, one allocation
-        a2, S, PHI, S1, G = torch.empty(B * (2 * n_s + d + 3), device=self.device).split(
-            (2 * B, B * n_s, B * d, B * n_s, B))
-        A = a2.view(torch.int64)
-        S, PHI, S1 = S.view(B, n_s), PHI.view(B, d), S1.view(B, n_s)
+        S, A, PHI, S1, G = self._out_slot(B, n_s, d)
         p = self._pptr[i]
         _lib.check(_lib.lib.sfx_replay_gather(
-            _lib.stream_ptr(self._dev_index()), rs.data_ptr(), rr.data_ptr(), rs1.data_ptr(), ra.data_ptr(),
+            stream, rs.data_ptr(), rr.data_ptr(), rs1.data_ptr(), ra.data_ptr(),
             self._gdev.data_ptr() if self._gdev is not None else None, p, p + 8 * B, B, S.data_ptr(),
             PHI.data_ptr(), S1.data_ptr(), A.data_ptr(), G.data_ptr(), n_s, d), "sfx_replay_gather")
-        ev = self._pev[i] = ev or torch.cuda.Event()
-        ev.record()
-        return S, A, PHI, S1, G
+        if last == self._BLOCK - 1:
+            ev = self._pev[blk] = self._pev[blk] or torch.cuda.Event()
+            ev.record()
+        return S, A, PHI, S1, G  # a new tuple: a caller holding it holds each tensor

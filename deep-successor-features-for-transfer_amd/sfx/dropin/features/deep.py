@@ -285,11 +285,14 @@ class DeepSF(SF):
         s = self._state(state)
         eng = self._engine(s.shape[0])
         self._flush()
-        _, q, task, _ = eng.gpi(s, w_index=task_index)
-        dev = self._out_device()
-        if q.device != dev:
+        dev = self._out_device()  # before the call: it returns once the pending update is settled
+        move = dev != eng.device
+        # one state: the task index is allocated 0-dim (what torch.squeeze would make of it)
+        _, q, task, _ = eng.gpi(s, w_index=task_index, task_shape=() if s.shape[0] == 1 else None)
+        if move:
             q, task = q.to(dev), task.to(dev)
-        task = torch.squeeze(task)
+        if task.dim():
+            task = torch.squeeze(task)
         if update_counters:
             self._count(task_index, task)
         return q, task

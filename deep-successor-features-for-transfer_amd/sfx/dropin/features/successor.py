@@ -115,9 +115,9 @@ class SF:
         self.__dict__["_gpi_counts"] = value
 
     def _count(self, task_index, task):
-        if torch.is_tensor(task) and task.device.type != "cpu":
+        if type(task) is torch.Tensor and task.is_cuda:
             pend = self.__dict__.setdefault("_gpi_pending", [])
-            pend.append((task_index, task.detach()))
+            pend.append((task_index, task))
             if len(pend) >= self._GPI_SETTLE:
                 self.gpi_counters
             return

@@ -299,8 +299,10 @@ class SFEngine:
         check(lib.sfx_synchronize(self._h), "sfx_synchronize")
 
     # ---------------------------------------------------------------- hot path
-    def gpi(self, S, w=None, w_index: Optional[int] = None, want_psi: bool = False, want_q: bool = True):
-        """GPI over all heads.  Returns (psi [B,T,A,d] or None, q [B,T,A] or None, task [B], next [B])."""
+    def gpi(self, S, w=None, w_index: Optional[int] = None, want_psi: bool = False, want_q: bool = True,
+            task_shape=None):
+        """GPI over all heads.  Returns (psi [B,T,A,d] or None, q [B,T,A] or None, task [B], next [B]);
+        task_shape: the task tensor's shape instead of [B] (B elements, e.g. () for one state)."""
         S = self._f(S)
         if S.dim() == 1:
             S = S.reshape(1, -1)
@@ -313,7 +315,9 @@ class SFEngine:
             w_ptr = w_keep.data_ptr()
         psi = torch.empty(B, self.T, self.A, self.d, device=self.device) if want_psi else None
         q = torch.empty(B, self.T, self.A, device=self.device) if want_q else None
-        task = torch.empty(B, dtype=torch.long, device=self.device)
+        task = torch.empty(B if task_shape is None else task_shape, dtype=torch.long, device=self.device)
+        if task.numel() != B:
+            raise ValueError(f"task_shape {task_shape} does not hold {B} elements")
         nxt = torch.empty(B, dtype=torch.long, device=self.device)
         check(lib.sfx_gpi(self._h, S.data_ptr(), B, w_ptr, dptr(psi), dptr(q), task.data_ptr(),
                           nxt.data_ptr()), "sfx_gpi")

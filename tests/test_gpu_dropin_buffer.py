@@ -51,3 +51,43 @@ def test_device_ring_matches_the_reference_collation():
                 assert torch.equal(x.cpu(), y)
     buf.reset()
     assert buf.replay() is None
+
+
+def test_held_minibatches_survive_slot_reuse_and_ring_wrap():
+    """replay() reuses a minibatch's memory only once nothing outside the buffer holds any of its
+    tensors (or a view of one); 300 replays queued without a synchronisation wrap the 256-slot
+    index ring (its per-block events), and every held minibatch still holds its own rows."""
+    from sfx.dropin.agents.buffer import ReplayBuffer
+
+    dev = torch.device("cuda", 0)
+    n_s, d, B, cap = 5, 3, 8, 40
+    buf = ReplayBuffer({}, n_samples=cap, n_batch=B)
+    buf.device = dev
+    S = torch.arange(cap * n_s, dtype=torch.float32).reshape(cap, n_s)
+    for k in range(cap):
+        buf.append(S[k:k + 1].to(dev), torch.tensor(k % 7, device=dev), torch.full((d,), float(k), device=dev),
+                   (S[k:k + 1] + 0.5).to(dev), 0.9)
+    np.random.seed(5)
+    held, want = [], []
+    for _ in range(300):
+        state = np.random.get_state()
+        held.append(buf.replay())
+        np.random.set_state(state)
+        want.append(np.random.randint(low=0, high=cap, size=(B,)))
+    for got, idx in zip(held, want):
+        assert torch.equal(got[0].cpu(), S[idx]) and torch.equal(got[3].cpu(), S[idx] + 0.5)
+        assert torch.equal(got[1].cpu(), torch.as_tensor(idx % 7)) and torch.equal(got[2][:, 0].cpu(), torch.as_tensor(idx, dtype=torch.float32))
+    # reuse: a dropped minibatch's memory comes back; one still viewed does not
+    del held
+    a = buf.replay()
+    pa = a[0].data_ptr()
+    del a
+    b = buf.replay()
+    assert b[0].data_ptr() == pa
+    keep = b[0][1:3]
+    ref = keep.clone()
+    del b
+    c = buf.replay()
+    assert c[0].data_ptr() != pa
+    torch.cuda.synchronize()
+    assert torch.equal(keep, ref)
