@@ -1630,8 +1630,9 @@ __device__ __forceinline__ void v0_tile(const float* x, int K, int m0, int rows,
 template <bool C>
 __device__ __forceinline__ void fused_v0(const Geo& G, const BwdArgs& A, const RoleGeo& L, int head, int nbase, const float* sW,
                          const float* sB, const float* sX, const float* sWt = nullptr, const float* sBt = nullptr,
-                         bool vrows = true) {
-  if (A.aM > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the look-ahead LDS-DMA has landed
+                         bool vrows = true, bool landed = false) {
+  // the look-ahead LDS-DMA has landed (role_dw waits for it before its Adam stores: landed)
+  if (A.aM > 0 && !landed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   PROBE_AT(3);
   const int K = L.K, N = L.N, VM = A.vM;
@@ -1838,6 +1839,9 @@ __device__ __forceinline__ void role_dw(const Geo& G, const BwdArgs& A, int head
   // + the other three row classes (lanes r + 16, r + 32, r + 48), fixed order
   bsum = __fadd_rn(bsum, __shfl_xor(bsum, 16));
   bsum = __fadd_rn(bsum, __shfl_xor(bsum, 32));
+  // the look-ahead LDS-DMA (issued first) waited for here, before the Adam stores are issued: a
+  // wait after them (in fused_v0) would also wait for every store to drain
+  if (fuse && A.aM > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PROBE_MARK();
   V0Smem& sm = v0_smem();
   float* sW = sm.sW;
@@ -1888,7 +1892,7 @@ __device__ __forceinline__ void role_dw(const Geo& G, const BwdArgs& A, int head
     }
     if (fuse) sB[nbias - nbase] = bp;
   }
-  if (fuse) fused_v0<C>(G, A, L, head, nbase, sW, sB, sX, sm.sWt, sm.sBt);
+  if (fuse) fused_v0<C>(G, A, L, head, nbase, sW, sB, sX, sm.sWt, sm.sBt, true, true);
 }
 
 // loss finalisation, optional w step, Adam step counter (one workgroup per head)
