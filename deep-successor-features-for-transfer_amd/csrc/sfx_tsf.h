@@ -293,6 +293,22 @@ __device__ __forceinline__ float tsf_dot4(const float* a, const float* b, int n4
   return __fadd_rn(__fadd_rn(acc.x, acc.y), __fadd_rn(acc.z, acc.w));
 }
 
+// glds16_rows: rows of 16-byte groups, dst[r][4 g .. 4 g + 3] = src[r * stride + 4 g ..] for r <
+// rows, g < row4 (dst dense; src rows 16-byte aligned), by the workgroup's first four waves;
+// completes at the caller's next __syncthreads()
+__device__ __forceinline__ void glds16_rows(float* dst, const float* src, int rows, int stride, int row4) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, n4 = rows * row4;
+  if (wv >= 4) return;
+  for (int c = wv; c * 64 < n4; c += 4) {
+    const int e = c * 64 + lane;
+    if (e < n4) {
+      const int r = e / row4, g = e - r * row4;
+      __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)r * stride + 4 * g), (tsf_lds_t)(dst + c * 256), 16,
+                                       0, 0);
+    }
+  }
+}
+
 // glds / tsf_lds_t (LDS-DMA staging): sfx_kernels.h.  glds16: a contiguous copy of n4 16-byte
 // groups (16-byte aligned source and destination) by global_load_lds_dwordx4, one KB per wave
 // instruction, by waves [w0, w0 + nw); completes at the caller's next __syncthreads()
@@ -780,14 +796,26 @@ __device__ __forceinline__ void tsf_bwd_block(const TsfArgs& A, const float* __r
   float* s_zk = sm + L.rzk;   // g-Linear role: [2B][NP] z_K
   float* s_dg = sm + L.rdg;   // g-Linear role: [B][TSF_QS]
   const int q0 = (role - A.nh) * TSF_QS, nq = min(TSF_QS, G - q0);
+  // staging by 16-byte LDS-DMA where the rows allow it (one KB per wave instruction; the dword
+  // form issues one 256-byte request per wave instruction at ≈140 ns each)
   if (!wrole && role < A.nh) {
-    glds(s_gf, R2 * G, [&](int j) { return A.gfeat + j; });
+    if (((R2 * G) & 3) == 0 && (((uintptr_t)A.gfeat) & 15) == 0)
+      glds16(s_gf, A.gfeat, R2 * G / 4);
+    else
+      glds(s_gf, R2 * G, [&](int j) { return A.gfeat + j; });
   } else if (!wrole) {
-    glds(s_whs, d * TSF_QS, [&](int j) {
-      const int c = j / TSF_QS, qq = j - c * TSF_QS;
-      return snap + A.Pg + c * G + q0 + (qq < nq ? qq : 0);  // columns past G: zeroed below
-    });
-    glds(s_zk, R2 * NP, [&](int j) { return A.zs + (size_t)K * R2 * NP + j; });
+    const float* wh = snap + A.Pg;
+    if ((G & 3) == 0 && (((uintptr_t)wh) & 15) == 0) {
+      // W_h rows' columns [q0, q0 + TSF_QS): past G (the last role) the group reads on into the
+      // next row / b_h (finite values; those columns' dg is zeroed below)
+      glds16_rows(s_whs, wh + q0, d, G, TSF_QS / 4);
+    } else {
+      glds(s_whs, d * TSF_QS, [&](int j) {
+        const int c = j / TSF_QS, qq = j - c * TSF_QS;
+        return wh + c * G + q0 + (qq < nq ? qq : 0);  // columns past G: zeroed below
+      });
+    }
+    glds16(s_zk, A.zs + (size_t)K * R2 * NP, R2 * NP / 4);  // NP is a multiple of 4
   }
   const float se = tsf_stage_daff(A, B, [](int rl) { return rl; }, s_tp, s_da, s_gc, s_dr, s_w, s_r, s_ab);
   PROBE_AT(1);
@@ -887,11 +915,14 @@ __device__ __forceinline__ void tsf_flow_block(const TsfArgs& A, float* sm, int 
   float *s_z = sm, *s_dz = sm + L.fdz, *s_da = sm + L.fda, *s_t = sm + L.ft;
   PROBE_T(t0_);
   const FDiv fnp = fdiv(NP);
-  glds(s_z, R2 * NP, [&](int j) { return A.zs + (size_t)k * R2 * NP + j; });
-  glds(s_dz, R2 * NP, [&](int j) {
-    const int r = j / fnp;
-    return A.part + ((size_t)k * R2 + r) * PST + (j - r * NP);
-  });
+  glds16(s_z, A.zs + (size_t)k * R2 * NP, R2 * NP / 4);  // NP is a multiple of 4
+  if ((PST & 3) == 0)
+    glds16_rows(s_dz, A.part + (size_t)k * R2 * PST, R2, PST, NP / 4);
+  else
+    glds(s_dz, R2 * NP, [&](int j) {
+      const int r = j / fnp;
+      return A.part + ((size_t)k * R2 + r) * PST + (j - r * NP);
+    });
   glds(s_da, R2, [&](int j) { return A.part + ((size_t)k * R2 + j) * PST + NP; });
   glds(s_t, R2, [&](int j) { return A.ts + tsf_ts_at(j, k, A.K); });
   __syncthreads();
