@@ -43,6 +43,8 @@ import torch  # noqa: E402
 
 METRIC = "env steps/sec (whole node), Reacher 8-task SF-DQN at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+MFMA_PEAK = {"fp32": 157.3e12, "bf16": 2.5e15}  # dense matrix peaks, MI355X_MICROARCH.md:42-43
+CLK_HZ, SIMDS = 2.4e9, 256 * 4  # max clock, CUs x SIMDs (MI355X_MICROARCH.md:30-34)
 SHAPE = dict(n_s=17, H=256, A=7, d=8, acts=("relu", "relu"))
 # BASELINE.json configs C3 / C5 (one GPU): Hopper-shape TSF-DQN, |s|=11, 27 actions, d=50, 16 source
 # tasks, g_i / h width 100; K planar layers in g_i for tsfdqn_nf.py (reacher.cfg n_coupling_layers=100)
@@ -72,8 +74,9 @@ def parse():
     p.add_argument("--replay", choices=["host", "device"], default="host",
                    help="replay ring on the host (north_star; the headline) or in HBM with on-device sampling "
                         "(SURVEY §8f rank 2; native loop only)")
-    p.add_argument("--spec-rounds", type=int, default=2,
-                   help="speculative rounds of the all-task step launched on the device (more run from the host)")
+    p.add_argument("--spec-rounds", type=int, default=0,
+                   help="speculative rounds of the all-task step launched on the device (more run from the host); "
+                        "0: libsfx's choice from the source-task count (2 below 16 tasks, 3 from 16)")
     p.add_argument("--prof-steps", type=int, default=50)
     p.add_argument("--repeats", type=int, default=3,
                    help="time the same K-step window this many more times after the measured one (spread only)")
@@ -135,6 +138,22 @@ def algorithmic_step_bytes(T: int, U: int, P: int, weight_bytes: int) -> float:
     (U·P·34); 4 is the same count for fp32 weights, the arithmetic this build runs (U·P·40)."""
     wb = weight_bytes
     return 2.0 * wb * T * P + U * P * (3 * wb + 28)
+
+
+def head_flops(sh) -> float:
+    """f of SURVEY 8(d): forward FLOPs of one ψ head for one row, 2(n_s·H + n_hidden·H² + H·A·d)."""
+    n_s, H, A, d, nh = sh["n_s"], sh["H"], sh["A"], sh["d"], len(sh["acts"])
+    return 2.0 * (n_s * H + nh * H * H + H * A * d)
+
+
+def mfma_from_profiles(kind: str, workload: str, precision: str):
+    """MFMA counters per launch of `kind` from the committed rocprofv3 --pmc pass
+    (profiles/pmc_mfma.json, tools/pmc_mfma.py), or None."""
+    try:
+        rec = json.load(open(os.path.join(ROOT, "profiles", "pmc_mfma.json")))
+        return rec.get(workload + ("@bf16" if precision == "bf16" else ""), {}).get(KIND_NAMES[kind])
+    except Exception:
+        return None
 
 
 def skippable_head_bytes(sh, M: int) -> float:
@@ -206,8 +225,9 @@ def cpu_baseline(args, seconds: float, threads: int = None):
     rep = Replay(100_000, spec.n_s, spec.d, rng)
     for _ in range(1000):
         s0 = task.initialize()
-        s1, phi, r, _ = task.transition(int(rng.integers(spec.A)))
-        rep.append(s0, 0, r, phi, s1, 0.9)
+        a0 = int(rng.integers(spec.A))  # random actions, as the runners' prefill draws them
+        s1, phi, r, _ = task.transition(a0)
+        rep.append(s0, a0, r, phi, s1, 0.9)
     s = task.initialize()
     steps = 0
     t0 = time.perf_counter()
@@ -805,6 +825,25 @@ def main():
             "skipped_policy_rounds_per_env_step": round(prof_skip["policies_skipped"] / max(args.prof_steps, 1), 3),
             "moved_bytes_per_env_step": round(launched_moved),
             "moved_over_fp32_algorithmic": round(launched_moved / alg32, 3), "unit": "GB/s"}
+        # compute side (north_star: "MFMA utilisation against gfx950 peak"): the dominant kind's
+        # algorithmic FLOPs per env step -- the backward half of 8(d)'s U*4*B*f, dX + dW = 2 forwards
+        # -- over its GPU time per env step, and the MFMA busy cycles of the committed --pmc pass over
+        # the live launch time (profiles/pmc_mfma.json)
+        f = head_flops(sh)
+        peak_c = MFMA_PEAK[args.precision]
+        kind_flops = {"bwd": U * 2.0 * B * f}.get(kind)
+        if kind_flops and us > 0:
+            roofline["compute_frac"] = round(kind_flops * args.prof_steps / (us * 1e-6) / peak_c, 5)
+            roofline["compute_peak_tflops"] = peak_c / 1e12
+        mf = mfma_from_profiles(kind, workload, args.precision)
+        if mf and avg_us > 0:
+            roofline["mfma_util"] = round(mf["mfma_busy_cycles_per_launch"] / (avg_us * 1e-6 * CLK_HZ * SIMDS), 5)
+            ex = mf["mfma_flops_f32_per_launch"] / MFMA_PEAK["fp32"] + mf["mfma_flops_bf16_per_launch"] / MFMA_PEAK["bf16"]
+            roofline["mfma_executed_frac"] = round(ex / (avg_us * 1e-6), 5)
+            roofline["mfma_source"] = ("profiles/pmc_mfma.json: SQ_VALU_MFMA_BUSY_CYCLES / (live avg launch x 2.4 GHz x "
+                                       "1024 SIMDs); executed = MOPS_F32/BF16 x 512 FLOPs / live launch / peak")
+        roofline["per_step"]["flops_per_env_step"] = round(T * f + T * B * f + U * 4 * B * f)
+        roofline["per_step"]["compute_frac"] = round((T * f + T * B * f + U * 4 * B * f) * per_gpu_rate / peak_c, 5)
         spec_stats = eng.step_stats()
         spec_stats.update(eng.skip_stats())
         if native:

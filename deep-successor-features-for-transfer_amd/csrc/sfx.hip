@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "sfx_kernels.h"
+#include "sfx_gpiw.h"
 #include "sfx_tsf.h"
 #include "sfx_phi.h"
 #include "../../include/sfx.h"
@@ -188,6 +189,7 @@ struct sfx_handle {
   long long steps_spec = 0, steps_fallback = 0, policies_rerun = 0, rounds_total = 0;
   int force_rerun_from = -1;  // test hook: treat the speculation as failed from this policy on
   int spec_rounds = 2;        // speculative rounds launched on the device per fused step
+  bool spec_rounds_auto = true;  // spec_rounds follows T_glob (auto_spec_rounds) until set explicitly
   // sharded heads (sfx_shard_*): this handle's heads are global [off, off + T) of Tg; w has Tg rows
   int Tg = 0, off = 0;
   struct sfx_tsf_state* tsf = nullptr;  // TSF-DQN state (sfx_tsf_setup)
@@ -526,9 +528,39 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
   return SFX_OK;
 }
 
+// GPI over many heads (sfx_gpiw.h): one workgroup per (row, WPC policies) instead of one per
+// (policy, row) once a row's q table (T·A entries) outgrows a workgroup
+bool wide_gpi(const sfx_handle* h) {
+  return (long)h->T * h->A > 256 && h->d % 4 == 0 && h->d <= 16 && h->A <= WAMAX;
+}
+
+#define SFX_WIDE(K) (h->d == 4 ? K<1> : h->d == 8 ? K<2> : h->d == 12 ? K<3> : K<4>)
+
 int run_tdg(sfx_handle* h, int pol0, int npol, int guess, int M, int use_gpi, const int64_t* a, const float* phi,
             const float* gamma, int64_t* next, int next_stride, int* flag = nullptr, const int* xmax = nullptr,
-            int poloff = 0, const float* dz_scale = nullptr) {
+            int poloff = 0, const float* dz_scale = nullptr, const int64_t* prev = nullptr, bool skip = false) {
+  const double nt = use_gpi ? h->T : 1;
+  const double by = 4.0 * npol * M * (nt * h->O + 2.0 * h->O + 2.0 * h->d + 4);
+  if (use_gpi && !xmax && !dz_scale && wide_gpi(h)) {
+    TdgwArgs W{};
+    W.M = M;
+    W.pol0 = pol0;
+    W.npol = npol;
+    W.guess = guess;
+    W.next_stride = next_stride;
+    W.flag_value = h->T;
+    W.a = a;
+    W.phi = phi;
+    W.gamma = gamma;
+    W.next = next;
+    W.flag = flag;
+    W.prev = skip ? prev : nullptr;
+    W.skip = skip ? h->skip : nullptr;
+    W.skipc = skip ? h->skipc : nullptr;
+    launch(h, K_TDG, by, SFX_WIDE(k_tdgw), dim3(M, cdiv(npol, WPC)), dim3(256), h->G, W);
+    LAUNCHCHK();
+    return SFX_OK;
+  }
   TdgArgs A{};
   A.dz_scale = dz_scale;
   A.xmax = xmax;
@@ -545,9 +577,10 @@ int run_tdg(sfx_handle* h, int pol0, int npol, int guess, int M, int use_gpi, co
   A.phi = phi;
   A.gamma = gamma;
   A.next = next;
-  const double nt = use_gpi ? h->T : 1;
-  launch(h, K_TDG, 4.0 * npol * M * (nt * h->O + 2.0 * h->O + 2.0 * h->d + 4), k_tdg, dim3(M, npol), dim3(256),
-         h->G, A);
+  A.prev = skip ? prev : nullptr;
+  A.skip = skip ? h->skip : nullptr;
+  A.skipc = skip ? h->skipc : nullptr;
+  launch(h, K_TDG, by, k_tdg, dim3(M, npol), dim3(256), h->G, A);
   LAUNCHCHK();
   return SFX_OK;
 }
@@ -612,9 +645,12 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   const bool fuse = can_fuse_tdg(h) && ((uintptr_t)phi & 15) == 0 &&  // fused K2 reads φ rows as float4
                     (!td.xmax || 32 * h->A <= 1024);                     // and up to 4 maxima per thread
   if (!fuse && td.xi_dst) SFX_FAIL(SFX_E_STATE, "run_bwd: maxima re-initialisation needs the fused TD launch");
+  // round skipping: decided in the fused TD launch (M <= 32: one row tile per policy) or, unfused,
+  // by the TD launch's per-policy arrivals (tdg_skip_report)
+  const bool armed = td.skip && (fuse ? M <= 32 : true);
   if (!fuse)
     RC(run_tdg(h, head0, nhead, td.guess, M, td.use_gpi, td.a, phi, td.gamma, td.next, td.next_stride, td.flag,
-               td.xmax, td.poloff, td.dz_scale));
+               td.xmax, td.poloff, td.dz_scale, td.prev, armed));
   BwdArgs A{};
   A.xcd = nhead > 1 ? 1 : 0;
   A.nhead = nhead;
@@ -630,11 +666,14 @@ int run_bwd(sfx_handle* h, int head0, int nhead, int M, const float* x0, const f
   A.flag = td.flag;
   A.flag_value = h->T;
   A.dz_scale = td.dz_scale;
-  const bool armed = fuse && td.skip && M <= 32;
-  if (armed) {
+  if (armed && fuse) {
     A.tdg_prev = td.prev;
     A.skip = h->skip;
     A.skipc = h->skipc;
+    A.skip_v0 = ex.skip_fwd ? 1 : 0;
+  }
+  if (armed) {
+    A.skip = h->skip;
     A.skip_v0 = ex.skip_fwd ? 1 : 0;
   }
   if (ex.skip_armed) *ex.skip_armed = armed;
@@ -778,7 +817,8 @@ int run_ver(sfx_handle* h, int M, int npol, bool sel, int post, const GpiArgs& g
   V.g = g;
   const int TA = h->T * h->A;
   V.rows = TA >= 256 ? 1 : (256 / TA < M ? 256 / TA : M);
-  const dim3 grid(npol + 1, cdiv(M, V.rows));
+  const bool wide = wide_gpi(h) && npol > 1;
+  const dim3 grid = wide ? dim3(M, cdiv(npol, WPC) + 1) : dim3(npol + 1, cdiv(M, V.rows));
   if (sel && h->pub_res && h->fold_publish) {
     V.pub = h->pub_res;
     V.pub_dctr = h->pub_dctr;
@@ -786,7 +826,11 @@ int run_ver(sfx_handle* h, int M, int npol, bool sel, int post, const GpiArgs& g
     V.nblocks = (int)(grid.x * grid.y);
     h->pub_folded = true;
   }
-  launch(h, K_VER, 4.0 * (double)M * npol * h->T * h->O + 4.0 * h->T * h->O, k_ver, grid, dim3(256), h->G, V);
+  const double by = 4.0 * (double)M * npol * h->T * h->O + 4.0 * h->T * h->O;
+  if (wide)
+    launch(h, K_VER, by, SFX_WIDE(k_verw), grid, dim3(256), h->G, V);
+  else
+    launch(h, K_VER, by, k_ver, grid, dim3(256), h->G, V);
   LAUNCHCHK();
   return SFX_OK;
 }
@@ -871,6 +915,16 @@ void free_all(sfx_handle* h) {
   if (h->dstall) (void)hipFree(h->dstall);
   if (h->cap) (void)hipStreamDestroy(h->cap);
 }
+
+// Device rounds of the all-task step when the caller has not chosen (sfx_set_spec_rounds 0): the
+// chain of the reference's in-order loop (agents/sfdqn.py:57-60) is T_glob policies deep, and the
+// rounds a step needs grow with it -- measured (tools/spec_sim.py, the bench's synthetic Reacher
+// stream, 2 device rounds): 10-13 % of steps need more at T = 8, 27 % at 16, 45-60 % at 32, 80 %
+// at 64; with 3 they are 0-1 % at 16, 2-4 % at 32, 2-8 % at 64.  A third round in a step that
+// verified after two costs its TD launch and early-exiting tiles (every policy skips); a host round
+// costs a host round trip on top of the round -- at T = 8 the host rounds are cheaper overall
+// (DESIGN.md §4), from 16 on the third device round.
+int auto_spec_rounds(int T_glob) { return T_glob >= 16 ? 3 : 2; }
 
 // Role of round r's post-update forward.  The launches of a round run in stream order, so every
 // round can write the same role (round r's TD launch has read round r-1's values before its
@@ -1306,6 +1360,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   }
   h->actSize = (aoff + 63) & ~63;
   h->Tg = T;
+  h->spec_rounds = auto_spec_rounds(T);
   h->since_target.assign(T, 0);
   h->host_step.assign(T, 0);
 
@@ -1346,7 +1401,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   alloc((void**)&h->dz, sizeof(float) * (size_t)T * h->actSize);
   alloc((void**)&h->rowloss, sizeof(float) * (size_t)T * MMAX);
   alloc((void**)&h->spec_next, sizeof(int64_t) * 2 * (size_t)T * MMAX);
-  alloc((void**)&h->skip, sizeof(int) * (size_t)T);
+  alloc((void**)&h->skip, sizeof(int) * 3 * (size_t)T);  // skip [T] | arrival accumulators [T] | arrivals [T]
   alloc((void**)&h->skipc, 64);
   alloc((void**)&h->dout, sizeof(StepOut));
   alloc((void**)&h->selk, sizeof(SelScratch));
@@ -1759,8 +1814,9 @@ float sfx_get_huber(sfx_t h) { return h ? h->G.huber : -1.f; }
 
 int sfx_set_spec_rounds(sfx_t h, int rounds) {
   RC(settle(h));
-  if (!h || rounds < 1) SFX_FAIL(SFX_E_ARG, "bad args");
-  h->spec_rounds = rounds;
+  if (!h || rounds < 0) SFX_FAIL(SFX_E_ARG, "bad args");
+  h->spec_rounds_auto = rounds == 0;
+  h->spec_rounds = rounds == 0 ? auto_spec_rounds(h->Tg) : rounds;
   return SFX_OK;
 }
 

@@ -1054,6 +1054,30 @@ __device__ __forceinline__ float td_loss(float huber, float x) {
 // of the previous speculative round (see k_ver).
 // Grid (M, npol), 256 threads.  Policies pol0 .. pol0+npol-1.
 // -------------------------------------------------------------------------------------
+// Round skipping for the TD launches that are not the fused one (k_tdg, k_tdgw; BwdArgs::skip):
+// every workgroup covering rows of policy `pol` reports whether any of its rows' next actions
+// differ from the previous round's (prev; null in round 0: always "differs"); the last of the
+// `nrep` reports for the policy writes skip[pol] = none differed, counts the statistics and
+// re-arms the two counters (acc, arr: [T] each after skip[T]) for the next launch.  The accumulate
+// is ordered before the arrival by the arrival's agent-scope release; the last arrival acquires.
+__device__ __forceinline__ void tdg_skip_report(int* skip, unsigned long long* skipc, int pol, int T, bool differs,
+                                                bool have_prev, int nrep) {
+  int* acc = skip + T;
+  int* arr = skip + 2 * T;
+  if (differs) __hip_atomic_fetch_or(acc + pol, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int prev = __hip_atomic_fetch_add(arr + pol, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (prev == nrep - 1) {
+    const int any = __hip_atomic_load(acc + pol, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    skip[pol] = any ? 0 : 1;
+    if (skipc && have_prev) {
+      atomicAdd(skipc, 1ull);
+      if (!any) atomicAdd(skipc + 1, 1ull);
+    }
+    __hip_atomic_store(acc + pol, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(arr + pol, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 struct TdgArgs {
   int M, use_gpi, pol0, npol, guess, next_stride, flag_value, pad_;
   const int64_t* a;
@@ -1066,6 +1090,11 @@ struct TdgArgs {
   const int* xmax;
   int poloff, pad2_;
   const float* dz_scale;  // learned φ: the output gradient is scaled by the loss coefficient λ (device)
+  // round skipping (tdg_skip_report): prev = the previous round's next actions (same indexing as
+  // next; null in round 0), skip / skipc as BwdArgs; skip null: no skipping
+  const int64_t* prev;
+  int* skip;
+  unsigned long long* skipc;
 };
 
 __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
@@ -1125,6 +1154,9 @@ __global__ __launch_bounds__(256) void k_tdg(Geo G, TdgArgs A) {
     s_next = am;
     SFX_CHK(b < A.next_stride || !A.next, b, A.next_stride, 0);
     if (A.next) A.next[(size_t)blockIdx.y * A.next_stride + b] = am;
+    if (A.skip)
+      tdg_skip_report(A.skip, A.skipc, pol, T, !A.prev || A.prev[(size_t)blockIdx.y * A.next_stride + b] != am,
+                      A.prev != nullptr, M);
   }
   __syncthreads();
   const float norm = td_norm(G, M, O, A.dz_scale);

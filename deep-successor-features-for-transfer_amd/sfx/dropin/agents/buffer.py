@@ -15,10 +15,22 @@ actions ``[B]`` int64, gammas ``[B]`` float32.
 """
 from __future__ import annotations
 
-import sys
+import weakref
 
 import numpy as np
 import torch
+
+
+def release_minibatch(states, stream=None) -> bool:
+    """Hand the minibatch whose states tensor is `states` back to the ReplayBuffer that lent it
+    (ReplayBuffer.release); False when it did not come from one."""
+    tok = getattr(states, "_sfx_slot", None)
+    buf = tok[0]() if tok is not None else None
+    return buf.release(states, stream) if buf is not None else False
+
+
+def _stream_handle(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
 
 
 def _device():
@@ -40,6 +52,8 @@ class ReplayBuffer:
         self._pidx = None
         self._pB = 0
         self._pev = None
+        self._outs = []
+        self._token = weakref.ref(self)  # identifies this buffer's lendings (ReplayBuffer.release)
         self.index = 0
         self.size = 0
 
@@ -149,26 +163,52 @@ class ReplayBuffer:
                 rs1.index_select(0, idx), gam)
 
     def _out_slot(self, B, n_s, d):
-        """Output tensors for one minibatch: a slot of the buffer's own whose tensors nobody else
-        holds any more (the storage's use count and each returned tensor's reference count are back
-        to what the slot itself holds), else a new allocation.  Reuse is in stream order: the
-        gather that refills a slot runs after every queued kernel that read it."""
-        from torch._C import _storage_Use_Count as use_count
-
+        """Output tensors for one minibatch: a slot of the buffer's own that its consumer handed back
+        (``release``, called by sfx's DeepSF once the update that read the minibatch has settled), else
+        a new allocation.  Ownership is never inferred: a minibatch nobody releases -- kept by the
+        caller, saved by autograd, held by any other consumer -- is never written again.  Reuse is in
+        stream order: the gather that refills a slot is queued after every kernel that read it (a
+        consumer on another stream leaves an event the gather's stream waits for)."""
         for k, sl in enumerate(self._outs):
-            if sl is not None and use_count(sl[0]) == sl[1] and all(
-                    sys.getrefcount(x) == 3 for x in sl[2]):  # the slot's tuple, the loop name, the argument
-                return sl[2]
+            if sl is not None and sl["free"]:
+                sl["free"] = False
+                sl["gen"] += 1
+                if sl["ev"] is not None:
+                    torch.cuda.current_stream(self.device).wait_event(sl["ev"])
+                    sl["ev"] = None
+                sl["views"][0]._sfx_slot = (self._token, k, sl["gen"])
+                return sl["views"]
         # A (int64, as 2B float words) | S | PHI | S1 | G, each contiguous, one allocation
         base = torch.empty(B * (2 * n_s + d + 3), device=self.device)
         a2, S, PHI, S1, G = base.split((2 * B, B * n_s, B * d, B * n_s, B))
         views = (S.view(B, n_s), a2.view(torch.int64), PHI.view(B, d), S1.view(B, n_s), G)
         for k, sl in enumerate(self._outs):
-            if sl is None:  # keep it as a slot (holding the storage object keeps its handle valid)
-                st = base.untyped_storage()
-                self._outs[k] = (st._cdata, use_count(st._cdata), views, (st, base, a2, S, PHI, S1))
+            if sl is None:  # becomes a slot of the buffer's: handed back by its consumer, reused
+                self._outs[k] = {"views": views, "free": False, "gen": 0, "ev": None}
+                views[0]._sfx_slot = (self._token, k, 0)
                 break
         return views
+
+    def release(self, states, stream=None) -> bool:
+        """Hand a minibatch returned by ``replay`` back to the buffer (its states tensor identifies
+        it): its device memory may hold a later minibatch from the next ``replay`` on.  Called by the
+        minibatch's consumer (sfx's DeepSF) after the update that read it has settled; ``stream`` is
+        the consumer's stream (a CUDA stream handle) when it is not the buffer's.  Returns whether
+        the tensors were one of the buffer's slots (a second release of the same lending is a no-op)."""
+        tok = getattr(states, "_sfx_slot", None)
+        if tok is None or tok[0] is not self._token:
+            return False
+        _, k, gen = tok
+        sl = self._outs[k] if self._outs and k < len(self._outs) else None
+        if sl is None or sl["free"] or sl["gen"] != gen or sl["views"][0] is not states:
+            return False
+        if stream is not None and stream != _stream_handle(self.device):
+            with torch.cuda.device(self.device):
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.ExternalStream(stream, device=self.device))
+            sl["ev"] = ev
+        sl["free"] = True
+        return True
 
     def _replay_dev(self, indices, B, rs, ra, rr, rs1):
         """Every field in one gather launch.  The indices and the minibatch's γ go to the kernel in a
@@ -181,7 +221,8 @@ class ReplayBuffer:
             if self._pidx is not None:  # a new batch size: no queued gather may still read the old slots
                 torch.cuda.synchronize(self.device)
             w = B + (B + 1) // 2
-            self._pidx = _lib.HostBuffer(self._RING * w)
+            with torch.cuda.device(self.device):
+                self._pidx = _lib.HostBuffer(self._RING * w)
             self._pB = B
             self._pnp = self._pidx.np.reshape(self._RING, w)
             self._pptr = [self._pidx.ptr + 8 * w * i for i in range(self._RING)]
@@ -209,6 +250,7 @@ class ReplayBuffer:
             self._gdev.data_ptr() if self._gdev is not None else None, p, p + 8 * B, B, S.data_ptr(),
             PHI.data_ptr(), S1.data_ptr(), A.data_ptr(), G.data_ptr(), n_s, d), "sfx_replay_gather")
         if last == self._BLOCK - 1:
-            ev = self._pev[blk] = self._pev[blk] or torch.cuda.Event()
-            ev.record()
+            with torch.cuda.device(self.device):  # the gathers' stream, on the buffer's device
+                ev = self._pev[blk] = self._pev[blk] or torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.device))
         return S, A, PHI, S1, G  # a new tuple: a caller holding it holds each tensor

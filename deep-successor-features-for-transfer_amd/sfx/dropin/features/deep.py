@@ -125,6 +125,7 @@ class DeepSF(SF):
             self._pending = []
             self._eng.close()
         self._eng, self._eng_T = None, 0
+        self._release_held()  # the handle is gone: nothing reads the last minibatch any more
 
     def build_successor(self, task, source=None):
         if self.n_tasks == 0:
@@ -254,6 +255,10 @@ class DeepSF(SF):
             if lb is None:
                 lb = eng._dropin_losses = torch.empty(T, 3, device=eng.device)
             eng.update_all(s, a, phi, s1, g, losses=lb)
+            # update_all settled the step before (host rounds included): its minibatch is read by
+            # nothing queued after this point -- hand it back to the ReplayBuffer that lent it
+            self._release_held()
+            self._held = s
         else:
             for _, i, (s, a, phi, s1, g) in pend:
                 eng.update(i, s, a, None, phi, s1, g, use_gpi=True)
@@ -263,6 +268,16 @@ class DeepSF(SF):
     def _state(self, state):
         s = torch.as_tensor(state)
         return s.reshape(1, -1) if s.dim() == 1 else s.reshape(s.shape[0], -1)
+
+    def _release_held(self):
+        """The minibatch of the last fused update, once a library call has settled that update, goes
+        back to the sfx ReplayBuffer that lent it (agents.buffer alias; a no-op for other tensors)."""
+        held = getattr(self, "_held", None)
+        if held is not None:
+            self._held = None
+            from sfx.dropin.agents.buffer import release_minibatch
+
+            release_minibatch(held, self._eng.stream if self._eng is not None else None)
 
     def get_successor(self, state, policy_index):
         return self.get_successors(state)[:, policy_index]
@@ -289,6 +304,7 @@ class DeepSF(SF):
         move = dev != eng.device
         # one state: the task index is allocated 0-dim (what torch.squeeze would make of it)
         _, q, task, _ = eng.gpi(s, w_index=task_index, task_shape=() if s.shape[0] == 1 else None)
+        self._release_held()  # gpi settled the pending update
         if move:
             q, task = q.to(dev), task.to(dev)
         if task.dim():

@@ -195,7 +195,8 @@ int sfx_step_finish(sfx_t h, int64_t* out_host);
 /* Test hook: make every following fused step run one more round as if the speculation had
  * failed at first_policy (-1: off).  Results must not change. */
 int sfx_debug_force_rerun(sfx_t h, int first_policy);
-/* Speculative rounds launched on the device per fused step (default 2).  Round r > 0
+/* Speculative rounds launched on the device per fused step; 0 = automatic (the default): 2 for
+ * fewer than 16 source tasks (T_glob, after sfx_shard_setup), 3 from 16 on.  Round r > 0
  * re-derives every policy's next actions from round r-1's updated heads; a step whose
  * last device round still flags a policy gets further rounds from sfx_step_finish. */
 int sfx_set_spec_rounds(sfx_t h, int rounds);

@@ -54,8 +54,7 @@ def test_device_ring_matches_the_reference_collation():
 
 
 def test_held_minibatches_survive_slot_reuse_and_ring_wrap():
-    """replay() reuses a minibatch's memory only once nothing outside the buffer holds any of its
-    tensors (or a view of one); 300 replays queued without a synchronisation wrap the 256-slot
+    """replay() reuses a minibatch's memory only after its consumer handed it back; 300 replays queued without a synchronisation wrap the 256-slot
     index ring (its per-block events), and every held minibatch still holds its own rows."""
     from sfx.dropin.agents.buffer import ReplayBuffer
 
@@ -77,17 +76,44 @@ def test_held_minibatches_survive_slot_reuse_and_ring_wrap():
     for got, idx in zip(held, want):
         assert torch.equal(got[0].cpu(), S[idx]) and torch.equal(got[3].cpu(), S[idx] + 0.5)
         assert torch.equal(got[1].cpu(), torch.as_tensor(idx % 7)) and torch.equal(got[2][:, 0].cpu(), torch.as_tensor(idx, dtype=torch.float32))
-    # reuse: a dropped minibatch's memory comes back; one still viewed does not
+    # reuse only after an explicit hand-back: dropping every Python reference is not enough
     del held
     a = buf.replay()
     pa = a[0].data_ptr()
     del a
     b = buf.replay()
-    assert b[0].data_ptr() == pa
-    keep = b[0][1:3]
-    ref = keep.clone()
+    assert b[0].data_ptr() != pa
+    assert buf.release(b[0]) and not buf.release(b[0])  # a second release of one lending is a no-op
+    pb = b[0].data_ptr()
     del b
     c = buf.replay()
-    assert c[0].data_ptr() != pa
+    assert c[0].data_ptr() == pb
+
+
+def test_minibatch_held_only_by_autograd_is_not_overwritten():
+    """a minibatch whose only holder is C++ (autograd saved it for a backward that runs
+    later) keeps its rows however many replays follow -- the buffer never infers ownership; only
+    its consumer's release (sfx DeepSF, after the update that read it settled) frees a slot."""
+    from sfx.dropin.agents.buffer import ReplayBuffer, release_minibatch
+
+    dev = torch.device("cuda", 0)
+    n_s, d, B, cap = 6, 4, 16, 64
+    buf = ReplayBuffer({}, n_samples=cap, n_batch=B)
+    buf.device = dev
+    gen = torch.Generator().manual_seed(3)
+    for k in range(cap):
+        buf.append(torch.randn(1, n_s, generator=gen).to(dev), torch.tensor(k % 5, device=dev),
+                   torch.rand(d, generator=gen).to(dev), torch.randn(1, n_s, generator=gen).to(dev), 0.9)
+    lin = torch.nn.Linear(n_s, 3).to(dev)
+    S = buf.replay()[0]
+    ref = S.clone()
+    out = (lin(S) ** 2).sum()  # autograd saves S for the weight gradient
+    del S
+    for _ in range(20):  # replays (some handed back) that would reuse an inferred-free slot
+        t = buf.replay()
+        release_minibatch(t[0])
+        del t
+    out.backward()
+    want = torch.autograd.grad((lin(ref) ** 2).sum(), lin.weight)[0]
     torch.cuda.synchronize()
-    assert torch.equal(keep, ref)
+    assert torch.allclose(lin.weight.grad, want, rtol=1e-6, atol=1e-6)

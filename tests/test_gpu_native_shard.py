@@ -120,6 +120,23 @@ def test_native_sharded_single_rank_rccl(fused, force, monkeypatch):
     _oracle_check(cfg, recs, final, heads, targets, ws)
 
 
+@pytest.mark.parametrize("t_loc,force", [(40, None), (64, 1)], ids=["40-heads", "64-heads-host-rounds"])
+def test_native_sharded_single_rank_many_heads(t_loc, force, monkeypatch):
+    """BASELINE config C4's 64 source tasks on ONE GPU: the sharded schedule at
+    world 1 with T_loc * A > 256 takes its GPI maxima from the wide kernels (k_qmaxw: one workgroup
+    per (row, 8 policies), lane = head), three device rounds by
+    default (T_glob >= 16) with round skipping in the unfused TD launch (tdg_skip_report) -- through
+    real RCCL all-reduces and, forced, host rounds.  Every env action bit-exact to the in-order
+    oracle."""
+    monkeypatch.setenv("SFX_RCCL_WORLD1", "1")
+    cfg = dict(SMALL, spec=dict(n_s=17, H=16, A=7, d=8, acts=("relu", "relu")), world=1, t_loc=t_loc, steps=14)
+    recs, final, heads, targets, ws, stats, counters = _run_rank(0, cfg, "rccl", force_rerun=force)
+    assert counters.sum() == cfg["steps"]
+    if force is not None:
+        assert stats["host_round_steps"] >= 4, stats
+    _oracle_check(cfg, recs, final, heads, targets, ws)
+
+
 def test_native_sharded_rccl_host_rounds_pipelined(monkeypatch):
     """Host rounds on the split communicator while the next step is pre-launched: RCCL forced at
     world 1, every step's device rounds treated as failed (sfx_debug_force_rerun), so each step's

@@ -112,6 +112,36 @@ def test_runner_four_heads_wide_backward():
     eng.close()
 
 
+@pytest.mark.parametrize("T,force", [(40, -1), (64, 1)], ids=["40-heads", "64-heads-host-rounds"])
+def test_runner_many_heads_matches_oracle(T, force):
+    """The all-task step over many heads (T·A > 256): next actions from k_tdgw, verification by
+    k_verw (one workgroup per (row, 8 policies), lane = head),
+    3 device rounds by default, host rounds forced in the second case.  Every greedy action of the
+    runner bit-exact to the oracle's in-order loop (agents/sfdqn.py:57-60), heads within the Adam
+    tolerance."""
+    from sfx.runner import NativeEnvLoop
+
+    spec = R.Spec(17, 16, 7, 8, ("relu", "relu"))
+    ev, alpha, n = 6, 0.05, 14
+    eng, st = make(spec, T, ev)
+    if force >= 0:
+        eng.debug_force_rerun(force)
+    loop = NativeEnvLoop(eng, batch=16, capacity=200, gamma=0.9, epsilon=0.3, alpha_w=alpha, episode_len=7, seed=6)
+    loop.prefill(20)
+    loop.set_task(T - 3)
+    loop.record(n)
+    loop.run(n)
+    recs = loop.records()
+    replay_with_oracle(st, spec, recs, alpha, ev, loop.action())
+    check_state(eng, st, T, n)
+    sk = eng.skip_stats()
+    assert sk["policies_checked"] > 0 and sk["policies_skipped"] > 0, sk
+    if force >= 0:
+        assert loop.stats()["host_round_steps"] >= n // 2
+    loop.close()
+    eng.close()
+
+
 def test_runner_with_python_env_callbacks():
     """A host env passed as callbacks (tasks/task.py interface) drives the same loop."""
     from sfx.runner import NativeEnvLoop
@@ -432,17 +462,19 @@ def test_runner_host_rounds_with_every_queue_shared():
             hip.hipStreamDestroy(s)
 
 
-@pytest.mark.parametrize("spec_rounds,force", [(2, -1), (2, 1), (3, -1)])
-def test_round_skip_is_bit_exact(spec_rounds, force, monkeypatch):
+@pytest.mark.parametrize("spec_rounds,force,T", [(2, -1, 6), (2, 1, 6), (3, -1, 6), (0, -1, 40), (0, 2, 40)],
+                         ids=["r2", "r2-host-rounds", "r3", "wide-auto", "wide-auto-host-rounds"])
+def test_round_skip_is_bit_exact(spec_rounds, force, T, monkeypatch):
     """Speculative rounds r >= 1 skip the backward and Adam of a policy whose next actions repeat
     round r-1's (BwdArgs::skip).  The skipped update would have repeated round r-1's bit for bit,
     so the heads, the moments and every action must be IDENTICAL with skipping off (SFX_SKIP=0)
     -- including steps finished by host rounds (force) -- and the device counters must show
-    skipped policies."""
+    skipped policies.  T = 40 (T·A > 256): the unfused TD launch (k_tdgw) decides the skips by
+    per-policy arrivals, 3 device rounds (the automatic count from 16 source tasks on)."""
     from sfx.runner import NativeEnvLoop
 
-    spec = R.Spec(17, 64, 7, 8, ("relu", "relu"))
-    T, ev, n = 6, 9, 30
+    spec = R.Spec(17, 64 if T < 16 else 16, 7, 8, ("relu", "relu"))
+    ev, n = 9, 30
     out = {}
     for skip in ("1", "0"):
         monkeypatch.setenv("SFX_SKIP", skip)
@@ -468,7 +500,8 @@ def test_round_skip_is_bit_exact(spec_rounds, force, monkeypatch):
     for (ma, va, sa), (mb, vb, sb) in zip(m1, m0):
         assert torch.equal(ma, mb) and torch.equal(va, vb) and sa == sb
     assert s0["policies_checked"] == 0
-    assert s1["policies_checked"] >= n * (spec_rounds - 1) * T // 2 and s1["policies_skipped"] > 0, s1
+    rounds = spec_rounds or (3 if T >= 16 else 2)
+    assert s1["policies_checked"] >= n * (rounds - 1) * T // 2 and s1["policies_skipped"] > 0, s1
 
 
 @pytest.mark.parametrize("force,ev", [(-1, 7), (1, 1000), (2, 1000)])
