@@ -332,26 +332,27 @@ def bench_sharded(args, world, rank, device, barrier, dist, steps=None, warmup=N
             "rounds": st}
 
 
-def bench_sharded_tsf(args, world, rank, device, barrier, dist):
+def bench_sharded_tsf(args, world, rank, device, barrier, dist, steps=None, warmup=None, heads=None):
     """BASELINE config C5 (tsfdqn_nf.py, 32 source tasks over 4 GPUs): T_loc = --heads per rank,
-    T_glob = T_loc * world, one lock-step env stream on every rank, GPI maxima and the action key
-    all-reduced (MAX) over RCCL, h and w_i broadcast from the active task's owner."""
+    T_glob = T_loc * world, one env / replay stream replicated on every rank (same seed), the native
+    runner's "sharded_tsf" schedule: the active policy's GPI maxima and (one call) the owner's h and
+    w_task ++ the env action's q table all-reduced (MAX) by libsfx inside the pre-launched step
+    graphs (RCCL; the host transport for gloo rehearsals)."""
     from sfx.engine import SFEngine
-    from sfx.runner import ShardedTSFEnvLoop
-    from sfx.shard import all_reduce_max_fn, broadcast_fn
+    from sfx.runner import NativeEnvLoop
+    from sfx.shard import init_comm, set_host_comm
 
-    sh, T_loc, B = TSF_SHAPE, args.heads, args.batch
+    sh, B = TSF_SHAPE, args.batch
+    T_loc = heads or args.heads
     Tg = T_loc * world
+    steps = args.shard_steps if steps is None else steps
+    warmup = max(20, steps // 10) if warmup is None else warmup
     eng = SFEngine(T_loc, sh["n_s"], sh["H"], sh["A"], sh["d"], sh["acts"], max_batch=B, device=device)
     eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
     eng.set_target_update_ev(1000)
     eng.tsf_setup(sh["G"], args.tsf_K, 1.0, 1e-3, 0.0, 1e-3, 0.0)
+    eng.shard_setup(Tg, rank * T_loc)
     online, w, g, h = tsf_problem(Tg, args.tsf_K, seed=0)
-    if world > 1:
-        ar, bc = all_reduce_max_fn(via_host=args.via_host), broadcast_fn(via_host=args.via_host)
-    else:
-        ar, bc = (lambda t: None), (lambda t, src: None)
-    loop = ShardedTSFEnvLoop(eng, Tg, rank, ar, bc, batch=B, seed=1)
     for t in range(T_loc):
         eng.load_head(t, online[rank * T_loc + t], 0)
         eng.load_head(t, online[rank * T_loc + t], 1)
@@ -359,26 +360,40 @@ def bench_sharded_tsf(args, world, rank, device, barrier, dist):
     for t in range(Tg):
         eng.load_w(t, w[t])
     eng.tsf_load_h(h)
+    if args.via_host:
+        set_host_comm(eng, rank, world)
+    else:
+        init_comm(eng, rank, world)
+    loop = NativeEnvLoop(eng, batch=B, seed=1, schedule="sharded_tsf", p_end=0.01)
+    loop.set_wait_timeout(30.0)
     loop.prefill(1000)
     loop.set_task(0)
-    loop.run(max(20, args.shard_steps // 10))
+    loop.warm()
+    loop.run(warmup)
     barrier()
     t0 = time.perf_counter()
-    loop.run(args.shard_steps)
+    loop.run(steps)
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
         t = torch.tensor([dt], device="cpu" if args.via_host else device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    st = loop.stats()
+    comm = eng.comm_state()
+    comm.update(eng.comm_size())
+    comm["rccl_forced_world1"] = os.environ.get("SFX_RCCL_WORLD1") == "1"
+    loop.close()
     eng.close()
-    v = args.shard_steps / dt
-    return {"value": round(v, 2), "unit": "env steps/s", "ms_per_step": round(1000.0 * dt / args.shard_steps, 4),
-            "steps": args.shard_steps, "heads_total": Tg, "heads_per_gpu": T_loc,
+    v = steps / dt
+    return {"value": round(v, 2), "unit": "env steps/s", "ms_per_step": round(1000.0 * dt / steps, 4),
+            "steps": steps, "warmup": warmup, "heads_total": Tg, "heads_per_gpu": T_loc,
             "parallelism": f"TSF heads sharded over {world} GPU(s)",
-            "collective": (("gloo via host (rehearsal)" if args.via_host else "RCCL") +
-                           " all-reduce(MAX) of GPI maxima [B,A] + int64 action key, broadcast of h and w_i "
-                           "from the active task's owner") if world > 1 else "none (1 rank)"}
+            "loop": "native C++ runner (sfx_runner schedule sharded_tsf): one pre-launched graph per env step",
+            "comm": comm, "prelaunched": st["prelaunched"],
+            "collective": ("gloo via host (rehearsal)" if args.via_host else "RCCL (library-owned communicator)") +
+                          " all-reduce(MAX): the active policy's GPI maxima [B,A], then the owner's h ++ w_task "
+                          "(raw bits, a broadcast) ++ the env action's q table [T_glob,A] in one call"}
 
 
 def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) -> dict:
@@ -759,6 +774,14 @@ def main():
                 os.environ.pop("SFX_RCCL_WORLD1", None)
     elif args.shard_steps > 0 and args.schedule == "tsf":
         sharded = bench_sharded_tsf(args, world, rank, device, barrier, dist)
+        if world == 1 and not args.via_host:
+            os.environ["SFX_RCCL_WORLD1"] = "1"  # the collectives really issued, at one rank
+            try:
+                sharded_rccl1 = bench_sharded_tsf(args, world, rank, device, barrier, dist)
+            except Exception as e:
+                sharded_rccl1 = {"error": repr(e)[:400]}
+            finally:
+                os.environ.pop("SFX_RCCL_WORLD1", None)
 
     workload = (f"reacher17-{args.schedule}-T{T}-B{B}" if args.tsf_K is None else
                 f"hopper11-tsf{'-nf' + str(args.tsf_K) if args.tsf_K else ''}-T{T}-B{B}")

@@ -215,6 +215,9 @@ struct sfx_handle {
   // sharded step, sortable int32: maxima buffers xb[2] ([Tg][Mmax][A] ++ q table [Tg][A]) and the
   // pre-step part xge ([Tg][Mmax][A]) of the fused path (shard_fused)
   int *xb[2] = {nullptr, nullptr}, *xge = nullptr;
+  // sharded TSF step (runner schedule sharded_tsf): the active policy's GPI maxima [Mmax][A] and the
+  // owner's h / w_task ++ the selection table [Ph + d + Tg * A] (sortable / raw int32 words)
+  int *tsx = nullptr, *tsz = nullptr;
   int *qh = nullptr, *qhs = nullptr;  // local heads' own maxima terms (FwdArgs::qh), qhs inside qh's block
   bool shard_qa = true;  // SFX_SHARD_QA=0: maxima by separate k_qmax launches
   struct ShardPending {
@@ -908,6 +911,8 @@ void free_all(sfx_handle* h) {
   if (h->on16) (void)hipFree(h->on16);
   if (h->tg16) (void)hipFree(h->tg16);
   if (h->host_ar_buf) (void)hipHostFree(h->host_ar_buf);
+  for (int* p : {h->tsx, h->tsz})
+    if (p) (void)hipFree(p);
   for (int* p : {h->xb[0], h->xb[1]})  // xge lives in xb[0]'s block
     if (p) (void)hipFree(p);
   if (h->comm_rounds) (void)rccl().CommDestroy(h->comm_rounds);

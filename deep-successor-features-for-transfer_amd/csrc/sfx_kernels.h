@@ -3020,4 +3020,37 @@ __global__ __launch_bounds__(256) void k_sfinish(SfinArgs F) {
   }
 }
 
+
+// -------------------------------------------------------------------------------------
+// TSF-DQN with the heads sharded (BASELINE config C5; the native runner's "sharded_tsf"
+// schedule): after the active task's owner has updated (tsfdqn.py:588-709), the
+// shared h and w_task go from the owner to every rank as ONE all-reduce(MAX) over int32 words --
+// the owner contributes their raw bits, every other rank INT_MIN, and max(b, INT_MIN) = b for
+// every 32-bit pattern b, so the reduced words are the owner's bits exactly (a broadcast, -0 and
+// NaN payloads included).  k_tsx_pack fills the words, k_tsx_unpack writes them back (every rank;
+// the owner rewrites its own values; nothing in a cancelled step).
+// -------------------------------------------------------------------------------------
+struct TsxArgs {
+  int nsh, Ph, own, pad_;
+  float* hp;     // h parameters [Ph]
+  float* w;      // w_task row [nsh - Ph]
+  int* z;        // [nsh]
+  const int* cancel;
+};
+
+__global__ __launch_bounds__(256) void k_tsx_pack(TsxArgs X) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < X.nsh) X.z[j] = X.own ? __float_as_int(j < X.Ph ? X.hp[j] : X.w[j - X.Ph]) : (int)0x80000000;
+}
+
+__global__ __launch_bounds__(256) void k_tsx_unpack(TsxArgs X) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= X.nsh || step_cancelled(X.cancel)) return;
+  const float v = __int_as_float(X.z[j]);
+  if (j < X.Ph)
+    X.hp[j] = v;
+  else
+    X.w[j - X.Ph] = v;
+}
+
 }  // namespace sfx

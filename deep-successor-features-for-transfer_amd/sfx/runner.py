@@ -225,8 +225,11 @@ class NativeEnvLoop:
     """The env-step loop of EnvLoop run by libsfx's native runner (include/sfx.h, sfx_runner_*):
     C++ env + replay ring on the host, one pre-launched hipGraph per env step whose gate kernel
     waits for the host's inputs.  schedule: "all" (main_sfdqn_torch.py), "active" (sfdqn.py /
-    agents/sfdqn_sequential.py: the active head with l2 and an Adam-trained w, no LMS) or "tsf"
-    (TSFDQN.update_successor; needs SFEngine.tsf_setup).  p_end: per-step episode-end
+    agents/sfdqn_sequential.py: the active head with l2 and an Adam-trained w, no LMS), "tsf"
+    (TSFDQN.update_successor; needs SFEngine.tsf_setup), "sharded" (the all-task step with the
+    heads split over ranks, BASELINE config C4) or "sharded_tsf" (the TSF step with the heads split
+    over ranks, config C5: tsf_setup + shard_setup + a communicator; the active task is a global
+    index and its owner updates).  p_end: per-step episode-end
     probability of the built-in synthetic task (0: never terminates, like tasks/reacher.py).
 
     env: None for the built-in synthetic Reacher-shape task, or an object with
@@ -235,7 +238,7 @@ class NativeEnvLoop:
     """
 
     FIELDS = ("s", "s1", "phi", "a", "gamma", "snext", "phi1", "r1", "rb")
-    SCHEDULES = {"all": 0, "active": 1, "tsf": 2, "sharded": 3}
+    SCHEDULES = {"all": 0, "active": 1, "tsf": 2, "sharded": 3, "sharded_tsf": 4}
 
     def __init__(self, engine: SFEngine, batch: int = 32, capacity: int = 1_000_000, gamma: float = 0.9,
                  epsilon: float = 0.1, alpha_w: float = 1e-3, episode_len: int = 500, use_gpi: bool = True,
@@ -349,7 +352,7 @@ class NativeEnvLoop:
                 "nonfinite_steps": nf.value, "ahead_pre_steps": ps.value, "ahead_own_forward_steps": ofs.value}
 
     def gpi_counters(self) -> np.ndarray:
-        T = self.eng.T_glob if self.schedule == "sharded" else self.eng.T
+        T = self.eng.T_glob if self.schedule.startswith("sharded") else self.eng.T
         out = np.zeros(T * T, dtype=np.int64)
         self._check(self._lib.sfx_runner_gpi_counters(self._r, out.ctypes.data_as(self._C.POINTER(self._C.c_longlong))),
                     "sfx_runner_gpi_counters")

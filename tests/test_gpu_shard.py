@@ -279,3 +279,114 @@ def _tsf_worker(rank, port, q, cfg=TSF_SMALL):
 @pytest.mark.parametrize("cfg", [TSF_SMALL, TSF_FULL, TSF_C5], ids=["small", "c5-shape", "c5-4x8-k100"])
 def test_tsf_two_ranks_on_one_gpu(cfg):
     _tsf_check(_two_ranks(_tsf_worker, cfg), True, cfg)
+
+
+# ---- the NATIVE sharded TSF loop (sfx_runner schedule "sharded_tsf") --------
+def _native_tsf_rank(rank, world, cfg, comm, use_gpi=True, steps=10, task=None):
+    """One rank of the native runner's sharded TSF step: T_glob / world heads, the env and replay
+    replicated (same seed), every collective issued by libsfx (RCCL inside the step graphs, or the
+    host transport for ranks sharing the GPU)."""
+    from sfx.engine import SFEngine
+    from sfx.runner import NativeEnvLoop
+    from sfx.shard import init_comm, set_host_comm
+
+    sp, TGc, Bc = cfg["spec"], cfg["tg"], cfg["b"]
+    online, w, gs, g, h = _tsf_problem(cfg)
+    T_loc = TGc // world
+    eng = SFEngine(T_loc, sp["n_s"], sp["H"], sp["A"], sp["d"], sp["acts"], max_batch=Bc)
+    eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
+    eng.set_target_update_ev(EV)
+    eng.tsf_setup(cfg["G"], cfg["K"], 1.0, 1e-3, 0.0, 1e-3, 0.0)
+    eng.shard_setup(TGc, rank * T_loc)
+    for t in range(T_loc):
+        eng.load_head(t, online[rank * T_loc + t], 0)
+        eng.load_head(t, online[rank * T_loc + t], 1)
+        eng.tsf_load_g(t, g[rank * T_loc + t])
+    for t in range(TGc):
+        eng.load_w(t, w[t])
+    eng.tsf_load_h(h)
+    if comm == "rccl":
+        init_comm(eng, rank, world)
+    else:
+        set_host_comm(eng, rank, world)
+    loop = NativeEnvLoop(eng, batch=Bc, capacity=300, gamma=0.9, epsilon=0.3, episode_len=9, seed=21,
+                         schedule="sharded_tsf", upd_use_gpi=use_gpi, p_end=0.1)
+    loop.prefill(Bc - 3)  # the first 2 steps run without a minibatch
+    loop.set_task(TGc - 2 if task is None else task)  # owned by the last rank
+    loop.record(steps)
+    loop.run(steps)
+    recs = loop.records()
+    final = loop.action()
+    stats = loop.stats()
+    out = (recs, final, torch.stack([eng.get_head(t) for t in range(T_loc)]),
+           torch.stack([eng.tsf_get_g(t)[0] for t in range(T_loc)]), eng.tsf_get_h(),
+           torch.stack([eng.get_w(t)[0] for t in range(TGc)]), stats, loop.gpi_counters())
+    loop.close()
+    eng.close()
+    return out
+
+
+def _native_tsf_check(cfg, recs, final, heads, gg, h, w, use_gpi=True):
+    from tests.test_gpu_engine import params_close, rel_close
+
+    spec = R.Spec(**cfg["spec"])
+    online, w0, gs, g0, h0 = _tsf_problem(cfg)
+    st = R.TSFState(spec, online.clone(), online.clone(), w0.clone(), gspec=gs, g=g0.clone(), h=h0.clone())
+    assert [r["have"] for r in recs[:4]] == [0, 0, 1, 1]
+    for k, rec in enumerate(recs):
+        task = rec["task"]
+        if rec["have"]:
+            batch = (torch.from_numpy(rec["s"]), torch.from_numpy(rec["a"]), torch.from_numpy(rec["rb"]).view(-1, 1),
+                     torch.from_numpy(rec["phi"]), torch.from_numpy(rec["s1"]), torch.from_numpy(rec["gamma"]))
+            R.tsf_update(st, batch, task, use_gpi=use_gpi, target_update_ev=EV)
+        q, tk = R.gpi_w(R.psi_all(st.online, spec, torch.from_numpy(rec["snext"]).view(1, -1)), st.w[task])
+        want = (int(tk[0]), R.select_action(q, tk[0], task, True))
+        got = (recs[k + 1]["c"], recs[k + 1]["a_greedy"]) if k + 1 < len(recs) else final
+        assert got == want, f"step {k}: runner selected {got}, oracle {want}"
+    n = len(recs)
+    params_close(heads, st.online, 1e-3 * n)
+    params_close(gg, st.g, 1e-3 * n)
+    params_close(h, st.h, 1e-3 * n)
+    rel_close(w, st.w, rtol=1e-4, atol=1e-7)
+
+
+@pytest.mark.parametrize("use_gpi", [True, False])
+def test_native_tsf_single_rank_rccl(use_gpi, monkeypatch):
+    """World 1 with the library's own RCCL communicator, the collectives forced (SFX_RCCL_WORLD1=1):
+    the GPI maxima all-reduce and the h / w_task ++ selection-table all-reduce are ncclAllReduce
+    calls inside the pre-launched step graphs.  Every recorded env action bit-exact to the
+    oracle's TSFDQN.update_successor replay (tsfdqn.py:588-709), parameters within tolerance."""
+    monkeypatch.setenv("SFX_RCCL_WORLD1", "1")
+    recs, final, heads, gg, h, w, stats, counters = _native_tsf_rank(0, 1, TSF_SMALL, "rccl", use_gpi, steps=16)
+    assert stats["prelaunched"] >= 8, stats
+    assert counters.sum() == 16
+    _native_tsf_check(TSF_SMALL, recs, final, heads, gg, h, w, use_gpi)
+
+
+def _native_tsf_worker(rank, port, q, cfg):
+    import torch.distributed as dist
+
+    world = cfg.get("world", 2)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        recs, final, heads, gg, h, w, stats, _ = _native_tsf_rank(rank, world, cfg, "host", steps=10)
+        parts = [None] * world
+        dist.all_gather_object(parts, (heads, gg, [(r["c"], r["a_greedy"], r["a_taken"]) for r in recs]))
+        if rank == 0:
+            q.put((recs, final, torch.cat([p[0] for p in parts]).numpy(), torch.cat([p[1] for p in parts]).numpy(),
+                   h.numpy(), w.numpy(), [p[2] for p in parts]))
+            q.close()
+            q.join_thread()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg", [TSF_SMALL, TSF_C5], ids=["2x2-small", "c5-4x8-k100"])
+def test_native_tsf_ranks_on_one_gpu(cfg):
+    """The native sharded TSF loop at several ranks sharing this GPU (host transport over gloo),
+    including BASELINE config C5 at its stated size (4 ranks x 8 Hopper TSF-NF heads, K = 100): the
+    ranks record the same stream, and the oracle's in-order replay reproduces every env action."""
+    recs, final, heads, gg, h, w, streams = _two_ranks(_native_tsf_worker, cfg)
+    assert all(s == streams[0] for s in streams), "ranks diverged"
+    _native_tsf_check(cfg, recs, final, heads, gg, h, w)
