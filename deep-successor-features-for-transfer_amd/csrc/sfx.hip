@@ -1118,8 +1118,11 @@ bool tsf_tail_rider(sfx_handle* h, int policy, int B, const float* S, const floa
 // (R_A, its own group) and of the minibatch share launches; then the selection's last layer, the
 // choice and the publication; the minibatch's last layer comes after them, so it runs while the
 // host turns the published action into the next step's inputs.
+// task: the active LOCAL head, or -1 when another rank owns it (the sharded TSF schedule: this
+// rank forwards the next minibatch's S1 through its heads only).  pick: the selection in place of
+// select_pick (sharded: this rank's q-table slice, the all-reduce, the pick and its publication).
 int select_ahead_body(sfx_handle* h, const float* s, const float* ax, const float* axphi, int B, int task,
-                      int use_gpi, int64_t* out, const SelPub* pub) {
+                      int use_gpi, int64_t* out, const SelPub* pub, const std::function<int()>* pick = nullptr) {
   const int T = h->T, n_s = h->n_s;
   const float* S = ax;
   const float* S1 = ax + (size_t)B * n_s;
@@ -1127,6 +1130,7 @@ int select_ahead_body(sfx_handle* h, const float* s, const float* ax, const floa
     FwdExtra fx = fx0;
     fx.lN = h->NL - 1;
     fx.xc = s;
+    if (task < 0) return run_fwd(h, {{R_A, P_ONLINE, 3, 0, T, 1, 0}, {R_NS1, P_ONLINE, 2, 0, T, B, 0}}, B, S, S1, fx);
     return run_fwd(h, {{R_A, P_ONLINE, 3, 0, T, 1, 0}, {R_NS1, P_ONLINE, 2, 0, T, B, 0}, {R_NS, P_ONLINE, 1, task, 1, B, 0},
                        {R_NS1T, P_TARGET, 2, task, 1, B, 0}},
                    B, S, S1, fx);
@@ -1134,15 +1138,20 @@ int select_ahead_body(sfx_handle* h, const float* s, const float* ax, const floa
   // TSF: the chains in the first launch, the Linear of g and φ̃ (the tail) in the selection
   // launch when it can take them, so they run beside the selection instead of after the chains
   TsfTail tail;
-  const bool split = axphi && T <= 64 && h->A <= 256 && tsf_tail_rider(h, task, B, S, S1, axphi, &tail);
-  if (axphi)
+  const bool split = axphi && !pick && task >= 0 && T <= 64 && h->A <= 256 &&
+                     tsf_tail_rider(h, task, B, S, S1, axphi, &tail);
+  if (axphi && task >= 0)
     RC(tsf_fwd_with(h, task, B, S, S1, axphi, early, s, split ? 1 : 0));
   else
     RC(early(FwdExtra()));
   FwdExtra last;
   last.l0 = h->NL - 1;
   RC(run_fwd(h, {{R_A, P_ONLINE, 3, 0, T}}, 1, nullptr, nullptr, last));
-  RC(select_pick(h, task, use_gpi, nullptr, out, pub, split ? &tail : nullptr));
+  if (pick)
+    RC((*pick)());
+  else
+    RC(select_pick(h, task, use_gpi, nullptr, out, pub, split ? &tail : nullptr));
+  if (task < 0) return run_fwd(h, {{R_NS1, P_ONLINE, 2, 0, T}}, B, nullptr, nullptr, last);
   return run_fwd(h, {{R_NS1, P_ONLINE, 2, 0, T}, {R_NS, P_ONLINE, 1, task, 1}, {R_NS1T, P_TARGET, 2, task, 1}}, B,
                  nullptr, nullptr, last);
 }
@@ -1406,7 +1415,7 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   alloc((void**)&h->dz, sizeof(float) * (size_t)T * h->actSize);
   alloc((void**)&h->rowloss, sizeof(float) * (size_t)T * MMAX);
   alloc((void**)&h->spec_next, sizeof(int64_t) * 2 * (size_t)T * MMAX);
-  alloc((void**)&h->skip, sizeof(int) * 3 * (size_t)T);  // skip [T] | arrival accumulators [T] | arrivals [T]
+  alloc((void**)&h->skip, sizeof(int) * 2 * (size_t)T);  // skip [T] | the unfused TD launch's report words [T]
   alloc((void**)&h->skipc, 64);
   alloc((void**)&h->dout, sizeof(StepOut));
   alloc((void**)&h->selk, sizeof(SelScratch));

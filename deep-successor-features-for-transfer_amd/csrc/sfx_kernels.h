@@ -1056,25 +1056,24 @@ __device__ __forceinline__ float td_loss(float huber, float x) {
 // -------------------------------------------------------------------------------------
 // Round skipping for the TD launches that are not the fused one (k_tdg, k_tdgw; BwdArgs::skip):
 // every workgroup covering rows of policy `pol` reports whether any of its rows' next actions
-// differ from the previous round's (prev; null in round 0: always "differs"); the last of the
-// `nrep` reports for the policy writes skip[pol] = none differed, counts the statistics and
-// re-arms the two counters (acc, arr: [T] each after skip[T]) for the next launch.  The accumulate
-// is ordered before the arrival by the arrival's agent-scope release; the last arrival acquires.
+// differ from the previous round's (prev; null in round 0: always "differs") with ONE relaxed
+// atomic add on the policy's word -- 1 per report, + 2^16 when it differs -- so the count and the
+// verdict travel in the same word and no release / acquire (an L2 write-back per workgroup on
+// gfx950's 8 XCDs) is needed; the report that completes the count (`nrep`) writes skip[pol] (read
+// by the later launches of the round: the kernel boundary orders it), counts the statistics and
+// re-arms the word ([T] after skip[T]) for the next launch.
 __device__ __forceinline__ void tdg_skip_report(int* skip, unsigned long long* skipc, int pol, int T, bool differs,
                                                 bool have_prev, int nrep) {
-  int* acc = skip + T;
-  int* arr = skip + 2 * T;
-  if (differs) __hip_atomic_fetch_or(acc + pol, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int prev = __hip_atomic_fetch_add(arr + pol, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-  if (prev == nrep - 1) {
-    const int any = __hip_atomic_load(acc + pol, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int* word = skip + T + pol;
+  const int old = __hip_atomic_fetch_add(word, differs ? 0x10001 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((old & 0xFFFF) == nrep - 1) {
+    const bool any = (old >> 16) != 0 || differs;
     skip[pol] = any ? 0 : 1;
     if (skipc && have_prev) {
       atomicAdd(skipc, 1ull);
       if (!any) atomicAdd(skipc + 1, 1ull);
     }
-    __hip_atomic_store(acc + pol, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(arr + pol, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(word, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -2963,9 +2962,9 @@ struct SfinArgs {
   long long* stall;       // test hook (sfx_debug_stall): one-shot delay before the publication
 };
 
-// One workgroup: verification of the speculated next actions (k_sverify), the env action, and
-// in runner steps the publication of both.
-__global__ __launch_bounds__(256) void k_sfinish(SfinArgs F) {
+// One workgroup of 1024 threads: verification of the speculated next actions (k_sverify), the env
+// action, and in runner steps the publication of both.
+__global__ __launch_bounds__(1024) void k_sfinish(SfinArgs F) {
   __shared__ int s_min;
   __shared__ unsigned long long s_best;
   const int tid = threadIdx.x, Aa = F.A;
@@ -2977,12 +2976,12 @@ __global__ __launch_bounds__(256) void k_sfinish(SfinArgs F) {
   int mine = F.Tg;
   if (F.X) {
     const FDiv fM = fdiv(F.M);
-    for (int j = tid; j < F.Tg * F.M; j += 256)
+    for (int j = tid; j < F.Tg * F.M; j += blockDim.x)
       if (first_argmax(F.X + (size_t)j * Aa, Aa) != first_argmax(F.Y + (size_t)j * Aa, Aa)) mine = min(mine, j / fM);
   }
   // packed (q, first index) keys as k_skey: the max key is argmax_t max_a, then argmax_a
   unsigned long long best = 0ull;
-  for (int j = tid; j < F.Tg * Aa; j += 256) {
+  for (int j = tid; j < F.Tg * Aa; j += blockDim.x) {
     const int qi = F.q[j];
     if (qi == SORT_EMPTY) continue;
     const unsigned long long key =

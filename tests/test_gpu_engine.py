@@ -214,6 +214,41 @@ def test_update_all_host_rounds_with_temporary_inputs():
     eng.close()
 
 
+def test_gpi_right_after_update_all_sees_the_host_rounds():
+    """while an update_all verdict is pending, sfx_gpi is queued speculatively on the
+    update's write slots and re-run only when settle() counts a fallback.  Force the fallback
+    (sfx_debug_force_rerun) and call gpi at once: q, the task and the next actions must be the
+    oracle's on the post-update heads (the re-run GPI, not the speculative one), and the step must
+    be counted as a host-round step."""
+    from sfx.init import reference_heads
+
+    spec, T, B = R.Spec(17, 64, 7, 8), 5, 32
+    online, w = reference_heads(T, spec.n_s, spec.H, spec.A, spec.d, spec.acts, seed=8)
+    eng = engine_for(spec, T)
+    for t in range(T):
+        eng.load_head(t, online[t], 0)
+        eng.load_head(t, online[t], 1)
+        eng.load_w(t, w[t])
+    st = R.SFState(spec, online.clone(), online.clone(), w.clone())
+    gen = torch.Generator().manual_seed(12)
+    for k in range(3):
+        b = (torch.randn(B, 17, generator=gen), torch.randint(0, 7, (B,), generator=gen),
+             torch.rand(B, 8, generator=gen), torch.randn(B, 17, generator=gen), torch.full((B,), 0.9))
+        S = torch.randn(6, 17, generator=gen)
+        before = eng.step_stats()["host_round_steps"]
+        eng.debug_force_rerun(1)
+        eng.update_all(*(x.cuda() for x in b))
+        _, q, task, nxt = eng.gpi(S.cuda(), w_index=k + 1)  # right away: the verdict is still pending
+        eng.debug_force_rerun(-1)
+        R.deep_all_task_step(st, b)
+        q_ref, task_ref = R.gpi_w(R.psi_all(st.online, spec, S), st.w[k + 1])
+        rel_close(q.cpu(), q_ref, rtol=1e-4, atol=1e-6)
+        assert torch.equal(task.cpu(), task_ref)
+        assert torch.equal(nxt.cpu(), R.gpi_next_actions(q_ref))
+        assert eng.step_stats()["host_round_steps"] == before + 1
+    eng.close()
+
+
 def test_full_size_update_vs_oracle():
     """BASELINE C2 shape (H=256, T=8): one active-task and one all-task step against the oracle."""
     from tests.golden.recipe import SHAPES, full_size_heads

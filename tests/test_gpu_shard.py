@@ -350,13 +350,17 @@ def _native_tsf_check(cfg, recs, final, heads, gg, h, w, use_gpi=True):
     rel_close(w, st.w, rtol=1e-4, atol=1e-7)
 
 
-@pytest.mark.parametrize("use_gpi", [True, False])
-def test_native_tsf_single_rank_rccl(use_gpi, monkeypatch):
+@pytest.mark.parametrize("use_gpi,ahead", [(True, "1"), (False, "1"), (True, "0")],
+                         ids=["gpi", "own-psi", "gpi-no-lookahead"])
+def test_native_tsf_single_rank_rccl(use_gpi, ahead, monkeypatch):
     """World 1 with the library's own RCCL communicator, the collectives forced (SFX_RCCL_WORLD1=1):
     the GPI maxima all-reduce and the h / w_task ++ selection-table all-reduce are ncclAllReduce
-    calls inside the pre-launched step graphs.  Every recorded env action bit-exact to the
-    oracle's TSFDQN.update_successor replay (tsfdqn.py:588-709), parameters within tolerance."""
+    calls inside the pre-launched step graphs; with the look-ahead (default) each step's selection
+    also forwards the next minibatch (select_ahead_body; the owner's TSF forward riding along).
+    Every recorded env action bit-exact to the oracle's TSFDQN.update_successor replay
+    (tsfdqn.py:588-709), parameters within tolerance."""
     monkeypatch.setenv("SFX_RCCL_WORLD1", "1")
+    monkeypatch.setenv("SFX_AHEAD", ahead)
     recs, final, heads, gg, h, w, stats, counters = _native_tsf_rank(0, 1, TSF_SMALL, "rccl", use_gpi, steps=16)
     assert stats["prelaunched"] >= 8, stats
     assert counters.sum() == 16
