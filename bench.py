@@ -451,6 +451,28 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
                      "steps": steps, "dtype": prec}
         loop.close()
         eng.close()
+    # BASELINE configs C4 / C5 in their sharded layouts on ONE GPU, every collective a real RCCL call
+    # at world 1 (SFX_RCCL_WORLD1=1): C4's 64 Reacher tasks (the sharded all-task step, 3 device
+    # rounds from 16 tasks on), and C5's per-rank share, 8 Hopper TSF-NF heads (schedule sharded_tsf)
+    os.environ["SFX_RCCL_WORLD1"] = "1"
+    try:
+        c4 = argparse.Namespace(**vars(args))
+        c4.heads, c4.spec_rounds, c4.via_host = 64, 0, False
+        r = bench_sharded(c4, 1, 0, device, torch.cuda.synchronize, None, steps=2000, warmup=200)
+        out["reacher17-sharded-T64-B32-rccl-world1"] = {k: r[k] for k in ("value", "unit", "ms_per_step", "steps",
+                                                                          "heads_total")} | {
+            "speculation": {k: r["rounds"][k] for k in ("steps", "host_round_steps", "rounds", "unverified_policies")},
+            "layout": "BASELINE C4's 64 source tasks on one GPU: sharded schedule at world 1, RCCL forced"}
+        c5 = argparse.Namespace(**vars(args))
+        c5.heads, c5.tsf_K, c5.via_host, c5.shard_steps = 8, 100, False, 1000
+        r = bench_sharded_tsf(c5, 1, 0, device, torch.cuda.synchronize, None, steps=1000, warmup=100)
+        out["hopper11-sharded-tsf-nf100-T8-B32-rccl-world1"] = {k: r[k] for k in ("value", "unit", "ms_per_step", "steps",
+                                                                                 "heads_total")} | {
+            "layout": "BASELINE C5's per-GPU share (8 of 32 TSF-NF heads) through the sharded_tsf schedule, RCCL forced"}
+    except Exception as e:  # an error return (a bounded collective), not a hang
+        out["sharded-one-gpu-error"] = repr(e)[:400]
+    finally:
+        os.environ.pop("SFX_RCCL_WORLD1", None)
     # the drop-in: features.deep.DeepSF under the reference user's Python agent loop (tools/dropin_loop.py)
     from tools import dropin_loop
 

@@ -1907,7 +1907,9 @@ __device__ __forceinline__ void role_dw(const Geo& G, const BwdArgs& A, int head
           st_param<C>(Pw + off, pp[e]);
           st_moment(Mw + off, pm[e]);
           st_moment(Vw + off, pv[e]);
-          if constexpr (BF) G.on16[wo + off] = (__bf16)pp[e];  // the bf16 copy of the write slot
+          // the bf16 copy of the write slot (2-byte stores: an LDS transpose into 16-byte row stores
+          // measured slower -- its barrier costs more than the stores, profiles/r06_probe_bf16_lds.txt)
+          if constexpr (BF) G.on16[wo + off] = (__bf16)pp[e];
         }
         if (fuse) sW[(n - nbase) * V0S + k] = pp[e];
       }

@@ -76,13 +76,19 @@ def test_held_minibatches_survive_slot_reuse_and_ring_wrap():
     for got, idx in zip(held, want):
         assert torch.equal(got[0].cpu(), S[idx]) and torch.equal(got[3].cpu(), S[idx] + 0.5)
         assert torch.equal(got[1].cpu(), torch.as_tensor(idx % 7)) and torch.equal(got[2][:, 0].cpu(), torch.as_tensor(idx, dtype=torch.float32))
-    # reuse only after an explicit hand-back: dropping every Python reference is not enough
+    # reuse only after an explicit hand-back: dropping every Python reference is not enough (a fresh
+    # buffer, so its first replays are its own slots, not torch allocations)
     del held
+    buf = ReplayBuffer({}, n_samples=cap, n_batch=B)
+    buf.device = dev
+    for k in range(cap):
+        buf.append(S[k:k + 1].to(dev), torch.tensor(k % 7, device=dev), torch.full((d,), float(k), device=dev),
+                   (S[k:k + 1] + 0.5).to(dev), 0.9)
     a = buf.replay()
     pa = a[0].data_ptr()
     del a
     b = buf.replay()
-    assert b[0].data_ptr() != pa
+    assert b[0].data_ptr() != pa  # the first slot was never handed back
     assert buf.release(b[0]) and not buf.release(b[0])  # a second release of one lending is a no-op
     pb = b[0].data_ptr()
     del b

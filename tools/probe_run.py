@@ -54,6 +54,7 @@ def main():
         eng.load_w(t, w[t])
     eng.set_adam(1e-3, 0.0, 1e-3, 0.0)
     eng.set_target_update_ev(1000)
+    eng.set_precision(os.environ.get("SFX_PROBE_PREC", "fp32"))  # bf16: the operand mode's timeline
     loop = NativeEnvLoop(eng, batch=B, seed=1, schedule="all" if work == "all" else ("active" if work == "active" else "tsf"),
                          p_end=0.0 if K is None else 0.01)
     loop.prefill(1000)
