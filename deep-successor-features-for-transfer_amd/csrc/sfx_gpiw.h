@@ -18,57 +18,86 @@ namespace sfx {
 constexpr int WPC = 8;     // policies per workgroup
 constexpr int WAMAX = 32;  // actions (wide kernels)
 
+// max over the 64 lanes of a wave, the result in every lane: DPP within rows of 16 (xor 1, xor 2,
+// half-row mirror, row mirror: one VALU op each), then the four row maxima by readlane -- instead of
+// six ds_bpermute shuffles per reduction (max is exact and order-free)
+#define SFX_DPP_MAX(v, ctrl) \
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false)))
 __device__ __forceinline__ float wave_fmax(float v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
-  return v;
+  SFX_DPP_MAX(v, 0xB1);   // quad_perm [1,0,3,2]
+  SFX_DPP_MAX(v, 0x4E);   // quad_perm [2,3,0,1]
+  SFX_DPP_MAX(v, 0x141);  // row_half_mirror
+  SFX_DPP_MAX(v, 0x140);  // row_mirror
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
 }
+#undef SFX_DPP_MAX
 
 // s_m[j][a] = max over this handle's heads t of ψ_{role(t)}(row b)[a]·w_{i0+j} for j < ni, where
 // role(t) = lt if off + t < i0 + j else ge.  s_w[j][k]: the policies' w rows (in LDS, complete).
-// d = 4 VD.  Every thread of the workgroup calls it; a barrier follows inside.
+// d = 4 VD.  Every thread of the workgroup calls it; a barrier follows inside.  A wave takes the
+// actions a = wave, wave + 4 (then + 8 ...), both of a pair's ψ rows requested before the first dot.
 template <int VD>
 __device__ __forceinline__ void wide_maxima(const Geo& G, int b, int i0, int ni, int off, int lt, int ge,
                                             const float (*s_w)[16], float (*s_m)[WAMAX]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int T = G.T, Aa = G.A, O = G.O, NLm = G.lastOff;
   const bool two = lt != ge;
-  for (int a = wave; a < Aa; a += 4) {
-    float mx[WPC];
+  for (int a0 = wave; a0 < Aa; a0 += 8) {
+    float mx[2][WPC];
 #pragma unroll
-    for (int j = 0; j < WPC; ++j) mx[j] = -INFINITY;
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < WPC; ++j) mx[u][j] = -INFINITY;
     for (int t0 = 0; t0 < T; t0 += 64) {  // wave-uniform trip count
       const int t = t0 + lane;
       const bool ok = t < T;
-      float4 pl[VD], pg[VD];
-      const float4* rl = reinterpret_cast<const float4*>(G.actp(lt, ok ? t : 0, NLm) + (size_t)b * O + a * 4 * VD);
-      const float4* rg = reinterpret_cast<const float4*>(G.actp(ge, ok ? t : 0, NLm) + (size_t)b * O + a * 4 * VD);
+      float4 pl[2][VD], pg[2][VD];
 #pragma unroll
-      for (int v = 0; v < VD; ++v) {
-        pl[v] = ok ? rl[v] : make_float4(0.f, 0.f, 0.f, 0.f);
-        pg[v] = ok && two ? rg[v] : pl[v];
-      }
+      for (int u = 0; u < 2; ++u) {
+        const int a = a0 + 4 * u;
+        const bool oka = ok && a < Aa;
+        const size_t ro = (size_t)b * O + (size_t)(oka ? a : 0) * 4 * VD;
+        const float4* rl = reinterpret_cast<const float4*>(G.actp(lt, ok ? t : 0, NLm) + ro);
+        const float4* rg = reinterpret_cast<const float4*>(G.actp(ge, ok ? t : 0, NLm) + ro);
 #pragma unroll
-      for (int j = 0; j < WPC; ++j) {
-        if (j < ni) {
-          const bool before = off + t < i0 + j;
-          float q = 0.f;
-#pragma unroll
-          for (int v = 0; v < VD; ++v) {
-            const float4 p = before ? pl[v] : pg[v];
-            q = __builtin_fmaf(p.x, s_w[j][4 * v], q);
-            q = __builtin_fmaf(p.y, s_w[j][4 * v + 1], q);
-            q = __builtin_fmaf(p.z, s_w[j][4 * v + 2], q);
-            q = __builtin_fmaf(p.w, s_w[j][4 * v + 3], q);
-          }
-          if (ok) mx[j] = fmaxf(mx[j], q);
+        for (int v = 0; v < VD; ++v) {
+          pl[u][v] = oka ? rl[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+          pg[u][v] = oka && two ? rg[v] : pl[u][v];
         }
       }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int j = 0; j < WPC; ++j) {
+          if (j < ni) {
+            const bool before = off + t < i0 + j;
+            float q = 0.f;
+#pragma unroll
+            for (int v = 0; v < VD; ++v) {
+              const float4 p = before ? pl[u][v] : pg[u][v];
+              q = __builtin_fmaf(p.x, s_w[j][4 * v], q);
+              q = __builtin_fmaf(p.y, s_w[j][4 * v + 1], q);
+              q = __builtin_fmaf(p.z, s_w[j][4 * v + 2], q);
+              q = __builtin_fmaf(p.w, s_w[j][4 * v + 3], q);
+            }
+            if (ok) mx[u][j] = fmaxf(mx[u][j], q);
+          }
+        }
     }
 #pragma unroll
-    for (int j = 0; j < WPC; ++j) {
-      const float m = wave_fmax(mx[j]);
-      if (lane == 0 && j < ni) s_m[j][a] = m;
+    for (int u = 0; u < 2; ++u) {
+      const int a = a0 + 4 * u;
+      if (a < Aa) {  // wave-uniform
+#pragma unroll
+        for (int j = 0; j < WPC; ++j) {
+          const float m = wave_fmax(mx[u][j]);
+          if (lane == 0 && j < ni) s_m[j][a] = m;
+        }
+      }
     }
   }
   __syncthreads();
