@@ -314,7 +314,12 @@ int sfx_runner_destroy(sfx_runner_t r);
 int sfx_runner_layout(sfx_runner_t r, int64_t* offsets_host /* [10] */);
 /* training schedule of the env steps: 0 all-task (default; agents/sfdqn.py:47-60 with LMS w),
  * 1 active task only (sfdqn.py:462-471, agents/sfdqn_sequential.py:63-76: l1 + l2, Adam w),
- * 2 TSF-DQN active task (tsfdqn.py:566-580; needs sfx_tsf_setup).  use_gpi: next actions of the
+ * 2 TSF-DQN active task (tsfdqn.py:566-580; needs sfx_tsf_setup), 3 all-task with the heads
+ * sharded over ranks (BASELINE config C4; needs sfx_shard_setup and a communicator), 4 TSF-DQN
+ * active task with the heads sharded over ranks (config C5, tsfdqn_nf.py:598-612: the active
+ * policy's GPI maxima all-reduced, its owner updates, h and w_task handed to every rank by libsfx
+ * collectives; needs sfx_tsf_setup, sfx_shard_setup and a communicator; the active task of
+ * sfx_runner_set_task is then a global index).  use_gpi: next actions of the
  * update by GPI (1) or the own head (0).  p_end: episode-end probability per step of the
  * built-in synthetic task (γ = 0 on that transition; 0 = never, like tasks/reacher.py:112).
  * Call between runs (before sfx_runner_set_task). */
