@@ -184,9 +184,15 @@ struct sfx_handle {
     bool pre = false;
     const float* ax = nullptr;
     int aM = 0;
+    // sfx_update_all_select: the selection's q table [T*A] and GPI task of s_next (gpi_row's
+    // q_out / task_out, as sfx_gpi writes them)
+    float* q_out = nullptr;
+    int64_t* task_out = nullptr;
+    const unsigned long long* out_ind = nullptr;  // q_out / task_out through host words instead
   } pend;
   // step statistics
   long long steps_spec = 0, steps_fallback = 0, policies_rerun = 0, rounds_total = 0;
+  long long graph_captures = 0, graph_launches = 0;  // sfx_graph_stats
   int force_rerun_from = -1;  // test hook: treat the speculation as failed from this policy on
   int spec_rounds = 2;        // speculative rounds launched on the device per fused step
   bool spec_rounds_auto = true;  // spec_rounds follows T_glob (auto_spec_rounds) until set explicitly
@@ -253,7 +259,13 @@ struct sfx_handle {
   int dxs_max = 1, dx_ntile = 1;
   float* dxpart = nullptr;
   unsigned* dxctr = nullptr;
-  StepOut* hout = nullptr;  // pinned host
+  StepOut* hout = nullptr;  // pinned host (coherent, mapped: the final k_ver may write it)
+  // set by sfx_step_all while it records a step: the final round's k_ver posts flag and selection
+  // to hout (run_ver post_host), which then needs no copy after the step (hout_posted)
+  bool post_hout = false, hout_posted = false;
+  // host-coherent inputs of sfx_update_all_select, written before each launch: [0] the fused LMS's
+  // reward (float), [1] / [2] the selection's q / task output pointers (GpiArgs::out_ind)
+  unsigned long long* xin = nullptr;
   // recorded after a fused step's graph (which ends with the StepOut copy): sfx_step_finish waits
   // for the step itself, not for work queued behind it (the drop-in's speculative GPI graph)
   hipEvent_t ev_step = nullptr;
@@ -353,8 +365,12 @@ int run_graph(sfx_handle* h, const GraphKey& key, F body, bool launch_it = true)
     HIPCHK(ei);
     if (h->graphs.size() > 256) clear_graphs(h);
     it = h->graphs.emplace(key, ex).first;
+    h->graph_captures += 1;
   }
-  if (launch_it) HIPCHK(hipGraphLaunch(it->second, h->stream));
+  if (launch_it) {
+    HIPCHK(hipGraphLaunch(it->second, h->stream));
+    h->graph_launches += 1;
+  }
   return SFX_OK;
 }
 
@@ -808,7 +824,8 @@ int run_gpi(sfx_handle* h, const GpiArgs& A) {
   return SFX_OK;
 }
 
-int run_ver(sfx_handle* h, int M, int npol, bool sel, int post, const GpiArgs& g, const int64_t* spec) {
+int run_ver(sfx_handle* h, int M, int npol, bool sel, int post, const GpiArgs& g, const int64_t* spec,
+            bool post_host = false) {
   VerArgs V{};
   V.M = M;
   V.post = post;
@@ -828,6 +845,12 @@ int run_ver(sfx_handle* h, int M, int npol, bool sel, int post, const GpiArgs& g
     V.done = &h->dout->done;
     V.nblocks = (int)(grid.x * grid.y);
     h->pub_folded = true;
+  } else if (post_host) {  // the step's verdict and selection straight to h->hout (no copy after)
+    V.h_sel = h->hout->sel;
+    V.h_flag = &h->hout->flag;
+    V.done = &h->dout->done;
+    V.nblocks = (int)(grid.x * grid.y);
+    h->hout_posted = true;
   }
   const double by = 4.0 * (double)M * npol * h->T * h->O + 4.0 * h->T * h->O;
   if (wide)
@@ -907,6 +930,7 @@ void free_all(sfx_handle* h) {
                   (void*)h->dout, (void*)h->dxpart, (void*)h->dxctr, (void*)h->qh, (void*)h->selk})
     if (p) (void)hipFree(p);
   if (h->hout) (void)hipHostFree(h->hout);
+  if (h->xin) (void)hipHostFree(h->xin);
   if (h->ev_step) (void)hipEventDestroy(h->ev_step);
   if (h->on16) (void)hipFree(h->on16);
   if (h->tg16) (void)hipFree(h->tg16);
@@ -999,14 +1023,16 @@ int launch_round(sfx_handle* h, const sfx_handle::Pending& p, int r, bool final)
   if (!final) return SFX_OK;
   const bool sel = p.sel && bx.fuse_v0;
   const bool verify = p.use_gpi != 0;
+  GpiArgs gs = gpi_args(out, B, 0, wsel, nullptr, p.q_out, p.task_out, nullptr, h->dout->sel, p.task, p.sel_use_gpi, 1);
+  gs.out_ind = p.out_ind;
+  // the ver launch posts the verdict to the host itself when nothing after it changes the selection
   if (verify || sel)
-    RC(run_ver(h, B, verify ? T : 1, sel, out,
-               gpi_args(out, B, 0, wsel, nullptr, nullptr, nullptr, nullptr, h->dout->sel, p.task, p.sel_use_gpi, 1),
-               spec_buf(h, r)));
+    RC(run_ver(h, B, verify ? T : 1, sel, out, gs, spec_buf(h, r), h->post_hout && (sel || !p.sel)));
   if (p.sel && !bx.fuse_v0) {  // selection through the plain forward path
     RC(run_fwd(h, {{R_A, P_NEW, 1, 0, T}}, 1, p.s_next, nullptr));
-    RC(run_gpi(h, gpi_args(R_A, 0, 0, wsel, nullptr, nullptr, nullptr, nullptr, h->dout->sel, p.task, p.sel_use_gpi,
-                           1)));
+    gs.role = R_A;
+    gs.rowoff = 0;
+    RC(run_gpi(h, gs));
   }
   return SFX_OK;
 }
@@ -1170,8 +1196,10 @@ int launch_step_all(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, c
   if (!p.update) {
     const float* wsel = h->w + (size_t)p.task * h->dpad;
     RC(run_fwd(h, {{R_A, P_ONLINE, 1, 0, T}}, 1, p.s_next, nullptr, ex));
-    return run_gpi(h, gpi_args(R_A, 0, 0, wsel, nullptr, nullptr, nullptr, nullptr, h->dout->sel, p.task,
-                               p.sel_use_gpi, 1));
+    GpiArgs gs = gpi_args(R_A, 0, 0, wsel, nullptr, p.q_out, p.task_out, nullptr, h->dout->sel, p.task,
+                          p.sel_use_gpi, 1);
+    gs.out_ind = p.out_ind;
+    return run_gpi(h, gs);
   }
   // a look-ahead step (p.pre) starts at its TD launch: the step before forwarded its minibatch
   // into these roles, its gate reset the flag and ran the LMS
@@ -1196,6 +1224,57 @@ __global__ void k_replay_put(float* __restrict__ rs, float* __restrict__ rphi, f
   }
   for (int k = threadIdx.x; k < d; k += blockDim.x) rphi[j * d + k] = phi[k];
   if (threadIdx.x == 0) ra[j] = *a;
+}
+
+// agents/buffer.py append (:62-82) and the replay right after it (:34-60) in one launch: workgroup B
+// writes ring row j from the new transition (and copies its next state / φ into s1c / phic, the
+// fixed inputs of a fused selection and LMS, when given); workgroup b < B gathers row idx[b] --
+// from the new transition's own vectors when idx[b] == j (that row is being written beside it).
+struct PutGather {
+  float *rs, *rphi, *rs1;
+  int64_t* ra;
+  const float* rg;  // γ ring on the device, or null: γ from gam
+  long long j;
+  const float *s, *phi, *s1;
+  const int64_t* a;
+  float *s1c, *phic;
+  const int64_t* idx;
+  const float* gam;
+  float *S, *PHI, *S1, *G;
+  int64_t* A;
+  int B, n_s, d;
+};
+__global__ void k_replay_put_gather(PutGather P) {
+  const int b = blockIdx.x, n_s = P.n_s, d = P.d;
+  if (b == P.B) {
+    for (int k = threadIdx.x; k < n_s; k += blockDim.x) {
+      P.rs[P.j * n_s + k] = P.s[k];
+      const float v = P.s1[k];
+      P.rs1[P.j * n_s + k] = v;
+      if (P.s1c) P.s1c[k] = v;
+    }
+    for (int k = threadIdx.x; k < d; k += blockDim.x) {
+      const float v = P.phi[k];
+      P.rphi[P.j * d + k] = v;
+      if (P.phic) P.phic[k] = v;
+    }
+    if (threadIdx.x == 0) P.ra[P.j] = *P.a;
+    return;
+  }
+  const long long i = P.idx[b];
+  const bool fresh = i == P.j;
+  const float* xs = fresh ? P.s : P.rs + i * n_s;
+  const float* xs1 = fresh ? P.s1 : P.rs1 + i * n_s;
+  const float* xphi = fresh ? P.phi : P.rphi + i * d;
+  for (int k = threadIdx.x; k < n_s; k += blockDim.x) {
+    P.S[(size_t)b * n_s + k] = xs[k];
+    P.S1[(size_t)b * n_s + k] = xs1[k];
+  }
+  for (int k = threadIdx.x; k < d; k += blockDim.x) P.PHI[(size_t)b * d + k] = xphi[k];
+  if (threadIdx.x == 0) {
+    P.A[b] = fresh ? *P.a : P.ra[i];
+    P.G[b] = P.rg ? P.rg[i] : P.gam[b];
+  }
 }
 
 // workgroup b: row idx[b] of each field; γ from the packed copy (gam) or from the ring (rg)
@@ -1264,6 +1343,19 @@ int sfx_replay_gather(void* stream, const float* rs, const float* rphi, const fl
     SFX_FAIL(SFX_E_ARG, "sfx_replay_gather: bad arguments");
   hipLaunchKernelGGL(k_replay_gather, dim3(B), dim3(64), 0, (hipStream_t)stream, rs, rphi, rs1, ra, rg, idx, gam, S,
                      PHI, S1, A, G, n_s, d);
+  LAUNCHCHK();
+  return SFX_OK;
+}
+
+int sfx_replay_put_gather(void* stream, float* rs, float* rphi, float* rs1, int64_t* ra, const float* rg, long long j,
+                          const float* s, const float* phi, const float* s1, const int64_t* a, float* s1_copy,
+                          float* phi_copy, const int64_t* idx, const float* gam, int B, float* S, float* PHI, float* S1,
+                          int64_t* A, float* G, int n_s, int d) {
+  if (!rs || !rphi || !rs1 || !ra || j < 0 || !s || !phi || !s1 || !a || !idx || (!rg && !gam) || B < 1 || !S ||
+      !PHI || !S1 || !A || !G || n_s < 1 || d < 1)
+    SFX_FAIL(SFX_E_ARG, "sfx_replay_put_gather: bad arguments");
+  const PutGather P{rs, rphi, rs1, ra, rg, j, s, phi, s1, a, s1_copy, phi_copy, idx, gam, S, PHI, S1, G, A, B, n_s, d};
+  hipLaunchKernelGGL(k_replay_put_gather, dim3(B + 1), dim3(64), 0, (hipStream_t)stream, P);
   LAUNCHCHK();
   return SFX_OK;
 }
@@ -1419,7 +1511,8 @@ int sfx_create(sfx_t* out, int T, int n_s, int H, int n_hidden, const int* acts,
   alloc((void**)&h->skipc, 64);
   alloc((void**)&h->dout, sizeof(StepOut));
   alloc((void**)&h->selk, sizeof(SelScratch));
-  if (rc == SFX_OK && hipHostMalloc((void**)&h->hout, sizeof(StepOut), hipHostMallocDefault) != hipSuccess) {
+  if (rc == SFX_OK &&
+      hipHostMalloc((void**)&h->hout, sizeof(StepOut), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
     g_err = "hipHostMalloc failed";
     rc = SFX_E_HIP;
   }
@@ -1701,9 +1794,11 @@ int sfx_update(sfx_t h, int policy, const float* S, const int64_t* a, const floa
   return maybe_sync_target(h, policy);
 }
 
-int sfx_step_all(sfx_t h, const float* S, const int64_t* a, const float* phi, const float* S1, const float* gamma,
-                 int B, int use_gpi, int lms_task, const float* lms_phi, const float* lms_r, float lms_alpha,
-                 const float* s_next, int task_index, int sel_use_gpi, float* losses) {
+static int step_all_impl(sfx_t h, const float* S, const int64_t* a, const float* phi, const float* S1,
+                         const float* gamma, int B, int use_gpi, int lms_task, const float* lms_phi,
+                         const float* lms_r, float lms_alpha, const float* s_next, int task_index, int sel_use_gpi,
+                         float* losses, float* q_out, int64_t* task_out,
+                         const unsigned long long* out_ind = nullptr) {
   RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   if (h->pend.active) SFX_FAIL(SFX_E_STATE, "sfx_step_all: previous step not finished");
@@ -1727,19 +1822,33 @@ int sfx_step_all(sfx_t h, const float* S, const int64_t* a, const float* phi, co
   p.a = a;
   p.s_next = s_next;
   p.losses = losses;
+  p.q_out = s_next && !out_ind ? q_out : nullptr;
+  p.task_out = s_next && !out_ind ? task_out : nullptr;
+  p.out_ind = s_next ? out_ind : nullptr;
   unsigned alpha_bits;
   std::memcpy(&alpha_bits, &lms_alpha, 4);
   const GraphKey key = make_key(5, {p.B, p.use_gpi, lms_task, p.task, p.sel_use_gpi, (int)alpha_bits, h->spec_rounds}, h->mask,
-                                {S, a, phi, S1, gamma, lms_phi, lms_r, s_next, losses});
+                                {S, a, phi, S1, gamma, lms_phi, lms_r, s_next, losses, p.q_out, p.task_out, p.out_ind});
   const int rounds = p.use_gpi ? h->spec_rounds : 1;
   RC(run_graph(h, key, [&]() -> int {
-    RC(launch_step_all(h, p, lms_task, lms_phi, lms_r, lms_alpha, rounds));
-    HIPCHK(hipMemcpyAsync(h->hout, h->dout, sizeof(StepOut), hipMemcpyDeviceToHost, h->stream));
+    h->post_hout = true;
+    h->hout_posted = false;
+    const int rc = launch_step_all(h, p, lms_task, lms_phi, lms_r, lms_alpha, rounds);
+    h->post_hout = false;
+    RC(rc);
+    if (!h->hout_posted) HIPCHK(hipMemcpyAsync(h->hout, h->dout, sizeof(StepOut), hipMemcpyDeviceToHost, h->stream));
     return SFX_OK;
   }));
   HIPCHK(hipEventRecord(h->ev_step, h->stream));
   h->pend = p;
   return SFX_OK;
+}
+
+int sfx_step_all(sfx_t h, const float* S, const int64_t* a, const float* phi, const float* S1, const float* gamma,
+                 int B, int use_gpi, int lms_task, const float* lms_phi, const float* lms_r, float lms_alpha,
+                 const float* s_next, int task_index, int sel_use_gpi, float* losses) {
+  return step_all_impl(h, S, a, phi, S1, gamma, B, use_gpi, lms_task, lms_phi, lms_r, lms_alpha, s_next, task_index,
+                       sel_use_gpi, losses, nullptr, nullptr);
 }
 
 int sfx_step_finish(sfx_t h, int64_t* out_host) {
@@ -1844,6 +1953,14 @@ int sfx_step_stats(sfx_t h, long long* steps, long long* fallbacks, long long* r
   return SFX_OK;
 }
 
+int sfx_graph_stats(sfx_t h, long long* captures, long long* launches, long long* cached) {
+  if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
+  if (captures) *captures = h->graph_captures;
+  if (launches) *launches = h->graph_launches;
+  if (cached) *cached = (long long)h->graphs.size();
+  return SFX_OK;
+}
+
 int sfx_skip_stats(sfx_t h, long long* checked, long long* skipped, int reset) {
   RC(settle(h));
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
@@ -1883,6 +2000,39 @@ int sfx_update_all(sfx_t h, const float* S, const int64_t* a, const float* phi, 
   RC(settle(h));
   RC(sfx_step_all(h, S, a, phi, S1, gamma, B, 1, -1, nullptr, nullptr, 0.f, nullptr, 0, 1, losses));
   h->lazy_finish = true;  // the verdict is collected by the next call (settle)
+  return SFX_OK;
+}
+
+int sfx_update_all_select(sfx_t h, const float* S, const int64_t* a, const float* phi, const float* S1,
+                          const float* gamma, int B, float* losses, const float* s_next, int task_index, float* q_out,
+                          int64_t* task_out, int lms_task, const float* lms_phi, float lms_r, float lms_alpha) {
+  if (!h || !S || !a || !phi || !S1 || !gamma || !s_next) SFX_FAIL(SFX_E_ARG, "bad args");
+  if (B < 1 || B > h->Mmax) SFX_FAIL(SFX_E_ARG, "batch exceeds max_batch");
+  if (task_index < 0 || task_index >= h->T) SFX_FAIL(SFX_E_ARG, "bad task_index");
+  if (lms_task >= h->T || (lms_task >= 0 && !lms_phi)) SFX_FAIL(SFX_E_ARG, "bad LMS args");
+  RC(settle(h));  // the step before has completed: nothing reads xin any more
+  if (!h->xin && hipHostMalloc((void**)&h->xin, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+    SFX_FAIL(SFX_E_HIP, "hipHostMalloc failed");
+  // read by the step's launches (kernel arguments would change the captured graph every step)
+  std::memcpy(h->xin, &lms_r, sizeof(float));
+  h->xin[1] = (unsigned long long)(uintptr_t)q_out;
+  h->xin[2] = (unsigned long long)(uintptr_t)task_out;
+  RC(step_all_impl(h, S, a, phi, S1, gamma, B, 1, lms_task, lms_phi,
+                   lms_task >= 0 ? reinterpret_cast<const float*>(h->xin) : nullptr, lms_alpha, s_next, task_index, 1,
+                   losses, q_out, task_out, h->xin + 1));
+  h->lazy_finish = true;  // the verdict (host rounds redo the selection) is collected by the next call
+  return SFX_OK;
+}
+
+int sfx_settle(sfx_t h, int* host_rounds) {
+  if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
+  const long long r0 = h->rounds_total, s0 = h->steps_spec;
+  RC(settle(h));
+  if (host_rounds) {
+    // rounds run by this settle beyond the device rounds of the step it collected
+    const long long ran = h->rounds_total - r0, dev = h->steps_spec > s0 ? h->spec_rounds : 0;
+    *host_rounds = (int)(ran > dev ? ran - dev : 0);
+  }
   return SFX_OK;
 }
 

@@ -168,12 +168,15 @@ __global__ __launch_bounds__(256) void k_verw(Geo G, VerArgs V) {
     __syncthreads();
     if (threadIdx.x == 0 && s_bad < V.npol) atomicMin(V.flag, s_bad);
   }
-  if (V.pub) {  // as k_ver: the barrier + agent-scope arrival order every wave's stores before it
+  if (V.pub || V.h_flag) {  // as k_ver: the barrier + agent-scope arrival order every wave's stores before it
     __syncthreads();
     if (threadIdx.x == 0) {
       const unsigned prev = __hip_atomic_fetch_add(V.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       if (prev == (unsigned)V.nblocks - 1) {
-        publish_result(V.g.sel_out, V.flag, V.pub, V.pub_dctr, G.cancel, G.nonfin);
+        if (V.pub)
+          publish_result(V.g.sel_out, V.flag, V.pub, V.pub_dctr, G.cancel, G.nonfin);
+        else
+          post_verdict(V);
         __hip_atomic_store(V.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }

@@ -2076,6 +2076,9 @@ struct GpiArgs {
   int64_t* task_out;
   int64_t* next_out;
   int64_t* sel_out;  // [2] or null
+  // sfx_update_all_select: q_out / task_out read at run time from host-coherent words (written by
+  // the host before each launch), so a captured step serves fresh output tensors every time
+  const unsigned long long* out_ind;
 };
 
 // argmax helpers: (value, index) packed so that an integer max picks the largest value and,
@@ -2145,7 +2148,12 @@ __device__ __forceinline__ int gpi_pick(const GpiArgs& A, const float* s_q, floa
   return picked;
 }
 
-__device__ void gpi_row(const Geo& G, const GpiArgs& A, int b) {
+__device__ void gpi_row(const Geo& G, const GpiArgs& A0, int b) {
+  GpiArgs A = A0;
+  if (A.out_ind) {  // issued first: the round trip to host memory overlaps the dot products
+    A.q_out = reinterpret_cast<float*>(A.out_ind[0]);
+    A.task_out = reinterpret_cast<int64_t*>(A.out_ind[1]);
+  }
   const int tid = threadIdx.x;
   const int T = G.T, Aa = G.A, d = G.d, O = G.O, NLm = G.lastOff, TA = T * Aa;
   __shared__ float s_q[QMAX];
@@ -2262,7 +2270,24 @@ struct VerArgs {
   const long long* pub_dctr;
   unsigned* done;
   int nblocks, pad_;
+  // library steps (sfx_step_all / sfx_update_all*): the last workgroup to arrive copies the
+  // selection and the flag to host-coherent memory instead of a copy after the launch.  Null: no.
+  int64_t* h_sel;
+  int* h_flag;
 };
+
+// The step's verdict and selection to host-coherent memory (VerArgs::h_sel / h_flag), read with
+// coherent loads after the arrivals, written with system scope; the launch's completion (the
+// host waits for it) makes them visible.
+__device__ __forceinline__ void post_verdict(const VerArgs& V) {
+  const long long s0 = __hip_atomic_load(V.g.sel_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long long s1 = __hip_atomic_load(V.g.sel_out + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int f = __hip_atomic_load(V.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(V.h_sel, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(V.h_sel + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(V.h_flag, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();
+}
 
 // Grid (npol + 1, ceil(M / rows)): one workgroup per (policy, `rows` minibatch rows), each
 // thread one q = ψ·w dot product, so every load is issued before the first reduction.
@@ -2353,7 +2378,7 @@ __device__ void ver_block(const Geo& G, const VerArgs& V) {
 __global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
   PROBE_T(pt0);
   ver_block(G, V);
-  if (V.pub) {
+  if (V.pub || V.h_flag) {
     // every wave's stores (the selection, the flag) are ordered before the arrival by the barrier
     // and the arrival's agent-scope release; the last arrival acquires them all before it reads
     // the selection and the flag and publishes (the counter is re-armed by the last arrival and by
@@ -2364,7 +2389,10 @@ __global__ __launch_bounds__(256) void k_ver(Geo G, VerArgs V) {
       const unsigned prev = __hip_atomic_fetch_add(V.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       PROBE_AT(4);
       if (prev == (unsigned)V.nblocks - 1) {
-        publish_result(V.g.sel_out, V.flag, V.pub, V.pub_dctr, G.cancel, G.nonfin);
+        if (V.pub)
+          publish_result(V.g.sel_out, V.flag, V.pub, V.pub_dctr, G.cancel, G.nonfin);
+        else
+          post_verdict(V);
         PROBE_AT(5);
         __hip_atomic_store(V.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }

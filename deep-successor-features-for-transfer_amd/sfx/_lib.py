@@ -43,6 +43,8 @@ SIGNATURES = {
     "sfx_test_reward_updates": (_I, [_VP, _I, _VP, _VP, _VP, _I, C.c_double, C.c_double, _VP]),
     "sfx_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP]),
     "sfx_update_all": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _VP]),
+    "sfx_update_all_select": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _VP, _VP, _I, _VP, _VP, _I, _VP, _F, _F]),
+    "sfx_settle": (_I, [_VP, C.POINTER(C.c_int)]),
     "sfx_lms": (_I, [_VP, _I, _VP, _VP, _F]),
     "sfx_lms_value": (_I, [_VP, _I, _VP, _F, _F]),
     "sfx_host_alloc": (_I, [C.c_size_t, C.POINTER(_VP)]),
@@ -52,11 +54,13 @@ SIGNATURES = {
     "sfx_debug_force_rerun": (_I, [_VP, _I]),
     "sfx_set_spec_rounds": (_I, [_VP, _I]),
     "sfx_step_stats": (_I, [_VP] + [C.POINTER(C.c_longlong)] * 4),
+    "sfx_graph_stats": (_I, [_VP] + [C.POINTER(C.c_longlong)] * 3),
     "sfx_skip_stats": (_I, [_VP, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong), _I]),
     "sfx_set_precision": (_I, [_VP, _I]),
     "sfx_get_precision": (_I, [_VP]),
     "sfx_set_huber": (_I, [_VP, _F]),
     "sfx_replay_put": (_I, [_VP] * 5 + [C.c_longlong] + [_VP] * 4 + [_I, _I]),
+    "sfx_replay_put_gather": (_I, [_VP] * 6 + [C.c_longlong] + [_VP] * 8 + [_I] + [_VP] * 5 + [_I, _I]),
     "sfx_replay_gather": (_I, [_VP] * 8 + [_I] + [_VP] * 5 + [_I, _I]),
     "sfx_get_huber": (_F, [_VP]),
     "sfx_set_target_update_ev": (_I, [_VP, _I]),

@@ -29,8 +29,23 @@ def release_minibatch(states, stream=None) -> bool:
     return buf.release(states, stream) if buf is not None else False
 
 
-def _stream_handle(device) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+def lending_buffer(states):
+    """The ReplayBuffer that lent the minibatch whose states tensor is `states`, or None."""
+    tok = getattr(states, "_sfx_slot", None)
+    return tok[0]() if tok is not None else None
+
+
+_L = None
+
+
+def _libsfx():
+    """sfx._lib, imported on first use (a CPU ring never loads libsfx)."""
+    global _L
+    if _L is None:
+        from sfx import _lib
+
+        _L = _lib
+    return _L
 
 
 def _device():
@@ -54,11 +69,23 @@ class ReplayBuffer:
         self._pev = None
         self._outs = []
         self._token = weakref.ref(self)  # identifies this buffer's lendings (ReplayBuffer.release)
+        # The reference's agent appends (s, a, φ, s1) right after update_reward(φ, ...) and asks GPI
+        # about s1 right after the update (agents/agent.py:238-256, agents/sfdqn.py:47-60): a consumer
+        # (sfx's DeepSF) may name device vectors that the write of each appended row also copies s1
+        # and φ into (``mirror`` [n_s], ``mirror_reward`` [d]), and reads back which tensors, at which
+        # versions, the last write copied there: (weak reference, version at append, mirror).
+        self.mirror = self.mirror_reward = None
+        self.last_next = self.last_reward = None
+        # a native append's row is written by the next replay's launch (sfx_replay_put_gather), or
+        # before the next append / an empty replay / reset: (j, state, action, reward, next_state)
+        self._pend = None
         self.index = 0
         self.size = 0
 
     def reset(self):
         """Removes all samples currently stored in the buffer (the ring's memory is kept)."""
+        if self._pend is not None:
+            self._flush_put()
         self.index = 0
         self.size = 0
 
@@ -76,6 +103,8 @@ class ReplayBuffer:
         self._gdev = None  # set once a γ arrives as a device tensor: then γ is gathered on the device
         self._ring_dev = self._ring[0].get_device() if self._ring[0].is_cuda else -2
         self._widths = (n_s, d, n_s1)
+        self._rp = tuple(x.data_ptr() for x in self._ring)  # rs, ra, rr, rs1
+        self._mcache = (None, None, None, None)  # (mirror, mirror_reward, their pointers)
 
     @staticmethod
     def _put(row, x):
@@ -103,21 +132,21 @@ class ReplayBuffer:
         """Adds the sample (agents/buffer.py:62-82); the oldest is overwritten once the ring is full."""
         if self._ring is None:
             self._alloc(state, reward, next_state)
+        if self._pend is not None:
+            self._flush_put()
         rs, ra, rr, rs1 = self._ring
         j = self.index
+        self.last_next = self.last_reward = None
         if self._native(state, action, reward, next_state) and action.numel() == 1:
             # the kernel reads the ring's widths from each tensor: a shorter one would be read past its end
-            n_s, d, _ = self._widths
             if (state.numel(), reward.numel(), next_state.numel()) != self._widths:
-                for name, x, w in (("state", state, n_s), ("reward", reward, d), ("next_state", next_state, n_s)):
+                for name, x, w in (("state", state, self._widths[0]), ("reward", reward, self._widths[1]),
+                                   ("next_state", next_state, self._widths[0])):
                     if x.numel() != w:
                         raise ValueError(f"ReplayBuffer.append: {name} has {x.numel()} entries, the ring {w}")
-            from sfx import _lib
-
-            _lib.check(_lib.lib.sfx_replay_put(_lib.stream_ptr(self._ring_dev), rs.data_ptr(),
-                                               rr.data_ptr(), rs1.data_ptr(), ra.data_ptr(), j, state.data_ptr(),
-                                               reward.data_ptr(), next_state.data_ptr(), action.data_ptr(),
-                                               n_s, d), "sfx_replay_put")
+            # written by the next replay's launch; like the reference's object ring, the row holds
+            # these tensors' values as they are then
+            self._pend = (j, state, action, reward, next_state, next_state._version, reward._version)
             self._put_gamma(j, gamma)
             self.size = min(self.size + 1, self.n_samples)
             self.index = (self.index + 1) % self.n_samples
@@ -132,6 +161,27 @@ class ReplayBuffer:
         self._put_gamma(j, gamma)
         self.size = min(self.size + 1, self.n_samples)
         self.index = (self.index + 1) % self.n_samples
+
+    def _flush_put(self):
+        """Write the pending native append's row (one launch)."""
+        _lib = _libsfx()
+        j, st, ac, rw, ns = self._pend[:5]
+        self._pend = None
+        rs, ra, rr, rs1 = self._rp
+        n_s, d, _ = self._widths
+        _lib.check(_lib.lib.sfx_replay_put(_lib.stream_ptr(self._ring_dev), rs, rr, rs1, ra, j, st.data_ptr(),
+                                           rw.data_ptr(), ns.data_ptr(), ac.data_ptr(), n_s, d), "sfx_replay_put")
+
+    def _mirror_ptrs(self):
+        """Pointers of (mirror, mirror_reward) when they are vectors the kernel may write, else None."""
+        c = self._mcache
+        if c[0] is not self.mirror or c[1] is not self.mirror_reward:
+            def ok(m, n):
+                return m.data_ptr() if (type(m) is torch.Tensor and m.is_cuda and m.get_device() == self._ring_dev
+                                        and m.numel() == n and m.is_contiguous() and m.dtype is torch.float32) else None
+            c = self._mcache = (self.mirror, self.mirror_reward, ok(self.mirror, self._widths[0]),
+                                ok(self.mirror_reward, self._widths[1]))
+        return c[2], c[3]
 
     def _put_gamma(self, j, gamma):
         if torch.is_tensor(gamma):
@@ -151,6 +201,8 @@ class ReplayBuffer:
     def replay(self):
         """A uniform minibatch (agents/buffer.py:34-60) or None while fewer than n_batch samples."""
         if self.size < self.n_batch:
+            if self._pend is not None:
+                self._flush_put()
             return None
         indices = np.random.randint(low=0, high=self.size, size=(self.n_batch,))
         B = self.n_batch
@@ -177,17 +229,18 @@ class ReplayBuffer:
                     torch.cuda.current_stream(self.device).wait_event(sl["ev"])
                     sl["ev"] = None
                 sl["views"][0]._sfx_slot = (self._token, k, sl["gen"])
-                return sl["views"]
+                return sl["views"], sl["ptrs"]
         # A (int64, as 2B float words) | S | PHI | S1 | G, each contiguous, one allocation
         base = torch.empty(B * (2 * n_s + d + 3), device=self.device)
         a2, S, PHI, S1, G = base.split((2 * B, B * n_s, B * d, B * n_s, B))
         views = (S.view(B, n_s), a2.view(torch.int64), PHI.view(B, d), S1.view(B, n_s), G)
+        ptrs = tuple(v.data_ptr() for v in views)
         for k, sl in enumerate(self._outs):
             if sl is None:  # becomes a slot of the buffer's: handed back by its consumer, reused
-                self._outs[k] = {"views": views, "free": False, "gen": 0, "ev": None}
+                self._outs[k] = {"views": views, "ptrs": ptrs, "free": False, "gen": 0, "ev": None}
                 views[0]._sfx_slot = (self._token, k, 0)
                 break
-        return views
+        return views, ptrs
 
     def release(self, states, stream=None) -> bool:
         """Hand a minibatch returned by ``replay`` back to the buffer (its states tensor identifies
@@ -202,7 +255,7 @@ class ReplayBuffer:
         sl = self._outs[k] if self._outs and k < len(self._outs) else None
         if sl is None or sl["free"] or sl["gen"] != gen or sl["views"][0] is not states:
             return False
-        if stream is not None and stream != _stream_handle(self.device):
+        if stream is not None and stream != _libsfx().stream_ptr(self._ring_dev):
             with torch.cuda.device(self.device):
                 ev = torch.cuda.Event()
                 ev.record(torch.cuda.ExternalStream(stream, device=self.device))
@@ -214,9 +267,8 @@ class ReplayBuffer:
         """Every field in one gather launch.  The indices and the minibatch's γ go to the kernel in a
         slot of coherent host memory it reads directly (no host->device copy); a block of slots is
         rewritten only after the gathers that read it have completed (its event)."""
-        from sfx import _lib
-
-        stream = _lib.stream_ptr(self._dev_index())
+        _lib = _libsfx()
+        stream = _lib.stream_ptr(self._ring_dev)
         if self._pidx is None or self._pB != B:  # slots of [B indices (int64) | B γ (float32 words)]
             if self._pidx is not None:  # a new batch size: no queued gather may still read the old slots
                 torch.cuda.synchronize(self.device)
@@ -242,15 +294,29 @@ class ReplayBuffer:
         host = self._pnp[i]
         host[:B] = indices
         host[B:].view(np.float32)[:B] = self._gam[indices]
-        n_s, d = rs.shape[1], rr.shape[1]
-        S, A, PHI, S1, G = self._out_slot(B, n_s, d)
+        n_s, d = self._widths[0], self._widths[1]
+        views, (pS, pA, pPHI, pS1, pG) = self._out_slot(B, n_s, d)
         p = self._pptr[i]
-        _lib.check(_lib.lib.sfx_replay_gather(
-            stream, rs.data_ptr(), rr.data_ptr(), rs1.data_ptr(), ra.data_ptr(),
-            self._gdev.data_ptr() if self._gdev is not None else None, p, p + 8 * B, B, S.data_ptr(),
-            PHI.data_ptr(), S1.data_ptr(), A.data_ptr(), G.data_ptr(), n_s, d), "sfx_replay_gather")
+        rg = self._gdev.data_ptr() if self._gdev is not None else None
+        prs, pra, prr, prs1 = self._rp
+        pend = self._pend
+        if pend is not None:  # the append before: its row written in the same launch
+            self._pend = None
+            j, st, ac, rw, ns, nsv, rwv = pend
+            mx, mr = self._mirror_ptrs()
+            _lib.check(_lib.lib.sfx_replay_put_gather(
+                stream, prs, prr, prs1, pra, rg, j, st.data_ptr(), rw.data_ptr(), ns.data_ptr(), ac.data_ptr(), mx, mr,
+                p, p + 8 * B, B, pS, pPHI, pS1, pA, pG, n_s, d), "sfx_replay_put_gather")
+            if mx is not None:
+                self.last_next = (weakref.ref(ns), nsv, self.mirror)
+            if mr is not None:
+                self.last_reward = (weakref.ref(rw), rwv, self.mirror_reward)
+        else:
+            _lib.check(_lib.lib.sfx_replay_gather(stream, prs, prr, prs1, pra, rg, p, p + 8 * B, B, pS, pPHI, pS1, pA,
+                                                  pG, n_s, d), "sfx_replay_gather")
         if last == self._BLOCK - 1:
             with torch.cuda.device(self.device):  # the gathers' stream, on the buffer's device
                 ev = self._pev[blk] = self._pev[blk] or torch.cuda.Event()
                 ev.record(torch.cuda.current_stream(self.device))
+        S, A, PHI, S1, G = views
         return S, A, PHI, S1, G  # a new tuple: a caller holding it holds each tensor

@@ -19,11 +19,15 @@ nothing from update_successor, and every method that reads state flushes first.
 """
 from __future__ import annotations
 
+import weakref
+
 import numpy as np
 import torch
 
+from sfx import _lib
 from sfx.dropin._host import copy_weights as update_models_weights
 from sfx.dropin._host import torch_device as get_torch_device
+from sfx.dropin.agents.buffer import lending_buffer, release_minibatch
 from .successor import SF
 
 
@@ -84,6 +88,7 @@ class _FitW(list):
         sf = self._sf
         if isinstance(i, int) and sf._eng is not None and sf._eng_T == len(self):
             sf._flush()
+            sf._pred = None  # a fused GPI computed with the old w
             sf._eng.load_w(i if i >= 0 else len(self) + i, v)
 
 
@@ -102,6 +107,10 @@ def _huber_delta(loss) -> float:
     raise NotImplementedError("sfx DeepSF trains with MSELoss, HuberLoss or SmoothL1Loss(beta=1), reduction='mean'")
 
 class DeepSF(SF):
+    _alpha_f = 0.0  # float(alpha_w) as the deferred LMS last took it
+    _lms_pend = None
+    _pred = None
+
     def __init__(self, pytorch_model_handle, *args, target_update_ev=1000, max_batch=256, **kwargs):
         super().__init__(*args, **kwargs)
         self.pytorch_model_handle = pytorch_model_handle
@@ -112,6 +121,13 @@ class DeepSF(SF):
         self._eng_T = 0
         self._pending = []
         self._host_stale = False
+        # the agent loop's next GPI, fused into the last all-task update (_flush): (weak reference to
+        # the state, its version, task index, q, task); _gpi_task: the task index of the last GPI
+        self._pred = None
+        self._gpi_task = None
+        # update_reward of a device φ and a host reward, deferred to ride in the next all-task step
+        # (sfx_update_all_select) or run before anything else reads w: (φ, its version, r, task)
+        self._lms_pend = None
 
     # ------------------------------------------------------------------ library
     def reset(self):
@@ -121,6 +137,8 @@ class DeepSF(SF):
         self._since = []
 
     def _close(self):
+        self._pred = None
+        self._lms_pend = None
         if getattr(self, "_eng", None) is not None:
             self._pending = []
             self._eng.close()
@@ -145,6 +163,7 @@ class DeepSF(SF):
 
     def add_training_task(self, task, source=None):
         self._flush()
+        self._pred = None
         self._sync_host()
         SF.add_training_task(self, task, source)
 
@@ -236,38 +255,95 @@ class DeepSF(SF):
         """Push the torch modules' current weights to the device (after editing ``psi``)."""
         if self._eng is not None:
             self._flush()
+            self._pred = None
             for t, ((m, _, _), (tm, _, _)) in enumerate(self._psi):
                 self._eng.load_head(t, _flat(m), 0)
                 self._eng.load_head(t, _flat(tm), 1)
             self._host_stale = False
 
     def _flush(self):
-        """Run deferred update_successor calls."""
+        """Run deferred update_successor calls (and a deferred update_reward before them)."""
+        lms = self._lms_pend
         if not self._pending or self._eng is None:
+            if lms is not None:
+                self._lms_now()
             return
         pend, self._pending = self._pending, []
         eng = self._eng
         T = self._eng_T
-        same = all(p[0] is pend[0][0] for p in pend)
-        if same and [p[1] for p in pend] == list(range(T)):
+        # update_successor queues a policy after the first only when it is the next one on the same
+        # minibatch, and flushes a queue that does not open with policy 0: T entries from policy 0
+        # are the all-task loop of agents/sfdqn.py:57-60
+        if len(pend) == T and pend[0][1] == 0:
             s, a, phi, s1, g = pend[0][2]
             lb = getattr(eng, "_dropin_losses", None)  # the losses nobody reads: one buffer per engine
             if lb is None:
                 lb = eng._dropin_losses = torch.empty(T, 3, device=eng.device)
-            eng.update_all(s, a, phi, s1, g, losses=lb)
+            buf = lending_buffer(s)
+            nxt = self._next_state(buf)
+            if nxt is not None:
+                # the agent's next GPI (on the transition's next state, which the buffer copied into
+                # the engine's selection input; with the task of its last GPI) rides in the update's
+                # final round: GPI returns its result if that state comes.  The deferred LMS rides in
+                # the step's first launch when the buffer copied its φ into the engine's LMS input.
+                lt = -1
+                if lms is not None:
+                    lr = buf.last_reward
+                    if (lr is not None and lr[2] is eng.lms_phi and lr[0]() is lms[0] and lr[1] == lms[1]
+                            and lms[0]._version == lms[1]):
+                        self._lms_pend, lt = None, lms[3]
+                    else:
+                        self._lms_now()
+                q, task = eng.update_all_select(s, a, phi, s1, g, self._gpi_task, losses=lb, lms_task=lt,
+                                                lms_r=lms[2] if lt >= 0 else 0.0, lms_alpha=self._alpha_f)
+                self._pred = (nxt[0], nxt[1], self._gpi_task, q, task)
+            else:
+                if lms is not None:
+                    self._lms_now()
+                eng.update_all(s, a, phi, s1, g, losses=lb)
             # update_all settled the step before (host rounds included): its minibatch is read by
             # nothing queued after this point -- hand it back to the ReplayBuffer that lent it
             self._release_held()
             self._held = s
         else:
+            if lms is not None:
+                self._lms_now()
             for _, i, (s, a, phi, s1, g) in pend:
                 eng.update(i, s, a, None, phi, s1, g, use_gpi=True)
         self._host_stale = True
+
+    def _lms_now(self):
+        """Launch the deferred update_reward."""
+        phi, _, r, t = self._lms_pend
+        self._lms_pend = None
+        self._eng.lms(t, phi.reshape(-1), r, self._alpha_f)
 
     # ------------------------------------------------------------------ ψ / GPI
     def _state(self, state):
         s = torch.as_tensor(state)
         return s.reshape(1, -1) if s.dim() == 1 else s.reshape(s.shape[0], -1)
+
+    def _next_state(self, buf):
+        """(weak reference, version) of the state the agent's next GPI will most likely get: the
+        next state the minibatch's ReplayBuffer (buf) was last given, when the buffer copied it into
+        the engine's selection input (on the engine's stream) and nothing changed it since.
+        Otherwise None -- and the buffer is asked to copy from its next append on (the next state
+        and φ: sfx_replay_put_gather)."""
+        eng = self._eng
+        if self._gpi_task is None or eng is None:
+            return None
+        if (buf is None or getattr(buf, "_ring_dev", None) != eng.device.index
+                or _lib.stream_ptr(eng.device.index) != eng.stream):
+            return None
+        x, _ = eng._select_slots()
+        if buf.mirror is not x:
+            buf.mirror, buf.mirror_reward = x, eng.lms_phi
+            return None
+        ln = buf.last_next
+        ns = ln[0]() if ln is not None and ln[2] is x else None
+        if ns is None or ns._version != ln[1]:
+            return None
+        return ln[0], ln[1]
 
     def _release_held(self):
         """The minibatch of the last fused update, once a library call has settled that update, goes
@@ -275,20 +351,20 @@ class DeepSF(SF):
         held = getattr(self, "_held", None)
         if held is not None:
             self._held = None
-            from sfx.dropin.agents.buffer import release_minibatch
-
             release_minibatch(held, self._eng.stream if self._eng is not None else None)
 
     def get_successor(self, state, policy_index):
         return self.get_successors(state)[:, policy_index]
 
     def get_successors(self, state):
+        self._pred = None
         s = self._state(state)
         eng = self._engine(s.shape[0])
         self._flush()
         return eng.successors(s).to(self._out_device())
 
     def GPI_w(self, state, w):
+        self._pred = None
         s = self._state(state)
         eng = self._engine(s.shape[0])
         self._flush()
@@ -297,6 +373,19 @@ class DeepSF(SF):
         return q.to(dev), torch.squeeze(task).to(dev)
 
     def GPI(self, state, task_index, update_counters=False):
+        pred, self._pred = self._pred, None
+        ref = pred[0]() if pred is not None else None
+        if (ref is not None and state is ref and not self._pending and state._version == pred[1]
+                and task_index == pred[2] and self._eng is not None and self._eng_T == self.n_tasks):
+            # computed by the last update's final round, on the heads and w this call would read
+            q, task = self._eng.settle_select(pred[3], pred[4])
+            self._release_held()
+            dev = self._out_device()
+            if dev != self._eng.device:
+                q, task = q.to(dev), task.to(dev)
+            if update_counters:
+                self._count(task_index, task)
+            return q, task
         s = self._state(state)
         eng = self._engine(s.shape[0])
         self._flush()
@@ -304,6 +393,7 @@ class DeepSF(SF):
         move = dev != eng.device
         # one state: the task index is allocated 0-dim (what torch.squeeze would make of it)
         _, q, task, _ = eng.gpi(s, w_index=task_index, task_shape=() if s.shape[0] == 1 else None)
+        self._gpi_task = task_index if s.shape[0] == 1 else None
         self._release_held()  # gpi settled the pending update
         if move:
             q, task = q.to(dev), task.to(dev)
@@ -315,8 +405,20 @@ class DeepSF(SF):
 
     # ------------------------------------------------------------------ training
     def update_reward(self, phi, r, task_index, exact=False):
-        eng = self._engine()
-        self._flush()
+        self._pred = None
+        eng = self._eng
+        if eng is None or self._eng_T != self.n_tasks:
+            eng = self._engine()
+        if self._pending or self._lms_pend is not None:
+            self._flush()
+        if (not exact and type(phi) is torch.Tensor and type(r) in (float, int) and eng._on_dev(phi, torch.float32)
+                and phi.numel() == eng.d and 0 <= task_index < self._eng_T):
+            # a device φ and a host reward (the reference agents' call): deferred -- it runs inside the
+            # next all-task step when that step's minibatch comes from the buffer this φ was appended
+            # to (one launch set), else before the next call that reads w
+            self._alpha_f = float(self.alpha_w)
+            self._lms_pend = (phi, phi._version, float(r), task_index)
+            return
         if isinstance(r, (float, int, np.floating, np.integer)) or (torch.is_tensor(r) and r.device.type == "cpu"
                                                                   and r.numel() == 1):
             rr = float(r)  # a host reward goes to the kernel as a value (rounded to float32 there)
@@ -330,6 +432,7 @@ class DeepSF(SF):
                 raise Exception(f"sampled reward {r} != linear reward {r_true} - please check task {task_index}!")
 
     def update_successor(self, transitions, policy_index):
+        self._pred = None
         if transitions is None:
             return
         pend = self._pending

@@ -405,6 +405,71 @@ class SFEngine:
         self._lazy_keep = (s, s1, a, phi, gamma, losses)
         return losses
 
+    def _select_slots(self):
+        """Persistent device inputs of the fused step (fixed pointers, so the step's graph is
+        captured once per minibatch slot): ``sel_state`` [n_s], the selection's state, and
+        ``lms_phi`` [d], the LMS features (filled by the caller -- the drop-in's buffer copies each
+        appended next state and φ into them, sfx_replay_put_gather)."""
+        if getattr(self, "sel_state", None) is None:
+            TA = self.T * self.A
+            self._sel_ta = TA + (TA & 1)
+            self.sel_state = torch.zeros(self.n_s, device=self.device)
+            self.lms_phi = torch.zeros(self.d, device=self.device)
+            self._sel_ptrs = (self.sel_state.data_ptr(), self.lms_phi.data_ptr())
+        return self.sel_state, self.lms_phi
+
+    _mb_ok = None
+    sel_state = None
+
+    def update_all_select(self, s, a, phi, s1, gamma, task_index: int, s_next=None,
+                          losses: Optional[torch.Tensor] = None, lms_task: int = -1, lms_r: float = 0.0,
+                          lms_alpha: float = 0.0):
+        """[LMS of w[lms_task] on (``lms_phi``, lms_r)], update_all, then the GPI of one next state
+        with w[task_index], fused into one launch set (sfx_update_all_select).  s_next: a float32
+        device tensor of n_s values, or None for ``sel_state`` (filled by the caller).  Returns
+        fresh device tensors (q [1, T, A], task []) that the step's selection writes -- what
+        lms + update_all + gpi(s_next, w_index=task_index) would return, bit for bit -- complete in
+        stream order once the step is settled (``settle_select``, or any later call)."""
+        self._select_slots()
+        xp, php = self._sel_ptrs
+        if s_next is not None:
+            if not (self._on_dev(s_next, torch.float32) and s_next.numel() == self.n_s):
+                raise ValueError("update_all_select: s_next must be a contiguous float32 device tensor of n_s values")
+            xp = s_next.data_ptr()
+            self._lazy_keep = s_next  # read again by host rounds
+        ok = self._mb_ok  # the last minibatch checked (the drop-in's buffer lends the same few slots)
+        if ok is not None and s is ok[0] and a is ok[1] and phi is ok[2] and s1 is ok[3] and gamma is ok[4] \
+                and losses is ok[5]:
+            ptrs = ok[6]
+        else:
+            s, s1, a, phi, gamma, _ = self._batch_in(s, s1, a, phi, gamma)
+            if losses is None:
+                losses = torch.empty(self.T, 3, device=self.device)
+            ptrs = (s.data_ptr(), a.data_ptr(), phi.data_ptr(), s1.data_ptr(), gamma.data_ptr(), s.shape[0],
+                    losses.data_ptr())
+            self._mb_ok = (s, a, phi, s1, gamma, losses, ptrs)
+        # q [T*A] then the task (int64, 8-byte aligned) in one fresh allocation; the step's graph
+        # reads the two output pointers from host words each launch, so it is captured once
+        out = torch.empty(self._sel_ta + 2, device=self.device)
+        op = out.data_ptr()
+        check(lib.sfx_update_all_select(self._h, *ptrs, xp, int(task_index), op, op + 4 * self._sel_ta,
+                                        int(lms_task), php, float(lms_r), float(lms_alpha)), "sfx_update_all_select")
+        TA = self.T * self.A
+        return out[:TA].view(1, self.T, self.A), out[self._sel_ta:self._sel_ta + 2].view(torch.int64).view(())
+
+    def settle_select(self, q, task):
+        """Collect the pending step's verdict (sfx_settle); (q, task) of update_all_select hold the
+        selection then (host rounds, if any, rewrote them in place)."""
+        check(lib.sfx_settle(self._h, None), "sfx_settle")
+        return q, task
+
+    def settle(self) -> int:
+        """sfx_settle: collect the verdict of a pending update_all / update_all_select; returns the
+        rounds that ran on the host."""
+        n = C.c_int()
+        check(lib.sfx_settle(self._h, C.byref(n)), "sfx_settle")
+        return n.value
+
     def step_all(self, s=None, a=None, phi=None, s1=None, gamma=None, *, use_gpi: bool = True, lms_task: int = -1,
                  lms_phi=None, lms_r=None, lms_alpha: float = 0.0, s_next=None, task_index: int = 0,
                  sel_use_gpi: bool = True, losses: Optional[torch.Tensor] = None):
@@ -451,6 +516,12 @@ class SFEngine:
         s, f, r, n = C.c_longlong(), C.c_longlong(), C.c_longlong(), C.c_longlong()
         check(lib.sfx_step_stats(self._h, C.byref(s), C.byref(f), C.byref(r), C.byref(n)), "sfx_step_stats")
         return {"steps": s.value, "host_round_steps": f.value, "unverified_policies": r.value, "rounds": n.value}
+
+    def graph_stats(self):
+        """sfx_graph_stats: graphs captured, graph launches, graphs cached on the handle."""
+        v = [C.c_longlong() for _ in range(3)]
+        check(lib.sfx_graph_stats(self._h, *[C.byref(x) for x in v]), "sfx_graph_stats")
+        return {"captures": v[0].value, "launches": v[1].value, "cached": v[2].value}
 
     def nonfinite(self, reset: bool = False) -> bool:
         """SURVEY §5 failure detection: whether any TD error since the last reset was NaN / Inf."""

@@ -171,6 +171,28 @@ int sfx_update_all(sfx_t h, const float* S_dev, const int64_t* a_dev, const floa
                    const float* S1_dev, const float* gamma_dev, int B, float* losses_dev);
 
 /*
+ * One env step's library work of the all-task agent in one launch set: the LMS reward fit of
+ * w[lms_task] on (lms_phi [d], lms_r) when lms_task >= 0 (SF.update_reward, features/
+ * successor.py:164-167, the reward as a value like sfx_lms_value), sfx_update_all,
+ * then the agent loop's next GPI (agents/agent.py:223-224 -> agents/sfdqn.py:39-45 ->
+ * features/successor.py:248-273) when its state is already known: the transition's next state
+ * s_next_dev [n_s] with w[task_index].  q_dev [T * A] and task_dev [1] (device, may be NULL)
+ * receive what sfx_lms + sfx_update_all + sfx_gpi(h, s_next, 1, w[task_index], NULL, q, task,
+ * NULL) write, bit for bit; the LMS rides in the step's first launch and the selection in its
+ * final round (and again in any host round).  Like sfx_update_all it returns once enqueued;
+ * sfx_settle (or any later call) collects the verdict.
+ */
+int sfx_update_all_select(sfx_t h, const float* S_dev, const int64_t* a_dev, const float* phi_dev,
+                          const float* S1_dev, const float* gamma_dev, int B, float* losses_dev,
+                          const float* s_next_dev, int task_index, float* q_dev, int64_t* task_dev, int lms_task,
+                          const float* lms_phi_dev, float lms_r, float lms_alpha);
+/* Collect the verdict of a pending sfx_update_all / sfx_update_all_select (waits for the step;
+ * host rounds when the device rounds left a policy unverified).  A no-op without one.
+ * host_rounds (may be NULL): the rounds this call ran on the host (0 when the device rounds held;
+ * sfx_update_all_select's q / task were then rewritten after the host rounds). */
+int sfx_settle(sfx_t h, int* host_rounds);
+
+/*
  * Fused env step of the all-task schedule: the device half of one Agent.next_sample
  * (agents/agent.py:195-261) with SFDQN.train_agent (agents/sfdqn.py:47-60):
  *   - LMS reward fit of w[lms_task] on (lms_phi [d], lms_r [1]) when lms_task >= 0
@@ -223,6 +245,10 @@ int sfx_step_stats(sfx_t h, long long* steps, long long* fallbacks, long long* r
  * would repeat bit for bit): policies checked and skipped so far, counted on the device
  * (synchronises the handle's stream); reset != 0 zeroes the counters afterwards. */
 int sfx_skip_stats(sfx_t h, long long* checked, long long* skipped, int reset);
+/* Launch-graph cache of the handle: graphs captured (and instantiated) so far, graph launches,
+ * graphs currently cached.  A call whose device pointers or configuration the cache has not seen
+ * captures a new graph; a steady loop should capture only while it warms up. */
+int sfx_graph_stats(sfx_t h, long long* captures, long long* launches, long long* cached);
 
 /*
  * Failure detection (the reference only prints NaN/Inf diagnostics,
@@ -243,6 +269,16 @@ int sfx_nonfinite(sfx_t h, int* flag_host, int reset);
  */
 int sfx_replay_put(void* stream, float* rs, float* rphi, float* rs1, int64_t* ra, long long j, const float* s,
                    const float* phi, const float* s1, const int64_t* a, int n_s, int d);
+/* sfx_replay_put of row j followed by sfx_replay_gather (rows idx[0, B); γ from rg, or gam when
+ * rg is NULL) in ONE launch -- the append and the replay of agents/agent.py:251-256 -- a row idx[b]
+ * == j read from the new transition itself.  s1_copy [n_s] / phi_copy [d] (may be NULL) receive
+ * copies of s1 and phi: the drop-in hands the agent's next GPI state and the LMS features to the
+ * fixed inputs of sfx_update_all_select this way (no launch of their own, graph keys that do not
+ * change). */
+int sfx_replay_put_gather(void* stream, float* rs, float* rphi, float* rs1, int64_t* ra, const float* rg, long long j,
+                          const float* s, const float* phi, const float* s1, const int64_t* a, float* s1_copy,
+                          float* phi_copy, const int64_t* idx, const float* gam, int B, float* S, float* PHI,
+                          float* S1, int64_t* A, float* G, int n_s, int d);
 int sfx_replay_gather(void* stream, const float* rs, const float* rphi, const float* rs1, const int64_t* ra,
                       const float* rg, const int64_t* idx, const float* gam, int B, float* S, float* PHI, float* S1,
                       int64_t* A, float* G, int n_s, int d);

@@ -18,7 +18,7 @@ def test_dropin_loop_fuses_every_env_step(buffer, monkeypatch):
     from tools import dropin_loop
 
     calls = {"all": 0, "one": 0}
-    real_all, real_one = SFEngine.update_all, SFEngine.update
+    real_all, real_one, real_sel = SFEngine.update_all, SFEngine.update, SFEngine.update_all_select
 
     def count_all(self, *a, **k):
         calls["all"] += 1
@@ -28,7 +28,12 @@ def test_dropin_loop_fuses_every_env_step(buffer, monkeypatch):
         calls["one"] += 1
         return real_one(self, *a, **k)
 
+    def count_sel(self, *a, **k):  # update_all with the next GPI fused in (agents.buffer alias)
+        calls["all"] += 1
+        return real_sel(self, *a, **k)
+
     monkeypatch.setattr(SFEngine, "update_all", count_all)
+    monkeypatch.setattr(SFEngine, "update_all_select", count_sel)
     monkeypatch.setattr(SFEngine, "update", count_one)
     loop = dropin_loop.DropinLoop(buffer=buffer, T=4, batch=8)
     loop.run(2)
