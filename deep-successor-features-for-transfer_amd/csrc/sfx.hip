@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <deque>
 #include <map>
@@ -138,6 +139,8 @@ struct StepOut {
   int64_t sel[2];
   int flag;
   unsigned done;  // k_ver arrivals when it publishes (reset by the last arrival)
+  int posted;     // host copy: the final k_ver posted sel / flag (VerArgs::h_posted)
+  int pad_;
 };
 
 }  // namespace
@@ -159,6 +162,7 @@ struct sfx_handle {
   std::vector<int> since_target, host_step;
   unsigned long long mask = 0;  // bit t: current slot of head t
   std::map<GraphKey, hipGraphExec_t> graphs;
+  std::map<GraphKey, bool> graph_posts;  // fused steps whose final k_ver posts to hout (no copy)
   Geo G{};
   // event instrumentation (bench roofline): packet timestamps per launch, eager only
   bool prof = false;
@@ -184,6 +188,7 @@ struct sfx_handle {
     bool pre = false;
     const float* ax = nullptr;
     int aM = 0;
+    bool posted = false;  // the step's final k_ver posts its verdict to hout (wait on hout->posted)
     // sfx_update_all_select: the selection's q table [T*A] and GPI task of s_next (gpi_row's
     // q_out / task_out, as sfx_gpi writes them)
     float* q_out = nullptr;
@@ -295,6 +300,7 @@ inline void touch(sfx_handle* h) {
 void clear_graphs(sfx_handle* h) {
   for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
   h->graphs.clear();
+  h->graph_posts.clear();
 }
 
 enum { K_FWD = 0, K_TDG = 1, K_BWD = 2, K_GPI = 3, K_LMS = 4, K_VER = 5, K_TSF = 6, K_NKIND = 7 };
@@ -848,6 +854,7 @@ int run_ver(sfx_handle* h, int M, int npol, bool sel, int post, const GpiArgs& g
   } else if (post_host) {  // the step's verdict and selection straight to h->hout (no copy after)
     V.h_sel = h->hout->sel;
     V.h_flag = &h->hout->flag;
+    V.h_posted = &h->hout->posted;
     V.done = &h->dout->done;
     V.nblocks = (int)(grid.x * grid.y);
     h->hout_posted = true;
@@ -1830,15 +1837,24 @@ static int step_all_impl(sfx_t h, const float* S, const int64_t* a, const float*
   const GraphKey key = make_key(5, {p.B, p.use_gpi, lms_task, p.task, p.sel_use_gpi, (int)alpha_bits, h->spec_rounds}, h->mask,
                                 {S, a, phi, S1, gamma, lms_phi, lms_r, s_next, losses, p.q_out, p.task_out, p.out_ind});
   const int rounds = p.use_gpi ? h->spec_rounds : 1;
+  h->hout->posted = 0;  // the step before has been collected: nothing writes hout now
+  bool recorded = false;
   RC(run_graph(h, key, [&]() -> int {
     h->post_hout = true;
     h->hout_posted = false;
     const int rc = launch_step_all(h, p, lms_task, lms_phi, lms_r, lms_alpha, rounds);
     h->post_hout = false;
     RC(rc);
+    recorded = true;
+    p.posted = h->hout_posted;
+    if (h->use_graphs && !h->prof) h->graph_posts[key] = p.posted;
     if (!h->hout_posted) HIPCHK(hipMemcpyAsync(h->hout, h->dout, sizeof(StepOut), hipMemcpyDeviceToHost, h->stream));
     return SFX_OK;
   }));
+  if (!recorded) {  // a cached graph: what its recording found
+    const auto it = h->graph_posts.find(key);
+    p.posted = it != h->graph_posts.end() && it->second;
+  }
   HIPCHK(hipEventRecord(h->ev_step, h->stream));
   h->pend = p;
   return SFX_OK;
@@ -1857,7 +1873,20 @@ int sfx_step_finish(sfx_t h, int64_t* out_host) {
   if (!h->pend.active) SFX_FAIL(SFX_E_STATE, "sfx_step_finish without sfx_step_all");
   sfx_handle::Pending p = h->pend;
   h->pend.active = false;
-  HIPCHK(hipEventSynchronize(h->ev_step));
+  if (p.posted) {
+    // the final k_ver posts the verdict to host memory: wait for that word (it lands before the
+    // launch's completion signal reaches the host); bounded, then the event as usual
+    volatile int* posted = &h->hout->posted;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (long spins = 0; !*posted; ++spins)
+      if ((spins & 1023) == 0 &&
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 1.0)
+        break;
+    if (!*posted) HIPCHK(hipEventSynchronize(h->ev_step));
+    std::atomic_thread_fence(std::memory_order_acquire);
+  } else {
+    HIPCHK(hipEventSynchronize(h->ev_step));
+  }
   int first = h->T, dev_flag = h->T;
   if (p.update) {
     first = p.use_gpi ? h->hout->flag : h->T;

@@ -2274,6 +2274,7 @@ struct VerArgs {
   // selection and the flag to host-coherent memory instead of a copy after the launch.  Null: no.
   int64_t* h_sel;
   int* h_flag;
+  int* h_posted;  // set to 1 last: the host waits for it instead of the launch's completion
 };
 
 // The step's verdict and selection to host-coherent memory (VerArgs::h_sel / h_flag), read with
@@ -2287,6 +2288,7 @@ __device__ __forceinline__ void post_verdict(const VerArgs& V) {
   __hip_atomic_store(V.h_sel + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(V.h_flag, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __threadfence_system();
+  __hip_atomic_store(V.h_posted, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Grid (npol + 1, ceil(M / rows)): one workgroup per (policy, `rows` minibatch rows), each
