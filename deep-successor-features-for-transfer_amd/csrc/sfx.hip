@@ -1304,6 +1304,20 @@ __global__ void k_replay_gather(const float* __restrict__ rs, const float* __res
   }
 }
 
+// A launch whose final k_ver posts the verdict to host memory (VerArgs::h_posted): wait for that
+// word -- it lands before the launch's completion signal reaches the host, and polling it skips
+// the runtime's wake-up.  Bounded (1 s); false when it did not come (the caller then waits for
+// the launch itself, which reports any error).
+bool wait_posted(sfx_handle* h) {
+  volatile int* posted = &h->hout->posted;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (long spins = 0; !*posted; ++spins)
+    if ((spins & 1023) == 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 1.0)
+      return false;
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return true;
+}
+
 // sfx_update_all returns once its step is enqueued; the speculation verdict -- and host rounds,
 // should the device rounds leave a policy unverified -- is collected by the next API call on the
 // handle (every entry point settles first), so the host never waits on a step it has not asked
@@ -1873,20 +1887,7 @@ int sfx_step_finish(sfx_t h, int64_t* out_host) {
   if (!h->pend.active) SFX_FAIL(SFX_E_STATE, "sfx_step_finish without sfx_step_all");
   sfx_handle::Pending p = h->pend;
   h->pend.active = false;
-  if (p.posted) {
-    // the final k_ver posts the verdict to host memory: wait for that word (it lands before the
-    // launch's completion signal reaches the host); bounded, then the event as usual
-    volatile int* posted = &h->hout->posted;
-    const auto t0 = std::chrono::steady_clock::now();
-    for (long spins = 0; !*posted; ++spins)
-      if ((spins & 1023) == 0 &&
-          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 1.0)
-        break;
-    if (!*posted) HIPCHK(hipEventSynchronize(h->ev_step));
-    std::atomic_thread_fence(std::memory_order_acquire);
-  } else {
-    HIPCHK(hipEventSynchronize(h->ev_step));
-  }
+  if (!p.posted || !wait_posted(h)) HIPCHK(hipEventSynchronize(h->ev_step));
   int first = h->T, dev_flag = h->T;
   if (p.update) {
     first = p.use_gpi ? h->hout->flag : h->T;
