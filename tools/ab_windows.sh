@@ -1,3 +1,6 @@
+#!/bin/bash
+# A/B of the headline's early windows (tools/first_windows.py) on ONE box, alternating: A = the
+# library as built, B = SFX_LIB=.../libsfx_ab.so (build it from the other revision first).
 cd "${GRAFT_REPO_ROOT:-/root/repo}" && mkdir -p gpurun_out/abw
 for i in 1 2 3; do
   TRIALS=2 timeout -k 10 120 python3 tools/first_windows.py > gpurun_out/abw/a$i.txt 2>&1 || exit 1

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""MFMA utilisation per kernel kind from one rocprofv3 --pmc pass (tools/r6_measure.sh):
+"""MFMA utilisation per kernel kind from one rocprofv3 --pmc pass (tools/round_end.sh):
 SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_MOPS_F32 / _BF16, SQ_BUSY_CYCLES, SQ_WAVE_CYCLES,
 GRBM_GUI_ACTIVE, with --kernel-trace in the same run for the dispatch durations.
 
