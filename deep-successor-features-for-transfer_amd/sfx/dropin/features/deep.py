@@ -313,9 +313,14 @@ class DeepSF(SF):
         self._host_stale = True
 
     def _lms_now(self):
-        """Launch the deferred update_reward."""
-        phi, _, r, t = self._lms_pend
+        """Launch the deferred update_reward.  Its φ is read now: a φ written in place since the
+        update_reward call would give another reward fit than the reference's (which fits at the
+        call) -- that raises instead of fitting silently on the new values."""
+        phi, v, r, t = self._lms_pend
         self._lms_pend = None
+        if phi._version != v:
+            raise RuntimeError("DeepSF.update_reward: the φ tensor was modified in place before the reward fit ran; "
+                               "pass a tensor that stays unchanged until the next DeepSF call (e.g. a clone)")
         self._eng.lms(t, phi.reshape(-1), r, self._alpha_f)
 
     # ------------------------------------------------------------------ ψ / GPI

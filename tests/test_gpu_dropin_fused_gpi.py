@@ -201,3 +201,24 @@ def test_buffer_copies_the_appended_next_state_and_features_with_the_replay():
         assert torch.equal(got[3], torch.vstack([order[i][3] for i in idx]))
         assert torch.equal(mx, s1.reshape(-1)) and torch.equal(mr, phi)
         assert buf.last_next[0]() is s1 and buf.last_reward[0]() is phi
+
+
+def test_deferred_reward_fit_refuses_a_phi_written_in_place():
+    """update_reward of a device φ runs with the next step (or the next call that reads w); a φ
+    changed in place before then would be fitted on other values than the reference fits: it
+    raises instead."""
+    from tools import dropin_loop
+
+    loop = dropin_loop.DropinLoop(buffer="reference", T=4, batch=8, seed=5)
+    loop.run(10)
+    sf = loop.sf
+    phi = torch.rand(sf.n_features, device=loop.device)
+    w0 = sf.fit_w[0].clone()
+    sf.update_reward(phi, 0.5, 0)
+    w1 = sf.fit_w[0]  # reading w runs the deferred fit
+    assert not torch.equal(w0, w1)
+    sf.update_reward(phi, 0.5, 0)
+    phi.mul_(2.0)
+    with pytest.raises(RuntimeError, match="modified in place"):
+        sf.fit_w[0]
+    loop.close()
