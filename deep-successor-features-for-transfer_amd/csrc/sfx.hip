@@ -163,6 +163,8 @@ struct sfx_handle {
   unsigned long long mask = 0;  // bit t: current slot of head t
   std::map<GraphKey, hipGraphExec_t> graphs;
   std::map<GraphKey, bool> graph_posts;  // fused steps whose final k_ver posts to hout (no copy)
+  std::map<GraphKey, int> keys_seen;     // library-call keys launched eagerly once (run_graph)
+  long long graph_eager = 0;             // those eager launches (sfx_graph_stats)
   Geo G{};
   // event instrumentation (bench roofline): packet timestamps per launch, eager only
   bool prof = false;
@@ -345,6 +347,14 @@ void launch(sfx_handle* h, int kind, double bytes, void (*kern)(KArgs...), dim3 
   launch_argv(h, kind, bytes, reinterpret_cast<const void*>(kern), grid, block, t, std::index_sequence_for<KArgs...>{});
 }
 
+// graph ops of the library's entry points (sfx_gpi 1, sfx_select_action 2, sfx_update 3,
+// sfx_step_all / sfx_update_all* 5, sfx_successors 21, sfx_test_actions 26, TSF 20 / 22-24,
+// learned φ 30): the first call with a new key runs eagerly (run_graph)
+bool eager_first_sight(int op) {
+  return op == 1 || op == 2 || op == 3 || op == 5 || op == 21 || op == 26 || op == 20 || (op >= 22 && op <= 24) ||
+         op == 30;
+}
+
 // Capture `body` (which launches on h->stream) into a graph keyed by `key`, then replay
 // (launch = false: instantiate only -- sfx_runner_warm).
 template <class F>
@@ -352,6 +362,17 @@ int run_graph(sfx_handle* h, const GraphKey& key, F body, bool launch_it = true)
   touch(h);
   if (!h->use_graphs || h->prof) return launch_it ? body() : SFX_OK;
   auto it = h->graphs.find(key);
+  if (it == h->graphs.end() && launch_it && eager_first_sight(key.op)) {
+    // a library call whose key this handle has not seen: launch it eagerly and capture it only
+    // when the same key comes again -- callers that pass fresh buffers every call (a new key each
+    // time) would otherwise pay a capture and an instantiation per call
+    int& n = h->keys_seen[key];
+    if (n++ == 0) {
+      if (h->keys_seen.size() > 4096) h->keys_seen.clear();
+      h->graph_eager += 1;
+      return body();
+    }
+  }
   if (it == h->graphs.end()) {
     hipStream_t saved = h->stream;
     h->stream = h->cap;
@@ -1986,7 +2007,7 @@ int sfx_step_stats(sfx_t h, long long* steps, long long* fallbacks, long long* r
 int sfx_graph_stats(sfx_t h, long long* captures, long long* launches, long long* cached) {
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   if (captures) *captures = h->graph_captures;
-  if (launches) *launches = h->graph_launches;
+  if (launches) *launches = h->graph_launches + h->graph_eager;
   if (cached) *cached = (long long)h->graphs.size();
   return SFX_OK;
 }

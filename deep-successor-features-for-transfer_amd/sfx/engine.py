@@ -125,11 +125,26 @@ class SFEngine:
             st = self._xstream = torch.cuda.ExternalStream(self.stream, device=self.device)
         return torch.cuda.stream(st)
 
-    def _pin_copy(self, i, nbytes) -> torch.Tensor:
-        """One non-blocking copy of slot i's first nbytes into a fresh device buffer, on the
-        handle's stream."""
+    def _settle_pending(self):
+        check(lib.sfx_settle(self._h, None), "sfx_settle")
+
+    def _site_buf(self, site, nbytes) -> torch.Tensor:
+        """The device staging buffer of one call site: the same memory every call, so the call's
+        captured graph is found again instead of captured anew (a fresh buffer per call would give
+        every call a new graph key).  Reuse is in stream order: the next copy into it is queued
+        after every kernel that read it."""
+        bufs = self.__dict__.setdefault("_sites", {})
+        b = bufs.get(site)
+        if b is None or b.numel() < nbytes:
+            b = bufs[site] = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=self.device)
+        return b[:nbytes]
+
+    def _pin_copy(self, i, nbytes, site=None) -> torch.Tensor:
+        """One non-blocking copy of slot i's first nbytes into device memory -- a fresh buffer, or
+        the call site's own (`site`) -- on the handle's stream."""
         with self._on_stream():
-            out = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            out = torch.empty(nbytes, dtype=torch.uint8, device=self.device) if site is None else \
+                self._site_buf(site, nbytes)
             out.copy_(self._pin[i, :nbytes], non_blocking=True)
             ev = self._pin_ev[i] = self._pin_ev[i] or torch.cuda.Event()
             ev.record()
@@ -144,13 +159,15 @@ class SFEngine:
             x = x.numpy()
         return np.asarray(x, dtype=npdt)
 
-    def _h2d(self, x, dtype) -> torch.Tensor:
-        return self._h2d_many([(x, dtype)])[0]
+    def _h2d(self, x, dtype, site=None) -> torch.Tensor:
+        return self._h2d_many([(x, dtype)], site)[0]
 
-    def _h2d_many(self, items):
+    def _h2d_many(self, items, site=None, settle=False):
         """Host inputs [(x, dtype)] -> device tensors of their shapes, staged together through ONE
         pinned slot and ONE non-blocking copy (a step's s, a, φ, s1, γ are one copy, not five).
-        Device tensors are converted in place of staging."""
+        Device tensors are converted in place of staging.  site: the device buffer of that call
+        site (the views returned are valid until the site's next call); settle: collect a pending
+        step first (its host rounds read the inputs it was given, possibly this site's)."""
         arrs = [self._host_array(x, self._NP[dt]) for x, dt in items]
         offs, tot = [], 0
         for a in arrs:
@@ -166,7 +183,9 @@ class SFEngine:
             for a, o in zip(arrs, offs):
                 if a is not None:
                     row[o:o + a.nbytes].view(a.dtype)[:] = a.reshape(-1)
-            dev = self._pin_copy(i, tot)
+            if settle:  # a pending step's host rounds may still read the site's last inputs
+                self._settle_pending()
+            dev = self._pin_copy(i, tot, site)
         out = []
         for (x, dt), a, o in zip(items, arrs, offs):
             if a is None:
@@ -181,10 +200,10 @@ class SFEngine:
         return (type(x) is torch.Tensor and x.is_cuda and x.dtype is dt and x.get_device() == self.device.index
                 and x.is_contiguous())
 
-    def _f(self, x, shape=None) -> torch.Tensor:
+    def _f(self, x, shape=None, site=None) -> torch.Tensor:
         if self._on_dev(x, torch.float32):
             return x if shape is None else x.view(shape)
-        t = self._h2d(x, torch.float32)
+        t = self._h2d(x, torch.float32, site)
         if shape is not None:
             t = t.reshape(shape)
         return t.contiguous()
@@ -205,7 +224,7 @@ class SFEngine:
                 return [s, s1, a, phi, gamma, r]
         items = [(s, torch.float32), (s1, torch.float32), (a, torch.long), (phi, torch.float32),
                  (gamma, torch.float32)] + ([] if r is None else [(r, torch.float32)])
-        t = self._h2d_many(items)
+        t = self._h2d_many(items, "batch", settle=True)
         B = t[0].shape[0]
         out = [t[0].contiguous(), t[1].contiguous(), t[2].reshape(-1).contiguous(),
                t[3].reshape(B, self.d).contiguous(), t[4].reshape(B).contiguous()]
@@ -303,7 +322,7 @@ class SFEngine:
             task_shape=None):
         """GPI over all heads.  Returns (psi [B,T,A,d] or None, q [B,T,A] or None, task [B], next [B]);
         task_shape: the task tensor's shape instead of [B] (B elements, e.g. () for one state)."""
-        S = self._f(S)
+        S = self._f(S, site="gpi_s")
         if S.dim() == 1:
             S = S.reshape(1, -1)
         B = S.shape[0]
@@ -311,7 +330,7 @@ class SFEngine:
             w_ptr = self._w_ptrs[w_index]
             w_keep = None
         else:
-            w_keep = self._f(w, (-1,))
+            w_keep = self._f(w, (-1,), site="gpi_w")
             w_ptr = w_keep.data_ptr()
         psi = torch.empty(B, self.T, self.A, self.d, device=self.device) if want_psi else None
         q = torch.empty(B, self.T, self.A, device=self.device) if want_q else None
@@ -326,7 +345,7 @@ class SFEngine:
     def successors(self, S, which: int = 0) -> torch.Tensor:
         """get_successors (which=0, online heads) / get_next_successors (which=1, target heads):
         [B, T, A, d]."""
-        S = self._f(S)
+        S = self._f(S, site="succ_s")
         if S.dim() == 1:
             S = S.reshape(1, -1)
         psi = torch.empty(S.shape[0], self.T, self.A, self.d, device=self.device)
@@ -335,7 +354,7 @@ class SFEngine:
 
     def select_action(self, s, task_index: int, use_gpi: bool = True, q_out: Optional[torch.Tensor] = None):
         """Greedy GPI action for one state; returns the device tensor [c, a] (not synchronized)."""
-        s = self._f(s, (-1,))
+        s = self._f(s, (-1,), site="sel_s")
         check(lib.sfx_select_action(self._h, s.data_ptr(), int(task_index), int(bool(use_gpi)), dptr(q_out),
                                     self._sel.data_ptr()), "sfx_select_action")
         return self._sel
@@ -563,7 +582,7 @@ class SFEngine:
             # a device φ and a host reward (the reference agents' call): r as a kernel argument
             check(lib.sfx_lms_value(self._h, int(t), phi.data_ptr(), float(r), float(alpha)), "sfx_lms_value")
             return
-        phi, r = self._h2d_many([(phi, torch.float32), (r, torch.float32)])  # host values: one copy
+        phi, r = self._h2d_many([(phi, torch.float32), (r, torch.float32)], "lms")  # host values: one copy
         phi, r = phi.reshape(-1).contiguous(), r.reshape(1).contiguous()
         check(lib.sfx_lms(self._h, int(t), phi.data_ptr(), r.data_ptr(), float(alpha)), "sfx_lms")
 

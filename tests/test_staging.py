@@ -24,9 +24,12 @@ class _CpuStaging(SFEngine):
         self._pin_i = (i + 1) % self._PIN_SLOTS
         return i
 
-    def _pin_copy(self, i, nbytes):
+    def _pin_copy(self, i, nbytes, site=None):
         self.copies.append(nbytes)
         return self._pin[i, :nbytes].clone()
+
+    def _settle_pending(self):
+        self.settled = getattr(self, "settled", 0) + 1
 
     def __del__(self):
         pass
@@ -50,6 +53,7 @@ def test_batch_in_packs_one_copy_and_round_trips():
         assert got.dtype == dt and got.is_contiguous()
         assert torch.equal(got, ref.to(dt))
     assert out[3].shape == (B, 3) and out[2].shape == (B,) and out[4].shape == (B,)
+    assert st.settled == 1  # a minibatch goes to the batch site only after a pending step is collected
 
 
 def test_staging_slots_rotate_and_offsets_are_aligned():

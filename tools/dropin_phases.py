@@ -62,7 +62,27 @@ def timed_step(loop, acc):
 
 def main():
     steps = int(os.environ.get("STEPS", "400"))
-    loop = DropinLoop(buffer="reference")
+    buf = os.environ.get("BUFFER", "reference")
+    loop = DropinLoop(buffer=buf)
+    if buf != "reference":  # the loop's own step (its buffer's calls differ)
+        loop.run(60)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        loop.run(steps)
+        loop.sf._flush()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        print(f"{buf}: {1e6 * dt / steps:.1f} us/step; graph cache:", loop.sf._eng.graph_stats())
+        pr = cProfile.Profile()
+        pr.enable()
+        loop.run(steps)
+        loop.sf._flush()
+        torch.cuda.synchronize()
+        pr.disable()
+        s = io.StringIO()
+        pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
+        print(s.getvalue())
+        return
     loop.run(60)
     loop.sf._flush()
     torch.cuda.synchronize()
