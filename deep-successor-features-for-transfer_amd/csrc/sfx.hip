@@ -422,6 +422,7 @@ struct FwdExtra {
   int lms_head = -1;     // LMS in block 0 of layer 0
   const float* lms_phi = nullptr;
   const float* lms_r = nullptr;
+  const unsigned long long* lms_r_ind = nullptr;  // FwdArgs::lms_r_ind
   float lms_alpha = 0.f;
   int* flag = nullptr;   // reset to flag_value in block 0 of the first layer
   int flag_value = 0;
@@ -482,6 +483,7 @@ int run_fwd(sfx_handle* h, std::initializer_list<FwdGroup> groups, int M, const 
     F.lms_head = first ? ex.lms_head : -1;
     F.lms_phi = ex.lms_phi;
     F.lms_r = ex.lms_r;
+    F.lms_r_ind = first ? ex.lms_r_ind : nullptr;
     F.lms_alpha = ex.lms_alpha;
     F.flag = first ? ex.flag : nullptr;
     F.flag_value = ex.flag_value;
@@ -1218,6 +1220,10 @@ int launch_step_all(sfx_handle* h, const sfx_handle::Pending& p, int lms_task, c
   ex.lms_head = lms_task;
   ex.lms_phi = lms_phi;
   ex.lms_r = lms_r;
+  if (h->xin && lms_r == reinterpret_cast<const float*>(h->xin + 3)) {  // sfx_update_all_select, device reward
+    ex.lms_r = nullptr;
+    ex.lms_r_ind = h->xin + 3;
+  }
   ex.lms_alpha = lms_alpha;
   ex.flag = &h->dout->flag;
   ex.flag_value = T;
@@ -2056,7 +2062,8 @@ int sfx_update_all(sfx_t h, const float* S, const int64_t* a, const float* phi, 
 
 int sfx_update_all_select(sfx_t h, const float* S, const int64_t* a, const float* phi, const float* S1,
                           const float* gamma, int B, float* losses, const float* s_next, int task_index, float* q_out,
-                          int64_t* task_out, int lms_task, const float* lms_phi, float lms_r, float lms_alpha) {
+                          int64_t* task_out, int lms_task, const float* lms_phi, float lms_r, const float* lms_r_dev,
+                          float lms_alpha) {
   if (!h || !S || !a || !phi || !S1 || !gamma || !s_next) SFX_FAIL(SFX_E_ARG, "bad args");
   if (B < 1 || B > h->Mmax) SFX_FAIL(SFX_E_ARG, "batch exceeds max_batch");
   if (task_index < 0 || task_index >= h->T) SFX_FAIL(SFX_E_ARG, "bad task_index");
@@ -2068,9 +2075,11 @@ int sfx_update_all_select(sfx_t h, const float* S, const int64_t* a, const float
   std::memcpy(h->xin, &lms_r, sizeof(float));
   h->xin[1] = (unsigned long long)(uintptr_t)q_out;
   h->xin[2] = (unsigned long long)(uintptr_t)task_out;
-  RC(step_all_impl(h, S, a, phi, S1, gamma, B, 1, lms_task, lms_phi,
-                   lms_task >= 0 ? reinterpret_cast<const float*>(h->xin) : nullptr, lms_alpha, s_next, task_index, 1,
-                   losses, q_out, task_out, h->xin + 1));
+  h->xin[3] = (unsigned long long)(uintptr_t)lms_r_dev;
+  // the reward: the value in xin[0], or the device float whose address xin[3] holds
+  const float* rp = lms_task < 0 ? nullptr : reinterpret_cast<const float*>(lms_r_dev ? h->xin + 3 : h->xin);
+  RC(step_all_impl(h, S, a, phi, S1, gamma, B, 1, lms_task, lms_phi, rp, lms_alpha, s_next, task_index, 1, losses,
+                   q_out, task_out, h->xin + 1));
   h->lazy_finish = true;  // the verdict (host rounds redo the selection) is collected by the next call
   return SFX_OK;
 }

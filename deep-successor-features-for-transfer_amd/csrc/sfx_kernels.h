@@ -437,6 +437,9 @@ struct FwdArgs {
   const float* xc;       // a third layer-0 input (the look-ahead select: s_next beside the next minibatch)
   const float* lms_phi;  // LMS (lms_head >= 0): w[lms_head] += α (r - φ·w) φ
   const float* lms_r;
+  // or, non-null: a host-coherent word holding r's device address (a device reward tensor of the
+  // caller's that changes every step, read without changing the captured launch)
+  const unsigned long long* lms_r_ind;
   float lms_alpha;
   int* flag;             // set to flag_value when non-null
   // sharded step (d | 16): GPI maxima accumulated by the last layer's tiles of group role qa_role
@@ -548,7 +551,8 @@ __device__ void lms_apply(float* w, const float* phi, const float* r, float alph
 }
 
 __device__ void lms_block(const Geo& G, const FwdArgs& F) {
-  lms_apply(G.w + (long long)F.lms_head * G.dpad, F.lms_phi, F.lms_r, F.lms_alpha, G.d, step_cancelled(G.cancel));
+  const float* r = F.lms_r_ind ? reinterpret_cast<const float*>(F.lms_r_ind[0]) : F.lms_r;
+  lms_apply(G.w + (long long)F.lms_head * G.dpad, F.lms_phi, r, F.lms_alpha, G.d, step_cancelled(G.cancel));
 }
 
 // L0 = true (layer-1 launches of a forward from the states): the workgroup first computes the

@@ -43,7 +43,7 @@ SIGNATURES = {
     "sfx_test_reward_updates": (_I, [_VP, _I, _VP, _VP, _VP, _I, C.c_double, C.c_double, _VP]),
     "sfx_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP]),
     "sfx_update_all": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _VP]),
-    "sfx_update_all_select": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _VP, _VP, _I, _VP, _VP, _I, _VP, _F, _F]),
+    "sfx_update_all_select": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _VP, _VP, _I, _VP, _VP, _I, _VP, _F, _VP, _F]),
     "sfx_settle": (_I, [_VP, C.POINTER(C.c_int)]),
     "sfx_lms": (_I, [_VP, _I, _VP, _VP, _F]),
     "sfx_lms_value": (_I, [_VP, _I, _VP, _F, _F]),

@@ -290,7 +290,8 @@ class DeepSF(SF):
                 if lms is not None:
                     lr = buf.last_reward
                     if (lr is not None and lr[2] is eng.lms_phi and lr[0]() is lms[0] and lr[1] == lms[1]
-                            and lms[0]._version == lms[1]):
+                            and lms[0]._version == lms[1]
+                            and (type(lms[2]) is not torch.Tensor or lms[2]._version == lms[4])):
                         self._lms_pend, lt = None, lms[3]
                     else:
                         self._lms_now()
@@ -316,11 +317,11 @@ class DeepSF(SF):
         """Launch the deferred update_reward.  Its φ is read now: a φ written in place since the
         update_reward call would give another reward fit than the reference's (which fits at the
         call) -- that raises instead of fitting silently on the new values."""
-        phi, v, r, t = self._lms_pend
+        phi, v, r, t, rv = self._lms_pend
         self._lms_pend = None
-        if phi._version != v:
-            raise RuntimeError("DeepSF.update_reward: the φ tensor was modified in place before the reward fit ran; "
-                               "pass a tensor that stays unchanged until the next DeepSF call (e.g. a clone)")
+        if phi._version != v or (type(r) is torch.Tensor and r._version != rv):
+            raise RuntimeError("DeepSF.update_reward: the φ or reward tensor was modified in place before the reward "
+                               "fit ran; pass tensors that stay unchanged until the next DeepSF call (e.g. clones)")
         self._eng.lms(t, phi.reshape(-1), r, self._alpha_f)
 
     # ------------------------------------------------------------------ ψ / GPI
@@ -416,13 +417,15 @@ class DeepSF(SF):
             eng = self._engine()
         if self._pending or self._lms_pend is not None:
             self._flush()
-        if (not exact and type(phi) is torch.Tensor and type(r) in (float, int) and eng._on_dev(phi, torch.float32)
+        host_r = isinstance(r, (float, int, np.floating, np.integer))
+        dev_r = not host_r and eng._on_dev(r, torch.float32) and r.numel() == 1  # tasks/reacher.py's reward
+        if (not exact and (host_r or dev_r) and type(phi) is torch.Tensor and eng._on_dev(phi, torch.float32)
                 and phi.numel() == eng.d and 0 <= task_index < self._eng_T):
-            # a device φ and a host reward (the reference agents' call): deferred -- it runs inside the
-            # next all-task step when that step's minibatch comes from the buffer this φ was appended
-            # to (one launch set), else before the next call that reads w
+            # a device φ and a host or device reward (the reference agents' call): deferred -- it runs
+            # inside the next all-task step when that step's minibatch comes from the buffer this φ was
+            # appended to (one launch set), else before the next call that reads w
             self._alpha_f = float(self.alpha_w)
-            self._lms_pend = (phi, phi._version, float(r), task_index)
+            self._lms_pend = (phi, phi._version, r if dev_r else float(r), task_index, r._version if dev_r else 0)
             return
         if isinstance(r, (float, int, np.floating, np.integer)) or (torch.is_tensor(r) and r.device.type == "cpu"
                                                                   and r.numel() == 1):

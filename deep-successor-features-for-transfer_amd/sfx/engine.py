@@ -441,9 +441,10 @@ class SFEngine:
     sel_state = None
 
     def update_all_select(self, s, a, phi, s1, gamma, task_index: int, s_next=None,
-                          losses: Optional[torch.Tensor] = None, lms_task: int = -1, lms_r: float = 0.0,
+                          losses: Optional[torch.Tensor] = None, lms_task: int = -1, lms_r=0.0,
                           lms_alpha: float = 0.0):
-        """[LMS of w[lms_task] on (``lms_phi``, lms_r)], update_all, then the GPI of one next state
+        """[LMS of w[lms_task] on (``lms_phi``, lms_r: a value, or a float32 device scalar read by
+        the step)], update_all, then the GPI of one next state
         with w[task_index], fused into one launch set (sfx_update_all_select).  s_next: a float32
         device tensor of n_s values, or None for ``sel_state`` (filled by the caller).  Returns
         fresh device tensors (q [1, T, A], task []) that the step's selection writes -- what
@@ -471,8 +472,15 @@ class SFEngine:
         # reads the two output pointers from host words each launch, so it is captured once
         out = torch.empty(self._sel_ta + 2, device=self.device)
         op = out.data_ptr()
+        if type(lms_r) is torch.Tensor:
+            if not (self._on_dev(lms_r, torch.float32) and lms_r.numel() == 1):
+                raise ValueError("update_all_select: a tensor reward must be one float32 on the engine's device")
+            self._lazy_keep_r = lms_r  # read by the step's first launch
+            rv, rdev = 0.0, lms_r.data_ptr()
+        else:
+            rv, rdev = float(lms_r), None
         check(lib.sfx_update_all_select(self._h, *ptrs, xp, int(task_index), op, op + 4 * self._sel_ta,
-                                        int(lms_task), php, float(lms_r), float(lms_alpha)), "sfx_update_all_select")
+                                        int(lms_task), php, rv, rdev, float(lms_alpha)), "sfx_update_all_select")
         TA = self.T * self.A
         return out[:TA].view(1, self.T, self.A), out[self._sel_ta:self._sel_ta + 2].view(torch.int64).view(())
 

@@ -172,8 +172,9 @@ int sfx_update_all(sfx_t h, const float* S_dev, const int64_t* a_dev, const floa
 
 /*
  * One env step's library work of the all-task agent in one launch set: the LMS reward fit of
- * w[lms_task] on (lms_phi [d], lms_r) when lms_task >= 0 (SF.update_reward, features/
- * successor.py:164-167, the reward as a value like sfx_lms_value), sfx_update_all,
+ * w[lms_task] on (lms_phi [d], r) when lms_task >= 0 (SF.update_reward, features/
+ * successor.py:164-167; r = *lms_r_dev when lms_r_dev != NULL -- the reference's tasks return the
+ * reward as a device tensor -- else the value lms_r), sfx_update_all,
  * then the agent loop's next GPI (agents/agent.py:223-224 -> agents/sfdqn.py:39-45 ->
  * features/successor.py:248-273) when its state is already known: the transition's next state
  * s_next_dev [n_s] with w[task_index].  q_dev [T * A] and task_dev [1] (device, may be NULL)
@@ -185,7 +186,7 @@ int sfx_update_all(sfx_t h, const float* S_dev, const int64_t* a_dev, const floa
 int sfx_update_all_select(sfx_t h, const float* S_dev, const int64_t* a_dev, const float* phi_dev,
                           const float* S1_dev, const float* gamma_dev, int B, float* losses_dev,
                           const float* s_next_dev, int task_index, float* q_dev, int64_t* task_dev, int lms_task,
-                          const float* lms_phi_dev, float lms_r, float lms_alpha);
+                          const float* lms_phi_dev, float lms_r, const float* lms_r_dev, float lms_alpha);
 /* Collect the verdict of a pending sfx_update_all / sfx_update_all_select (waits for the step;
  * host rounds when the device rounds left a policy unverified).  A no-op without one.
  * host_rounds (may be NULL): the rounds this call ran on the host (0 when the device rounds held;

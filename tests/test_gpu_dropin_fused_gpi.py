@@ -67,7 +67,8 @@ def test_update_all_select_matches_update_all_then_gpi(geom, force, slot):
         if slot:  # the state through the engine's persistent selection input, the LMS fused in
             e1._select_slots()[0].copy_(s_next)
             e1.lms_phi.copy_(lphi)
-            q1, c1 = e1.update_all_select(s, a, phi, s1, gam, task, losses=lb, lms_task=1, lms_r=r, lms_alpha=0.05)
+            rr = torch.tensor(r, device=dev) if step % 2 else r  # odd steps: the reward as a device scalar
+            q1, c1 = e1.update_all_select(s, a, phi, s1, gam, task, losses=lb, lms_task=1, lms_r=rr, lms_alpha=0.05)
         else:
             q1, c1 = e1.update_all_select(s, a, phi, s1, gam, task, s_next=s_next, losses=lb)
         q1, c1 = e1.settle_select(q1, c1)
@@ -92,7 +93,7 @@ def test_update_all_select_matches_update_all_then_gpi(geom, force, slot):
     e2.close()
 
 
-def _run_loop(fuse, steps, monkeypatch):
+def _run_loop(fuse, steps, monkeypatch, dev_reward=False):
     from sfx.dropin.features.deep import DeepSF
     from sfx.engine import SFEngine
     from tools import dropin_loop
@@ -116,7 +117,10 @@ def _run_loop(fuse, steps, monkeypatch):
 
             def rec(a, on_device=True, _real=real_tr):
                 actions.append(int(a))
-                return _real(a, on_device)
+                s1, phi, r, term = _real(a, on_device)
+                if dev_reward:  # tasks/reacher.py:51 returns the reward as a device tensor
+                    r = torch.tensor(r, dtype=torch.float32, device=loop.device)
+                return s1, phi, r, term
 
             task.transition = rec
         loop.run(steps)
@@ -128,10 +132,11 @@ def _run_loop(fuse, steps, monkeypatch):
     return actions, heads, w, counters, calls
 
 
-def test_dropin_loop_same_run_with_fused_gpi(monkeypatch):
+@pytest.mark.parametrize("dev_reward", [False, True])
+def test_dropin_loop_same_run_with_fused_gpi(monkeypatch, dev_reward):
     steps = 90  # 32 to fill the minibatch, then fused steps
-    a0, h0, w0, c0, n0 = _run_loop(False, steps, monkeypatch)
-    a1, h1, w1, c1, n1 = _run_loop(True, steps, monkeypatch)
+    a0, h0, w0, c0, n0 = _run_loop(False, steps, monkeypatch, dev_reward)
+    a1, h1, w1, c1, n1 = _run_loop(True, steps, monkeypatch, dev_reward)
     # fused: every step but the first (which names the buffer's copy targets), LMS included
     assert n0["select"] == 0 and n1["select"] >= steps - 33 and n1["lms"] == n1["select"], (n0, n1)
     assert a0 == a1
