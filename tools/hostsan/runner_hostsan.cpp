@@ -218,6 +218,88 @@ void engine_scenario() {
   CK(sfx_destroy(h));
 }
 
+// the drop-in's fused agent step (round 6): sfx_replay_put_gather (append + replay in one launch,
+// copying the next state and φ into the fused step's fixed inputs), sfx_update_all_select (LMS with a
+// host or a device reward, update, next GPI through host words), sfx_settle (host rounds forced on
+// odd steps: the posted-verdict wait and the host rounds' selection), sfx_graph_stats
+void dropin_scenario() {
+  std::printf("drop-in fused step (T=3)\n");
+  std::fflush(stdout);
+  const int T = 3, B = 16, CAP = 64;
+  sfx_t h = make_handle(T);
+  float *rs, *rphi, *rs1, *S, *S1, *PHI, *G, *x, *lphi, *q, *st, *sp, *s1p, *rdev;
+  int64_t *ra, *Aout, *task, *ap;
+  if (hipMalloc(&rs, 4 * CAP * NS) || hipMalloc(&rphi, 4 * CAP * D) || hipMalloc(&rs1, 4 * CAP * NS) ||
+      hipMalloc(&ra, 8 * CAP) || hipMalloc(&S, 4 * B * NS) || hipMalloc(&S1, 4 * B * NS) || hipMalloc(&PHI, 4 * B * D) ||
+      hipMalloc(&G, 4 * B) || hipMalloc(&Aout, 8 * B) || hipMalloc(&x, 4 * NS) || hipMalloc(&lphi, 4 * D) ||
+      hipMalloc(&q, 4 * T * A) || hipMalloc(&task, 8) || hipMalloc(&st, 4 * NS) || hipMalloc(&sp, 4 * D) ||
+      hipMalloc(&s1p, 4 * NS) || hipMalloc(&ap, 8) || hipMalloc(&rdev, 4)) {
+    std::fprintf(stderr, "FAIL dropin: hipMalloc\n");
+    std::exit(1);
+  }
+  (void)hipMemset(rs, 0, 4 * CAP * NS);
+  (void)hipMemset(rs1, 0, 4 * CAP * NS);
+  (void)hipMemset(rphi, 0, 4 * CAP * D);
+  (void)hipMemset(ra, 0, 8 * CAP);
+  int64_t* hidx = nullptr;  // indices and γ in coherent host memory, as the drop-in hands them over
+  if (sfx_host_alloc(8 * (B + B), reinterpret_cast<void**>(&hidx)) != 0) {
+    std::fprintf(stderr, "FAIL dropin: sfx_host_alloc\n");
+    std::exit(1);
+  }
+  float* hgam = reinterpret_cast<float*>(hidx + B);
+  std::vector<float> hs(NS), hp(D), hs1(NS);
+  for (int it = 0; it < 8; ++it) {
+    for (float& v : hs) v = urand() - 0.5f;
+    for (float& v : hp) v = urand();
+    for (float& v : hs1) v = urand() - 0.5f;
+    const int64_t a = (int64_t)(urand() * A) % A;
+    const float r = urand();
+    if (hipMemcpy(st, hs.data(), 4 * NS, hipMemcpyHostToDevice) || hipMemcpy(sp, hp.data(), 4 * D, hipMemcpyHostToDevice) ||
+        hipMemcpy(s1p, hs1.data(), 4 * NS, hipMemcpyHostToDevice) || hipMemcpy(ap, &a, 8, hipMemcpyHostToDevice) ||
+        hipMemcpy(rdev, &r, 4, hipMemcpyHostToDevice)) {
+      std::fprintf(stderr, "FAIL dropin: hipMemcpy\n");
+      std::exit(1);
+    }
+    const int j = it % CAP, size = it + 1 < B ? B : it + 1;
+    for (int b = 0; b < B; ++b) {
+      hidx[b] = b % 2 ? j : (int64_t)(urand() * size) % size;  // every other draw: the new row
+      hgam[b] = 0.9f;
+    }
+    CK(sfx_replay_put_gather(nullptr, rs, rphi, rs1, ra, nullptr, j, st, sp, s1p, ap, x, lphi, hidx,
+                             reinterpret_cast<const float*>(hgam), B, S, PHI, S1, Aout, G, NS, D));
+    CK(sfx_debug_force_rerun(h, it % 2 ? 1 : -1));
+    CK(sfx_update_all_select(h, S, Aout, PHI, S1, G, B, nullptr, x, 1, q, task, 1, lphi, r, it % 4 >= 2 ? rdev : nullptr,
+                             0.05f));
+    int hr = -1;
+    CK(sfx_settle(h, &hr));
+    if ((it % 2) && hr <= 0) {
+      std::fprintf(stderr, "FAIL dropin: forced host rounds did not run (%d)\n", hr);
+      std::exit(1);
+    }
+  }
+  std::vector<float> hq(T * A);
+  int64_t ht = -1;
+  if (hipMemcpy(hq.data(), q, 4 * T * A, hipMemcpyDeviceToHost) || hipMemcpy(&ht, task, 8, hipMemcpyDeviceToHost)) {
+    std::fprintf(stderr, "FAIL dropin: hipMemcpy back\n");
+    std::exit(1);
+  }
+  for (float v : hq)
+    if (!std::isfinite(v)) {
+      std::fprintf(stderr, "FAIL dropin: non-finite q\n");
+      std::exit(1);
+    }
+  long long cap_n = 0, launches = 0, cached = 0;
+  CK(sfx_graph_stats(h, &cap_n, &launches, &cached));
+  std::printf("  8 steps, task %lld, graphs captured %lld, launches %lld, cached %lld\n", (long long)ht, cap_n, launches,
+              cached);
+  std::fflush(stdout);
+  for (void* p : {(void*)rs, (void*)rphi, (void*)rs1, (void*)ra, (void*)S, (void*)S1, (void*)PHI, (void*)G, (void*)Aout,
+                  (void*)x, (void*)lphi, (void*)q, (void*)task, (void*)st, (void*)sp, (void*)s1p, (void*)ap, (void*)rdev})
+    (void)hipFree(p);
+  CK(sfx_host_free(hidx));
+  CK(sfx_destroy(h));
+}
+
 }  // namespace
 
 int main() {
@@ -245,6 +327,8 @@ int main() {
     scenario("all-task, graphs, no pre-launch", 0, 3, false);
     unsetenv("SFX_RUNNER_PIPELINE");
   }
+  engine_scenario();
+  dropin_scenario();
   scenario("all-task", 0, 3, false);
   scenario("all-task", 0, 4, true);
   scenario("active-task", 1, 3, true);
