@@ -2084,10 +2084,18 @@ int sfx_update_all_select(sfx_t h, const float* S, const int64_t* a, const float
   return SFX_OK;
 }
 
-int sfx_settle(sfx_t h, int* host_rounds) {
+int sfx_settle(sfx_t h, int* host_rounds, int64_t* sel) {
   if (!h) SFX_FAIL(SFX_E_ARG, "null handle");
   const long long r0 = h->rounds_total, s0 = h->steps_spec;
-  RC(settle(h));
+  int64_t out[3] = {-1, -1, -1};
+  if (h->lazy_finish) {
+    h->lazy_finish = false;
+    RC(sfx_step_finish(h, out));
+  }
+  if (sel) {
+    sel[0] = out[0];
+    sel[1] = out[1];
+  }
   if (host_rounds) {
     // rounds run by this settle beyond the device rounds of the step it collected
     const long long ran = h->rounds_total - r0, dev = h->steps_spec > s0 ? h->spec_rounds : 0;

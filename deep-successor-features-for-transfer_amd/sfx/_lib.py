@@ -44,7 +44,7 @@ SIGNATURES = {
     "sfx_update": (_I, [_VP, _I, _VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _VP, _VP]),
     "sfx_update_all": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _VP]),
     "sfx_update_all_select": (_I, [_VP, _VP, _VP, _VP, _VP, _VP, _I, _VP, _VP, _I, _VP, _VP, _I, _VP, _F, _VP, _F]),
-    "sfx_settle": (_I, [_VP, C.POINTER(C.c_int)]),
+    "sfx_settle": (_I, [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int64)]),
     "sfx_lms": (_I, [_VP, _I, _VP, _VP, _F]),
     "sfx_lms_value": (_I, [_VP, _I, _VP, _F, _F]),
     "sfx_host_alloc": (_I, [C.c_size_t, C.POINTER(_VP)]),

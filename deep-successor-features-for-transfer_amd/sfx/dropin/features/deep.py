@@ -384,7 +384,7 @@ class DeepSF(SF):
         if (ref is not None and state is ref and not self._pending and state._version == pred[1]
                 and task_index == pred[2] and self._eng is not None and self._eng_T == self.n_tasks):
             # computed by the last update's final round, on the heads and w this call would read
-            q, task = self._eng.settle_select(pred[3], pred[4])
+            q, task, _ = self._eng.settle_select(pred[3], pred[4])
             self._release_held()
             dev = self._out_device()
             if dev != self._eng.device:

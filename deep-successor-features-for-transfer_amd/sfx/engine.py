@@ -126,7 +126,7 @@ class SFEngine:
         return torch.cuda.stream(st)
 
     def _settle_pending(self):
-        check(lib.sfx_settle(self._h, None), "sfx_settle")
+        check(lib.sfx_settle(self._h, None, None), "sfx_settle")
 
     def _site_buf(self, site, nbytes) -> torch.Tensor:
         """The device staging buffer of one call site: the same memory every call, so the call's
@@ -486,15 +486,17 @@ class SFEngine:
 
     def settle_select(self, q, task):
         """Collect the pending step's verdict (sfx_settle); (q, task) of update_all_select hold the
-        selection then (host rounds, if any, rewrote them in place)."""
-        check(lib.sfx_settle(self._h, None), "sfx_settle")
-        return q, task
+        selection then (host rounds, if any, rewrote them in place).  Returns (q, task, c): c the
+        task index as the host read it from the step (-1 when no step with a selection was pending)."""
+        sel = (C.c_int64 * 2)()
+        check(lib.sfx_settle(self._h, None, sel), "sfx_settle")
+        return q, task, int(sel[0])
 
     def settle(self) -> int:
         """sfx_settle: collect the verdict of a pending update_all / update_all_select; returns the
         rounds that ran on the host."""
         n = C.c_int()
-        check(lib.sfx_settle(self._h, C.byref(n)), "sfx_settle")
+        check(lib.sfx_settle(self._h, C.byref(n), None), "sfx_settle")
         return n.value
 
     def step_all(self, s=None, a=None, phi=None, s1=None, gamma=None, *, use_gpi: bool = True, lms_task: int = -1,

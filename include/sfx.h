@@ -190,8 +190,10 @@ int sfx_update_all_select(sfx_t h, const float* S_dev, const int64_t* a_dev, con
 /* Collect the verdict of a pending sfx_update_all / sfx_update_all_select (waits for the step;
  * host rounds when the device rounds left a policy unverified).  A no-op without one.
  * host_rounds (may be NULL): the rounds this call ran on the host (0 when the device rounds held;
- * sfx_update_all_select's q / task were then rewritten after the host rounds). */
-int sfx_settle(sfx_t h, int* host_rounds);
+ * sfx_update_all_select's q / task were then rewritten after the host rounds).  sel (may be NULL):
+ * [2] the collected step's selection (GPI task c, greedy action) -- c is the task sfx_update_all_select
+ * wrote -- or -1 when this call collected no step with a selection. */
+int sfx_settle(sfx_t h, int* host_rounds, int64_t* sel);
 
 /*
  * Fused env step of the all-task schedule: the device half of one Agent.next_sample

@@ -71,7 +71,7 @@ def test_update_all_select_matches_update_all_then_gpi(geom, force, slot):
             q1, c1 = e1.update_all_select(s, a, phi, s1, gam, task, losses=lb, lms_task=1, lms_r=rr, lms_alpha=0.05)
         else:
             q1, c1 = e1.update_all_select(s, a, phi, s1, gam, task, s_next=s_next, losses=lb)
-        q1, c1 = e1.settle_select(q1, c1)
+        q1, c1, ch = e1.settle_select(q1, c1)
         if slot:
             e2.lms(1, lphi, r, 0.05)
         e2.update_all(s, a, phi, s1, gam)
@@ -79,7 +79,7 @@ def test_update_all_select_matches_update_all_then_gpi(geom, force, slot):
         torch.cuda.synchronize()
         assert q1.shape == q2.shape and c1.shape == c2.shape == ()
         assert torch.equal(q1, q2), (step, (q1 - q2).abs().max().item())
-        assert int(c1) == int(c2)
+        assert int(c1) == int(c2) == ch  # the host's copy of the selection is the device's
         for t in range(T):
             assert torch.equal(e1.get_head(t, 0), e2.get_head(t, 0)), (step, t)
             assert torch.equal(e1.get_w(t)[0], e2.get_w(t)[0]), (step, t)

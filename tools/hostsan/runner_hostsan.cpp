@@ -271,7 +271,7 @@ void dropin_scenario() {
     CK(sfx_update_all_select(h, S, Aout, PHI, S1, G, B, nullptr, x, 1, q, task, 1, lphi, r, it % 4 >= 2 ? rdev : nullptr,
                              0.05f));
     int hr = -1;
-    CK(sfx_settle(h, &hr));
+    CK(sfx_settle(h, &hr, nullptr));
     if ((it % 2) && hr <= 0) {
       std::fprintf(stderr, "FAIL dropin: forced host rounds did not run (%d)\n", hr);
       std::exit(1);
