@@ -476,10 +476,11 @@ def bench_other_workloads(args, device, steps: int = 1000, warmup: int = 200) ->
     # the drop-in: features.deep.DeepSF under the reference user's Python agent loop (tools/dropin_loop.py)
     from tools import dropin_loop
 
-    # 1,000 timed steps (≈0.25 s with the alias buffer): a 300-step window moved ±5 % run to run
+    # the median of three consecutive 1,000-step windows (≈0.25 s each with the alias buffer): one
+    # 300-step window moved ±5 % run to run
     for buf in ("reference", "objring", "host"):
-        out[f"reacher17-all-T8-B32-dropin-{buf}-buffer"] = dropin_loop.measure(buf, steps=1000, warmup=60,
-                                                                                batch=args.batch, device=device)
+        out[f"reacher17-all-T8-B32-dropin-{buf}-buffer"] = dropin_loop.measure(
+            buf, steps=1000, warmup=60, windows=3 if buf != "objring" else 1, batch=args.batch, device=device)
     # the test phase (agents/sfdqn.py:111-115): 8 test tasks one after the other as the reference
     # runs them, and in lockstep (sfx/lockstep.py, one sfx_test_actions launch set per step)
     from tools import test_phase

@@ -192,20 +192,29 @@ class DropinLoop:
         self.sf._close()
 
 
-def measure(buffer="reference", steps=300, warmup=60, **kw) -> dict:
+def measure(buffer="reference", steps=300, warmup=60, windows=1, **kw) -> dict:
+    """env-steps/s of the loop: `warmup` untimed steps, then `windows` consecutive timed windows of
+    `steps` steps each; the value is their median (every window's rate is in the record)."""
     loop = DropinLoop(buffer=buffer, **kw)
     loop.run(warmup)
     loop.sf._flush()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    loop.run(steps)
-    loop.sf._flush()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    dts = []
+    for _ in range(windows):
+        t0 = time.perf_counter()
+        loop.run(steps)
+        loop.sf._flush()
+        torch.cuda.synchronize()
+        dts.append(time.perf_counter() - t0)
     loop.close()
-    return {"value": round(steps / dt, 2), "unit": "env steps/s", "ms_per_step": round(1000.0 * dt / steps, 4),
-            "steps": steps, "dtype": "fp32",
-            "path": f"drop-in features.deep.DeepSF under a Python agents/sfdqn.py loop ({buffer} replay buffer)"}
+    dt = sorted(dts)[len(dts) // 2]
+    out = {"value": round(steps / dt, 2), "unit": "env steps/s", "ms_per_step": round(1000.0 * dt / steps, 4),
+           "steps": steps, "dtype": "fp32",
+           "path": f"drop-in features.deep.DeepSF under a Python agents/sfdqn.py loop ({buffer} replay buffer)"}
+    if windows > 1:
+        out["windows"] = [round(steps / t, 2) for t in dts]
+        out["statistic"] = f"median of {windows} consecutive {steps}-step windows after {warmup} warm-up steps"
+    return out
 
 
 if __name__ == "__main__":
